@@ -1,0 +1,242 @@
+// Python bindings for the CDNA4 kernels in csrc/ops/*.hip.
+// Every entry point validates shapes/dtypes/devices on the host (so a bad call
+// fails loudly instead of faulting the GPU) and launches on the caller's
+// current HIP stream, which keeps them hipGraph-capturable.
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+#include <hip/hip_runtime_api.h>
+
+extern "C" {
+int pa_rmsnorm(void* out, const void* x, const void* w, int T, int D, float eps, hipStream_t st);
+int pa_fused_add_rmsnorm(void* out, void* resid, const void* x, const void* w, int T, int D,
+                         float eps, hipStream_t st);
+int pa_rope_cache(void* q_out, void* k_cache, void* v_cache, const void* qkv, const int* positions,
+                  const int* slot_mapping, const float* cos_sin, int T, int H, int KV, int ld,
+                  int block_size, int apply_rope, hipStream_t st);
+int pa_silu_mul(void* out, const void* in, int T, int F, hipStream_t st);
+int pa_paged_attention(void* out, float* part_o, float* part_ml, const void* q, const void* k_cache,
+                       const void* v_cache, const int* items, const int* n_items, int max_items,
+                       const int* ritems, const int* n_ritems, int max_ritems, const int* q_start,
+                       const int* q_len, const int* ctx_len, const int* block_table,
+                       int max_blocks, int H, int KV, float scale_log2, hipStream_t st);
+int pa_sample_workspace_floats(int rows, int V);
+int pa_sample(int* out_tokens, float* out_keys, float* workspace, const void* logits, int rows,
+              int V, int ld, int vocab_offset, const float* temperature, const int* mask_class,
+              const uint32_t* class_masks, int mask_words, const int64_t* seeds,
+              const int* offsets, const int* forced, hipStream_t st);
+int pa_cosine_topk_workspace_bytes(int Q, int N, int K);
+int pa_cosine_topk(float* out_scores, int* out_rows, void* workspace, const void* queries,
+                   const void* index, int Q, int N, int D, int K, const int* row_priority,
+                   const uint64_t* row_tags, const float* row_expiry, const int* q_min_priority,
+                   const uint64_t* q_tags, float now, int n_valid, hipStream_t st);
+}
+
+namespace {
+
+hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+void check_gpu(const at::Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+  TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
+}
+void check_dtype(const at::Tensor& t, at::ScalarType dt, const char* name) {
+  TORCH_CHECK(t.scalar_type() == dt, name, " has dtype ", t.scalar_type(), ", expected ", dt);
+}
+void check_rc(int rc, const char* what) {
+  TORCH_CHECK(rc == 0, what, " launch failed with code ", rc, " (",
+              rc > 0 ? hipGetErrorString((hipError_t)rc) : "bad arguments", ")");
+}
+
+void rmsnorm(at::Tensor out, at::Tensor x, at::Tensor w, double eps) {
+  check_gpu(out, "out"); check_gpu(x, "x"); check_gpu(w, "w");
+  check_dtype(x, at::kBFloat16, "x"); check_dtype(out, at::kBFloat16, "out");
+  check_dtype(w, at::kBFloat16, "w");
+  const int D = x.size(-1);
+  const int T = x.numel() / D;
+  TORCH_CHECK(w.numel() == D && out.numel() == x.numel(), "rmsnorm shape mismatch");
+  check_rc(pa_rmsnorm(out.data_ptr(), x.data_ptr(), w.data_ptr(), T, D, (float)eps, cur_stream()),
+           "rmsnorm");
+}
+
+void fused_add_rmsnorm(at::Tensor out, at::Tensor resid, at::Tensor x, at::Tensor w, double eps) {
+  check_gpu(out, "out"); check_gpu(resid, "resid"); check_gpu(x, "x"); check_gpu(w, "w");
+  check_dtype(x, at::kBFloat16, "x"); check_dtype(resid, at::kBFloat16, "resid");
+  check_dtype(out, at::kBFloat16, "out"); check_dtype(w, at::kBFloat16, "w");
+  const int D = x.size(-1);
+  const int T = x.numel() / D;
+  TORCH_CHECK(w.numel() == D && out.numel() == x.numel() && resid.numel() == x.numel(),
+              "fused_add_rmsnorm shape mismatch");
+  check_rc(pa_fused_add_rmsnorm(out.data_ptr(), resid.data_ptr(), x.data_ptr(), w.data_ptr(), T,
+                                D, (float)eps, cur_stream()),
+           "fused_add_rmsnorm");
+}
+
+void rope_cache(at::Tensor q_out, at::Tensor k_cache, at::Tensor v_cache, at::Tensor qkv,
+                at::Tensor positions, at::Tensor slot_mapping, at::Tensor cos_sin, int64_t H,
+                int64_t KV, bool apply_rope) {
+  check_gpu(q_out, "q_out"); check_gpu(k_cache, "k_cache"); check_gpu(v_cache, "v_cache");
+  check_gpu(positions, "positions"); check_gpu(slot_mapping, "slot_mapping");
+  check_gpu(cos_sin, "cos_sin");
+  TORCH_CHECK(qkv.is_cuda() && qkv.stride(-1) == 1, "qkv must be a GPU tensor with unit inner stride");
+  check_dtype(qkv, at::kBFloat16, "qkv"); check_dtype(q_out, at::kBFloat16, "q_out");
+  check_dtype(k_cache, at::kBFloat16, "k_cache"); check_dtype(v_cache, at::kBFloat16, "v_cache");
+  check_dtype(positions, at::kInt, "positions"); check_dtype(slot_mapping, at::kInt, "slot_mapping");
+  check_dtype(cos_sin, at::kFloat, "cos_sin");
+  const int T = qkv.size(0);
+  TORCH_CHECK(qkv.size(1) >= (H + 2 * KV) * 128, "qkv too narrow");
+  TORCH_CHECK(positions.numel() >= T && slot_mapping.numel() >= T, "positions/slots too short");
+  TORCH_CHECK(k_cache.dim() == 4 && k_cache.size(1) == KV && k_cache.size(3) == 128,
+              "k_cache must be [blocks, KV, block, 128]");
+  TORCH_CHECK(v_cache.dim() == 4 && v_cache.size(1) == KV && v_cache.size(2) == 128,
+              "v_cache must be [blocks, KV, 128, block]");
+  TORCH_CHECK(cos_sin.size(1) == 128, "cos_sin must be [max_pos, 128]");
+  const int block = k_cache.size(2);
+  check_rc(pa_rope_cache(q_out.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(), qkv.data_ptr(),
+                         positions.data_ptr<int>(), slot_mapping.data_ptr<int>(),
+                         cos_sin.data_ptr<float>(), T, H, KV, qkv.stride(0), block,
+                         apply_rope ? 1 : 0, cur_stream()),
+           "rope_cache");
+}
+
+void silu_mul(at::Tensor out, at::Tensor in) {
+  check_gpu(out, "out"); check_gpu(in, "in");
+  check_dtype(out, at::kBFloat16, "out"); check_dtype(in, at::kBFloat16, "in");
+  const int F = out.size(-1);
+  const int T = out.numel() / F;
+  TORCH_CHECK(in.size(-1) == 2 * F && in.numel() == 2 * out.numel(), "silu_mul shape mismatch");
+  check_rc(pa_silu_mul(out.data_ptr(), in.data_ptr(), T, F, cur_stream()), "silu_mul");
+}
+
+void paged_attention(at::Tensor out, at::Tensor part_o, at::Tensor part_ml, at::Tensor q,
+                     at::Tensor k_cache, at::Tensor v_cache, at::Tensor items, at::Tensor n_items,
+                     at::Tensor ritems, at::Tensor n_ritems, at::Tensor q_start, at::Tensor q_len,
+                     at::Tensor ctx_len, at::Tensor block_table, double scale) {
+  for (auto* t : {&out, &part_o, &part_ml, &q, &k_cache, &v_cache, &items, &n_items, &ritems,
+                  &n_ritems, &q_start, &q_len, &ctx_len, &block_table})
+    check_gpu(*t, "paged_attention arg");
+  check_dtype(q, at::kBFloat16, "q"); check_dtype(out, at::kBFloat16, "out");
+  check_dtype(k_cache, at::kBFloat16, "k_cache"); check_dtype(v_cache, at::kBFloat16, "v_cache");
+  check_dtype(part_o, at::kFloat, "part_o"); check_dtype(part_ml, at::kFloat, "part_ml");
+  for (auto* t : {&items, &n_items, &ritems, &n_ritems, &q_start, &q_len, &ctx_len, &block_table})
+    check_dtype(*t, at::kInt, "paged_attention int arg");
+  TORCH_CHECK(q.dim() == 3 && q.size(2) == 128, "q must be [T, H, 128]");
+  TORCH_CHECK(k_cache.dim() == 4 && k_cache.size(2) == 16 && k_cache.size(3) == 128,
+              "k_cache must be [blocks, KV, 16, 128]");
+  TORCH_CHECK(v_cache.dim() == 4 && v_cache.size(2) == 128 && v_cache.size(3) == 16,
+              "v_cache must be [blocks, KV, 128, 16]");
+  const int H = q.size(1), KV = k_cache.size(1);
+  TORCH_CHECK(items.dim() == 2 && items.size(1) == 4, "items must be [max_items, 4]");
+  TORCH_CHECK(ritems.dim() == 2 && ritems.size(1) == 4, "ritems must be [max_ritems, 4]");
+  TORCH_CHECK(block_table.dim() == 2, "block_table must be [seqs, max_blocks]");
+  const int max_items = items.size(0), max_ritems = ritems.size(0);
+  TORCH_CHECK(part_o.numel() >= (int64_t)max_items * KV * 16 * 128 || max_ritems == 0,
+              "part_o workspace too small");
+  TORCH_CHECK(part_ml.numel() >= (int64_t)max_items * KV * 16 * 2 || max_ritems == 0,
+              "part_ml workspace too small");
+  const float scale_log2 = (float)(scale * 1.4426950408889634);
+  check_rc(pa_paged_attention(out.data_ptr(), part_o.data_ptr<float>(), part_ml.data_ptr<float>(),
+                              q.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(),
+                              items.data_ptr<int>(), n_items.data_ptr<int>(), max_items,
+                              ritems.data_ptr<int>(), n_ritems.data_ptr<int>(), max_ritems,
+                              q_start.data_ptr<int>(), q_len.data_ptr<int>(),
+                              ctx_len.data_ptr<int>(), block_table.data_ptr<int>(),
+                              block_table.size(1), H, KV, scale_log2, cur_stream()),
+           "paged_attention");
+}
+
+int64_t sample_workspace_floats(int64_t rows, int64_t V) {
+  return pa_sample_workspace_floats(rows, V);
+}
+
+void sample(at::Tensor out_tokens, c10::optional<at::Tensor> out_keys, at::Tensor workspace,
+            at::Tensor logits, int64_t vocab_offset, at::Tensor temperature, at::Tensor mask_class,
+            at::Tensor class_masks, at::Tensor seeds, at::Tensor offsets,
+            c10::optional<at::Tensor> forced) {
+  check_gpu(out_tokens, "out_tokens"); check_gpu(workspace, "workspace");
+  check_gpu(temperature, "temperature"); check_gpu(mask_class, "mask_class");
+  check_gpu(class_masks, "class_masks"); check_gpu(seeds, "seeds"); check_gpu(offsets, "offsets");
+  TORCH_CHECK(logits.is_cuda() && logits.dim() == 2 && logits.stride(1) == 1,
+              "logits must be a 2-D GPU tensor with unit inner stride");
+  check_dtype(logits, at::kBFloat16, "logits"); check_dtype(out_tokens, at::kInt, "out_tokens");
+  check_dtype(workspace, at::kFloat, "workspace"); check_dtype(temperature, at::kFloat, "temperature");
+  check_dtype(mask_class, at::kInt, "mask_class"); check_dtype(class_masks, at::kInt, "class_masks");
+  check_dtype(seeds, at::kLong, "seeds"); check_dtype(offsets, at::kInt, "offsets");
+  const int rows = logits.size(0), V = logits.size(1);
+  TORCH_CHECK(out_tokens.numel() >= rows && temperature.numel() >= rows &&
+                  mask_class.numel() >= rows && seeds.numel() >= rows && offsets.numel() >= rows,
+              "per-row sampling parameter tensors too short");
+  TORCH_CHECK(workspace.numel() >= pa_sample_workspace_floats(rows, V), "sample workspace too small");
+  TORCH_CHECK(class_masks.dim() == 2, "class_masks must be [classes, words]");
+  TORCH_CHECK(class_masks.size(1) * 32 >= vocab_offset + V, "class_masks too narrow for vocab");
+  float* keys = nullptr;
+  if (out_keys.has_value()) {
+    check_gpu(*out_keys, "out_keys"); check_dtype(*out_keys, at::kFloat, "out_keys");
+    keys = out_keys->data_ptr<float>();
+  }
+  const int* fp = nullptr;
+  if (forced.has_value()) {
+    check_gpu(*forced, "forced"); check_dtype(*forced, at::kInt, "forced");
+    fp = forced->data_ptr<int>();
+  }
+  check_rc(pa_sample(out_tokens.data_ptr<int>(), keys, workspace.data_ptr<float>(),
+                     logits.data_ptr(), rows, V, logits.stride(0), vocab_offset,
+                     temperature.data_ptr<float>(), mask_class.data_ptr<int>(),
+                     reinterpret_cast<const uint32_t*>(class_masks.data_ptr<int>()),
+                     class_masks.size(1), seeds.data_ptr<int64_t>(), offsets.data_ptr<int>(), fp,
+                     cur_stream()),
+           "sample");
+}
+
+int64_t cosine_topk_workspace_bytes(int64_t Q, int64_t N, int64_t K) {
+  return pa_cosine_topk_workspace_bytes(Q, N, K);
+}
+
+void cosine_topk(at::Tensor out_scores, at::Tensor out_rows, at::Tensor workspace,
+                 at::Tensor queries, at::Tensor index, int64_t n_valid, int64_t K,
+                 at::Tensor row_priority, at::Tensor row_tags, at::Tensor row_expiry,
+                 at::Tensor q_min_priority, at::Tensor q_tags, double now) {
+  for (auto* t : {&out_scores, &out_rows, &workspace, &queries, &index, &row_priority, &row_tags,
+                  &row_expiry, &q_min_priority, &q_tags})
+    check_gpu(*t, "cosine_topk arg");
+  check_dtype(queries, at::kBFloat16, "queries"); check_dtype(index, at::kBFloat16, "index");
+  check_dtype(out_scores, at::kFloat, "out_scores"); check_dtype(out_rows, at::kInt, "out_rows");
+  check_dtype(row_priority, at::kInt, "row_priority"); check_dtype(row_tags, at::kLong, "row_tags");
+  check_dtype(row_expiry, at::kFloat, "row_expiry");
+  check_dtype(q_min_priority, at::kInt, "q_min_priority"); check_dtype(q_tags, at::kLong, "q_tags");
+  TORCH_CHECK(queries.dim() == 2 && index.dim() == 2 && queries.size(1) == index.size(1),
+              "queries [Q, D] and index [N, D] must agree on D");
+  const int Q = queries.size(0), N = index.size(0), D = index.size(1);
+  TORCH_CHECK(n_valid <= N, "n_valid exceeds index rows");
+  TORCH_CHECK(out_scores.numel() >= (int64_t)Q * K && out_rows.numel() >= (int64_t)Q * K,
+              "output too small");
+  TORCH_CHECK(workspace.numel() * workspace.element_size() >=
+                  pa_cosine_topk_workspace_bytes(Q, n_valid, K),
+              "cosine_topk workspace too small");
+  check_rc(pa_cosine_topk(out_scores.data_ptr<float>(), out_rows.data_ptr<int>(),
+                          workspace.data_ptr(), queries.data_ptr(), index.data_ptr(), Q,
+                          (int)n_valid, D, K, row_priority.data_ptr<int>(),
+                          reinterpret_cast<const uint64_t*>(row_tags.data_ptr<int64_t>()),
+                          row_expiry.data_ptr<float>(), q_min_priority.data_ptr<int>(),
+                          reinterpret_cast<const uint64_t*>(q_tags.data_ptr<int64_t>()),
+                          (float)now, (int)n_valid, cur_stream()),
+           "cosine_topk");
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_C, m) {
+  m.doc() = "pilottai_amd CDNA4 (gfx950) HIP kernels";
+  m.def("rmsnorm", &rmsnorm);
+  m.def("fused_add_rmsnorm", &fused_add_rmsnorm);
+  m.def("rope_cache", &rope_cache);
+  m.def("silu_mul", &silu_mul);
+  m.def("paged_attention", &paged_attention);
+  m.def("sample_workspace_floats", &sample_workspace_floats);
+  m.def("sample", &sample, py::arg("out_tokens"), py::arg("out_keys"), py::arg("workspace"),
+        py::arg("logits"), py::arg("vocab_offset"), py::arg("temperature"), py::arg("mask_class"),
+        py::arg("class_masks"), py::arg("seeds"), py::arg("offsets"), py::arg("forced"));
+  m.def("cosine_topk_workspace_bytes", &cosine_topk_workspace_bytes);
+  m.def("cosine_topk", &cosine_topk);
+  m.attr("ATT_PART") = 512;
+  m.attr("SAMPLE_CHUNK") = 4096;
+}

@@ -1,0 +1,69 @@
+// Shared device helpers for the pilottai_amd CDNA4 (gfx950) kernels.
+//
+// Conventions used by every kernel in csrc/ops:
+//   * wave64 everywhere (block sizes are multiples of 64, lane = threadIdx.x & 63),
+//   * bf16 tensors are moved as 16-byte vectors (8 x bf16) whenever the row
+//     length allows it (guide Guideline 13: scalar bf16 loads cost ~2x),
+//   * accumulation is fp32; conversion back to bf16 uses the hardware
+//     v_cvt_pk_bf16_f32 path (plain __bf16 casts, NaN-preserving),
+//   * launchers are plain C functions that take raw device pointers and a
+//     hipStream_t so they can be captured into hipGraphs (no syncs, no mallocs).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace pa {
+
+typedef __bf16 bf16;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ float bf2f(bf16 x) { return (float)x; }
+__device__ __forceinline__ bf16 f2bf(float x) { return (bf16)x; }
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Block-wide sum for blocks of NWAVES waves; `red` must hold NWAVES floats.
+template <int NWAVES>
+__device__ __forceinline__ float block_sum(float v, float* red) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  v = wave_sum(v);
+  if (lane == 0) red[wid] = v;
+  __syncthreads();
+  float t = 0.f;
+#pragma unroll
+  for (int i = 0; i < NWAVES; ++i) t += red[i];
+  __syncthreads();
+  return t;
+}
+
+// Cheap stateless 32-bit hash (splitmix-style finaliser) used as a counter-based
+// RNG for sampling: u = hash(seed, row, col) -> uniform in (0, 1).
+__device__ __forceinline__ uint32_t mix32(uint32_t x) {
+  x ^= x >> 16; x *= 0x7feb352dU;
+  x ^= x >> 15; x *= 0x846ca68bU;
+  x ^= x >> 16;
+  return x;
+}
+__device__ __forceinline__ float uniform01(uint64_t seed, uint32_t row, uint32_t col) {
+  uint32_t h = mix32((uint32_t)seed ^ mix32(row * 0x9E3779B9U + (uint32_t)(seed >> 32)));
+  h = mix32(h ^ (col * 0x85EBCA6BU + 0x27d4eb2fU));
+  // 24 random bits -> (0,1), never exactly 0 or 1
+  return ((float)(h >> 8) + 0.5f) * (1.0f / 16777216.0f);
+}
+
+}  // namespace pa

@@ -1,0 +1,16 @@
+"""CDNA4 kernels (HIP, gfx950) and their fp32 PyTorch references."""
+from .kernels import (  # noqa: F401
+    cosine_topk,
+    fused_add_rmsnorm,
+    native_available,
+    native_module_path,
+    paged_attention,
+    require_native,
+    rmsnorm,
+    rope_cache,
+    sample,
+    sample_workspace,
+    silu_mul,
+)
+from .attn_meta import ATT_PART, build_attention_items  # noqa: F401
+from . import reference  # noqa: F401

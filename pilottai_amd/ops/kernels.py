@@ -1,0 +1,169 @@
+"""Dispatch layer for the CDNA4 HIP kernels (pilottai_amd/_C.so).
+
+Device tensors ALWAYS go to the native kernels: if the extension failed to load
+on a machine with a GPU, every call raises (no silent PyTorch fallback — the
+round-end driver checks which .so files the GPU tests actually loaded). CPU
+tensors run the fp32 reference implementations in ops/reference.py, which is
+how the control-plane tests execute the whole engine without a GPU.
+"""
+from __future__ import annotations
+
+import importlib
+from typing import Optional
+
+import torch
+
+from . import reference as ref
+
+_C = None
+_LOAD_ERROR: Optional[BaseException] = None
+
+
+def _load():
+    global _C, _LOAD_ERROR
+    if _C is not None or _LOAD_ERROR is not None:
+        return _C
+    try:
+        _C = importlib.import_module("pilottai_amd._C")
+    except BaseException as e:  # noqa: BLE001 — surfaced by require_native()
+        _LOAD_ERROR = e
+    return _C
+
+
+def native_available() -> bool:
+    return _load() is not None
+
+
+def require_native():
+    mod = _load()
+    if mod is None:
+        raise RuntimeError(
+            "pilottai_amd native kernels (_C.so) are not available: "
+            f"{_LOAD_ERROR!r}. Build them with `python -m pilottai_amd._build` "
+            "(hipcc --offload-arch=gfx950).")
+    return mod
+
+
+def native_module_path() -> Optional[str]:
+    mod = _load()
+    return getattr(mod, "__file__", None) if mod is not None else None
+
+
+def _on_gpu(t: torch.Tensor) -> bool:
+    return t.device.type == "cuda"
+
+
+# ---------------------------------------------------------------------------
+
+
+def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float, out: Optional[torch.Tensor] = None):
+    if _on_gpu(x):
+        out = torch.empty_like(x) if out is None else out
+        require_native().rmsnorm(out, x, w, float(eps))
+        return out
+    r = ref.rmsnorm(x, w, eps)
+    if out is not None:
+        out.copy_(r)
+        return out
+    return r
+
+
+def fused_add_rmsnorm(resid: torch.Tensor, x: torch.Tensor, w: torch.Tensor, eps: float,
+                      out: Optional[torch.Tensor] = None):
+    """resid <- resid + x (in place); returns rmsnorm(resid) * w."""
+    if _on_gpu(x):
+        out = torch.empty_like(x) if out is None else out
+        require_native().fused_add_rmsnorm(out, resid, x, w, float(eps))
+        return out
+    y, nr = ref.fused_add_rmsnorm(resid, x, w, eps)
+    resid.copy_(nr)
+    if out is not None:
+        out.copy_(y)
+        return out
+    return y
+
+
+def silu_mul(x: torch.Tensor, out: Optional[torch.Tensor] = None):
+    if _on_gpu(x):
+        F = x.shape[-1] // 2
+        out = torch.empty(*x.shape[:-1], F, dtype=x.dtype, device=x.device) if out is None else out
+        require_native().silu_mul(out, x)
+        return out
+    r = ref.silu_mul(x)
+    if out is not None:
+        out.copy_(r)
+        return out
+    return r
+
+
+def rope_cache(q_out, k_cache, v_cache, qkv, positions, slot_mapping, cos_sin, H: int, KV: int,
+               apply_rope: bool = True):
+    if _on_gpu(qkv):
+        require_native().rope_cache(q_out, k_cache, v_cache, qkv, positions, slot_mapping, cos_sin,
+                                    int(H), int(KV), bool(apply_rope))
+        return q_out
+    ref.rope_cache(q_out, k_cache, v_cache, qkv, positions, slot_mapping, cos_sin, H, KV,
+                   apply_rope)
+    return q_out
+
+
+def paged_attention(out, part_o, part_ml, q, k_cache, v_cache, items, n_items, ritems, n_ritems,
+                    q_start, q_len, ctx_len, block_table, scale: float, num_seqs: Optional[int] = None):
+    """Attention over the paged cache. On GPU `items`/`ritems` must be device int32
+    [max, 4] tensors with device counts (graph-capturable); on CPU the reference
+    path ignores the item lists."""
+    if _on_gpu(q):
+        require_native().paged_attention(out, part_o, part_ml, q, k_cache, v_cache, items, n_items,
+                                         ritems, n_ritems, q_start, q_len, ctx_len, block_table,
+                                         float(scale))
+        return out
+    ns = len(q_len) if num_seqs is None else num_seqs
+    r = ref.paged_attention(q, k_cache, v_cache, q_start[:ns], q_len[:ns], ctx_len[:ns],
+                            block_table, scale)
+    n_tok = int(q_start[ns - 1] + q_len[ns - 1]) if ns > 0 else 0
+    out[:n_tok].copy_(r[:n_tok])
+    return out
+
+
+def sample_workspace(rows: int, V: int, device) -> torch.Tensor:
+    n = require_native().sample_workspace_floats(rows, V)
+    return torch.empty(n, dtype=torch.float32, device=device)
+
+
+def sample(logits, temperature, mask_class, class_masks, seeds, offsets, forced=None,
+           out: Optional[torch.Tensor] = None, workspace: Optional[torch.Tensor] = None,
+           vocab_offset: int = 0, out_keys: Optional[torch.Tensor] = None):
+    rows = logits.shape[0]
+    if _on_gpu(logits):
+        C = require_native()
+        out = torch.empty(rows, dtype=torch.int32, device=logits.device) if out is None else out
+        if workspace is None:
+            workspace = sample_workspace(rows, logits.shape[1], logits.device)
+        C.sample(out, out_keys, workspace, logits, int(vocab_offset), temperature, mask_class,
+                 class_masks, seeds, offsets, forced)
+        return out
+    toks, keys = ref.sample(logits, temperature, mask_class, class_masks, seeds, offsets, forced,
+                            vocab_offset, return_keys=True)
+    if out_keys is not None:
+        out_keys[:rows].copy_(keys)
+    if out is not None:
+        out[:rows].copy_(toks)
+        return out
+    return toks
+
+
+def cosine_topk(queries, index, n_valid: int, K: int, row_priority, row_tags, row_expiry,
+                q_min_priority, q_tags, now: float, workspace: Optional[torch.Tensor] = None):
+    if _on_gpu(index):
+        C = require_native()
+        Q = queries.shape[0]
+        out_s = torch.empty(Q, K, dtype=torch.float32, device=index.device)
+        out_r = torch.empty(Q, K, dtype=torch.int32, device=index.device)
+        need = C.cosine_topk_workspace_bytes(Q, max(1, int(n_valid)), K)
+        if workspace is None or workspace.numel() * workspace.element_size() < need:
+            workspace = torch.empty(max(need, 16), dtype=torch.uint8, device=index.device)
+        C.cosine_topk(out_s, out_r, workspace, queries, index, int(n_valid), int(K), row_priority,
+                      row_tags, row_expiry, q_min_priority, q_tags, float(now))
+        return out_s, out_r
+    return ref.cosine_topk(queries, index, n_valid, K, row_priority, row_tags, row_expiry,
+                           q_min_priority, q_tags, now)

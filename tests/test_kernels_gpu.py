@@ -1,0 +1,203 @@
+"""Numerics of the CDNA4 HIP kernels vs the fp32 PyTorch references (ops/reference.py)."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from pilottai_amd import ops
+from pilottai_amd.ops import reference as ref
+
+pytestmark = pytest.mark.gpu
+
+
+def _bf(*shape, dev, scale=1.0):
+    return (torch.randn(*shape, device=dev) * scale).to(torch.bfloat16)
+
+
+@pytest.mark.parametrize("D", [4096, 8192, 1024, 256, 4104])
+def test_rmsnorm(gpu, D):
+    torch.manual_seed(0)
+    x = _bf(37, D, dev=gpu)
+    w = _bf(D, dev=gpu)
+    y = ops.rmsnorm(x, w, 1e-5)
+    r = ref.rmsnorm(x.cpu(), w.cpu(), 1e-5)
+    torch.testing.assert_close(y.cpu().float(), r.float(), atol=2e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("D", [4096, 8192, 520])
+def test_fused_add_rmsnorm(gpu, D):
+    torch.manual_seed(1)
+    x = _bf(19, D, dev=gpu)
+    res = _bf(19, D, dev=gpu)
+    w = _bf(D, dev=gpu)
+    r_y, r_res = ref.fused_add_rmsnorm(res.cpu(), x.cpu(), w.cpu(), 1e-5)
+    y = ops.fused_add_rmsnorm(res, x, w, 1e-5)
+    torch.testing.assert_close(res.cpu().float(), r_res.float(), atol=1e-2, rtol=1e-2)
+    torch.testing.assert_close(y.cpu().float(), r_y.float(), atol=2e-2, rtol=2e-2)
+
+
+def test_silu_mul(gpu):
+    torch.manual_seed(2)
+    x = _bf(33, 2 * 14336, dev=gpu)
+    y = ops.silu_mul(x)
+    torch.testing.assert_close(y.cpu().float(), ref.silu_mul(x.cpu()).float(), atol=2e-2, rtol=2e-2)
+
+
+def _make_cache(nblocks, KV, dev, blk=16):
+    k = _bf(nblocks, KV, blk, 128, dev=dev)
+    v = _bf(nblocks, KV, 128, blk, dev=dev)
+    return k, v
+
+
+def test_rope_cache(gpu):
+    torch.manual_seed(3)
+    H, KV, T = 32, 8, 29
+    qkv = _bf(T, (H + 2 * KV) * 128, dev=gpu)
+    pos = torch.randint(0, 4000, (T,), dtype=torch.int32, device=gpu)
+    slots = torch.randperm(64 * 16, device=gpu)[:T].int()
+    slots[5] = -1  # padding token: must not be written
+    cs = ref.rope_cos_sin(4096).to(gpu)
+    kc, vc = _make_cache(64, KV, gpu)
+    kc_r, vc_r = kc.cpu().clone(), vc.cpu().clone()
+    q = torch.empty(T, H, 128, dtype=torch.bfloat16, device=gpu)
+    q_r = torch.empty(T, H, 128, dtype=torch.bfloat16)
+    ops.rope_cache(q, kc, vc, qkv, pos, slots, cs, H, KV)
+    ref.rope_cache(q_r, kc_r, vc_r, qkv.cpu(), pos.cpu(), slots.cpu(), cs.cpu(), H, KV)
+    torch.testing.assert_close(q.cpu().float(), q_r.float(), atol=2e-2, rtol=2e-2)
+    torch.testing.assert_close(kc.cpu().float(), kc_r.float(), atol=2e-2, rtol=2e-2)
+    torch.testing.assert_close(vc.cpu().float(), vc_r.float(), atol=0, rtol=0)
+
+
+def _run_attention(gpu, H, KV, q_lens, ctx_lens, seed=0, split=True):
+    torch.manual_seed(seed)
+    G = H // KV
+    blk = 16
+    ns = len(q_lens)
+    nbs = [(c + blk - 1) // blk for c in ctx_lens]
+    total_blocks = sum(nbs) + 4
+    max_blocks = max(nbs)
+    kc, vc = _make_cache(total_blocks, KV, gpu)
+    perm = torch.randperm(total_blocks).tolist()
+    bt = torch.zeros(ns, max_blocks, dtype=torch.int32)
+    c = 0
+    for s, nb in enumerate(nbs):
+        bt[s, :nb] = torch.tensor(perm[c:c + nb], dtype=torch.int32)
+        c += nb
+    q_start = np.concatenate([[0], np.cumsum(q_lens)[:-1]]).astype(np.int32)
+    T = int(sum(q_lens))
+    q = _bf(T, H, 128, dev=gpu)
+    items, ritems, nslots = ops.build_attention_items(q_lens, ctx_lens, G, split=split)
+    it = torch.tensor(items + [(0, 0, 0, 0)], dtype=torch.int32, device=gpu)
+    rit = torch.tensor(ritems + [(0, 0, 0, 0)], dtype=torch.int32, device=gpu)
+    n_it = torch.tensor([len(items)], dtype=torch.int32, device=gpu)
+    n_rit = torch.tensor([len(ritems)], dtype=torch.int32, device=gpu)
+    maxit = it.shape[0]
+    part_o = torch.empty(maxit * KV * 16 * 128, dtype=torch.float32, device=gpu)
+    part_ml = torch.empty(maxit * KV * 16 * 2, dtype=torch.float32, device=gpu)
+    out = torch.zeros(T, H, 128, dtype=torch.bfloat16, device=gpu)
+    scale = 1.0 / math.sqrt(128)
+    dev_i = lambda a: torch.tensor(a, dtype=torch.int32, device=gpu)  # noqa: E731
+    ops.paged_attention(out, part_o, part_ml, q, kc, vc, it, n_it, rit, n_rit, dev_i(q_start),
+                        dev_i(q_lens), dev_i(ctx_lens), bt.to(gpu), scale)
+    torch.cuda.synchronize()
+    r = ref.paged_attention(q.cpu(), kc.cpu(), vc.cpu(), q_start, q_lens, ctx_lens, bt, scale)
+    return out.cpu().float(), r.float()
+
+
+@pytest.mark.parametrize("H,KV", [(32, 8), (8, 1), (16, 16)])
+def test_attention_decode(gpu, H, KV):
+    ctx = [1, 15, 16, 17, 33, 100, 511, 512, 513, 1500, 2049, 64]
+    o, r = _run_attention(gpu, H, KV, [1] * len(ctx), ctx)
+    torch.testing.assert_close(o, r, atol=2e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("H,KV", [(32, 8), (8, 1)])
+def test_attention_prefill_and_mixed(gpu, H, KV):
+    q_lens = [37, 1, 100, 3, 16, 5, 250]
+    ctx = [37, 700, 164, 40, 16, 1029, 260]
+    o, r = _run_attention(gpu, H, KV, q_lens, ctx, seed=5)
+    torch.testing.assert_close(o, r, atol=2e-2, rtol=2e-2)
+
+
+def test_attention_nosplit_long(gpu):
+    o, r = _run_attention(gpu, 32, 8, [1, 2], [3000, 1200], seed=7, split=False)
+    torch.testing.assert_close(o, r, atol=2e-2, rtol=2e-2)
+
+
+def test_sample_greedy_and_masks(gpu):
+    torch.manual_seed(4)
+    rows, V = 9, 128256
+    logits = _bf(rows, V, dev=gpu, scale=3.0)
+    words = (V + 31) // 32
+    masks = torch.zeros(3, words, dtype=torch.int32)
+    masks[0] = -1  # all allowed
+    allowed = np.zeros(V, dtype=bool)
+    allowed[[5, 77, 1000, 128000]] = True
+    masks[1] = ref.pack_mask(allowed)
+    temp = torch.zeros(rows)
+    mcls = torch.tensor([-1, 0, 1, 1, -1, 0, 1, -1, 0], dtype=torch.int32)
+    forced = torch.full((rows,), -1, dtype=torch.int32)
+    forced[4] = 1234
+    seeds = torch.arange(rows, dtype=torch.int64) * 7919
+    offs = torch.arange(rows, dtype=torch.int32)
+    tok = ops.sample(logits, temp.to(gpu), mcls.to(gpu), masks.to(gpu), seeds.to(gpu), offs.to(gpu),
+                     forced.to(gpu))
+    r = ref.sample(logits.cpu(), temp, mcls, masks, seeds, offs, forced)
+    assert tok.cpu().tolist() == r.tolist()
+
+
+def test_sample_temperature_matches_reference(gpu):
+    torch.manual_seed(5)
+    rows, V = 16, 32000
+    logits = _bf(rows, V, dev=gpu, scale=2.0)
+    masks = torch.full((1, (V + 31) // 32), -1, dtype=torch.int32)
+    temp = torch.full((rows,), 0.7)
+    mcls = torch.full((rows,), -1, dtype=torch.int32)
+    seeds = torch.randint(0, 2 ** 62, (rows,), dtype=torch.int64)
+    offs = torch.randint(0, 1000, (rows,), dtype=torch.int32)
+    keys = torch.empty(rows, device=gpu)
+    tok = ops.sample(logits, temp.to(gpu), mcls.to(gpu), masks.to(gpu), seeds.to(gpu), offs.to(gpu),
+                     None, out_keys=keys)
+    r, rk = ref.sample(logits.cpu(), temp, mcls, masks, seeds, offs, None, return_keys=True)
+    # the hash is bit-identical; fast-math logs may flip near-ties only
+    agree = (tok.cpu() == r).float().mean().item()
+    assert agree >= 0.9
+    torch.testing.assert_close(keys.cpu(), rk, atol=1e-2, rtol=5e-3)
+
+
+def test_sample_distribution(gpu):
+    """Gumbel-max samples follow softmax(logits / T)."""
+    V = 64
+    rows = 4096
+    base = torch.linspace(-2, 2, V)
+    logits = base.repeat(rows, 1).to(torch.bfloat16).to(gpu)
+    masks = torch.full((1, 2), -1, dtype=torch.int32, device=gpu)
+    temp = torch.full((rows,), 0.7, device=gpu)
+    mcls = torch.full((rows,), -1, dtype=torch.int32, device=gpu)
+    seeds = torch.full((rows,), 12345, dtype=torch.int64, device=gpu)
+    offs = torch.arange(rows, dtype=torch.int32, device=gpu)
+    tok = ops.sample(logits, temp, mcls, masks, seeds, offs, None).cpu()
+    emp = torch.bincount(tok.long(), minlength=V).float() / rows
+    exp = torch.softmax(base.to(torch.bfloat16).float() / 0.7, 0)
+    assert (emp - exp).abs().max().item() < 0.03
+
+
+def test_cosine_topk(gpu):
+    torch.manual_seed(6)
+    N, D, Q, K = 20000, 1024, 5, 8
+    idx = torch.nn.functional.normalize(torch.randn(N, D), dim=1).to(torch.bfloat16)
+    qs = torch.nn.functional.normalize(torch.randn(Q, D), dim=1).to(torch.bfloat16)
+    qs[1] = idx[1234]  # exact hit
+    prio = torch.randint(0, 5, (N,), dtype=torch.int32)
+    tags = torch.randint(0, 8, (N,), dtype=torch.int64)
+    exp = torch.zeros(N)
+    exp[::7] = 50.0  # expired at now=100
+    qmin = torch.tensor([0, 0, 2, 4, 0], dtype=torch.int32)
+    qt = torch.tensor([0, 0, 1, 2, 3], dtype=torch.int64)
+    s, r = ops.cosine_topk(qs.to(gpu), idx.to(gpu), N, K, prio.to(gpu), tags.to(gpu), exp.to(gpu),
+                           qmin.to(gpu), qt.to(gpu), 100.0)
+    rs, rr = ref.cosine_topk(qs, idx, N, K, prio, tags, exp, qmin, qt, 100.0)
+    torch.testing.assert_close(s.cpu(), rs, atol=2e-3, rtol=2e-3)
+    # rows agree except for exact score ties
+    assert (r.cpu() == rr).float().mean().item() > 0.95
