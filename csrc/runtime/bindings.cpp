@@ -1,0 +1,147 @@
+// pybind11 bindings of the native serving runtime (pilottai_amd/_runtime.so).
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include "grammar.h"
+#include "scheduler.h"
+#include "tokenizer.h"
+
+namespace py = pybind11;
+using namespace rt;
+
+namespace {
+
+std::unique_ptr<Grammar> make_grammar(const py::object& segs) {
+  if (segs.is_none()) return nullptr;
+  std::vector<Segment> out;
+  for (const auto& item : segs) {
+    py::tuple t = item.cast<py::tuple>();
+    Segment s;
+    s.kind = t[0].cast<int32_t>();
+    s.tokens = t[1].cast<std::vector<int32_t>>();
+    s.cls = t[2].cast<int32_t>();
+    s.cls_last = t[3].cast<int32_t>();
+    s.end_tok = t[4].cast<int32_t>();
+    s.sep_tok = t[5].cast<int32_t>();
+    s.max_tokens = t[6].cast<int32_t>();
+    s.min_items = t[7].cast<int32_t>();
+    s.max_items = t[8].cast<int32_t>();
+    out.push_back(std::move(s));
+  }
+  return std::make_unique<Grammar>(std::move(out));
+}
+
+py::list outputs_to_py(const std::vector<SeqOutput>& outs) {
+  py::list l;
+  for (const auto& o : outs)
+    l.append(py::make_tuple(o.id, o.tokens, o.finish_reason, o.prompt_len, o.cached_prompt_tokens,
+                            o.num_sampled, o.num_forced, o.t_first_token, o.t_finish));
+  return l;
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_runtime, m) {
+  m.doc() = "pilottai_amd native serving runtime (scheduler, paged KV, grammar, tokenizer)";
+  m.def("now", &now_seconds);
+  m.def("hash_block", [](uint64_t parent, const std::vector<int32_t>& toks) {
+    return hash_block(parent, toks.data(), (int)toks.size());
+  });
+
+  py::class_<Tokenizer>(m, "Tokenizer")
+      .def(py::init([](const std::vector<py::bytes>& vocab) {
+        std::vector<std::string> v;
+        v.reserve(vocab.size());
+        for (const auto& b : vocab) v.push_back(b);
+        return std::make_unique<Tokenizer>(v);
+      }))
+      .def("encode", [](const Tokenizer& t, const py::object& text) {
+        std::string s = py::isinstance<py::bytes>(text) ? text.cast<std::string>()
+                                                          : text.cast<std::string>();
+        py::gil_scoped_release nogil;
+        return t.encode(s);
+      })
+      .def("decode", [](const Tokenizer& t, const std::vector<int32_t>& ids) {
+        return py::bytes(t.decode(ids));
+      })
+      .def("lookup", [](const Tokenizer& t, const py::bytes& p) { return t.lookup(p); })
+      .def_property_readonly("vocab_size", &Tokenizer::vocab_size);
+
+  py::class_<Grammar>(m, "Grammar")
+      .def(py::init([](const py::object& segs) { return make_grammar(segs); }))
+      .def("done", &Grammar::done)
+      .def("next", [](const Grammar& g) {
+        int32_t c, f;
+        g.next(&c, &f);
+        return py::make_tuple(c, f);
+      })
+      .def("advance", &Grammar::advance)
+      .def("take_forced_run", [](Grammar& g, int32_t max) {
+        std::vector<int32_t> out;
+        g.take_forced_run(out, max);
+        return out;
+      });
+
+  py::class_<Scheduler>(m, "Scheduler")
+      .def(py::init([](const py::dict& d) {
+        SchedulerConfig c;
+        if (d.contains("num_blocks")) c.num_blocks = d["num_blocks"].cast<int32_t>();
+        if (d.contains("block_size")) c.block_size = d["block_size"].cast<int32_t>();
+        if (d.contains("max_num_seqs")) c.max_num_seqs = d["max_num_seqs"].cast<int32_t>();
+        if (d.contains("max_num_batched_tokens"))
+          c.max_num_batched_tokens = d["max_num_batched_tokens"].cast<int32_t>();
+        if (d.contains("max_prefill_tokens"))
+          c.max_prefill_tokens = d["max_prefill_tokens"].cast<int32_t>();
+        if (d.contains("max_model_len")) c.max_model_len = d["max_model_len"].cast<int32_t>();
+        if (d.contains("gqa_group")) c.gqa_group = d["gqa_group"].cast<int32_t>();
+        if (d.contains("prefix_caching")) c.prefix_caching = d["prefix_caching"].cast<bool>();
+        if (d.contains("split_decode")) c.split_decode = d["split_decode"].cast<bool>();
+        if (d.contains("eos_ids")) c.eos_ids = d["eos_ids"].cast<std::vector<int32_t>>();
+        return std::make_unique<Scheduler>(c);
+      }))
+      .def("layout", [](const Scheduler& s) {
+        const StepLayout& L = s.layout();
+        py::dict d;
+        d["max_tokens"] = L.max_tokens; d["max_seqs"] = L.max_seqs; d["max_blocks"] = L.max_blocks;
+        d["max_items"] = L.max_items; d["max_ritems"] = L.max_ritems;
+        d["input_ids"] = L.input_ids; d["positions"] = L.positions; d["slots"] = L.slots;
+        d["q_start"] = L.q_start; d["q_len"] = L.q_len; d["ctx_len"] = L.ctx_len;
+        d["logit_rows"] = L.logit_rows; d["mask_class"] = L.mask_class; d["forced"] = L.forced;
+        d["offsets"] = L.offsets; d["temperature"] = L.temperature; d["seeds"] = L.seeds;
+        d["items"] = L.items; d["n_items"] = L.n_items; d["ritems"] = L.ritems;
+        d["n_ritems"] = L.n_ritems; d["counts"] = L.counts; d["block_table"] = L.block_table;
+        d["total"] = L.total;
+        return d;
+      })
+      .def("add_request",
+           [](Scheduler& s, int64_t id, const std::vector<int32_t>& prompt, float temperature,
+              int32_t max_tokens, int64_t seed, bool ignore_eos,
+              const std::vector<int32_t>& stop_ids, const py::object& grammar) {
+             s.add_request(id, prompt, temperature, max_tokens, seed, ignore_eos, stop_ids,
+                           make_grammar(grammar));
+           })
+      .def("schedule", [](Scheduler& s, uintptr_t buf) {
+        py::gil_scoped_release nogil;
+        return s.schedule(reinterpret_cast<int32_t*>(buf));
+      })
+      .def("commit", [](Scheduler& s, uintptr_t sampled, int32_t n) {
+        std::vector<SeqOutput> outs;
+        {
+          py::gil_scoped_release nogil;
+          outs = s.commit(reinterpret_cast<const int32_t*>(sampled), n);
+        }
+        return outputs_to_py(outs);
+      })
+      .def("abort", &Scheduler::abort)
+      .def("drain_aborted", [](Scheduler& s) { return outputs_to_py(s.drain_aborted()); })
+      .def("has_work", &Scheduler::has_work)
+      .def("reset_prefix_cache", &Scheduler::reset_prefix_cache)
+      .def_property_readonly("num_running", &Scheduler::num_running)
+      .def_property_readonly("num_waiting", &Scheduler::num_waiting)
+      .def_property_readonly("num_free_blocks", &Scheduler::num_free_blocks)
+      .def_property_readonly("num_cached_blocks", &Scheduler::num_cached_blocks)
+      .def_property_readonly("total_prompt_tokens", &Scheduler::total_prompt_tokens)
+      .def_property_readonly("total_cached_tokens", &Scheduler::total_cached_tokens)
+      .def_property_readonly("total_preemptions", &Scheduler::total_preemptions)
+      .def_property_readonly("steps", &Scheduler::steps);
+}

@@ -1,0 +1,390 @@
+#include "scheduler.h"
+
+#include <algorithm>
+#include <chrono>
+#include <cstring>
+
+namespace rt {
+
+double now_seconds() {
+  using namespace std::chrono;
+  return duration<double>(steady_clock::now().time_since_epoch()).count();
+}
+
+static int32_t align4(int32_t x) { return (x + 3) & ~3; }
+
+Scheduler::Scheduler(const SchedulerConfig& cfg)
+    : cfg_(cfg), bm_(cfg.num_blocks, cfg.block_size, cfg.prefix_caching) {
+  StepLayout& L = lay_;
+  L.max_tokens = cfg.max_num_batched_tokens;
+  L.max_seqs = cfg.max_num_seqs;
+  L.max_blocks = (cfg.max_model_len + cfg.block_size - 1) / cfg.block_size;
+  const int32_t tpw = 16 / std::max(1, cfg.gqa_group);
+  const int32_t max_parts = (cfg.max_model_len + 511) / 512;
+  L.max_items = L.max_tokens / (4 * tpw) + L.max_seqs * (max_parts + 1) + 4;
+  L.max_ritems = L.max_seqs + 4;
+  int32_t o = 0;
+  auto take = [&](int32_t n) {
+    const int32_t at = o;
+    o = align4(o + n);
+    return at;
+  };
+  L.counts = take(8);
+  L.n_items = take(1);
+  L.n_ritems = take(1);
+  L.input_ids = take(L.max_tokens);
+  L.positions = take(L.max_tokens);
+  L.slots = take(L.max_tokens);
+  L.q_start = take(L.max_seqs);
+  L.q_len = take(L.max_seqs);
+  L.ctx_len = take(L.max_seqs);
+  L.logit_rows = take(L.max_seqs);
+  L.mask_class = take(L.max_seqs);
+  L.forced = take(L.max_seqs);
+  L.offsets = take(L.max_seqs);
+  L.temperature = take(L.max_seqs);
+  L.seeds = take(2 * L.max_seqs);
+  L.items = take(4 * L.max_items);
+  L.ritems = take(4 * L.max_ritems);
+  L.block_table = take(L.max_seqs * L.max_blocks);
+  L.total = o;
+}
+
+void Scheduler::add_request(int64_t id, std::vector<int32_t> prompt, float temperature,
+                            int32_t max_tokens, int64_t seed, bool ignore_eos,
+                            std::vector<int32_t> stop_ids, std::unique_ptr<Grammar> grammar) {
+  auto s = std::make_unique<Sequence>();
+  s->id = id;
+  if ((int32_t)prompt.size() >= cfg_.max_model_len)
+    prompt.resize(cfg_.max_model_len - 1);  // keep room for at least one generated token
+  if (prompt.empty()) prompt.push_back(0);
+  s->tokens = std::move(prompt);
+  s->prompt_len = (int32_t)s->tokens.size();
+  s->temperature = temperature;
+  s->max_tokens = std::max(1, max_tokens);
+  s->seed = seed;
+  s->ignore_eos = ignore_eos;
+  s->stop_ids = std::move(stop_ids);
+  s->grammar = std::move(grammar);
+  s->arrival = arrival_counter_++;
+  // a grammar that starts with forced text (e.g. '{"key": ') is jump-forwarded into the prompt
+  if (s->grammar) {
+    const int32_t room = cfg_.max_model_len - (int32_t)s->tokens.size() - 1;
+    const int32_t k = s->grammar->take_forced_run(s->tokens, std::min(room, s->max_tokens - 1));
+    s->num_generated += k;
+    s->num_forced += k;
+  }
+  Sequence* raw = s.get();
+  seqs_.emplace(id, std::move(s));
+  waiting_.push_back(raw);
+}
+
+void Scheduler::free_seq(Sequence* s) {
+  for (int32_t b : s->blocks) bm_.release(b);
+  s->blocks.clear();
+  s->block_hashes.clear();
+}
+
+void Scheduler::preempt(Sequence* s) {
+  free_seq(s);
+  s->num_computed = 0;
+  s->running = false;
+  waiting_.push_front(s);
+  ++stat_preemptions_;
+}
+
+bool Scheduler::ensure_blocks(Sequence* s, int32_t upto_tokens) {
+  const int32_t need =
+      (upto_tokens + cfg_.block_size - 1) / cfg_.block_size - (int32_t)s->blocks.size();
+  if (need <= 0) return true;
+  return bm_.allocate(need, s->blocks);
+}
+
+void Scheduler::match_prefix(Sequence* s) {
+  const int32_t B = cfg_.block_size;
+  if (cfg_.prefix_caching) {
+    const int32_t n_full = ((int32_t)s->tokens.size() - 1) / B;  // never reuse the last token
+    uint64_t parent = 0;
+    for (int32_t b = 0; b < n_full; ++b) {
+      const int32_t* t = s->tokens.data() + (size_t)b * B;
+      const uint64_t h = hash_block(parent, t, B);
+      const int32_t blk = bm_.lookup(h, t);
+      if (blk < 0) break;
+      s->blocks.push_back(blk);
+      s->block_hashes.push_back(h);
+      parent = h;
+    }
+  }
+  s->num_computed = (int32_t)s->blocks.size() * B;
+  if (s->cached_prompt_tokens < 0) {
+    s->cached_prompt_tokens = std::min(s->num_computed, s->prompt_len);
+    stat_cached_tokens_ += s->cached_prompt_tokens;
+    stat_prompt_tokens_ += s->prompt_len;
+  }
+}
+
+void Scheduler::register_full_blocks(Sequence* s) {
+  if (!cfg_.prefix_caching) return;
+  const int32_t B = cfg_.block_size;
+  const int32_t full = std::min<int32_t>(s->num_computed / B, (int32_t)s->blocks.size());
+  for (int32_t b = (int32_t)s->block_hashes.size(); b < full; ++b) {
+    const uint64_t parent = b ? s->block_hashes[b - 1] : 0;
+    const int32_t* t = s->tokens.data() + (size_t)b * B;
+    const uint64_t h = hash_block(parent, t, B);
+    bm_.register_block(s->blocks[b], h, t);
+    s->block_hashes.push_back(h);
+  }
+}
+
+int32_t Scheduler::schedule(int32_t* buf) {
+  const StepLayout& L = lay_;
+  const int32_t B = cfg_.block_size;
+  last_plan_.clear();
+  int32_t tok_budget = cfg_.max_num_batched_tokens;
+  int32_t prefill_budget = cfg_.max_prefill_tokens;
+
+  // 1) running sequences: decode tokens, jump-forward runs, unfinished prefill chunks
+  for (size_t i = 0; i < running_.size(); ++i) {
+    Sequence* s = running_[i];
+    if (!s->running) continue;
+    const int32_t pending = (int32_t)s->tokens.size() - s->num_computed;
+    if (pending <= 0 || tok_budget <= 0) continue;
+    const int32_t n = std::min(pending, tok_budget);
+    bool ok = ensure_blocks(s, s->num_computed + n);
+    while (!ok) {
+      // preempt the most recently arrived running sequence that is not yet planned
+      Sequence* victim = nullptr;
+      for (size_t j = running_.size(); j-- > i + 1;) {
+        if (running_[j]->running) {
+          victim = running_[j];
+          break;
+        }
+      }
+      if (!victim) break;
+      preempt(victim);
+      ok = ensure_blocks(s, s->num_computed + n);
+    }
+    if (!ok) {
+      preempt(s);
+      continue;
+    }
+    last_plan_.push_back({s, n, s->num_computed + n == (int32_t)s->tokens.size()});
+    tok_budget -= n;
+  }
+  running_.erase(std::remove_if(running_.begin(), running_.end(),
+                                [](Sequence* s) { return !s->running; }),
+                 running_.end());
+
+  // 2) admit waiting sequences (FCFS) into the remaining budget
+  const int32_t watermark = std::max(1, cfg_.num_blocks / 100);
+  while (!waiting_.empty() && (int32_t)last_plan_.size() < cfg_.max_num_seqs &&
+         (int32_t)running_.size() < cfg_.max_num_seqs && tok_budget > 0 && prefill_budget > 0) {
+    Sequence* s = waiting_.front();
+    if (s->blocks.empty()) match_prefix(s);
+    const int32_t pending = (int32_t)s->tokens.size() - s->num_computed;
+    const int32_t n = std::min(pending, std::min(tok_budget, prefill_budget));
+    const int32_t need =
+        (s->num_computed + n + B - 1) / B - (int32_t)s->blocks.size();
+    if (need > 0 && bm_.num_free() - need < (running_.empty() ? 0 : watermark)) break;
+    if (!ensure_blocks(s, s->num_computed + n)) break;
+    waiting_.pop_front();
+    s->running = true;
+    running_.push_back(s);
+    last_plan_.push_back({s, n, s->num_computed + n == (int32_t)s->tokens.size()});
+    tok_budget -= n;
+    prefill_budget -= n;
+  }
+
+  // 3) emit the step description
+  int32_t* counts = buf + L.counts;
+  int32_t* ids = buf + L.input_ids;
+  int32_t* pos = buf + L.positions;
+  int32_t* slots = buf + L.slots;
+  int32_t* qs = buf + L.q_start;
+  int32_t* ql = buf + L.q_len;
+  int32_t* cl = buf + L.ctx_len;
+  int32_t* lr = buf + L.logit_rows;
+  int32_t* mc = buf + L.mask_class;
+  int32_t* fc = buf + L.forced;
+  int32_t* off = buf + L.offsets;
+  float* temp = reinterpret_cast<float*>(buf + L.temperature);
+  int64_t* seeds = reinterpret_cast<int64_t*>(buf + L.seeds);
+  int32_t* items = buf + L.items;
+  int32_t* ritems = buf + L.ritems;
+  int32_t* bt = buf + L.block_table;
+  const int32_t tpw = 16 / std::max(1, cfg_.gqa_group);
+
+  int32_t T = 0, ns = 0, nsamp = 0, nit = 0, nrit = 0, pslot = 0;
+  for (const Planned& p : last_plan_) {
+    Sequence* s = p.s;
+    const int32_t n = p.n, c0 = s->num_computed, ctx = c0 + n;
+    qs[ns] = T;
+    ql[ns] = n;
+    cl[ns] = ctx;
+    for (int32_t j = 0; j < n; ++j) {
+      const int32_t ppos = c0 + j;
+      ids[T + j] = s->tokens[ppos];
+      pos[T + j] = ppos;
+      slots[T + j] = s->blocks[ppos / B] * B + ppos % B;
+    }
+    const int32_t nb = (ctx + B - 1) / B;
+    std::memcpy(bt + (size_t)ns * L.max_blocks, s->blocks.data(), sizeof(int32_t) * nb);
+    if (p.sample) {
+      lr[nsamp] = T + n - 1;
+      int32_t cls = -1, forced = -1;
+      if (s->grammar) s->grammar->next(&cls, &forced);
+      mc[nsamp] = cls;
+      fc[nsamp] = forced;
+      off[nsamp] = (int32_t)s->tokens.size();
+      temp[nsamp] = s->temperature;
+      seeds[nsamp] = s->seed;
+      ++nsamp;
+    }
+    // attention work items (mirrors pilottai_amd/ops/attn_meta.py)
+    if (n <= tpw) {
+      const int32_t nparts = cfg_.split_decode ? std::max(1, (ctx + 511) / 512) : 1;
+      if (nparts > 1) {
+        for (int32_t q = 0; q < nparts; ++q) {
+          int32_t* it = items + 4 * nit++;
+          it[0] = ns; it[1] = 0; it[2] = n | (q << 8) | (nparts << 20); it[3] = pslot + q;
+        }
+        int32_t* r = ritems + 4 * nrit++;
+        r[0] = ns; r[1] = pslot; r[2] = nparts; r[3] = 0 | (n << 16);
+        pslot += nparts;
+      } else {
+        int32_t* it = items + 4 * nit++;
+        it[0] = ns; it[1] = 0; it[2] = n | (1 << 20); it[3] = 0;
+      }
+    } else {
+      const int32_t tile = 4 * tpw;
+      for (int32_t qb = 0; qb < n; qb += tile) {
+        int32_t* it = items + 4 * nit++;
+        it[0] = ns; it[1] = qb; it[2] = std::min(tile, n - qb) | (1 << 20); it[3] = 0;
+      }
+    }
+    s->num_computed = ctx;
+    T += n;
+    ++ns;
+  }
+  // padding: tokens write no KV, sample rows are greedy on row 0
+  for (int32_t t = T; t < L.max_tokens; ++t) {
+    ids[t] = 0;
+    pos[t] = 0;
+    slots[t] = -1;
+  }
+  for (int32_t r = nsamp; r < L.max_seqs; ++r) {
+    lr[r] = 0;
+    mc[r] = -1;
+    fc[r] = -1;
+    off[r] = 0;
+    temp[r] = 0.f;
+    seeds[r] = 0;
+  }
+  for (int32_t r = ns; r < L.max_seqs; ++r) {
+    qs[r] = T;
+    ql[r] = 0;
+    cl[r] = 0;
+  }
+  counts[0] = T;
+  counts[1] = ns;
+  counts[2] = nsamp;
+  counts[3] = nit;
+  counts[4] = nrit;
+  counts[5] = pslot;
+  buf[L.n_items] = nit;
+  buf[L.n_ritems] = nrit;
+  if (T > 0) ++stat_steps_;
+  return T;
+}
+
+SeqOutput Scheduler::finish(Sequence* s, int32_t reason, double now) {
+  SeqOutput o;
+  o.id = s->id;
+  o.tokens.assign(s->tokens.begin() + s->prompt_len, s->tokens.end());
+  o.finish_reason = reason;
+  o.prompt_len = s->prompt_len;
+  o.cached_prompt_tokens = std::max(0, s->cached_prompt_tokens);
+  o.num_sampled = s->num_sampled;
+  o.num_forced = s->num_forced;
+  o.t_first_token = s->t_first_token;
+  o.t_finish = now;
+  free_seq(s);
+  s->running = false;
+  return o;
+}
+
+std::vector<SeqOutput> Scheduler::commit(const int32_t* sampled, int32_t n) {
+  std::vector<SeqOutput> outs;
+  const double now = now_seconds();
+  int32_t idx = 0;
+  std::vector<Sequence*> done;
+  for (const Planned& p : last_plan_) {
+    Sequence* s = p.s;
+    if (!p.sample) {
+      register_full_blocks(s);
+      continue;
+    }
+    if (idx >= n) break;
+    const int32_t tok = sampled[idx++];
+    if (s->t_first_token < 0) s->t_first_token = now;
+    s->tokens.push_back(tok);
+    ++s->num_generated;
+    ++s->num_sampled;
+    int32_t fin = NOT_FINISHED;
+    if (s->grammar) {
+      s->grammar->advance(tok);
+      if (s->grammar->done()) fin = FINISH_STOP;
+    } else if (!s->ignore_eos) {
+      if (std::find(cfg_.eos_ids.begin(), cfg_.eos_ids.end(), tok) != cfg_.eos_ids.end() ||
+          std::find(s->stop_ids.begin(), s->stop_ids.end(), tok) != s->stop_ids.end())
+        fin = FINISH_STOP;
+    }
+    if (fin == NOT_FINISHED && s->num_generated >= s->max_tokens) fin = FINISH_LENGTH;
+    if (fin == NOT_FINISHED && (int32_t)s->tokens.size() >= cfg_.max_model_len) fin = FINISH_LENGTH;
+    if (fin == NOT_FINISHED && s->grammar) {
+      const int32_t room = std::min(s->max_tokens - s->num_generated,
+                                    cfg_.max_model_len - (int32_t)s->tokens.size());
+      const int32_t k = s->grammar->take_forced_run(s->tokens, room);
+      s->num_generated += k;
+      s->num_forced += k;
+      if (s->grammar->done()) fin = FINISH_STOP;
+      else if (s->num_generated >= s->max_tokens) fin = FINISH_LENGTH;
+    }
+    register_full_blocks(s);
+    if (fin != NOT_FINISHED) {
+      outs.push_back(finish(s, fin, now));
+      done.push_back(s);
+    }
+  }
+  last_plan_.clear();
+  if (!done.empty()) {
+    running_.erase(std::remove_if(running_.begin(), running_.end(),
+                                  [](Sequence* s) { return !s->running; }),
+                   running_.end());
+    for (Sequence* s : done) seqs_.erase(s->id);
+  }
+  return outs;
+}
+
+bool Scheduler::abort(int64_t id) {
+  auto it = seqs_.find(id);
+  if (it == seqs_.end()) return false;
+  Sequence* s = it->second.get();
+  waiting_.erase(std::remove(waiting_.begin(), waiting_.end(), s), waiting_.end());
+  aborted_.push_back(finish(s, FINISH_ABORT, now_seconds()));
+  running_.erase(std::remove(running_.begin(), running_.end(), s), running_.end());
+  seqs_.erase(it);
+  return true;
+}
+
+std::vector<SeqOutput> Scheduler::drain_aborted() {
+  std::vector<SeqOutput> o;
+  o.swap(aborted_);
+  return o;
+}
+
+void Scheduler::reset_prefix_cache() {
+  if (running_.empty()) bm_.reset();
+}
+
+}  // namespace rt

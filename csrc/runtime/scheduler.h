@@ -1,0 +1,138 @@
+// Continuous-batching scheduler for the on-node inference engine
+// (replaces the reference's bounded asyncio.Queue +
+// LLMHandler Semaphore(5) — pilott/pilott.py:105,272-303, engine/llm.py:36).
+//
+// Every engine step runs ONE forward over a ragged token batch that mixes
+//   * decode tokens of running sequences (1 token, or a jump-forward run of
+//     grammar-forced tokens + the last sampled token),
+//   * prefill chunks of newly admitted sequences (after prefix-cache reuse),
+// bounded by max_num_batched_tokens / max_num_seqs. The scheduler writes the
+// complete step description (token ids, positions, KV slots, per-sequence
+// q/ctx lengths, block tables, attention work items, sampling parameters and
+// grammar masks) straight into a caller-provided pinned int32 buffer with a fixed
+// layout, so the Python side issues a single H2D copy and replays a hipGraph.
+#pragma once
+#include <cstdint>
+#include <deque>
+#include <memory>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "block_manager.h"
+#include "grammar.h"
+
+namespace rt {
+
+struct SchedulerConfig {
+  int32_t num_blocks = 1024;
+  int32_t block_size = 16;
+  int32_t max_num_seqs = 256;
+  int32_t max_num_batched_tokens = 2048;
+  int32_t max_prefill_tokens = 2048;  // per-step budget for new prompt tokens
+  int32_t max_model_len = 8192;
+  int32_t gqa_group = 4;               // query heads per KV head (attention work items)
+  bool prefix_caching = true;
+  bool split_decode = true;            // flash-decoding partitions for long contexts
+  std::vector<int32_t> eos_ids;
+};
+
+struct StepLayout {
+  int32_t max_tokens, max_seqs, max_blocks, max_items, max_ritems;
+  int32_t input_ids, positions, slots, q_start, q_len, ctx_len, logit_rows, mask_class, forced,
+      offsets, temperature, seeds, items, n_items, ritems, n_ritems, counts, block_table, total;
+};
+
+enum FinishReason : int32_t { NOT_FINISHED = -1, FINISH_STOP = 0, FINISH_LENGTH = 1, FINISH_ABORT = 2 };
+
+struct SeqOutput {
+  int64_t id;
+  std::vector<int32_t> tokens;  // generated tokens (sampled + grammar-forced)
+  int32_t finish_reason;
+  int32_t prompt_len;
+  int32_t cached_prompt_tokens;
+  int32_t num_sampled;
+  int32_t num_forced;
+  double t_first_token;
+  double t_finish;
+};
+
+struct Sequence {
+  int64_t id;
+  std::vector<int32_t> tokens;
+  int32_t prompt_len = 0;
+  int32_t num_computed = 0;
+  int32_t num_generated = 0;
+  int32_t num_sampled = 0;
+  int32_t num_forced = 0;
+  int32_t cached_prompt_tokens = -1;
+  std::vector<int32_t> blocks;
+  std::vector<uint64_t> block_hashes;  // hash chain of registered leading blocks
+  std::unique_ptr<Grammar> grammar;
+  float temperature = 0.7f;
+  int32_t max_tokens = 256;
+  int64_t seed = 0;
+  bool ignore_eos = false;
+  std::vector<int32_t> stop_ids;
+  int64_t arrival = 0;
+  double t_first_token = -1.0;
+  bool running = false;
+};
+
+class Scheduler {
+ public:
+  explicit Scheduler(const SchedulerConfig& cfg);
+  const StepLayout& layout() const { return lay_; }
+  const SchedulerConfig& config() const { return cfg_; }
+
+  void add_request(int64_t id, std::vector<int32_t> prompt, float temperature, int32_t max_tokens,
+                   int64_t seed, bool ignore_eos, std::vector<int32_t> stop_ids,
+                   std::unique_ptr<Grammar> grammar);
+  bool abort(int64_t id);
+  // Fill `buf` (layout()) for the next step. Returns the number of tokens in the
+  // step (0 = nothing to run).
+  int32_t schedule(int32_t* buf);
+  // Consume the sampled tokens of the last scheduled step (one per sampling row).
+  std::vector<SeqOutput> commit(const int32_t* sampled, int32_t n);
+  // Finished-by-abort outputs are returned here as well.
+  std::vector<SeqOutput> drain_aborted();
+
+  int32_t num_running() const { return (int32_t)running_.size(); }
+  int32_t num_waiting() const { return (int32_t)waiting_.size(); }
+  int32_t num_free_blocks() const { return bm_.num_free(); }
+  int32_t num_cached_blocks() const { return bm_.num_cached(); }
+  int64_t total_prompt_tokens() const { return stat_prompt_tokens_; }
+  int64_t total_cached_tokens() const { return stat_cached_tokens_; }
+  int64_t total_preemptions() const { return stat_preemptions_; }
+  int64_t steps() const { return stat_steps_; }
+  bool has_work() const { return !running_.empty() || !waiting_.empty(); }
+  void reset_prefix_cache();
+
+ private:
+  bool ensure_blocks(Sequence* s, int32_t upto_tokens);
+  void preempt(Sequence* s);
+  void match_prefix(Sequence* s);
+  void register_full_blocks(Sequence* s);
+  SeqOutput finish(Sequence* s, int32_t reason, double now);
+  void free_seq(Sequence* s);
+
+  SchedulerConfig cfg_;
+  StepLayout lay_;
+  BlockManager bm_;
+  std::unordered_map<int64_t, std::unique_ptr<Sequence>> seqs_;
+  std::deque<Sequence*> waiting_;
+  std::vector<Sequence*> running_;
+  struct Planned {
+    Sequence* s;
+    int32_t n;
+    bool sample;
+  };
+  std::vector<Planned> last_plan_;
+  std::vector<SeqOutput> aborted_;
+  int64_t arrival_counter_ = 0;
+  int64_t stat_prompt_tokens_ = 0, stat_cached_tokens_ = 0, stat_preemptions_ = 0, stat_steps_ = 0;
+};
+
+double now_seconds();
+
+}  // namespace rt

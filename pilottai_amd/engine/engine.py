@@ -1,0 +1,487 @@
+"""On-node LLM inference engine (replaces the reference's remote litellm provider,
+pilott/engine/llm.py:12-219, with a local Llama-3 on MI355X).
+
+Architecture (one engine per GPU / per TP group, one process per GPU):
+
+    asyncio agents ──submit()──► inbox ──► engine thread ──► native Scheduler (C++)
+                                                  │   schedule(): writes the whole step into a
+                                                  │   pinned int32 buffer (ids, positions, KV slots,
+                                                  │   block tables, attention items, sampling params)
+                                                  ▼
+                        one H2D copy ─► hipGraph replay of [embed → 32 x layer → LM head → sample]
+                                                  │   captured per token bucket (ragged batches of
+                                                  │   decode + prefill + grammar jump-forward tokens)
+                                                  ▼
+                        sampled ids ─► Scheduler.commit(): grammar advance, jump-forward, stops,
+                                       prefix-cache registration ─► completion callbacks
+
+The LLM protocol used by agents (generate_response / apredict) lives in
+engine/local_llm.py on top of `LLMEngine.submit`.
+"""
+from __future__ import annotations
+
+import logging
+import queue
+import threading
+import time
+from dataclasses import dataclass, field
+from typing import Callable, Dict, List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from pilottai_amd import ops
+from pilottai_amd.models.llama import KVCache, LlamaModel, StepMeta, get_config
+from pilottai_amd.parallel.comm import TPGroup
+
+from .grammar import MAX_CLASSES, GrammarCompiler
+from .tokenizer import Tokenizer, get_tokenizer
+
+log = logging.getLogger("pilottai_amd.engine")
+
+DEFAULT_BUCKETS = [8, 16, 32, 48, 64, 80, 96, 112, 128, 160, 192, 224, 256, 320, 384, 448, 512,
+                   640, 768, 1024, 1280, 1536, 2048, 3072, 4096, 6144, 8192]
+
+
+@dataclass
+class EngineConfig:
+    model: str = "llama-3-8b"
+    max_num_seqs: int = 256
+    max_num_batched_tokens: int = 2048
+    max_prefill_tokens: int = 2048
+    max_model_len: int = 8192
+    block_size: int = 16
+    num_kv_blocks: Optional[int] = None
+    kv_cache_gb: Optional[float] = None
+    kv_cache_fraction: float = 0.5
+    prefix_caching: bool = True
+    split_decode: bool = True
+    use_graphs: bool = True
+    token_buckets: Optional[List[int]] = None
+    seed: int = 0
+    weights_path: Optional[str] = None
+    capture_on_start: bool = True
+
+
+@dataclass
+class GenerationOutput:
+    request_id: int
+    token_ids: List[int]
+    finish_reason: str
+    prompt_tokens: int
+    cached_prompt_tokens: int
+    completion_tokens: int
+    sampled_tokens: int
+    forced_tokens: int
+    t_arrival: float
+    t_first_token: float
+    t_finish: float
+    _tok: Optional[Tokenizer] = field(default=None, repr=False)
+
+    @property
+    def text(self) -> str:
+        return self._tok.decode(self.token_ids) if self._tok else ""
+
+    @property
+    def ttft(self) -> float:
+        return max(0.0, self.t_first_token - self.t_arrival) if self.t_first_token > 0 else 0.0
+
+    @property
+    def latency(self) -> float:
+        return max(0.0, self.t_finish - self.t_arrival)
+
+
+_REASONS = {0: "stop", 1: "length", 2: "abort"}
+
+
+@dataclass
+class _Request:
+    rid: int
+    prompt_ids: List[int]
+    temperature: float
+    max_tokens: int
+    seed: int
+    ignore_eos: bool
+    stop_ids: List[int]
+    grammar: Optional[list]
+    callback: Callable[[GenerationOutput], None]
+    t_arrival: float
+
+
+class LLMEngine:
+    def __init__(self, cfg: Optional[EngineConfig] = None, device=None, tp: Optional[TPGroup] = None,
+                 tokenizer: Optional[Tokenizer] = None):
+        from pilottai_amd import _runtime
+
+        self._rt = _runtime
+        self.cfg = cfg = cfg or EngineConfig()
+        if device is None:
+            device = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() \
+                else torch.device("cpu")
+        self.device = torch.device(device)
+        self.on_gpu = self.device.type == "cuda"
+        if self.on_gpu:
+            ops.require_native()
+            torch.cuda.set_device(self.device)
+        self.tp = tp or TPGroup.single()
+        self.tok = tokenizer or get_tokenizer()
+        self.grammar = GrammarCompiler(self.tok)
+        self.model_cfg = get_config(cfg.model)
+        mc = self.model_cfg
+        t0 = time.time()
+        self.model = LlamaModel(mc, self.device, tp=self.tp, seed=cfg.seed, weights_path=cfg.weights_path)
+        self.load_time = time.time() - t0
+        self.max_model_len = min(cfg.max_model_len, mc.max_position)
+        # ---- KV cache sizing (288 GB HBM: the default leaves room for graphs/activations)
+        kv_local = self.model.kv_local
+        bpb = KVCache.bytes_per_block(mc.num_layers, kv_local, cfg.block_size)
+        nb = cfg.num_kv_blocks
+        if nb is None:
+            if cfg.kv_cache_gb is not None:
+                nb = int(cfg.kv_cache_gb * (1 << 30)) // bpb
+            elif self.on_gpu:
+                free, _total = torch.cuda.mem_get_info(self.device)
+                nb = int(free * cfg.kv_cache_fraction) // bpb
+            else:
+                nb = 2048
+        need_min = (self.max_model_len + cfg.block_size - 1) // cfg.block_size + 1
+        nb = max(nb, need_min)
+        self.kv = KVCache(mc.num_layers, nb, kv_local, self.device, block_size=cfg.block_size)
+        self.num_kv_blocks = nb
+        # ---- native scheduler + step buffers
+        self.sched = _runtime.Scheduler({
+            "num_blocks": nb, "block_size": cfg.block_size, "max_num_seqs": cfg.max_num_seqs,
+            "max_num_batched_tokens": cfg.max_num_batched_tokens,
+            "max_prefill_tokens": cfg.max_prefill_tokens, "max_model_len": self.max_model_len,
+            "gqa_group": self.model.h_local // self.model.kv_local,
+            "prefix_caching": cfg.prefix_caching, "split_decode": cfg.split_decode,
+            "eos_ids": list(self.tok.eos_ids)})
+        L = self.L = self.sched.layout()
+        pin = self.on_gpu
+        self._host_meta = torch.zeros(L["total"], dtype=torch.int32, pin_memory=pin)
+        self._host_ptr = self._host_meta.data_ptr()
+        self._host_np = self._host_meta.numpy()
+        self._dev_meta = torch.zeros(L["total"], dtype=torch.int32, device=self.device) if self.on_gpu \
+            else self._host_meta
+        self._init_views()
+        V = mc.vocab_size
+        self._mask_words = (V + 31) // 32
+        self._class_masks = torch.zeros(MAX_CLASSES, self._mask_words, dtype=torch.int32, device=self.device)
+        self._mask_version = -1
+        self._sync_masks()
+        S = cfg.max_num_seqs
+        self._sampled_dev = torch.zeros(S, dtype=torch.int32, device=self.device)
+        self._sampled_host = torch.zeros(S, dtype=torch.int32, pin_memory=pin)
+        self._keys_dev = torch.zeros(S, dtype=torch.float32, device=self.device)
+        tpw = 16 // (self.model.h_local // self.model.kv_local)
+        self._tpw = tpw
+        self._max_parts = (self.max_model_len + ops.ATT_PART - 1) // ops.ATT_PART
+        max_items = L["max_items"]
+        self._part_o = torch.empty(max_items * kv_local * 16 * 128, dtype=torch.float32, device=self.device)
+        self._part_ml = torch.empty(max_items * kv_local * 16 * 2, dtype=torch.float32, device=self.device)
+        self._sample_ws = ops.sample_workspace(S, self.model.v_local, self.device) if self.on_gpu else None
+        buckets = cfg.token_buckets or DEFAULT_BUCKETS
+        self.buckets = sorted({b for b in buckets if b <= cfg.max_num_batched_tokens} |
+                              {cfg.max_num_batched_tokens})
+        self._graphs: Dict[int, "torch.cuda.CUDAGraph"] = {}
+        self._graph_pool = None
+        self.use_graphs = cfg.use_graphs and self.on_gpu
+        # ---- request plumbing
+        self._inbox: "queue.SimpleQueue" = queue.SimpleQueue()
+        self._aborts: "queue.SimpleQueue" = queue.SimpleQueue()
+        self._wake = threading.Event()
+        self._reqs: Dict[int, _Request] = {}
+        self._next_id = 1
+        self._id_lock = threading.Lock()
+        self._thread: Optional[threading.Thread] = None
+        self._stop = False
+        self._err: Optional[BaseException] = None
+        self.stats = {"steps": 0, "tokens": 0, "sampled": 0, "requests": 0, "finished": 0,
+                      "busy_s": 0.0, "prefill_tokens": 0, "decode_steps": 0, "graph_replays": 0,
+                      "bucket_tokens": 0}
+        if self.use_graphs and cfg.capture_on_start:
+            self.capture_graphs()
+
+    # ------------------------------------------------------------------ setup
+    def _init_views(self):
+        L, d = self.L, self._dev_meta
+        ms, mb = L["max_seqs"], L["max_blocks"]
+
+        def sl(name, n):
+            o = L[name]
+            return d[o:o + n]
+
+        self.meta = StepMeta(
+            input_ids=sl("input_ids", L["max_tokens"]),
+            positions=sl("positions", L["max_tokens"]),
+            slots=sl("slots", L["max_tokens"]),
+            q_start=sl("q_start", ms), q_len=sl("q_len", ms), ctx_len=sl("ctx_len", ms),
+            block_table=sl("block_table", ms * mb).view(ms, mb),
+            items=sl("items", 4 * L["max_items"]).view(L["max_items"], 4),
+            n_items=sl("n_items", 1),
+            ritems=sl("ritems", 4 * L["max_ritems"]).view(L["max_ritems"], 4),
+            n_ritems=sl("n_ritems", 1),
+            logit_rows=sl("logit_rows", ms))
+        self._temp = sl("temperature", ms).view(torch.float32)
+        self._mask_cls = sl("mask_class", ms)
+        self._forced = sl("forced", ms)
+        self._offsets = sl("offsets", ms)
+        self._seeds = sl("seeds", 2 * ms).view(torch.int64)
+
+    def _sync_masks(self):
+        reg = self.grammar.reg
+        if reg.version == self._mask_version:
+            return
+        packed = torch.from_numpy(reg.packed())
+        self._class_masks[: packed.shape[0]].copy_(packed.to(self.device))
+        self._mask_version = reg.version
+
+    def _items_for_bucket(self, bucket: int, s_b: int) -> int:
+        return min(self.L["max_items"], bucket // (4 * self._tpw) + s_b * (self._max_parts + 1) + 4)
+
+    def _meta_for(self, bucket: int, s_b: int, ns: int) -> StepMeta:
+        m = self.meta
+        n_it = self._items_for_bucket(bucket, s_b)
+        return StepMeta(m.input_ids, m.positions, m.slots, m.q_start, m.q_len, m.ctx_len,
+                        m.block_table, m.items[:n_it], m.n_items, m.ritems[:min(s_b + 4, m.ritems.shape[0])],
+                        m.n_ritems, m.logit_rows, num_seqs=ns)
+
+    def _forward_and_sample(self, bucket: int, s_b: int, ns: int):
+        meta = self._meta_for(bucket, s_b, ns)
+        logits = self.model.forward(meta, self.kv, bucket, s_b, self._part_o, self._part_ml)
+        if self.tp.size == 1:
+            ops.sample(logits, self._temp[:s_b], self._mask_cls[:s_b], self._class_masks,
+                       self._seeds[:s_b], self._offsets[:s_b], self._forced[:s_b],
+                       out=self._sampled_dev[:s_b], workspace=self._sample_ws)
+        else:
+            # vocab-parallel: local winners + keys, all-gather, global argmax (identical
+            # to the TP=1 token because the Gumbel noise is keyed on the global index)
+            ops.sample(logits, self._temp[:s_b], self._mask_cls[:s_b], self._class_masks,
+                       self._seeds[:s_b], self._offsets[:s_b], self._forced[:s_b],
+                       out=self._sampled_dev[:s_b], workspace=self._sample_ws,
+                       vocab_offset=self.model.vocab_offset, out_keys=self._keys_dev[:s_b])
+            keys = self.tp.all_gather(self._keys_dev[:s_b])        # [tp, s_b]
+            toks = self.tp.all_gather(self._sampled_dev[:s_b])     # [tp, s_b]
+            best = keys.argmax(0, keepdim=True)
+            self._sampled_dev[:s_b].copy_(toks.gather(0, best).squeeze(0))
+
+    def _seq_bucket(self, bucket: int) -> int:
+        return min(bucket, self.cfg.max_num_seqs)
+
+    def _dummy_meta(self):
+        """A metadata state under which a forward touches no KV and no attention item."""
+        L = self.L
+        d = torch.zeros(L["total"], dtype=torch.int32)
+        d[L["slots"]:L["slots"] + L["max_tokens"]] = -1
+        self._dev_meta.copy_(d.to(self.device))
+
+    def capture_graphs(self, buckets: Optional[Sequence[int]] = None):
+        """Capture one hipGraph per token bucket (shared memory pool)."""
+        if not self.use_graphs:
+            return
+        self._dummy_meta()
+        if self._graph_pool is None:
+            self._graph_pool = torch.cuda.graph_pool_handle()
+        t0 = time.time()
+        for b in sorted(buckets or self.buckets, reverse=True):
+            if b in self._graphs:
+                continue
+            s_b = self._seq_bucket(b)
+            st = torch.cuda.Stream(device=self.device)
+            st.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(st):
+                for _ in range(2):
+                    self._forward_and_sample(b, s_b, 0)
+            torch.cuda.current_stream().wait_stream(st)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, pool=self._graph_pool):
+                self._forward_and_sample(b, s_b, 0)
+            self._graphs[b] = g
+        torch.cuda.synchronize()
+        log.info("captured %d hipGraphs in %.1fs", len(self._graphs), time.time() - t0)
+
+    # ------------------------------------------------------------------ API
+    def new_request_id(self) -> int:
+        with self._id_lock:
+            rid = self._next_id
+            self._next_id += 1
+            return rid
+
+    def submit(self, prompt_ids: Sequence[int], callback: Callable[[GenerationOutput], None], *,
+               temperature: float = 0.7, max_tokens: int = 256, seed: Optional[int] = None,
+               ignore_eos: bool = False, stop_ids: Sequence[int] = (), grammar: Optional[list] = None,
+               request_id: Optional[int] = None) -> int:
+        """Thread-safe; `callback` runs on the engine thread when the request finishes."""
+        if self._err is not None:
+            raise RuntimeError(f"engine failed: {self._err!r}")
+        rid = request_id if request_id is not None else self.new_request_id()
+        if seed is None:
+            seed = (self.cfg.seed * 0x9E3779B1 + rid * 0x85EBCA77) & 0x7FFFFFFFFFFFFFFF
+        req = _Request(rid, list(prompt_ids), float(temperature), int(max_tokens), int(seed),
+                       bool(ignore_eos), list(stop_ids), grammar, callback, self._rt.now())
+        self._inbox.put(req)
+        self._wake.set()
+        return rid
+
+    def abort(self, rid: int):
+        self._aborts.put(rid)
+        self._wake.set()
+
+    def generate(self, prompts: Sequence[Sequence[int]], **kw) -> List[GenerationOutput]:
+        """Blocking batch generation (drives the loop inline if no thread is running)."""
+        results: Dict[int, GenerationOutput] = {}
+        done = threading.Event()
+        ids = []
+        lock = threading.Lock()
+
+        def cb(o: GenerationOutput):
+            with lock:
+                results[o.request_id] = o
+                if len(results) == len(prompts):
+                    done.set()
+
+        for p in prompts:
+            ids.append(self.submit(p, cb, **kw))
+        if self._thread is None:
+            while not done.is_set():
+                if not self.step():
+                    if not self.sched.has_work() and self._inbox.empty():
+                        break
+        else:
+            done.wait()
+        if self._err is not None:
+            raise RuntimeError(f"engine failed: {self._err!r}")
+        return [results[i] for i in ids]
+
+    def start(self):
+        if self._thread is not None:
+            return
+        self._stop = False
+        self._thread = threading.Thread(target=self._loop, name="pilottai-engine", daemon=True)
+        self._thread.start()
+
+    def stop(self):
+        self._stop = True
+        self._wake.set()
+        if self._thread is not None:
+            self._thread.join(timeout=30)
+            self._thread = None
+
+    @property
+    def failed(self) -> Optional[BaseException]:
+        return self._err
+
+    # ------------------------------------------------------------------ loop
+    def _drain_inbox(self):
+        while True:
+            try:
+                req: _Request = self._inbox.get_nowait()
+            except queue.Empty:
+                break
+            self._reqs[req.rid] = req
+            self.sched.add_request(req.rid, req.prompt_ids, req.temperature, req.max_tokens, req.seed,
+                                   req.ignore_eos, req.stop_ids, req.grammar)
+            self.stats["requests"] += 1
+        while True:
+            try:
+                rid = self._aborts.get_nowait()
+            except queue.Empty:
+                break
+            self.sched.abort(rid)
+        for o in self.sched.drain_aborted():
+            self._deliver(o)
+
+    def _deliver(self, o):
+        rid, toks, reason, plen, cached, nsamp, nforced, t_first, t_fin = o
+        req = self._reqs.pop(rid, None)
+        self.stats["finished"] += 1
+        if req is None:
+            return
+        out = GenerationOutput(rid, list(toks), _REASONS.get(reason, "stop"), plen, cached, len(toks),
+                               nsamp, nforced, req.t_arrival, t_first, t_fin, self.tok)
+        try:
+            req.callback(out)
+        except Exception:  # noqa: BLE001 — a bad callback must not kill the engine
+            log.exception("completion callback failed")
+
+    def step(self) -> bool:
+        """Run one engine step. Returns False when there was nothing to run."""
+        self._drain_inbox()
+        if not self.sched.has_work():
+            return False
+        L = self.L
+        t0 = time.perf_counter()
+        T = self.sched.schedule(self._host_ptr)
+        if T == 0:
+            if self.sched.num_running == 0 and self.sched.num_waiting > 0:
+                raise RuntimeError("KV cache too small for the head request")
+            return False
+        c = self._host_np[L["counts"]:L["counts"] + 8]
+        ns, nsamp = int(c[1]), int(c[2])
+        bucket = next(b for b in self.buckets if b >= T)
+        s_b = self._seq_bucket(bucket)
+        self._sync_masks()
+        if self.on_gpu:
+            n_copy = L["block_table"] + ns * L["max_blocks"]
+            self._dev_meta[:n_copy].copy_(self._host_meta[:n_copy], non_blocking=True)
+        with torch.inference_mode():
+            g = self._graphs.get(bucket) if self.use_graphs else None
+            if g is None and self.use_graphs:
+                self.capture_graphs([bucket])  # clobbers the device metadata: restore it
+                self._dev_meta.copy_(self._host_meta)
+                g = self._graphs[bucket]
+            if g is not None:
+                g.replay()
+                self.stats["graph_replays"] += 1
+            else:
+                self._forward_and_sample(bucket, s_b, ns)
+        if nsamp:
+            self._sampled_host[:nsamp].copy_(self._sampled_dev[:nsamp], non_blocking=self.on_gpu)
+        if self.on_gpu:
+            torch.cuda.current_stream().synchronize()
+        outs = self.sched.commit(self._sampled_host.data_ptr(), nsamp)
+        st = self.stats
+        st["steps"] += 1
+        st["tokens"] += T
+        st["bucket_tokens"] += bucket
+        st["sampled"] += nsamp
+        st["busy_s"] += time.perf_counter() - t0
+        for o in outs:
+            self._deliver(o)
+        return True
+
+    def _loop(self):
+        if self.on_gpu:
+            torch.cuda.set_device(self.device)
+        try:
+            while not self._stop:
+                if not self.step():
+                    self._wake.wait(0.01)
+                    self._wake.clear()
+        except BaseException as e:  # noqa: BLE001
+            self._err = e
+            log.exception("engine loop crashed")
+            # fail every pending request loudly
+            for rid in list(self._reqs):
+                req = self._reqs.pop(rid)
+                try:
+                    req.callback(GenerationOutput(rid, [], "error", len(req.prompt_ids), 0, 0, 0, 0,
+                                                  req.t_arrival, -1.0, self._rt.now(), self.tok))
+                except Exception:  # noqa: BLE001
+                    pass
+
+    # ------------------------------------------------------------------ info
+    def metrics(self) -> dict:
+        s = self.sched
+        st = dict(self.stats)
+        st.update({
+            "running": s.num_running, "waiting": s.num_waiting, "free_kv_blocks": s.num_free_blocks,
+            "total_kv_blocks": self.num_kv_blocks, "cached_kv_blocks": s.num_cached_blocks,
+            "prompt_tokens": s.total_prompt_tokens, "prefix_cache_hit_tokens": s.total_cached_tokens,
+            "preemptions": s.total_preemptions, "graphs": len(self._graphs),
+            "kv_cache_gb": self.kv.k.numel() * 2 * 2 / 2**30,
+            "weights_gb": self.model.weight_bytes() / 2**30,
+        })
+        if self.on_gpu:
+            st["hbm_used_gb"] = torch.cuda.memory_allocated(self.device) / 2**30
+        return st

@@ -1,0 +1,131 @@
+"""Process groups and collectives (RCCL over xGMI on MI355X, gloo on CPU).
+
+One process per GPU. `torch.distributed` with backend "nccl" is RCCL on ROCm.
+Groups used by the framework:
+
+* world   — agent-DP control plane: load counters (all-reduce), shared-context
+            broadcast, sharded semantic-index candidate all-gather, barriers.
+* TP      — tensor-parallel group of one model replica (70B: TP=8 on one node);
+            row-parallel outputs are all-reduced, sampling winners all-gathered.
+
+xGMI is point-to-point (7 links per GPU): decode-size TP all-reduces are latency
+bound, so the engine keeps them inside the captured hipGraph (RCCL supports
+graph capture) and never splits them into extra small collectives.
+"""
+from __future__ import annotations
+
+import datetime
+import os
+from dataclasses import dataclass
+from typing import List, Optional
+
+import torch
+import torch.distributed as dist
+
+
+@dataclass
+class TPGroup:
+    group: Optional["dist.ProcessGroup"] = None
+    rank: int = 0
+    size: int = 1
+
+    @staticmethod
+    def single() -> "TPGroup":
+        return TPGroup(None, 0, 1)
+
+    def all_reduce(self, t: torch.Tensor) -> torch.Tensor:
+        if self.size > 1:
+            dist.all_reduce(t, group=self.group)
+        return t
+
+    def all_gather(self, t: torch.Tensor) -> torch.Tensor:
+        """Concatenate `t` from every rank along a new leading dim: [size, *t.shape]."""
+        if self.size == 1:
+            return t.unsqueeze(0)
+        out = torch.empty((self.size,) + tuple(t.shape), dtype=t.dtype, device=t.device)
+        dist.all_gather_into_tensor(out, t.contiguous(), group=self.group)
+        return out
+
+
+def env_rank_world():
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    return rank, world, local
+
+
+def init_distributed(backend: Optional[str] = None, timeout_s: int = 600) -> tuple:
+    """Initialise the default process group from torchrun-style env vars.
+
+    Returns (rank, world_size, local_rank). backend defaults to "nccl" (RCCL)
+    when a GPU is visible, else "gloo". Safe to call twice.
+    """
+    rank, world, local = env_rank_world()
+    if world <= 1:
+        return 0, 1, 0
+    if not dist.is_initialized():
+        if backend is None:
+            backend = "nccl" if torch.cuda.is_available() else "gloo"
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29511")
+        kw = {}
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+            kw["device_id"] = torch.device("cuda", local)
+        dist.init_process_group(backend=backend, rank=rank, world_size=world,
+                                timeout=datetime.timedelta(seconds=timeout_s), **kw)
+    return rank, world, local
+
+
+def new_tp_groups(tp_size: int) -> TPGroup:
+    """Split the world into contiguous TP groups of `tp_size`; return this rank's group."""
+    if not dist.is_initialized() or tp_size <= 1:
+        return TPGroup.single()
+    world = dist.get_world_size()
+    rank = dist.get_rank()
+    assert world % tp_size == 0, "world size must be a multiple of the TP size"
+    mine = None
+    for start in range(0, world, tp_size):
+        ranks = list(range(start, start + tp_size))
+        g = dist.new_group(ranks)
+        if rank in ranks:
+            mine = TPGroup(g, rank - start, tp_size)
+    return mine
+
+
+def barrier():
+    if dist.is_initialized():
+        if dist.get_backend() == "nccl":
+            dist.barrier(device_ids=[torch.cuda.current_device()])
+        else:
+            dist.barrier()
+
+
+def all_reduce_max(x: float, device=None) -> float:
+    if not dist.is_initialized():
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device=device or _coll_device())
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def all_reduce_sum(values: List[float], device=None) -> List[float]:
+    if not dist.is_initialized():
+        return list(values)
+    t = torch.tensor(values, dtype=torch.float64, device=device or _coll_device())
+    dist.all_reduce(t)
+    return t.tolist()
+
+
+def broadcast_object(obj, src: int = 0):
+    if not dist.is_initialized():
+        return obj
+    lst = [obj]
+    dist.broadcast_object_list(lst, src=src)
+    return lst[0]
+
+
+def _coll_device():
+    if dist.is_initialized() and dist.get_backend() == "nccl":
+        return torch.device("cuda", torch.cuda.current_device())
+    return torch.device("cpu")
