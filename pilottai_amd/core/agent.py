@@ -1,0 +1,538 @@
+"""LLM-driven agent (reference: pilott/core/agent.py:59-627).
+
+Per task: validate -> task analysis (LLM) -> tool selection (LLM) -> ordered
+tool-lock acquisition -> step loop (LLM plans the next step, the tool or the
+function-calling LLM executes it; at most `max_iter` steps) -> self-evaluation
+(LLM) -> TaskResult. Every LLM call carries its reply schema
+(`response_format`), so a local engine constrains decoding and every reply parses.
+
+Fixes relative to the reference: prompts format (#1/#2), the LLM
+reply is read as a string or a dict (#3), the step schema is
+{"task_complete", "next_step": {"tool", "inputs", ...}} (#4), tools are a
+name->Tool mapping (#5), timeouts use asyncio.wait_for (#6), the step counter is
+per task (#7), suitability reads the merged AgentConfig (#8), `child_agents`
+exists (#9), `send_heartbeat` exists (#30). Both constructor styles work:
+`BaseAgent(role=..., goal=..., llm=...)` and the documented
+`BaseAgent(agent_config, llm_config)` (docs example).
+"""
+from __future__ import annotations
+
+import asyncio
+import json
+import logging
+import time
+import uuid
+from collections import deque
+from datetime import datetime
+from typing import Any, Callable, Deque, Dict, List, Optional, Sequence, Union
+
+import psutil
+
+from .config import AgentConfig, LLMConfig
+from .policy import DEFAULT_POLICY, ControlPolicy
+from .prompts import PromptManager, parse_json_response
+from .role import AgentRole, AgentStatus
+from .task import Task, TaskResult, TaskStatus
+
+_DEFAULT_LLM: Dict[str, Any] = {"llm": None, "factory": None}
+
+
+def set_default_llm(llm: Any = None, factory: Optional[Callable[[], Any]] = None):
+    """Process-wide LLM used by agents created without one (e.g. by AgentFactory)."""
+    _DEFAULT_LLM["llm"] = llm
+    _DEFAULT_LLM["factory"] = factory
+
+
+def _resolve_default_llm():
+    if _DEFAULT_LLM["llm"] is None:
+        if _DEFAULT_LLM["factory"] is not None:
+            _DEFAULT_LLM["llm"] = _DEFAULT_LLM["factory"]()
+        else:
+            from pilottai_amd.engine.local_llm import make_llm
+
+            _DEFAULT_LLM["llm"] = make_llm(LLMConfig())
+    return _DEFAULT_LLM["llm"]
+
+
+def _content(resp: Any) -> str:
+    if isinstance(resp, dict):
+        return resp.get("content") or ""
+    return "" if resp is None else str(resp)
+
+
+def _short(x: Any, n: int = 400) -> Any:
+    s = json.dumps(x, default=str)
+    return x if len(s) <= n else s[:n] + "..."
+
+
+class BaseAgent:
+    TASK_TIMEOUT = 300.0
+    MAX_HISTORY_SIZE = 100
+
+    def __init__(self, role: Union[str, AgentConfig, None] = None, goal: Optional[Union[str, LLMConfig, dict]] = None,
+                 backstory: Optional[str] = None, knowledge: Optional[List[str]] = None,
+                 config: Optional[Union[Dict[str, Any], AgentConfig]] = None, llm: Any = None,
+                 function_calling_llm: Any = None, max_iter: Optional[int] = None, verbose: bool = False,
+                 allow_delegation: Optional[bool] = None, tools: Optional[Sequence[Any]] = None,
+                 step_callback: Optional[Callable] = None, *, agent_config: Optional[AgentConfig] = None,
+                 llm_config: Optional[Union[LLMConfig, dict]] = None, policy: Optional[ControlPolicy] = None,
+                 memory: Any = None):
+        # --- accept BaseAgent(agent_config, llm_config) and factory-style cls(config)
+        if isinstance(role, AgentConfig):
+            agent_config, role = role, None
+        if isinstance(config, AgentConfig):
+            agent_config, config = config, None
+        if isinstance(goal, (LLMConfig, dict)) and agent_config is not None:
+            llm_config, goal = goal, None
+        if agent_config is None:
+            if not role:
+                raise ValueError("Agent role is required")
+            agent_config = AgentConfig(role=role, goal=goal or f"Complete tasks as {role}", backstory=backstory,
+                                       knowledge=knowledge or [], max_iterations=max_iter or 10,
+                                       verbose=verbose, can_delegate=bool(allow_delegation),
+                                       additional_config=dict(config or {}))
+        else:
+            upd = {}
+            if max_iter:
+                upd["max_iter"] = max_iter
+            if allow_delegation is not None:
+                upd["allow_delegation"] = allow_delegation
+            if upd:
+                agent_config = agent_config.model_copy(update=upd)
+                agent_config._sync_aliases()
+        self.config: AgentConfig = agent_config
+        self.agent_config = agent_config  # documented alias (docs example)
+        self.id = str(uuid.uuid4())
+        self._llm = llm
+        self._llm_config = LLMConfig(**llm_config) if isinstance(llm_config, dict) else llm_config
+        self.function_calling_llm = function_calling_llm
+        self.tools: Dict[str, Any] = {}
+        for t in tools or []:
+            self.add_tool(t)
+        self.policy = policy or DEFAULT_POLICY
+        self.prompts = PromptManager("agent")
+        self.step_callback = step_callback
+        self.status = AgentStatus.STOPPED
+        self.current_task: Optional[Task] = None
+        self.iteration_count = 0
+        self.conversation_history: Deque[Dict[str, str]] = deque(maxlen=self.MAX_HISTORY_SIZE)
+        self.execution_locks: Dict[str, asyncio.Lock] = {}
+        self._tool_locks: Dict[str, asyncio.Lock] = {}
+        self.tasks: Dict[str, Task] = {}
+        self.active_tasks: set = set()
+        self.task_history: Deque[Dict[str, Any]] = deque(maxlen=1000)
+        self.task_metrics: Dict[str, int] = {"completed": 0, "failed": 0, "timeout": 0}
+        self.metrics = self.task_metrics  # documented alias `agent.metrics[...]`
+        self.child_agents: Dict[str, "BaseAgent"] = {}
+        self.parent: Optional["BaseAgent"] = None
+        self._memory = memory
+        self.last_error: Optional[str] = None
+        self.last_heartbeat = datetime.now()
+        self._accepting = True
+        self.llm_usage = {"calls": 0, "prompt_tokens": 0, "completion_tokens": 0}
+        self.logger = logging.getLogger(f"pilottai_amd.agent.{self.config.role}")
+        self.logger.setLevel(logging.DEBUG if self.config.verbose else logging.INFO)
+
+    # ------------------------------------------------------------------ properties
+    @property
+    def llm(self):
+        if self._llm is None:
+            if self._llm_config is not None:
+                from pilottai_amd.engine.local_llm import make_llm
+
+                self._llm = make_llm(self._llm_config)
+            else:
+                self._llm = _resolve_default_llm()
+        return self._llm
+
+    @llm.setter
+    def llm(self, v):
+        self._llm = v
+
+    @property
+    def role(self) -> str:
+        return self.config.role
+
+    @property
+    def specializations(self) -> List[str]:
+        return list(self.config.specializations)
+
+    @property
+    def max_concurrent_tasks(self) -> int:
+        return self.config.max_concurrent_tasks
+
+    @property
+    def enhanced_memory(self):
+        """Per-agent semantic memory (documented API: agent.enhanced_memory.store_semantic)."""
+        if self._memory is None:
+            from pilottai_amd.memory.enhanced_memory import EnhancedMemory
+
+            self._memory = EnhancedMemory()
+        return self._memory
+
+    def add_tool(self, tool: Any):
+        from pilottai_amd.tools.tool import Tool
+
+        if isinstance(tool, Tool):
+            self.tools[tool.name] = tool
+        elif callable(tool):
+            t = Tool.from_callable(tool)
+            self.tools[t.name] = t
+        elif isinstance(tool, str):
+            self.tools[tool] = None  # name-only placeholder: an LLM-only step
+        else:
+            raise TypeError(f"unsupported tool {tool!r}")
+
+    # ------------------------------------------------------------------ lifecycle
+    async def start(self):
+        self.status = AgentStatus.IDLE
+        self._accepting = True
+        self.last_heartbeat = datetime.now()
+
+    async def stop(self):
+        self.status = AgentStatus.STOPPED
+        for lock in list(self.execution_locks.values()):
+            if lock.locked():
+                try:
+                    lock.release()
+                except RuntimeError:
+                    pass
+        self.execution_locks.clear()
+        self.conversation_history.clear()
+        self.current_task = None
+        self.iteration_count = 0
+
+    async def reset(self):
+        self.status = AgentStatus.IDLE
+        self.current_task = None
+        self.iteration_count = 0
+        self.conversation_history.clear()
+        self._tool_locks.clear()
+        self.tasks.clear()
+        self.active_tasks.clear()
+        self.task_metrics.update(completed=0, failed=0, timeout=0)
+        self.last_error = None
+        self._accepting = True
+
+    async def cleanup_resources(self):
+        for lock in self._tool_locks.values():
+            if lock.locked():
+                try:
+                    lock.release()
+                except RuntimeError:
+                    pass
+        self._tool_locks.clear()
+        self.conversation_history.clear()
+        if self._memory is not None and hasattr(self._memory, "stop"):
+            await self._memory.stop()
+
+    async def send_heartbeat(self) -> datetime:
+        """Liveness probe used by FaultTolerance (missing in the reference, App. A #30)."""
+        if self.status == AgentStatus.STOPPED:
+            raise RuntimeError(f"agent {self.id} is stopped")
+        self.last_heartbeat = datetime.now()
+        return self.last_heartbeat
+
+    # ------------------------------------------------------------------ task queue
+    async def add_task(self, task: Union[Task, Dict[str, Any]]) -> str:
+        t = Task.from_any(task)
+        if t.id in self.tasks:
+            raise ValueError(f"Task {t.id} already exists")
+        if len(self.tasks) >= self.config.max_queue_size:
+            raise RuntimeError("agent task queue is full")
+        self.tasks[t.id] = t
+        return t.id
+
+    async def remove_task(self, task_id: str) -> Optional[Task]:
+        if task_id in self.active_tasks:
+            raise ValueError(f"Cannot remove active task {task_id}")
+        return self.tasks.pop(task_id, None)
+
+    async def wait_for_tasks(self, poll: float = 0.05, timeout: Optional[float] = None):
+        t0 = time.monotonic()
+        while self.active_tasks:
+            if timeout is not None and time.monotonic() - t0 > timeout:
+                raise asyncio.TimeoutError("tasks still active")
+            await asyncio.sleep(poll)
+
+    async def pause_task_acceptance(self):
+        self._accepting = False
+        if self.status == AgentStatus.IDLE:
+            self.status = AgentStatus.BUSY
+
+    async def resume_task_acceptance(self):
+        self._accepting = True
+        if self.status == AgentStatus.BUSY and not self.active_tasks:
+            self.status = AgentStatus.IDLE
+
+    @property
+    def accepting_tasks(self) -> bool:
+        return self._accepting and self.status not in (AgentStatus.STOPPED, AgentStatus.ERROR)
+
+    # ------------------------------------------------------------------ children
+    async def add_child_agent(self, agent: "BaseAgent"):
+        if len(self.child_agents) >= self.config.max_child_agents:
+            raise RuntimeError("max_child_agents reached")
+        agent.parent = self
+        self.child_agents[agent.id] = agent
+        if agent.status == AgentStatus.STOPPED:
+            await agent.start()
+
+    async def remove_child_agent(self, agent_id: str) -> Optional["BaseAgent"]:
+        a = self.child_agents.pop(agent_id, None)
+        if a is not None:
+            a.parent = None
+        return a
+
+    async def create_agent(self, **kw) -> "BaseAgent":
+        """Orchestrator-protocol hook (used by DynamicScaling on manager agents)."""
+        role = kw.get("role") or f"{self.config.role}-child"
+        cfg = AgentConfig(role=role, goal=kw.get("goal", self.config.goal), description=kw.get("description", ""),
+                          role_type=AgentRole.WORKER)
+        return type(self)(cfg, llm=self._llm, tools=list(self.tools.values()), policy=self.policy)
+
+    # ------------------------------------------------------------------ execution
+    async def execute_task(self, task: Union[Task, Dict[str, Any]]) -> TaskResult:
+        task = Task.from_any(task)
+        if task.id in self.active_tasks:
+            raise ValueError(f"Task {task.id} is already being executed")
+        self.status = AgentStatus.BUSY
+        self.current_task = task
+        self.active_tasks.add(task.id)
+        self.tasks.setdefault(task.id, task)
+        t0 = time.perf_counter()
+        timeout = task.timeout or float(self.config.task_timeout or self.TASK_TIMEOUT)
+        lock = self.execution_locks.setdefault(task.id, asyncio.Lock())
+        try:
+            async with lock:
+                try:
+                    result = await asyncio.wait_for(self._execute_task_internal(task), timeout=timeout)
+                except asyncio.TimeoutError:
+                    self.task_metrics["timeout"] += 1
+                    self.task_metrics["failed"] += 1
+                    self.last_error = "Task execution timed out"
+                    task.update_status(TaskStatus.TIMEOUT)
+                    return TaskResult(success=False, error="Task execution timed out",
+                                      execution_time=time.perf_counter() - t0)
+            if result.success:
+                self.task_metrics["completed"] += 1
+                task.update_status(TaskStatus.COMPLETED)
+            else:
+                self.task_metrics["failed"] += 1
+                self.last_error = result.error
+                task.update_status(TaskStatus.FAILED)
+            task.result = result
+            self.task_history.append({"task_id": task.id, "success": result.success,
+                                      "execution_time": result.execution_time, "ts": datetime.now().isoformat()})
+            return result
+        finally:
+            self.active_tasks.discard(task.id)
+            self.tasks.pop(task.id, None)
+            self.execution_locks.pop(task.id, None)
+            self.current_task = None
+            if self.status == AgentStatus.BUSY and not self.active_tasks:
+                self.status = AgentStatus.IDLE if self._accepting else AgentStatus.BUSY
+            self.last_heartbeat = datetime.now()
+
+    async def _execute_task_internal(self, task: Task) -> TaskResult:
+        t0 = time.perf_counter()
+        held: List[str] = []
+        iterations = 0
+        try:
+            self._validate_task(task)
+            analysis = await self._analyze_task(task)
+            if analysis.get("can_execute", True) is False:
+                raise ValueError(f"Cannot execute task: {analysis.get('reason')}")
+            selection = await self._select_tools(task)
+            chosen = [t for t in selection.get("selected_tools", []) if t in self.tools]
+            for name in sorted(set(chosen)):  # fixed order -> no deadlock
+                lock = self._tool_locks.setdefault(name, asyncio.Lock())
+                await lock.acquire()
+                held.append(name)
+            steps, iterations = await self._execute_steps(task, chosen)
+            evaluation = await self._evaluate_result(task, steps)
+            ok = bool(evaluation.get("success", False))
+            return TaskResult(success=ok, output=steps, error=None if ok else evaluation.get("reasoning", "evaluation failed"),
+                              execution_time=time.perf_counter() - t0,
+                              metadata={"analysis": analysis, "tools_used": selection, "evaluation": evaluation,
+                                        "iterations": iterations, "agent_id": self.id, "agent_role": self.config.role})
+        except Exception as e:  # noqa: BLE001
+            return TaskResult(success=False, output=None, error=str(e), execution_time=time.perf_counter() - t0,
+                              metadata={"agent_id": self.id, "iterations": iterations})
+        finally:
+            for name in reversed(sorted(held)):
+                lock = self._tool_locks.get(name)
+                if lock is not None and lock.locked():
+                    lock.release()
+
+    def _validate_task(self, task: Task):
+        if not task.description:
+            raise ValueError("Task must have a description")
+        for dep in task.dependencies:
+            d = self.tasks.get(dep)
+            if d is not None and d.status != TaskStatus.COMPLETED:
+                raise ValueError(f"Dependency {dep} not yet completed")
+        if task.max_retries < 0:
+            raise ValueError("Task max_retries must be a non-negative integer")
+        if task.is_expired():
+            raise ValueError("Task deadline has passed")
+
+    # ------------------------------------------------------------------ LLM calls
+    async def _llm_json(self, kind: str, fixed: Optional[Dict[str, Any]] = None, **kw) -> Dict[str, Any]:
+        prompt = self.prompts.format_prompt(kind, **kw)
+        system = self.prompts.format_prompt("system_base", role=self.config.role, goal=self.config.goal,
+                                            backstory=self.config.backstory or "No specific backstory.")
+        messages = [{"role": "system", "content": system}, {"role": "user", "content": prompt}]
+        rf = {"schema": f"agent.{kind}", "fixed": fixed or {}}
+        try:
+            resp = await self.llm.generate_response(messages, response_format=rf)
+        except TypeError:  # a third-party LLM without structured-output support
+            resp = await self.llm.generate_response(messages)
+        text = _content(resp)
+        if not text and not isinstance(resp, dict):
+            raise ValueError("Empty response from LLM")
+        if isinstance(resp, dict) and "usage" in resp:
+            u = resp["usage"]
+            self.llm_usage["calls"] += 1
+            self.llm_usage["prompt_tokens"] += u.get("prompt_tokens", 0)
+            self.llm_usage["completion_tokens"] += u.get("completion_tokens", 0)
+        self.conversation_history.extend(messages + [{"role": "assistant", "content": text}])
+        return parse_json_response(resp if isinstance(resp, dict) and "content" not in resp else text)
+
+    async def _analyze_task(self, task: Task) -> Dict[str, Any]:
+        return await self._llm_json("task_analysis", self.policy.agent_analysis(), role=self.config.role,
+                                    goal=self.config.goal, task_description=task.description)
+
+    async def _select_tools(self, task: Task) -> Dict[str, Any]:
+        names = [n for n in self.tools]
+        return await self._llm_json("tool_selection", self.policy.tool_selection(names),
+                                    tools=json.dumps(names), task_description=task.description)
+
+    async def _execute_steps(self, task: Task, tools: List[str]):
+        completed: List[Dict[str, Any]] = []
+        step_inputs = task.metadata.get("tool_inputs", {}) if isinstance(task.metadata, dict) else {}
+        iterations = 0
+        while iterations < self.config.max_iter:
+            tool = tools[iterations % len(tools)] if tools else "none"
+            fixed = self.policy.step_planning(iterations, tool)
+            if self.policy.fixed_mode:
+                fixed["next_step.inputs"] = step_inputs
+            plan = await self._llm_json("step_planning", fixed, task_description=task.description,
+                                        completed_steps=json.dumps(_short(completed, 800)),
+                                        available_tools=json.dumps(tools),
+                                        last_result=json.dumps(_short(completed[-1] if completed else None)))
+            if plan.get("task_complete", False):
+                break
+            step = plan.get("next_step") or {k: plan[k] for k in ("tool", "inputs") if k in plan}
+            result = await self._execute_step(step)
+            completed.append({"step": step, "result": result})
+            iterations += 1
+            self.iteration_count += 1
+            if self.step_callback:
+                await self._execute_callback(self.step_callback, step=step, result=result,
+                                             context={"task": task.id, "completed_steps": completed})
+        return completed, iterations
+
+    async def _execute_step(self, step: Dict[str, Any]) -> Any:
+        name = step.get("tool")
+        inputs = step.get("inputs") or {}
+        tool = self.tools.get(name)
+        if tool is None:
+            # no executable tool for this step: an LLM-only reasoning step
+            return {"status": "llm_only", "output": step.get("expected_outcome")}
+        if step.get("requires_llm") and self.function_calling_llm is not None:
+            resp = await asyncio.wait_for(self.function_calling_llm.generate_response(
+                messages=[{"role": "user", "content": json.dumps(step)}], tools=[tool.spec()]), 60)
+            calls = (resp or {}).get("tool_calls") or []
+            if calls:
+                args = json.loads(calls[0]["function"].get("arguments") or "{}")
+                inputs = {**inputs, **args}
+        try:
+            out = await asyncio.wait_for(tool.execute(**inputs), 30)
+            return {"status": "success", "output": out}
+        except asyncio.TimeoutError:
+            raise TimeoutError(f"Step execution timed out for tool {name}")
+
+    async def _evaluate_result(self, task: Task, steps: Any) -> Dict[str, Any]:
+        return await self._llm_json("result_evaluation", self.policy.agent_evaluation(), role=self.config.role,
+                                    goal=self.config.goal, task_description=task.description,
+                                    result=json.dumps(_short(steps, 800)))
+
+    async def _execute_callback(self, cb: Callable, **kw):
+        try:
+            if asyncio.iscoroutinefunction(cb):
+                await cb(**kw)
+            else:
+                await asyncio.to_thread(cb, **kw)
+        except Exception as e:  # noqa: BLE001
+            self.logger.error("callback failed: %s", e)
+
+    # ------------------------------------------------------------------ metrics
+    async def get_metrics(self) -> Dict[str, Any]:
+        done = self.task_metrics["completed"] + self.task_metrics["failed"]
+        cpu = psutil.cpu_percent(interval=None) / 100.0
+        mem = psutil.virtual_memory().percent / 100.0
+        m = {
+            "queue_size": len(self.tasks),
+            "active_tasks": len(self.active_tasks),
+            "success_rate": self.task_metrics["completed"] / done if done else 0.0,
+            "queue_utilization": len(self.tasks) / self.config.max_queue_size,
+            "cpu_usage": cpu,
+            "memory_usage": mem,
+            "total_tasks": done,
+            "error_count": self.task_metrics["failed"],
+            "last_error": self.last_error,
+            "resource_usage": max(cpu, mem),
+            "llm_usage": dict(self.llm_usage),
+        }
+        eng = getattr(getattr(self._llm, "engine", None), "metrics", None)
+        if callable(eng):
+            em = eng()
+            m["kv_cache_utilization"] = 1.0 - em["free_kv_blocks"] / max(1, em["total_kv_blocks"])
+        return m
+
+    async def get_health(self) -> Dict[str, Any]:
+        return {"status": self.status, "active_tasks": len(self.active_tasks), "total_tasks": len(self.tasks),
+                "metrics": dict(self.task_metrics), "memory_usage": len(self.conversation_history),
+                "last_heartbeat": self.last_heartbeat.isoformat(),
+                "locks": {k: v.locked() for k, v in self.execution_locks.items()}}
+
+    async def evaluate_task_suitability(self, task: Union[Dict[str, Any], Task]) -> float:
+        """0 if capabilities missing; 0.7 (+0.2 specialisation) - 0.3 queue_util."""
+        try:
+            if isinstance(task, Task):
+                task = {"type": task.type or task.metadata.get("type"), "required_capabilities": task.required_skills}
+            req = set(task.get("required_capabilities") or [])
+            if req - set(self.config.required_capabilities) - set(self.config.specializations):
+                return 0.0
+            score = 0.7
+            if task.get("type") and task["type"] in self.config.specializations:
+                score += 0.2
+            score -= 0.3 * (len(self.tasks) / self.config.max_queue_size)
+            return max(0.0, min(1.0, score))
+        except Exception:  # noqa: BLE001
+            return 0.0
+
+    # ------------------------------------------------------------------ manager hooks
+    async def determine_strategy(self, task: Task) -> Dict[str, Any]:
+        return {"parallel_execution": True, "priority_level": task.priority,
+                "resource_allocation": {"max_agents": 1, "time_allocation": 30, "tool_requirements": []},
+                "coordination_needs": [], "monitoring_points": [], "abort_conditions": []}
+
+    async def select_agent(self, task: Task) -> Optional["BaseAgent"]:
+        best, best_s = None, -1.0
+        for a in self.child_agents.values():
+            if a.status in (AgentStatus.BUSY, AgentStatus.STOPPED, AgentStatus.ERROR):
+                continue
+            s = await a.evaluate_task_suitability(task)
+            if s > best_s:
+                best, best_s = a, s
+        return best
+
+    async def evaluate_result(self, task: Task, result: TaskResult) -> Dict[str, Any]:
+        return {"success": result.success, "quality_score": 5, "matches_requirements": True, "goal_alignment": 5,
+                "improvements": [], "next_actions": [], "requires_retry": not result.success,
+                "reasoning": str(result.error) if not result.success else "Task completed"}
+
+    def __repr__(self) -> str:
+        return f"<{type(self).__name__} role={self.config.role!r} id={self.id[:8]} status={self.status}>"
