@@ -1,0 +1,85 @@
+"""Text embedders for the semantic store.
+
+`HashingEmbedder` (default): signed feature hashing of lower-cased word unigrams
+and bigrams plus character trigrams into D=1024 dims, L2-normalised. It is
+deterministic, needs no weights, and makes cosine similarity track lexical
+overlap — a strict generalisation of the reference's case-insensitive
+substring search (pilott/memory/enhanced_memory.py:110), which it replaces.
+
+`EngineEmbedder`: mean-pooled token embeddings of the local Llama engine's model,
+projected to D by a fixed random orthogonal map (meaningful with real weights).
+"""
+from __future__ import annotations
+
+import re
+import zlib
+from typing import List, Sequence
+
+import numpy as np
+
+_TOK = re.compile(r"[a-z0-9]+")
+
+
+def _h(s: str) -> int:
+    return zlib.crc32(s.encode("utf-8"))
+
+
+class HashingEmbedder:
+    def __init__(self, dim: int = 1024):
+        self.dim = dim
+
+    def features(self, text: str):
+        t = text.lower()
+        words = _TOK.findall(t)
+        feats = [("w", w) for w in words]
+        feats += [("b", f"{a} {b}") for a, b in zip(words, words[1:])]
+        squeezed = " ".join(words)
+        feats += [("c", squeezed[i:i + 3]) for i in range(max(0, len(squeezed) - 2))]
+        return feats
+
+    def embed(self, texts: Sequence[str]) -> np.ndarray:
+        out = np.zeros((len(texts), self.dim), dtype=np.float32)
+        wts = {"w": 1.0, "b": 0.7, "c": 0.35}
+        for r, text in enumerate(texts):
+            row = out[r]
+            for kind, f in self.features(text):
+                h = _h(kind + ":" + f)
+                row[h % self.dim] += wts[kind] * (1.0 if (h >> 31) & 1 else -1.0)
+            n = np.linalg.norm(row)
+            if n > 0:
+                row /= n
+        return out
+
+    def __call__(self, texts: Sequence[str]) -> np.ndarray:
+        return self.embed(texts)
+
+
+class EngineEmbedder:
+    """Mean-pooled token embeddings of the local engine's model, projected to `dim`."""
+
+    def __init__(self, engine, dim: int = 1024, seed: int = 0):
+        import torch
+
+        self.engine = engine
+        self.dim = dim
+        d = engine.model_cfg.hidden_size
+        g = torch.Generator().manual_seed(seed)
+        q, _ = torch.linalg.qr(torch.randn(d, max(d, dim), generator=g))
+        self.proj = q[:, :dim].contiguous().to(engine.device, torch.float32)
+
+    def embed(self, texts: Sequence[str]) -> np.ndarray:
+        import torch
+        import torch.nn.functional as F
+
+        m = self.engine.model
+        rows: List[np.ndarray] = []
+        with torch.inference_mode():
+            for t in texts:
+                ids = torch.tensor(self.engine.tok.encode(t)[:512] or [0], device=self.engine.device)
+                h = F.embedding(ids, m.embed).float().mean(0)
+                v = (h @ self.proj)
+                rows.append(torch.nn.functional.normalize(v, dim=0).cpu().numpy())
+        return np.stack(rows) if rows else np.zeros((0, self.dim), np.float32)
+
+    def __call__(self, texts):
+        return self.embed(texts)

@@ -1,0 +1,228 @@
+"""HBM-resident embedding index with fused filter + cosine top-k.
+
+Rows are L2-normalised bf16 vectors in one preallocated device matrix
+[capacity, D] (100M x 1024 bf16 = 204.8 GB fits one 288 GB MI355X next to an 8B
+model), with per-row filter metadata kept beside them on the device:
+priority (int32), tag bitmask (int64), expiry (float32 seconds on the index's
+clock, 0 = never). Search runs `ops.cosine_topk` (csrc/ops/similarity.hip):
+one streaming MFMA pass over the rows for a batch of queries, filters applied
+in-kernel, per-slice top-k merged on device.
+
+The index is a ring buffer once full, which is the reference's bounded-deque
+eviction (pilott/memory/enhanced_memory.py:27) without its stale-index bug
+(App. A #26): row ids are stable until the row is overwritten.
+
+Tags map to bits 0..62 through a registry; further distinct tags share bit 63
+and are re-checked exactly on the host for the (few) returned candidates.
+`ShardedSemanticIndex` splits rows across ranks and merges per-rank top-k with
+one all-gather (RCCL over xGMI).
+"""
+from __future__ import annotations
+
+import threading
+import time
+from typing import Dict, Iterable, List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from pilottai_amd import ops
+
+OVERFLOW_BIT = 63
+
+
+class TagRegistry:
+    def __init__(self):
+        self.bits: Dict[str, int] = {}
+
+    def bit(self, tag: str, create: bool = True) -> int:
+        b = self.bits.get(tag)
+        if b is None:
+            if not create:
+                return -1
+            b = len(self.bits) if len(self.bits) < OVERFLOW_BIT else OVERFLOW_BIT
+            if b < OVERFLOW_BIT:
+                self.bits[tag] = b
+        return b
+
+    def mask(self, tags: Iterable[str], create: bool = True) -> Tuple[int, bool]:
+        """(bitmask, exact) — exact is False when an overflow tag is involved."""
+        m, exact = 0, True
+        for t in tags or ():
+            b = self.bit(t, create)
+            if b < 0:
+                return -1, True  # unknown tag: nothing can match
+            if b == OVERFLOW_BIT:
+                exact = False
+            m |= 1 << b
+        if m >= 1 << 63:
+            m -= 1 << 64  # two's complement for int64 storage
+        return m, exact
+
+
+class SemanticIndex:
+    def __init__(self, dim: int = 1024, capacity: int = 1 << 16, device=None, growable: bool = True,
+                 max_capacity: Optional[int] = None):
+        if device is None:
+            device = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() \
+                else torch.device("cpu")
+        self.device = torch.device(device)
+        self.dim = dim
+        self.growable = growable
+        self.max_capacity = max_capacity or capacity if not growable else (max_capacity or 1 << 31)
+        self._alloc(capacity)
+        self.size = 0          # rows ever written (ring position = size % capacity)
+        self.tags = TagRegistry()
+        self.row_tags_py: Dict[int, frozenset] = {}
+        self.epoch = time.time()
+        self._lock = threading.Lock()
+        self._ws: Optional[torch.Tensor] = None
+
+    def _alloc(self, cap: int):
+        d = self.device
+        self.capacity = cap
+        self.vectors = torch.zeros(cap, self.dim, dtype=torch.bfloat16, device=d)
+        self.priority = torch.full((cap,), -(1 << 30), dtype=torch.int32, device=d)
+        self.tagbits = torch.zeros(cap, dtype=torch.int64, device=d)
+        self.expiry = torch.zeros(cap, dtype=torch.float32, device=d)
+
+    def _grow(self, need: int):
+        new = self.capacity
+        while new < need:
+            new *= 2
+        new = min(new, self.max_capacity)
+        if new <= self.capacity:
+            return
+        old = (self.vectors, self.priority, self.tagbits, self.expiry, self.capacity)
+        self._alloc(new)
+        n = old[4]
+        self.vectors[:n] = old[0]
+        self.priority[:n] = old[1]
+        self.tagbits[:n] = old[2]
+        self.expiry[:n] = old[3]
+
+    @property
+    def count(self) -> int:
+        return min(self.size, self.capacity)
+
+    def now(self) -> float:
+        return time.time() - self.epoch
+
+    def add(self, vectors, priorities: Sequence[int], tags: Sequence[Iterable[str]],
+            expires_at: Sequence[Optional[float]]) -> List[int]:
+        """Append rows; returns their row ids. `expires_at` is wall-clock time.time() or None."""
+        v = torch.as_tensor(np.asarray(vectors, dtype=np.float32))
+        n = v.shape[0]
+        with self._lock:
+            if self.growable and self.size + n > self.capacity and self.capacity < self.max_capacity:
+                self._grow(self.size + n)
+            rows = [(self.size + i) % self.capacity for i in range(n)]
+            self.size += n
+            idx = torch.tensor(rows, dtype=torch.long, device=self.device)
+            v = torch.nn.functional.normalize(v, dim=1)
+            self.vectors.index_copy_(0, idx, v.to(self.device, torch.bfloat16))
+            self.priority.index_copy_(0, idx, torch.tensor(list(priorities), dtype=torch.int32, device=self.device))
+            masks = []
+            for r, ts in zip(rows, tags):
+                ts = frozenset(ts or ())
+                self.row_tags_py[r] = ts
+                masks.append(self.tags.mask(ts)[0])
+            self.tagbits.index_copy_(0, idx, torch.tensor(masks, dtype=torch.int64, device=self.device))
+            exp = [0.0 if e is None else max(1e-3, float(e) - self.epoch) for e in expires_at]
+            self.expiry.index_copy_(0, idx, torch.tensor(exp, dtype=torch.float32, device=self.device))
+        return rows
+
+    def delete(self, rows: Sequence[int]):
+        with self._lock:
+            idx = torch.tensor(list(rows), dtype=torch.long, device=self.device)
+            self.priority.index_fill_(0, idx, -(1 << 30))
+            for r in rows:
+                self.row_tags_py.pop(r, None)
+
+    def search(self, queries, k: int, min_priority: Sequence[int], tags: Sequence[Iterable[str]],
+               now: Optional[float] = None) -> List[List[Tuple[int, float]]]:
+        """Batched filtered top-k: returns per query [(row, score), ...] best first."""
+        q = torch.as_tensor(np.asarray(queries, dtype=np.float32))
+        Q = q.shape[0]
+        if Q == 0:
+            return []
+        k = max(1, min(int(k), 64))
+        tag_sets = [frozenset(t or ()) for t in tags]
+        qmasks, exact = [], []
+        for ts in tag_sets:
+            m, ex = self.tags.mask(ts, create=False)
+            qmasks.append(m)
+            exact.append(ex)
+        # unknown tag (-1 sentinel == all bits) can never match a real row mask
+        n = self.count
+        if n == 0:
+            return [[] for _ in range(Q)]
+        kk = k if all(exact) else min(64, 4 * k)
+        with self._lock:
+            qd = torch.nn.functional.normalize(q, dim=1).to(self.device, torch.bfloat16)
+            minp = torch.tensor(list(min_priority), dtype=torch.int32, device=self.device)
+            qt = torch.tensor(qmasks, dtype=torch.int64, device=self.device)
+            s, r = ops.cosine_topk(qd, self.vectors, n, kk, self.priority, self.tagbits, self.expiry, minp, qt,
+                                   self.now() if now is None else now - self.epoch, workspace=self._ws)
+            s, r = s.cpu().numpy(), r.cpu().numpy()
+        out = []
+        for i in range(Q):
+            res = []
+            for row, sc in zip(r[i], s[i]):
+                if row < 0:
+                    break
+                if not exact[i] and not tag_sets[i] <= self.row_tags_py.get(int(row), frozenset()):
+                    continue
+                res.append((int(row), float(sc)))
+                if len(res) >= k:
+                    break
+            out.append(res)
+        return out
+
+    def memory_bytes(self) -> int:
+        return self.vectors.numel() * 2 + self.capacity * (4 + 8 + 4)
+
+
+class ShardedSemanticIndex:
+    """Row-sharded index over the ranks of a process group (one shard per GPU).
+
+    Inserts go to the local shard (global row = local_row * world + rank); a
+    search runs the local top-k and merges all ranks' candidates with one
+    all-gather. All ranks must call `search` collectively with the same queries.
+    """
+
+    def __init__(self, local: SemanticIndex, group=None):
+        import torch.distributed as dist
+
+        self.local = local
+        self.group = group
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+
+    def add_local(self, *a, **kw) -> List[int]:
+        return [r * self.world + self.rank for r in self.local.add(*a, **kw)]
+
+    def search(self, queries, k: int, min_priority, tags, now=None) -> List[List[Tuple[int, float]]]:
+        import torch.distributed as dist
+
+        res = self.local.search(queries, k, min_priority, tags, now)
+        if self.world == 1:
+            return res
+        Q = len(res)
+        t = torch.full((Q, k, 2), -1.0, dtype=torch.float64)
+        for i, lst in enumerate(res):
+            for j, (row, sc) in enumerate(lst[:k]):
+                t[i, j, 0] = row * self.world + self.rank
+                t[i, j, 1] = sc
+        dev = self.local.device if dist.get_backend(self.group) == "nccl" else torch.device("cpu")
+        t = t.to(dev)
+        allt = torch.empty((self.world,) + tuple(t.shape), dtype=t.dtype, device=dev)
+        dist.all_gather_into_tensor(allt, t, group=self.group)
+        allt = allt.cpu()
+        out = []
+        for i in range(Q):
+            cand = allt[:, i].reshape(-1, 2)
+            cand = cand[cand[:, 0] >= 0]
+            order = torch.argsort(cand[:, 1], descending=True)[:k]
+            out.append([(int(cand[j, 0]), float(cand[j, 1])) for j in order])
+        return out
