@@ -1,0 +1,197 @@
+"""Manager-side delegation (reference: pilott/delegation/task_delegator.py:8-360).
+
+Delegate iff the manager allows delegation AND (its own queue_util > 0.8 OR the
+task's complexity exceeds max_task_complexity OR it lacks a required capability).
+Candidates: children not stopped/error, under their max_concurrent_tasks active
+delegations, with queue/cpu/mem utilisation < 0.8; best by
+    0.4*suitability + 0.3*(1-queue_util) + 0.2*success_rate + 0.1*(1-max(cpu,mem)).
+Outcomes are recorded per child (success/failure counts, mean time, error
+histogram); history older than 24 h and delegations stale for 1 h are dropped.
+The one implementation replaces the reference's duplicate stub.
+"""
+from __future__ import annotations
+
+import asyncio
+import logging
+from collections import defaultdict, deque
+from datetime import datetime, timedelta
+from typing import Any, Deque, Dict, List, Optional, Tuple
+
+from pydantic import BaseModel, Field
+
+
+class DelegationMetrics(BaseModel):
+    success_count: int = 0
+    failure_count: int = 0
+    total_execution_time: float = 0.0
+    avg_execution_time: float = 0.0
+    last_success: Optional[datetime] = None
+    last_failure: Optional[datetime] = None
+    error_types: Dict[str, int] = Field(default_factory=dict)
+
+
+def _as_dict(task) -> Dict[str, Any]:
+    if isinstance(task, dict):
+        return task
+    d = {"id": task.id, "type": getattr(task, "type", None) or task.metadata.get("type"),
+         "complexity": task.complexity or task.metadata.get("complexity", 1),
+         "required_capabilities": list(task.required_skills or task.metadata.get("required_capabilities", []))}
+    return d
+
+
+class TaskDelegator:
+    MAX_HISTORY_PER_AGENT = 1000
+    HISTORY_RETENTION = timedelta(hours=24)
+    STALE_DELEGATION = timedelta(hours=1)
+    HISTORY_CLEANUP_INTERVAL = 3600.0
+
+    def __init__(self, agent: Any):
+        self.agent = agent
+        self.delegation_history: Dict[str, Deque[Dict[str, Any]]] = defaultdict(
+            lambda: deque(maxlen=self.MAX_HISTORY_PER_AGENT))
+        self.agent_metrics: Dict[str, DelegationMetrics] = {}
+        self.active_delegations: Dict[str, Dict[str, Any]] = {}
+        self._lock = asyncio.Lock()
+        self._last_cleanup = datetime.now()
+        self._cleanup_task: Optional[asyncio.Task] = None
+        self.logger = logging.getLogger("pilottai_amd.delegator")
+
+    async def start(self):
+        if self._cleanup_task is None:
+            self._cleanup_task = asyncio.create_task(self._periodic_cleanup())
+
+    async def stop(self):
+        if self._cleanup_task:
+            self._cleanup_task.cancel()
+            try:
+                await self._cleanup_task
+            except (asyncio.CancelledError, Exception):  # noqa: BLE001
+                pass
+            self._cleanup_task = None
+
+    async def evaluate_delegation(self, task) -> Tuple[bool, Optional[str]]:
+        t = _as_dict(task)
+        async with self._lock:
+            if not await self._should_delegate(t):
+                return False, None
+            best = await self._find_best_agent(t)
+            if best is None:
+                return False, None
+            self.active_delegations[t["id"]] = {"agent_id": best.id, "started_at": datetime.now(), "task": t}
+            return True, best.id
+
+    async def delegate(self, task) -> Optional[Any]:
+        """Evaluate and, if warranted, run the task on the chosen child; returns its TaskResult."""
+        ok, aid = await self.evaluate_delegation(task)
+        if not ok:
+            return None
+        child = self.agent.child_agents[aid]
+        t0 = datetime.now()
+        result = await child.execute_task(task)
+        await self.record_delegation(aid, _as_dict(task), {
+            "status": "completed" if result.success else "failed",
+            "execution_time": (datetime.now() - t0).total_seconds(), "error": result.error,
+            "error_type": (result.error or "").split(":")[0] or None})
+        return result
+
+    async def _should_delegate(self, t: Dict[str, Any]) -> bool:
+        cfg = self.agent.config
+        if not getattr(cfg, "allow_delegation", False):
+            return False
+        m = await self.agent.get_metrics()
+        if m.get("queue_utilization", 0.0) > 0.8:
+            return True
+        if (t.get("complexity") or 1) > getattr(cfg, "max_task_complexity", 10):
+            return True
+        req = set(t.get("required_capabilities") or [])
+        return bool(req - set(getattr(cfg, "required_capabilities", [])))
+
+    def _get_available_agents(self) -> Dict[str, Any]:
+        out = {}
+        for aid, a in getattr(self.agent, "child_agents", {}).items():
+            if str(getattr(a, "status", "")) in ("stopped", "error"):
+                continue
+            active = sum(1 for d in self.active_delegations.values() if d["agent_id"] == aid)
+            if active < getattr(a, "max_concurrent_tasks", 5):
+                out[aid] = a
+        return out
+
+    async def _can_accept_task(self, a) -> bool:
+        try:
+            m = await a.get_metrics()
+        except Exception:  # noqa: BLE001
+            return False
+        return (m.get("queue_utilization", 1.0) < 0.8 and m.get("cpu_usage", 1.0) < 0.8
+                and max(m.get("memory_usage", 1.0), m.get("kv_cache_utilization", 0.0)) < 0.8)
+
+    async def _calculate_total_score(self, a, t: Dict[str, Any]) -> float:
+        suit = await a.evaluate_task_suitability(t)
+        m = await a.get_metrics()
+        sr = m.get("success_rate", 0.5) if m.get("total_tasks") else 0.5
+        return (0.4 * suit + 0.3 * (1 - m.get("queue_utilization", 0.0)) + 0.2 * sr
+                + 0.1 * (1 - max(m.get("cpu_usage", 0.0), m.get("memory_usage", 0.0))))
+
+    async def _find_best_agent(self, t: Dict[str, Any]):
+        best, best_s = None, 0.0
+        for aid, a in self._get_available_agents().items():
+            try:
+                if not await self._can_accept_task(a):
+                    continue
+                s = await asyncio.wait_for(self._calculate_total_score(a, t), 10)
+            except Exception as e:  # noqa: BLE001
+                self.logger.debug("score for %s failed: %s", aid, e)
+                continue
+            if s > best_s:
+                best, best_s = a, s
+        return best
+
+    async def record_delegation(self, agent_id: str, task: Dict[str, Any], result: Dict[str, Any]):
+        async with self._lock:
+            ok = result.get("status") == "completed"
+            entry = {"task_id": task.get("id"), "task": task, "timestamp": datetime.now(), "success": ok,
+                     "execution_time": float(result.get("execution_time", 0.0)), "error": result.get("error"),
+                     "error_type": result.get("error_type")}
+            self.delegation_history[agent_id].append(entry)
+            m = self.agent_metrics.setdefault(agent_id, DelegationMetrics())
+            if ok:
+                m.success_count += 1
+                m.last_success = datetime.now()
+            else:
+                m.failure_count += 1
+                m.last_failure = datetime.now()
+                et = entry["error_type"] or "unknown"
+                m.error_types[et] = m.error_types.get(et, 0) + 1
+            n = m.success_count + m.failure_count
+            m.total_execution_time += entry["execution_time"]
+            m.avg_execution_time = m.total_execution_time / n
+            self.active_delegations.pop(task.get("id"), None)
+
+    def get_agent_metrics(self, agent_id: str) -> Optional[Dict[str, Any]]:
+        m = self.agent_metrics.get(agent_id)
+        if m is None:
+            return None
+        n = m.success_count + m.failure_count
+        return {"success_rate": m.success_count / n if n else 0.0, "avg_execution_time": m.avg_execution_time,
+                "total_tasks": n, "last_success": m.last_success, "last_failure": m.last_failure,
+                "error_distribution": dict(m.error_types)}
+
+    async def _periodic_cleanup(self):
+        while True:
+            await asyncio.sleep(self.HISTORY_CLEANUP_INTERVAL)
+            await self._cleanup_old_history()
+
+    async def _cleanup_old_history(self):
+        now = datetime.now()
+        async with self._lock:
+            for aid, h in self.delegation_history.items():
+                while h and now - h[0]["timestamp"] > self.HISTORY_RETENTION:
+                    h.popleft()
+            for tid in [t for t, d in self.active_delegations.items() if now - d["started_at"] > self.STALE_DELEGATION]:
+                self.active_delegations.pop(tid, None)
+            self._last_cleanup = now
+
+    async def get_metrics(self) -> Dict[str, Any]:
+        return {"active_delegations": len(self.active_delegations),
+                "agent_metrics": {k: v.model_dump() for k, v in self.agent_metrics.items()},
+                "history_size": sum(len(h) for h in self.delegation_history.values()),
+                "last_cleanup": self._last_cleanup.isoformat()}

@@ -1,0 +1,149 @@
+"""Native runtime (tokenizer, grammar automaton, scheduler, block manager) and the
+CPU execution of the full inference engine (tiny model, fp32 reference kernels)."""
+import json
+
+import numpy as np
+import pytest
+import torch
+
+from pilottai_amd import _runtime
+from pilottai_amd.engine.grammar import GrammarCompiler, load_schemas, max_output_tokens
+from pilottai_amd.engine.tokenizer import BOS_ID, EOT_ID, VOCAB_SIZE, get_tokenizer
+from pilottai_amd.ops import build_attention_items
+from pilottai_amd.ops import reference as ref
+
+
+@pytest.fixture(scope="module")
+def tok():
+    return get_tokenizer()
+
+
+@pytest.fixture(scope="module")
+def gc(tok):
+    return GrammarCompiler(tok)
+
+
+def test_tokenizer_roundtrip_and_specials(tok):
+    assert tok.vocab_size == VOCAB_SIZE == 128256
+    s = 'Task: summarize {"a": [1, 2]} – naïve ünïcode ✓'
+    ids = tok.encode(s)
+    assert tok.decode(ids) == s
+    assert len(ids) < len(s.encode())  # merges beyond bytes
+    assert tok.token_id("<|eot_id|>") == EOT_ID and tok.token_id("<|begin_of_text|>") == BOS_ID
+    assert EOT_ID not in tok.encode("<|eot_id|>")  # specials are never produced from text
+
+
+def test_grammar_automaton_jump_forward(gc, tok):
+    segs = gc.compile("orchestrator.execution_strategy", {"parallel_execution": True})
+    g = _runtime.Grammar(segs)
+    out = g.take_forced_run(1000)
+    assert tok.decode(out).startswith('{"parallel_execution": true, "priority": ')
+    cls, forced = g.next()
+    assert forced == -1 and cls >= 0
+    g.advance(tok.token_id("7"))
+    out += [tok.token_id("7")] + g.take_forced_run(1000)
+    g.advance(tok.token_id("3"))
+    out += [tok.token_id("3")] + g.take_forced_run(1000)
+    assert g.done()
+    assert json.loads(tok.decode(out)) == {"parallel_execution": True, "priority": 7, "max_agents": 3}
+
+
+def test_all_schemas_produce_valid_json_under_random_sampling(gc, tok):
+    masks = gc.reg.packed().view(np.uint32)
+    rng = np.random.default_rng(0)
+    schemas = load_schemas()
+    for name in schemas:
+        segs = gc.compile(name)
+        g = _runtime.Grammar(segs)
+        out = []
+        for _ in range(max_output_tokens(segs) + 5):
+            if g.done():
+                break
+            cls, f = g.next()
+            if f < 0:
+                allowed = np.nonzero(np.unpackbits(masks[cls].view(np.uint8), bitorder="little"))[0]
+                f = int(rng.choice(allowed))
+            g.advance(f)
+            out.append(f)
+        assert g.done(), name
+        obj = json.loads(tok.decode(out))
+        assert set(obj) == set(schemas[name]), name
+
+
+def test_scheduler_prefix_cache_preemption_and_layout():
+    L_cfg = {"num_blocks": 12, "block_size": 16, "max_num_seqs": 4, "max_num_batched_tokens": 64,
+             "max_prefill_tokens": 64, "max_model_len": 128, "gqa_group": 4, "eos_ids": [128009]}
+    s = _runtime.Scheduler(L_cfg)
+    L = s.layout()
+    buf = np.zeros(L["total"], dtype=np.int32)
+    prompt = list(range(100, 150))  # 50 tokens -> 3 full blocks + 2
+    s.add_request(1, prompt, 0.0, 3, 7, True, [], None)
+    T = s.schedule(buf.ctypes.data)
+    assert T == 50
+    c = buf[L["counts"]:L["counts"] + 8]
+    assert c[1] == 1 and c[2] == 1
+    assert list(buf[L["positions"]:L["positions"] + 3]) == [0, 1, 2]
+    assert buf[L["logit_rows"]] == 49
+    items = buf[L["items"]:L["items"] + 4 * c[3]].reshape(-1, 4)
+    ref_items, _, _ = build_attention_items([50], [50], 4)
+    assert [tuple(x) for x in items] == ref_items
+    for _ in range(3):
+        outs = s.commit(np.array([5], np.int32).ctypes.data, 1)
+        if outs:
+            break
+        s.schedule(buf.ctypes.data)
+    assert outs and outs[0][1] == [5, 5, 5] and outs[0][2] == 1  # finish reason: length
+    # same prompt again: the 3 full prompt blocks come from the prefix cache
+    s.add_request(2, prompt, 0.0, 1, 7, True, [], None)
+    T = s.schedule(buf.ctypes.data)
+    assert T == 50 - 48
+    outs = s.commit(np.array([9], np.int32).ctypes.data, 1)
+    assert outs[0][4] == 48  # cached prompt tokens
+    assert s.total_cached_tokens == 48
+
+
+def test_scheduler_preempts_when_out_of_blocks():
+    s = _runtime.Scheduler({"num_blocks": 6, "block_size": 16, "max_num_seqs": 4, "max_num_batched_tokens": 256,
+                            "max_model_len": 256, "prefix_caching": False})
+    L = s.layout()
+    buf = np.zeros(L["total"], dtype=np.int32)
+    s.add_request(1, list(range(40)), 0.0, 200, 1, True, [], None)
+    s.add_request(2, list(range(1000, 1030)), 0.0, 200, 1, True, [], None)
+    s.schedule(buf.ctypes.data)
+    assert s.num_running == 2
+    for _ in range(60):
+        c = buf[L["counts"]:L["counts"] + 8]
+        s.commit(np.full(4, 3, np.int32).ctypes.data, int(c[2]))
+        if s.schedule(buf.ctypes.data) == 0:
+            break
+    assert s.total_preemptions >= 1
+
+
+def test_engine_cpu_tiny_end_to_end(tok):
+    from pilottai_amd.engine.engine import EngineConfig, LLMEngine
+
+    e = LLMEngine(EngineConfig(model="tiny", max_num_seqs=8, max_num_batched_tokens=128, max_model_len=512,
+                               num_kv_blocks=128), device="cpu")
+    segs = e.grammar.compile("orchestrator.result_evaluation")
+    p = tok.encode("Task: evaluate. Result: ok")
+    outs = e.generate([p, p + p], temperature=0.7, max_tokens=64, grammar=segs)
+    for o in outs:
+        obj = json.loads(o.text)
+        assert set(obj) == {"success", "quality", "requires_retry"}
+        assert o.finish_reason == "stop"
+    # greedy decode matches the dense reference forward (fp32 CPU path)
+    g = e.generate([p], temperature=0.0, max_tokens=4, ignore_eos=True)[0]
+    ref_logits = e.model.reference_logits(p + g.token_ids[:-1])
+    for i, t in enumerate(g.token_ids):
+        row = ref_logits[len(p) - 1 + i]
+        assert row[t] >= row.max() - 0.05
+
+
+def test_reference_sampler_masks_and_forced():
+    V = 256
+    logits = torch.randn(3, V).to(torch.bfloat16)
+    allowed = np.zeros(V, bool)
+    allowed[[3, 200]] = True
+    masks = torch.stack([ref.pack_mask(np.ones(V, bool)), ref.pack_mask(allowed)])
+    t = ref.sample(logits, [0.0, 0.7, 0.0], [0, 1, -1], masks, [1, 2, 3], [0, 0, 0], [-1, -1, 77])
+    assert int(t[0]) == int(logits[0].float().argmax()) and int(t[1]) in (3, 200) and int(t[2]) == 77
