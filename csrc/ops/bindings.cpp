@@ -24,6 +24,8 @@ int pa_sample(int* out_tokens, float* out_keys, float* workspace, const void* lo
               int V, int ld, int vocab_offset, const float* temperature, const int* mask_class,
               const uint32_t* class_masks, int mask_words, const int64_t* seeds,
               const int* offsets, const int* forced, hipStream_t st);
+void pa_skinny_set_variant(int v);
+int pa_skinny_gemm(void* y, const void* x, const void* w, int M, int N, int K, int ldy, hipStream_t st);
 int pa_cosine_topk_workspace_bytes(int Q, int N, int K);
 int pa_cosine_topk(float* out_scores, int* out_rows, void* workspace, const void* queries,
                    const void* index, int Q, int N, int D, int K, const int* row_priority,
@@ -144,6 +146,19 @@ void paged_attention(at::Tensor out, at::Tensor part_o, at::Tensor part_ml, at::
            "paged_attention");
 }
 
+// y[M, N] = x[M, K] . w[N, K]^T for M <= 128; returns false if the shape is not handled.
+bool skinny_gemm(at::Tensor y, at::Tensor x, at::Tensor w) {
+  check_gpu(x, "x"); check_gpu(w, "w");
+  TORCH_CHECK(y.is_cuda() && y.stride(-1) == 1, "y must be a GPU tensor with unit inner stride");
+  check_dtype(x, at::kBFloat16, "x"); check_dtype(w, at::kBFloat16, "w"); check_dtype(y, at::kBFloat16, "y");
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && y.dim() == 2, "skinny_gemm expects 2-D tensors");
+  const int M = x.size(0), K = x.size(1), N = w.size(0);
+  TORCH_CHECK(w.size(1) == K && y.size(0) == M && y.size(1) == N, "skinny_gemm shape mismatch");
+  const int rc = pa_skinny_gemm(y.data_ptr(), x.data_ptr(), w.data_ptr(), M, N, K, y.stride(0), cur_stream());
+  TORCH_CHECK(rc >= 0, "skinny_gemm launch failed");
+  return rc == 0;
+}
+
 int64_t sample_workspace_floats(int64_t rows, int64_t V) {
   return pa_sample_workspace_floats(rows, V);
 }
@@ -230,6 +245,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("fused_add_rmsnorm", &fused_add_rmsnorm);
   m.def("rope_cache", &rope_cache);
   m.def("silu_mul", &silu_mul);
+  m.def("skinny_gemm", &skinny_gemm);
+  m.def("skinny_set_variant", [](int v) { pa_skinny_set_variant(v); });
   m.def("paged_attention", &paged_attention);
   m.def("sample_workspace_floats", &sample_workspace_floats);
   m.def("sample", &sample, py::arg("out_tokens"), py::arg("out_keys"), py::arg("workspace"),

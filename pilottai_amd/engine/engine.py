@@ -17,6 +17,14 @@ Architecture (one engine per GPU / per TP group, one process per GPU):
 
 The LLM protocol used by agents (generate_response / apredict) lives in
 engine/local_llm.py on top of `LLMEngine.submit`.
+
+Tensor parallelism (Llama-3-70B, TP=8 over xGMI): only TP rank 0 (the driver)
+owns requests, the scheduler, grammars and the tokenizer. Each step it sends a
+7-int header over a gloo group, then broadcasts the step metadata it already
+holds on the device (one RCCL broadcast); the other ranks sit in `follow()`,
+replay the same hipGraph, and take part in the row-parallel all-reduces and
+the vocab-parallel sampling all-gather inside it. Their schedulers stay idle, so
+nothing on the host has to be kept consistent between ranks.
 """
 from __future__ import annotations
 
@@ -61,6 +69,10 @@ class EngineConfig:
     seed: int = 0
     weights_path: Optional[str] = None
     capture_on_start: bool = True
+
+
+# TP step header: [op, T, ns, nsamp, bucket, masks_changed, n_copy]
+_OP_STOP, _OP_STEP = 0, 1
 
 
 @dataclass
@@ -146,6 +158,10 @@ class LLMEngine:
                 nb = 2048
         need_min = (self.max_model_len + cfg.block_size - 1) // cfg.block_size + 1
         nb = max(nb, need_min)
+        if self.tp.size > 1:  # block ids travel in the metadata: every rank needs the same pool
+            t = torch.tensor([nb], dtype=torch.int64)
+            torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MIN, group=self.tp.cpu_group)
+            nb = int(t.item())
         self.kv = KVCache(mc.num_layers, nb, kv_local, self.device, block_size=cfg.block_size)
         self.num_kv_blocks = nb
         # ---- native scheduler + step buffers
@@ -186,6 +202,9 @@ class LLMEngine:
         self._graphs: Dict[int, "torch.cuda.CUDAGraph"] = {}
         self._graph_pool = None
         self.use_graphs = cfg.use_graphs and self.on_gpu
+        self.is_driver = self.tp.rank == 0
+        self._tp_header = torch.zeros(7, dtype=torch.int64)
+        self._tp_closed = False
         # ---- request plumbing
         self._inbox: "queue.SimpleQueue" = queue.SimpleQueue()
         self._aborts: "queue.SimpleQueue" = queue.SimpleQueue()
@@ -199,7 +218,8 @@ class LLMEngine:
         self.stats = {"steps": 0, "tokens": 0, "sampled": 0, "requests": 0, "finished": 0,
                       "busy_s": 0.0, "prefill_tokens": 0, "decode_steps": 0, "graph_replays": 0,
                       "bucket_tokens": 0}
-        if self.use_graphs and cfg.capture_on_start:
+        # graphs contain the TP collectives, so every rank captures every bucket up front
+        if self.use_graphs and (cfg.capture_on_start or self.tp.size > 1):
             self.capture_graphs()
 
     # ------------------------------------------------------------------ setup
@@ -228,13 +248,14 @@ class LLMEngine:
         self._offsets = sl("offsets", ms)
         self._seeds = sl("seeds", 2 * ms).view(torch.int64)
 
-    def _sync_masks(self):
+    def _sync_masks(self) -> bool:
         reg = self.grammar.reg
         if reg.version == self._mask_version:
-            return
+            return False
         packed = torch.from_numpy(reg.packed())
         self._class_masks[: packed.shape[0]].copy_(packed.to(self.device))
         self._mask_version = reg.version
+        return True
 
     def _items_for_bucket(self, bucket: int, s_b: int) -> int:
         return min(self.L["max_items"], bucket // (4 * self._tpw) + s_b * (self._max_parts + 1) + 4)
@@ -366,6 +387,52 @@ class LLMEngine:
         if self._thread is not None:
             self._thread.join(timeout=30)
             self._thread = None
+        self.release_followers()
+
+    # ------------------------------------------------------------------ TP
+    def _tp_send(self, op: int, *vals: int):
+        h = self._tp_header
+        h.zero_()
+        h[0] = op
+        for i, v in enumerate(vals):
+            h[1 + i] = int(v)
+        self.tp.broadcast(h, cpu=True)
+
+    def release_followers(self):
+        """Driver: tell the follower ranks to leave `follow()` (idempotent)."""
+        if self.tp.size > 1 and self.is_driver and not self._tp_closed:
+            self._tp_closed = True
+            self._tp_send(_OP_STOP)
+
+    def follow(self) -> int:
+        """Follower ranks (TP rank > 0): mirror the driver's steps until it stops.
+
+        Returns the number of steps executed."""
+        if self.is_driver:
+            raise RuntimeError("follow() is for TP ranks > 0")
+        if self.on_gpu:
+            torch.cuda.set_device(self.device)
+        n = 0
+        h = self._tp_header
+        with torch.inference_mode():
+            while True:
+                self.tp.broadcast(h, cpu=True)
+                op, T, ns, nsamp, bucket, masks_changed, n_copy = (int(v) for v in h.tolist())
+                if op == _OP_STOP:
+                    break
+                if masks_changed:
+                    self.tp.broadcast(self._class_masks)
+                self.tp.broadcast(self._dev_meta[:n_copy])
+                g = self._graphs.get(bucket) if self.use_graphs else None
+                if g is not None:
+                    g.replay()
+                else:
+                    self._forward_and_sample(bucket, self._seq_bucket(bucket), ns)
+                if self.on_gpu:
+                    torch.cuda.current_stream().synchronize()
+                n += 1
+        self.stats["steps"] += n
+        return n
 
     @property
     def failed(self) -> Optional[BaseException]:
@@ -420,10 +487,15 @@ class LLMEngine:
         ns, nsamp = int(c[1]), int(c[2])
         bucket = next(b for b in self.buckets if b >= T)
         s_b = self._seq_bucket(bucket)
-        self._sync_masks()
+        masks_changed = self._sync_masks()
+        n_copy = L["block_table"] + ns * L["max_blocks"]
         if self.on_gpu:
-            n_copy = L["block_table"] + ns * L["max_blocks"]
             self._dev_meta[:n_copy].copy_(self._host_meta[:n_copy], non_blocking=True)
+        if self.tp.size > 1:
+            self._tp_send(_OP_STEP, T, ns, nsamp, bucket, int(masks_changed), n_copy)
+            if masks_changed:
+                self.tp.broadcast(self._class_masks)
+            self.tp.broadcast(self._dev_meta[:n_copy])
         with torch.inference_mode():
             g = self._graphs.get(bucket) if self.use_graphs else None
             if g is None and self.use_graphs:

@@ -141,31 +141,52 @@ class LlamaModel:
 
     # -- weights -----------------------------------------------------------------
     def _init_random(self, seed: int):
+        """Random init in canonical shards: every parallel matrix is generated as
+        C = num_kv_heads chunks along its split dimension, chunk j from its own
+        seed. TP=k rank r generates only its chunks, so any TP degree that divides
+        C holds exactly the slices of the TP=1 weights (TP tests compare token for
+        token), and no rank ever materialises a full matrix."""
         cfg, dev, dt = self.cfg, self.device, self.dtype
-        g = torch.Generator(device=dev)
-        g.manual_seed(seed * 1000 + self.tp.rank)
-        std = cfg.init_std
+        C = cfg.num_kv_heads
+        ts, r = self.tp.size, self.tp.rank
+        if C % ts:
+            raise ValueError(f"TP size {ts} must divide num_kv_heads={C}")
+        mine = range(r * C // ts, (r + 1) * C // ts)
+        std, d, hd = cfg.init_std, cfg.hidden_size, cfg.head_dim
 
-        def w(*shape):
+        def chunk(tag: int, j: int, *shape):
+            g = torch.Generator(device=dev)
+            g.manual_seed((seed * 1_000_003 + tag * 7919 + j) & 0x7FFFFFFF)
             t = torch.empty(*shape, dtype=dt, device=dev)
             t.normal_(0.0, std, generator=g)
             return t
 
-        d = cfg.hidden_size
-        qkv_out = (self.h_local + 2 * self.kv_local) * cfg.head_dim
-        self.embed = w(self.v_local, d)
+        def rows(tag, total_rows, cols):  # column-parallel: split the output rows
+            return torch.cat([chunk(tag, j, total_rows // C, cols) for j in mine], 0)
+
+        def colsplit(tag, rows_, total_cols):  # row-parallel: split the input columns
+            return torch.cat([chunk(tag, j, rows_, total_cols // C) for j in mine], 1)
+
+        self.embed = rows(1, cfg.vocab_size, d)
         self.layers: List[Dict[str, torch.Tensor]] = []
-        for _ in range(cfg.num_layers):
+        for li in range(cfg.num_layers):
+            t = 100 + 10 * li
+            q = rows(t + 0, cfg.num_heads * hd, d)
+            k = rows(t + 1, cfg.num_kv_heads * hd, d)
+            v = rows(t + 2, cfg.num_kv_heads * hd, d)
+            gate = rows(t + 4, cfg.intermediate_size, d)
+            up = rows(t + 5, cfg.intermediate_size, d)
             self.layers.append({
                 "ln1": torch.ones(d, dtype=dt, device=dev),
-                "wqkv": w(qkv_out, d),
-                "wo": w(d, self.h_local * cfg.head_dim),
+                "wqkv": torch.cat([q, k, v], 0),
+                "wo": colsplit(t + 3, d, cfg.num_heads * hd),
                 "ln2": torch.ones(d, dtype=dt, device=dev),
-                "w13": w(2 * self.f_local, d),
-                "w2": w(d, self.f_local),
+                "w13": torch.cat([gate, up], 0),
+                "w2": colsplit(t + 6, d, cfg.intermediate_size),
             })
+            del q, k, v, gate, up
         self.norm = torch.ones(d, dtype=dt, device=dev)
-        self.lm_head = self.embed if cfg.tie_embeddings else w(self.v_local, d)
+        self.lm_head = self.embed if cfg.tie_embeddings else rows(2, cfg.vocab_size, d)
 
     def _load_hf(self, path: str):
         """Load a HF Llama checkpoint directory of *.safetensors (no pickle)."""
@@ -243,20 +264,20 @@ class LlamaModel:
         resid = h
         x = ops.rmsnorm(h, self.layers[0]["ln1"], cfg.rms_eps)
         for li, L in enumerate(self.layers):
-            qkv = F.linear(x, L["wqkv"])
+            qkv = ops.linear(x, L["wqkv"], "qkv")
             q = torch.empty(T, H, hd, dtype=self.dtype, device=self.device)
             ops.rope_cache(q, kv.k[li], kv.v[li], qkv, meta.positions, meta.slots, self.cos_sin, H, KVh)
             attn = torch.empty(T, H, hd, dtype=self.dtype, device=self.device)
             ops.paged_attention(attn, part_o, part_ml, q, kv.k[li], kv.v[li], meta.items, meta.n_items,
                                 meta.ritems, meta.n_ritems, meta.q_start, meta.q_len, meta.ctx_len,
                                 meta.block_table, self.scale, num_seqs=meta.num_seqs)
-            o = F.linear(attn.view(T, H * hd), L["wo"])
+            o = ops.linear(attn.view(T, H * hd), L["wo"], "o")
             if self.tp.size > 1:
                 self.tp.all_reduce(o)
             x = ops.fused_add_rmsnorm(resid, o, L["ln2"], cfg.rms_eps)
-            gu = F.linear(x, L["w13"])
+            gu = ops.linear(x, L["w13"], "gate_up")
             a = ops.silu_mul(gu)
-            d = F.linear(a, L["w2"])
+            d = ops.linear(a, L["w2"], "down")
             if self.tp.size > 1:
                 self.tp.all_reduce(d)
             nxt = self.layers[li + 1]["ln1"] if li + 1 < len(self.layers) else self.norm
@@ -264,7 +285,7 @@ class LlamaModel:
         rows = meta.logit_rows[:num_logit_rows]
         rows = rows.long() if self.device.type == "cpu" else rows
         xs = x.index_select(0, rows)
-        return F.linear(xs, self.lm_head)
+        return ops.linear(xs, self.lm_head, "lm_head")
 
     # -- reference (dense, no cache) forward used by numerics tests ----------------
     @torch.no_grad()

@@ -2,6 +2,7 @@
 from .kernels import (  # noqa: F401
     cosine_topk,
     fused_add_rmsnorm,
+    linear,
     native_available,
     native_module_path,
     paged_attention,
@@ -11,6 +12,8 @@ from .kernels import (  # noqa: F401
     sample,
     sample_workspace,
     silu_mul,
+    skinny_gemm,
+    SKINNY_MAX_M,
 )
 from .attn_meta import ATT_PART, build_attention_items  # noqa: F401
 from . import reference  # noqa: F401

@@ -167,3 +167,32 @@ def cosine_topk(queries, index, n_valid: int, K: int, row_priority, row_tags, ro
         return out_s, out_r
     return ref.cosine_topk(queries, index, n_valid, K, row_priority, row_tags, row_expiry,
                            q_min_priority, q_tags, now)
+
+
+def skinny_gemm(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """y = x @ w.T via the weight-streaming MFMA kernel (csrc/ops/gemm_skinny.hip)."""
+    y = out if out is not None else torch.empty(x.shape[0], w.shape[0], dtype=x.dtype, device=x.device)
+    if not _on_gpu(x):
+        y.copy_(torch.nn.functional.linear(x.float(), w.float()).to(y.dtype))
+        return y
+    if not require_native().skinny_gemm(y, x, w):
+        raise ValueError(f"skinny_gemm does not handle M={x.shape[0]} N={w.shape[0]} K={x.shape[1]}")
+    return y
+
+
+# Largest token count at which the skinny kernel beats hipBLASLt, per projection
+# kind, measured cache-cold on MI355X with Llama-3-8B shapes
+# (tools/gemm_bench.py, profiles/r1_skinny_gemm_cold.md). 0 = never.
+SKINNY_MAX_M = {"qkv": 8, "o": 32, "gate_up": 16, "down": 0, "lm_head": 0}
+
+
+def linear(x: torch.Tensor, w: torch.Tensor, kind: str) -> torch.Tensor:
+    """Projection dispatcher: skinny MFMA kernel at decode sizes, hipBLASLt otherwise.
+
+    The choice depends only on the (static) token count, so it is fixed per
+    captured hipGraph bucket."""
+    M, K = x.shape
+    if (_on_gpu(x) and M <= SKINNY_MAX_M.get(kind, 0) and K % 256 == 0 and w.shape[0] % 16 == 0
+            and x.is_contiguous()):
+        return skinny_gemm(x, w)
+    return torch.nn.functional.linear(x, w)

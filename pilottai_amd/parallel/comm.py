@@ -28,6 +28,8 @@ class TPGroup:
     group: Optional["dist.ProcessGroup"] = None
     rank: int = 0
     size: int = 1
+    root: int = 0                                   # global rank of TP rank 0 (the step driver)
+    cpu_group: Optional["dist.ProcessGroup"] = None  # gloo group for host-side step headers
 
     @staticmethod
     def single() -> "TPGroup":
@@ -42,9 +44,19 @@ class TPGroup:
         """Concatenate `t` from every rank along a new leading dim: [size, *t.shape]."""
         if self.size == 1:
             return t.unsqueeze(0)
+        if t.device.type == "cpu":  # gloo: list form
+            parts = [torch.empty_like(t) for _ in range(self.size)]
+            dist.all_gather(parts, t.contiguous(), group=self.group)
+            return torch.stack(parts)
         out = torch.empty((self.size,) + tuple(t.shape), dtype=t.dtype, device=t.device)
         dist.all_gather_into_tensor(out, t.contiguous(), group=self.group)
         return out
+
+    def broadcast(self, t: torch.Tensor, cpu: bool = False) -> torch.Tensor:
+        """Broadcast from the driver (TP rank 0)."""
+        if self.size > 1:
+            dist.broadcast(t, src=self.root, group=self.cpu_group if cpu else self.group)
+        return t
 
 
 def env_rank_world():
@@ -85,11 +97,13 @@ def new_tp_groups(tp_size: int) -> TPGroup:
     rank = dist.get_rank()
     assert world % tp_size == 0, "world size must be a multiple of the TP size"
     mine = None
+    gloo_needed = dist.get_backend() != "gloo"
     for start in range(0, world, tp_size):
         ranks = list(range(start, start + tp_size))
         g = dist.new_group(ranks)
+        cg = dist.new_group(ranks, backend="gloo") if gloo_needed else g
         if rank in ranks:
-            mine = TPGroup(g, rank - start, tp_size)
+            mine = TPGroup(g, rank - start, tp_size, root=start, cpu_group=cg)
     return mine
 
 

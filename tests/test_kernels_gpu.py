@@ -201,3 +201,17 @@ def test_cosine_topk(gpu):
     torch.testing.assert_close(s.cpu(), rs, atol=2e-3, rtol=2e-3)
     # rows agree except for exact score ties
     assert (r.cpu() == rr).float().mean().item() > 0.95
+
+
+@pytest.mark.parametrize("M,N,K", [(1, 4096, 4096), (13, 6144, 4096), (64, 28672, 4096), (64, 4096, 14336),
+                                   (100, 4096, 4096), (128, 1024, 512), (37, 128256, 4096)])
+def test_skinny_gemm(gpu, M, N, K):
+    from pilottai_amd.ops import kernels
+
+    torch.manual_seed(8)
+    x = _bf(M, K, dev=gpu)
+    w = _bf(N, K, dev=gpu, scale=0.05)
+    y = torch.empty(M, N, dtype=torch.bfloat16, device=gpu)
+    assert kernels.require_native().skinny_gemm(y, x, w)
+    r = (x.float() @ w.float().T)
+    torch.testing.assert_close(y.float(), r, atol=3e-2, rtol=2e-2)

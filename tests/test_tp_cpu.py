@@ -1,0 +1,99 @@
+"""Tensor-parallel engine on CPU (gloo, world_size 2): driver/follower protocol,
+vocab-parallel embedding + sampling, row-parallel all-reduce, canonical sharded
+init. Mirrors the TP=8 70B path (BASELINE config 5) at test size."""
+import json
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _cfg():
+    from pilottai_amd.engine.engine import EngineConfig
+
+    return EngineConfig(model="tiny-gqa4", max_num_seqs=8, max_num_batched_tokens=128, max_model_len=512,
+                        num_kv_blocks=96, use_graphs=False)
+
+
+def _prompts(tok):
+    return [tok.encode("Task: summarize the quarterly report."), tok.encode("Task: plan a trip")]
+
+
+def _worker(rank, world, port, out_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    torch.set_num_threads(2)
+    from pilottai_amd.engine.engine import LLMEngine
+    from pilottai_amd.parallel.comm import init_distributed, new_tp_groups
+
+    init_distributed("gloo")
+    tp = new_tp_groups(world)
+    e = LLMEngine(_cfg(), device="cpu", tp=tp)
+    if rank != 0:
+        e.follow()
+        torch.distributed.destroy_process_group()
+        return
+    ps = _prompts(e.tok)
+    greedy = e.generate(ps, temperature=0.0, max_tokens=6, ignore_eos=True)
+    segs = e.grammar.compile("orchestrator.result_evaluation")
+    js = e.generate([ps[0]], temperature=0.8, max_tokens=64, grammar=segs)[0]
+    e.release_followers()
+    torch.distributed.destroy_process_group()
+    with open(out_path, "w") as f:
+        json.dump({"greedy": [o.token_ids for o in greedy], "json": js.text,
+                   "steps": e.stats["steps"]}, f)
+
+
+def test_tp2_engine_matches_tp1(tmp_path):
+    out = str(tmp_path / "tp.json")
+    port = _free_port()
+    mp.start_processes(_worker, args=(2, port, out), nprocs=2, join=True, start_method="spawn")
+    res = json.load(open(out))
+    # structured output is valid JSON of the schema under TP sampling
+    obj = json.loads(res["json"])
+    assert set(obj) == {"success", "quality", "requires_retry"}
+
+    from pilottai_amd.engine.engine import LLMEngine
+
+    e1 = LLMEngine(_cfg(), device="cpu")
+    ref = e1.generate(_prompts(e1.tok), temperature=0.0, max_tokens=6, ignore_eos=True)
+    # identical weights (canonical shards) -> identical greedy tokens, up to bf16
+    # rounding of the split all-reduce: require the first token and most others.
+    agree = tot = 0
+    for a, b in zip(res["greedy"], [o.token_ids for o in ref]):
+        assert a[0] == b[0]
+        for x, y in zip(a, b):
+            if x != y:
+                break
+            agree += 1
+        tot += len(b)
+    assert agree >= tot // 2
+
+
+def test_sharded_init_slices_match_full():
+    """Rank r of TP=k holds exactly the r-th slice of the TP=1 weights."""
+    from pilottai_amd.models.llama import LlamaModel, get_config
+    from pilottai_amd.parallel.comm import TPGroup
+
+    cfg = get_config("tiny-gqa4")
+    full = LlamaModel(cfg, "cpu", seed=3)
+    for r in range(2):
+        part = LlamaModel(cfg, "cpu", seed=3, tp=TPGroup(None, r, 2))
+        L0, P0 = full.layers[0], part.layers[0]
+        hd = cfg.head_dim
+        qh = cfg.num_heads // 2
+        q_full = L0["wqkv"][: cfg.num_heads * hd]
+        assert torch.equal(P0["wqkv"][: qh * hd], q_full[r * qh * hd:(r + 1) * qh * hd])
+        w = cfg.num_heads * hd // 2
+        assert torch.equal(P0["wo"], L0["wo"][:, r * w:(r + 1) * w])
+        assert torch.equal(part.embed, full.embed[r * cfg.vocab_size // 2:(r + 1) * cfg.vocab_size // 2])
