@@ -144,6 +144,7 @@ async def run_rank(a, rank: int, world: int, device):
         "prompt_tokens": u1["prompt_tokens"] - u0["prompt_tokens"],
         "completion_tokens": u1["completion_tokens"] - u0["completion_tokens"],
         "busy_s": st1["busy_s"] - st0["busy_s"], "prefix_hit": em["prefix_cache_hit_tokens"],
+        "bucket_tokens": st1["bucket_tokens"] - st0["bucket_tokens"],
         "prompt_total": em["prompt_tokens"], "hbm_used_gb": em.get("hbm_used_gb", 0.0),
     }
     return local
@@ -214,6 +215,7 @@ def main():
             "engine_steps": tot("steps"),
             "engine_busy_frac": round(tot("busy_s") / (dt * len(gathered)), 3),
             "prefix_cache_hit_frac": round(tot("prefix_hit") / max(1, tot("prompt_total")), 3),
+            "graph_pad_frac": round(1 - tot("tokens") / max(1, tot("bucket_tokens")), 3),
             "init_s": round(max(g["init_s"] for g in gathered), 1),
             "hbm_used_gb_per_gpu": round(max(g["hbm_used_gb"] for g in gathered), 1),
             "notes": "BASELINE.md publishes no number for this config (vs_baseline null); the reference's "

@@ -3,8 +3,10 @@
 //
 // Layout (written by rope_cache.hip):
 //   q        [T, H, 128] bf16 (already rotated)
-//   k_cache  [num_blocks, KV, 16, 128]   keys row-major inside a 16-token page
+//   k_cache  [num_blocks, KV, 16, 16, 8] keys fragment-major: [dim/8][key][dim%8]
 //   v_cache  [num_blocks, KV, 128, 16]   values transposed inside a page
+// so that each MFMA A-fragment load (8 dims x 16 keys of K, 8 keys x 16 dims of
+// V^T) is one contiguous 256-B run: whole cache lines per load instruction.
 //
 // MFMA formulation (v_mfma_f32_16x16x32_bf16, wave64):
 //   The 16 MFMA columns are (G query heads of one KV head) x (16/G query tokens),
@@ -24,9 +26,10 @@
 //   nq <= 16/G : "kv-split" — the 4 waves of the workgroup share the query
 //                columns and interleave 32-key tiles; merged through LDS. Long
 //                contexts are further split into 512-key partitions (flash-
-//                decoding); partitions are combined by attn_reduce_kernel.
-//   nq >  16/G : "q-split" — wave w owns tokens [q_begin + w*16/G, ...) and
-//                walks its causal key range alone.
+//                decoding); the last partition to finish merges them (ticket
+//                counter per (sequence, KV head), no second launch).
+//   nq >  16/G : "prefill" — items of 32/G tokens = 32 columns on 32x32x16
+//                MFMAs; the 4 waves interleave key tiles and merge through LDS.
 // The grid is (max_items, KV) with a device-side item count so the launch is
 // shape-stable under hipGraph capture.
 #include "common.h"
@@ -38,19 +41,20 @@ constexpr int ATT_BLK = 16;
 constexpr int ATT_PART = 512;  // keys per decode partition (multiple of 32)
 constexpr float NEG_BIG = -1.0e30f;
 
+// ---------------------------------------------------------------------------
+// kv-split path (decode tokens / short runs, nq <= 16/G): 16x16x32 MFMA, the 4
+// waves interleave 32-key tiles and merge through LDS.
+constexpr int ATT_LDS_DECODE_BYTES = (4 * 16 * (ATT_HD + 4) + 2 * 4 * 16) * 4;
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+typedef __attribute__((address_space(1))) int gi32;
+
 template <int G>
-__global__ __launch_bounds__(256) void paged_attn_kernel(
-    bf16* __restrict__ out, float* __restrict__ part_o, float* __restrict__ part_ml,
-    const bf16* __restrict__ q, const bf16* __restrict__ k_cache,
-    const bf16* __restrict__ v_cache, const int4* __restrict__ items,
-    const int* __restrict__ n_items, const int* __restrict__ q_start,
-    const int* __restrict__ q_len, const int* __restrict__ ctx_len,
-    const int* __restrict__ block_table, int max_blocks, int H, int KV, float scale_log2) {
-  constexpr int TPW = 16 / G;
-  const int item = blockIdx.x;
-  if (item >= n_items[0]) return;
-  const int kvh = blockIdx.y;
-  const int4 it = items[item];
+__device__ __forceinline__ void decode_item(
+    const int4 it, char* smem, bf16* __restrict__ out, float* __restrict__ part_o,
+    float* __restrict__ part_ml, int* __restrict__ counters, const bf16* __restrict__ q, const bf16* __restrict__ k_cache,
+    const bf16* __restrict__ v_cache, const int* __restrict__ q_start, const int* __restrict__ q_len,
+    const int* __restrict__ ctx_len, const int* __restrict__ block_table, int max_blocks, int H,
+    int KV, int kvh, float scale_log2) {
   const int s = it.x, qb = it.y;
   const int nq = it.z & 0xff, part = (it.z >> 8) & 0xfff, nparts = it.z >> 20;
   const int pidx = it.w;
@@ -58,28 +62,16 @@ __global__ __launch_bounds__(256) void paged_attn_kernel(
   const int g = lane >> 4, col = lane & 15;
   const int hg = col % G, tq = col / G;
   const int ctx = ctx_len[s], ql = q_len[s], q0 = q_start[s];
-  const bool kvsplit = nq <= TPW;
-  if (!kvsplit && wid * TPW >= nq) return;  // idle wave in a short q-split tile (no barrier follows)
 
-  const int tokbase = kvsplit ? qb : qb + wid * TPW;
-  const int ncols_tok = kvsplit ? nq : min(TPW, nq - wid * TPW);
-  const bool colvalid = tq < ncols_tok;
-  const int tok = tokbase + tq;
+  const bool colvalid = tq < nq;
+  const int tok = qb + tq;
   const int key_limit = colvalid ? (ctx - ql + tok + 1) : 0;
   const int head = kvh * G + hg;
-
-  int kv_begin, kv_end;
-  if (kvsplit) {
-    const int causal_end = ctx - ql + qb + nq;
-    kv_begin = nparts > 1 ? part * ATT_PART : 0;
-    kv_end = nparts > 1 ? min(causal_end, kv_begin + ATT_PART) : causal_end;
-  } else {
-    kv_begin = 0;
-    kv_end = ctx - ql + tokbase + ncols_tok;
-  }
+  const int causal_end = ctx - ql + qb + nq;
+  const int kv_begin = nparts > 1 ? part * ATT_PART : 0;
+  const int kv_end = nparts > 1 ? min(causal_end, kv_begin + ATT_PART) : causal_end;
   const int t_first = kv_begin >> 5;
   const int t_last = (kv_end + 31) >> 5;
-  const int t_step = kvsplit ? 4 : 1;
 
   // Q^T fragments (B operand): column col, dims 32m + 8g + j.
   bf16x8 qf[4];
@@ -98,7 +90,6 @@ __global__ __launch_bounds__(256) void paged_attn_kernel(
 
   const int* bt = block_table + (size_t)s * max_blocks;
   const int nblk = (ctx + ATT_BLK - 1) / ATT_BLK;
-  // lane-constant parts of the K / V addresses
   const int kin = 8 * (col >> 2) + (col & 3);  // key within tile for chunk 0 (chunk 1: +4)
   const size_t kv_stride_blk = (size_t)KV * ATT_BLK * ATT_HD;  // elements per page (all heads)
 
@@ -107,20 +98,19 @@ __global__ __launch_bounds__(256) void paged_attn_kernel(
   for (int n = 0; n < 8; ++n) o[n] = f32x4{0.f, 0.f, 0.f, 0.f};
   float m_run = NEG_BIG, l_run = 0.f;
 
-  for (int t = t_first + (kvsplit ? wid : 0); t < t_last; t += t_step) {
+  for (int t = t_first + wid; t < t_last; t += 4) {
     const int b0 = min(2 * t, nblk - 1), b1 = min(2 * t + 1, nblk - 1);
     const int pb0 = bt[b0], pb1 = bt[b1];
-    // K fragments: key = 32t + kin + 4c  -> page (kin >= 16), slot (kin & 15) + 4c
     const int pk = (kin >= 16) ? pb1 : pb0;
-    const bf16* kbase =
-        k_cache + (size_t)pk * kv_stride_blk + ((size_t)kvh * ATT_BLK + (kin & 15)) * ATT_HD + 8 * g;
+    // dims 32m + 8g = chunk 4m + g; key (kin & 15) + 4c
+    const bf16* kbase = k_cache + (size_t)pk * kv_stride_blk +
+                        (((size_t)kvh * 16 + g) * ATT_BLK + (kin & 15)) * 8;
     bf16x8 kf[2][4];
 #pragma unroll
     for (int c = 0; c < 2; ++c)
 #pragma unroll
       for (int m = 0; m < 4; ++m)
-        kf[c][m] = *reinterpret_cast<const bf16x8*>(kbase + 4 * c * ATT_HD + 32 * m);
-    // V^T fragments: dim 16n + col, keys 8g..8g+7 -> page (g >> 1), slot 8*(g&1)
+        kf[c][m] = *reinterpret_cast<const bf16x8*>(kbase + (4 * m * ATT_BLK + 4 * c) * 8);
     const int pv = (g >> 1) ? pb1 : pb0;
     const bf16* vbase =
         v_cache + (size_t)pv * kv_stride_blk + ((size_t)kvh * ATT_HD + col) * ATT_BLK + 8 * (g & 1);
@@ -129,7 +119,6 @@ __global__ __launch_bounds__(256) void paged_attn_kernel(
     for (int n = 0; n < 8; ++n)
       vf[n] = *reinterpret_cast<const bf16x8*>(vbase + (size_t)16 * n * ATT_BLK);
 
-    // S^T for the two 16-key chunks
     f32x4 sc[2];
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
@@ -139,7 +128,6 @@ __global__ __launch_bounds__(256) void paged_attn_kernel(
         acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[c][m], qf[m], acc, 0, 0, 0);
       sc[c] = acc;
     }
-    // scale + causal/length mask; lane holds keys 32t + 8g + 4c + r
     float tmax = NEG_BIG;
     const int kb = 32 * t + 8 * g;
 #pragma unroll
@@ -174,28 +162,13 @@ __global__ __launch_bounds__(256) void paged_attn_kernel(
       o[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf[n], pf, o[n], 0, 0, 0);
     }
   }
-  // per-column denominator: sum the four lane groups' partial sums
   l_run += __shfl_xor(l_run, 16, 64);
   l_run += __shfl_xor(l_run, 32, 64);
 
-  if (!kvsplit) {
-    if (!colvalid) return;
-    const float inv = 1.f / l_run;
-    bf16* orow = out + ((size_t)(q0 + tok) * H + head) * ATT_HD + 4 * g;
-#pragma unroll
-    for (int n = 0; n < 8; ++n) {
-      bf16x4 w;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) w[r] = (bf16)(o[n][r] * inv);
-      *reinterpret_cast<bf16x4*>(orow + 16 * n) = w;
-    }
-    return;
-  }
-
-  // kv-split: merge the four waves through LDS
-  __shared__ float lds_o[4][16][ATT_HD + 4];
-  __shared__ float lds_m[4][16];
-  __shared__ float lds_l[4][16];
+  // merge the four waves through LDS
+  float(*lds_o)[16][ATT_HD + 4] = reinterpret_cast<float(*)[16][ATT_HD + 4]>(smem);
+  float(*lds_m)[16] = reinterpret_cast<float(*)[16]>(smem + 4 * 16 * (ATT_HD + 4) * sizeof(float));
+  float(*lds_l)[16] = lds_m + 4;
 #pragma unroll
   for (int n = 0; n < 8; ++n)
 #pragma unroll
@@ -226,14 +199,66 @@ __global__ __launch_bounds__(256) void paged_attn_kernel(
   }
   const int ctq = ccol / G, chg = ccol % G;
   if (nparts > 1) {
-    float* po = part_o + (((size_t)pidx * KV + kvh) * 16 + ccol) * ATT_HD + d0;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) po[j] = acc[j];
+    // Partition hand-off inside the launch (cdna_hip_programming.md §6 G16, sc1
+    // form): the slab is stored write-through (sc1) and (m, l) as one relaxed
+    // agent-scope 64-bit atomic, every wave drains, then one lane takes a ticket;
+    // the holder of ticket nparts-1 merges all partitions reading them with sc1
+    // loads — no release/acquire fences (no L2 writeback), no second launch.
+    const __amdgpu_buffer_rsrc_t ps = __builtin_amdgcn_make_buffer_rsrc(
+        part_o + ((size_t)pidx * KV + kvh) * 16 * ATT_HD, 0, 16 * ATT_HD * 4, 0x00020000);
+    const int soff = (ccol * ATT_HD + d0) * 4;
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, f32x4{acc[0], acc[1], acc[2], acc[3]}),
+                                           ps, soff, 0, 16);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, f32x4{acc[4], acc[5], acc[6], acc[7]}),
+                                           ps, soff + 16, 0, 16);
     if ((threadIdx.x & 15) == 0) {
-      float* pm = part_ml + (((size_t)pidx * KV + kvh) * 16 + ccol) * 2;
-      pm[0] = mt;
-      pm[1] = L;
+      const unsigned long long mlv =
+          ((unsigned long long)__float_as_uint(L) << 32) | (unsigned long long)__float_as_uint(mt);
+      __hip_atomic_store((gu64*)(part_ml + (((size_t)pidx * KV + kvh) * 16 + ccol) * 2), mlv,
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    int* lflag = reinterpret_cast<int*>(smem + ATT_LDS_DECODE_BYTES);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      gi32* c = (gi32*)(counters + (size_t)s * KV + kvh);
+      const int tk = __hip_atomic_fetch_add(c, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int last = tk == nparts - 1;
+      if (last) __hip_atomic_store(c, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
+      *lflag = last;
+    }
+    __syncthreads();
+    if (!*lflag || ctq >= nq) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // orders the loads below the ticket only
+    const int p0 = pidx - part;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        part_o + (size_t)p0 * KV * 16 * ATT_HD, 0, nparts * KV * 16 * ATT_HD * 4, 0x00020000);
+    auto load_ml = [&](int p) {
+      return __hip_atomic_load((gu64*)(part_ml + (((size_t)(p0 + p) * KV + kvh) * 16 + ccol) * 2),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    };
+    float gm = NEG_BIG;
+    for (int p = 0; p < nparts; ++p) gm = fmaxf(gm, __uint_as_float((unsigned)load_ml(p)));
+    float GL = 0.f, ga[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int p = 0; p < nparts; ++p) {
+      const unsigned long long v = load_ml(p);
+      const float pmv = __uint_as_float((unsigned)v), plv = __uint_as_float((unsigned)(v >> 32));
+      const float w = exp2f(pmv - gm);
+      GL += w * plv;
+      const int roff = (((p * KV + kvh) * 16 + ccol) * ATT_HD + d0) * 4;
+      const f32x4 a = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, roff, 0, 16));
+      const f32x4 b = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, roff + 16, 0, 16));
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        ga[j] += w * a[j];
+        ga[4 + j] += w * b[j];
+      }
+    }
+    const float ginv = 1.f / GL;
+    bf16x8 g8;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) g8[j] = (bf16)(ga[j] * ginv);
+    *reinterpret_cast<bf16x8*>(out + ((size_t)(q0 + qb + ctq) * H + kvh * G + chg) * ATT_HD + d0) = g8;
     return;
   }
   if (ctq >= nq) return;
@@ -244,67 +269,231 @@ __global__ __launch_bounds__(256) void paged_attn_kernel(
   *reinterpret_cast<bf16x8*>(out + ((size_t)(q0 + qb + ctq) * H + kvh * G + chg) * ATT_HD + d0) = w8;
 }
 
-// Combine decode partitions: ritem = (seq, first partial slot, nparts, q_begin | nq << 16)
+// ---------------------------------------------------------------------------
+// prefill path (nq > 16/G): 32x32x16 MFMA, an item is 32/G tokens = 32 columns
+// (G heads x 32/G tokens); like the decode path, the 4 waves of the workgroup
+// interleave the item's 32-key tiles (loaded straight into registers) and merge
+// through LDS, so a chunk of n tokens yields n*G/32 items per KV head with
+// short per-wave chains, and each K/V byte serves 32 columns.
+//
+//   S^T[32 keys x 32 cols] = K · Q^T    A = K rows, B = Q^T (registers)
+//   O^T[128 x 32 cols]    += V^T · P^T  A = V^T rows, B = P^T = the S^T registers
+//
+// 32x32 accumulator row rho of lane (r, h), register g: rho = (g&3) + 8(g>>2) + 4h.
+// Lane r loads K row pi(r) = r with bits 2 and 3 swapped, so registers 8s..8s+7
+// of a lane hold keys 16s + 8h + 0..7 — exactly the B fragment of the PV MFMA
+// for k-step s, whose V^T A fragment is one 16-B load (keys 8h..8h+7 of page s).
+__device__ __forceinline__ int swap23(int x) { return (x & ~12) | ((x & 4) << 1) | ((x & 8) >> 1); }
+constexpr int PF_LD = ATT_HD + 4;  // padded LDS row (floats) of the merge image
+
 template <int G>
-__global__ __launch_bounds__(256) void attn_reduce_kernel(
-    bf16* __restrict__ out, const float* __restrict__ part_o, const float* __restrict__ part_ml,
-    const int4* __restrict__ ritems, const int* __restrict__ n_ritems,
-    const int* __restrict__ q_start, int H, int KV) {
-  const int item = blockIdx.x;
-  if (item >= n_ritems[0]) return;
-  const int kvh = blockIdx.y;
-  const int4 it = ritems[item];
-  const int s = it.x, p0 = it.y, np = it.z, qb = it.w & 0xffff, nq = it.w >> 16;
-  const int ccol = threadIdx.x >> 4, d0 = (threadIdx.x & 15) * 8;
+__device__ __forceinline__ void prefill_item(
+    const int4 it, char* smem, bf16* __restrict__ out, const bf16* __restrict__ q,
+    const bf16* __restrict__ k_cache, const bf16* __restrict__ v_cache,
+    const int* __restrict__ q_start, const int* __restrict__ q_len, const int* __restrict__ ctx_len,
+    const int* __restrict__ block_table, int max_blocks, int H, int KV, int kvh, float scale_log2) {
+  const int s = it.x, qb = it.y, nq = it.z & 0xff;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  const int hg = r % G, tq = r / G;
+  const int ctx = ctx_len[s], ql = q_len[s], q0 = q_start[s];
+  const bool colvalid = tq < nq;
+  const int tok = qb + tq;
+  const int key_limit = colvalid ? (ctx - ql + tok + 1) : 0;
+  const int head = kvh * G + hg;
+  const int ntiles = (ctx - ql + qb + nq + 31) >> 5;
+
+  bf16x8 qf[8];
+  {
+    const bf16* qrow = q + ((size_t)(q0 + (colvalid ? tok : 0)) * H + head) * ATT_HD + 8 * h;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      bf16x8 v = *reinterpret_cast<const bf16x8*>(qrow + 16 * i);
+      if (!colvalid) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = (bf16)0.f;
+      }
+      qf[i] = v;
+    }
+  }
+  const int* bt = block_table + (size_t)s * max_blocks;
+  const int nblk = (ctx + ATT_BLK - 1) / ATT_BLK;
+  const size_t kv_stride_blk = (size_t)KV * ATT_BLK * ATT_HD;
+  const int krow = swap23(r);
+
+  f32x16 o[4];
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int j = 0; j < 16; ++j) o[m][j] = 0.f;
+  float m_run = NEG_BIG, l_run = 0.f;
+
+  for (int t = wid; t < ntiles; t += 4) {
+    const int pb0 = bt[min(2 * t, nblk - 1)], pb1 = bt[min(2 * t + 1, nblk - 1)];
+    // dims 16i + 8h = chunk 2i + h; key krow & 15 of page krow >> 4
+    const bf16* kbase = k_cache + (size_t)(krow >= 16 ? pb1 : pb0) * kv_stride_blk +
+                        (((size_t)kvh * 16 + h) * ATT_BLK + (krow & 15)) * 8;
+    bf16x8 kf[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) kf[i] = *reinterpret_cast<const bf16x8*>(kbase + (size_t)2 * i * ATT_BLK * 8);
+    bf16x8 vf[2][4];
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+      const bf16* vbase = v_cache + (size_t)(st ? pb1 : pb0) * kv_stride_blk +
+                          ((size_t)kvh * ATT_HD + r) * ATT_BLK + 8 * h;
+#pragma unroll
+      for (int m = 0; m < 4; ++m) vf[st][m] = *reinterpret_cast<const bf16x8*>(vbase + (size_t)32 * m * ATT_BLK);
+    }
+    // two independent accumulation chains over the head dimension
+    f32x16 sa, sb;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) { sa[j] = 0.f; sb[j] = 0.f; }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      sa = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[i], qf[i], sa, 0, 0, 0);
+      sb = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[4 + i], qf[4 + i], sb, 0, 0, 0);
+    }
+    float tmax = NEG_BIG;
+    float sc[16];
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {
+      const int key = 32 * t + 16 * (g >> 3) + 8 * h + (g & 7);
+      float v = (sa[g] + sb[g]) * scale_log2;
+      v = key < key_limit ? v : NEG_BIG;
+      sc[g] = v;
+      tmax = fmaxf(tmax, v);
+    }
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+    const float m_new = fmaxf(m_run, tmax);
+    const float alpha = exp2f(m_run - m_new);
+    m_run = m_new;
+    float psum = 0.f;
+    bf16x8 pf[2];
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {
+      const float p = exp2f(sc[g] - m_new);
+      psum += p;
+      pf[g >> 3][g & 7] = (bf16)p;
+    }
+    l_run = l_run * alpha + psum;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) o[m] *= alpha;
+#pragma unroll
+    for (int st = 0; st < 2; ++st)
+#pragma unroll
+      for (int m = 0; m < 4; ++m) o[m] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[st][m], pf[st], o[m], 0, 0, 0);
+  }
+  l_run += __shfl_xor(l_run, 32, 64);
+
+  // merge the four waves: O^T images [wave][col][dim] (fp32) + per-column (m, l)
+  float* lo = reinterpret_cast<float*>(smem);
+  float* lm = lo + 4 * 32 * PF_LD;
+  float* ll = lm + 4 * 32;
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int gq = 0; gq < 4; ++gq) {
+      f32x4 v = {o[m][4 * gq], o[m][4 * gq + 1], o[m][4 * gq + 2], o[m][4 * gq + 3]};
+      *reinterpret_cast<f32x4*>(lo + (wid * 32 + r) * PF_LD + 32 * m + 8 * gq + 4 * h) = v;
+    }
+  if (h == 0) {
+    lm[wid * 32 + r] = m_run;
+    ll[wid * 32 + r] = l_run;
+  }
+  __syncthreads();
+  const int ccol = threadIdx.x >> 3, d0 = (threadIdx.x & 7) * 16;
   const int ctq = ccol / G, chg = ccol % G;
   if (ctq >= nq) return;
   float mt = NEG_BIG;
-  for (int p = 0; p < np; ++p)
-    mt = fmaxf(mt, part_ml[(((size_t)(p0 + p) * KV + kvh) * 16 + ccol) * 2]);
-  float L = 0.f, acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  for (int p = 0; p < np; ++p) {
-    const size_t base = ((size_t)(p0 + p) * KV + kvh) * 16 + ccol;
-    const float w = exp2f(part_ml[base * 2] - mt);
-    L += w * part_ml[base * 2 + 1];
-    const f32x4* po = reinterpret_cast<const f32x4*>(part_o + base * ATT_HD + d0);
-    const f32x4 a = po[0], b = po[1];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      acc[j] += w * a[j];
-      acc[4 + j] += w * b[j];
-    }
+  for (int w = 0; w < 4; ++w) mt = fmaxf(mt, lm[w * 32 + ccol]);
+  float wgt[4], L = 0.f;
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    wgt[w] = exp2f(lm[w * 32 + ccol] - mt);
+    L += wgt[w] * ll[w * 32 + ccol];
   }
   const float inv = 1.f / L;
-  bf16x8 w8;
+  bf16* orow = out + ((size_t)(q0 + qb + ctq) * H + kvh * G + chg) * ATT_HD + d0;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) w8[j] = (bf16)(acc[j] * inv);
-  *reinterpret_cast<bf16x8*>(out + ((size_t)(q_start[s] + qb + ctq) * H + kvh * G + chg) * ATT_HD +
-                             d0) = w8;
+  for (int c8 = 0; c8 < 2; ++c8) {
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const f32x4* src = reinterpret_cast<const f32x4*>(lo + (w * 32 + ccol) * PF_LD + d0 + 8 * c8);
+      const f32x4 a = src[0], b = src[1];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        acc[j] += wgt[w] * a[j];
+        acc[4 + j] += wgt[w] * b[j];
+      }
+    }
+    bf16x8 w8;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) w8[j] = (bf16)(acc[j] * inv);
+    *reinterpret_cast<bf16x8*>(orow + 8 * c8) = w8;
+  }
+}
+
+constexpr int ATT_LDS_DECODE = ATT_LDS_DECODE_BYTES + 16;  // + last-arriver flag
+constexpr int ATT_LDS_PREFILL = (4 * 32 * PF_LD + 2 * 4 * 32) * 4;
+constexpr int ATT_LDS_BYTES = ATT_LDS_PREFILL > ATT_LDS_DECODE ? ATT_LDS_PREFILL : ATT_LDS_DECODE;
+
+// One launch serves a whole ragged step: items (seq, q_begin, nq | part<<8 |
+// nparts<<20, partial slot) are strided over the grid, so the shape-stable
+// (graph-captured) grid can be sized to the chip rather than to the worst case.
+template <int G>
+__global__ __launch_bounds__(256, 2) void paged_attn_kernel(
+    bf16* __restrict__ out, float* __restrict__ part_o, float* __restrict__ part_ml,
+    int* __restrict__ counters, const bf16* __restrict__ q, const bf16* __restrict__ k_cache,
+    const bf16* __restrict__ v_cache, const int4* __restrict__ items,
+    const int* __restrict__ n_items, const int* __restrict__ q_start,
+    const int* __restrict__ q_len, const int* __restrict__ ctx_len,
+    const int* __restrict__ block_table, int max_blocks, int H, int KV, float scale_log2) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int TPW = 16 / G;
+  const int n = n_items[0];
+  const int kvh = blockIdx.y;
+  for (int item = blockIdx.x; item < n; item += gridDim.x) {
+    const int4 it = items[item];
+    if ((it.z & 0xff) <= TPW)
+      decode_item<G>(it, smem, out, part_o, part_ml, counters, q, k_cache, v_cache, q_start, q_len, ctx_len,
+                     block_table, max_blocks, H, KV, kvh, scale_log2);
+    else
+      prefill_item<G>(it, smem, out, q, k_cache, v_cache, q_start, q_len, ctx_len, block_table,
+                      max_blocks, H, KV, kvh, scale_log2);
+    __syncthreads();  // LDS reuse by the next item
+  }
 }
 
 }  // namespace pa
 
 extern "C" int pa_paged_attention(void* out, float* part_o, float* part_ml, const void* q,
                                   const void* k_cache, const void* v_cache, const int* items,
-                                  const int* n_items, int max_items, const int* ritems,
-                                  const int* n_ritems, int max_ritems, const int* q_start,
+                                  const int* n_items, int max_items, int* counters, const int* q_start,
                                   const int* q_len, const int* ctx_len, const int* block_table,
                                   int max_blocks, int H, int KV, float scale_log2,
                                   hipStream_t st) {
   if (H % KV != 0) return -1;
   const int G = H / KV;
-  dim3 grid(max_items, KV), rgrid(max_ritems, KV);
+  // items are strided over the grid: ~8 resident workgroups per CU over all KV heads
+  const int gx = max_items < 1 ? 1 : (max_items < 2048 / KV ? max_items : (2048 / KV > 0 ? 2048 / KV : 1));
+  dim3 grid(gx, KV);
 #define PA_ATT(GG)                                                                          \
   do {                                                                                      \
+    static bool attr_##GG = false;                                                          \
+    if (!attr_##GG) {                                                                       \
+      (void)hipFuncSetAttribute((const void*)pa::paged_attn_kernel<GG>,                           \
+                          hipFuncAttributeMaxDynamicSharedMemorySize, pa::ATT_LDS_BYTES);   \
+      attr_##GG = true;                                                                     \
+    }                                                                                       \
     if (max_items > 0)                                                                      \
-      hipLaunchKernelGGL(pa::paged_attn_kernel<GG>, grid, dim3(256), 0, st, (pa::bf16*)out, \
-                         part_o, part_ml, (const pa::bf16*)q, (const pa::bf16*)k_cache,      \
-                         (const pa::bf16*)v_cache, (const int4*)items, n_items, q_start,     \
-                         q_len, ctx_len, block_table, max_blocks, H, KV, scale_log2);       \
-    if (max_ritems > 0)                                                                     \
-      hipLaunchKernelGGL(pa::attn_reduce_kernel<GG>, rgrid, dim3(256), 0, st,               \
-                         (pa::bf16*)out, part_o, part_ml, (const int4*)ritems, n_ritems,     \
-                         q_start, H, KV);                                                   \
+      hipLaunchKernelGGL(pa::paged_attn_kernel<GG>, grid, dim3(256), pa::ATT_LDS_BYTES, st, \
+                         (pa::bf16*)out,                                                    \
+                         part_o, part_ml, counters, (const pa::bf16*)q,                      \
+                         (const pa::bf16*)k_cache, (const pa::bf16*)v_cache,                \
+                         (const int4*)items, n_items, q_start, q_len, ctx_len, block_table, \
+                         max_blocks, H, KV, scale_log2);                                    \
   } while (0)
   switch (G) {
     case 1: PA_ATT(1); break;

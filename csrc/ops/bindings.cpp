@@ -16,7 +16,7 @@ int pa_rope_cache(void* q_out, void* k_cache, void* v_cache, const void* qkv, co
 int pa_silu_mul(void* out, const void* in, int T, int F, hipStream_t st);
 int pa_paged_attention(void* out, float* part_o, float* part_ml, const void* q, const void* k_cache,
                        const void* v_cache, const int* items, const int* n_items, int max_items,
-                       const int* ritems, const int* n_ritems, int max_ritems, const int* q_start,
+                       int* counters, const int* q_start,
                        const int* q_len, const int* ctx_len, const int* block_table,
                        int max_blocks, int H, int KV, float scale_log2, hipStream_t st);
 int pa_sample_workspace_floats(int rows, int V);
@@ -87,12 +87,12 @@ void rope_cache(at::Tensor q_out, at::Tensor k_cache, at::Tensor v_cache, at::Te
   const int T = qkv.size(0);
   TORCH_CHECK(qkv.size(1) >= (H + 2 * KV) * 128, "qkv too narrow");
   TORCH_CHECK(positions.numel() >= T && slot_mapping.numel() >= T, "positions/slots too short");
-  TORCH_CHECK(k_cache.dim() == 4 && k_cache.size(1) == KV && k_cache.size(3) == 128,
-              "k_cache must be [blocks, KV, block, 128]");
+  TORCH_CHECK(k_cache.dim() == 5 && k_cache.size(1) == KV && k_cache.size(2) == 16 && k_cache.size(4) == 8,
+              "k_cache must be [blocks, KV, 16, block, 8]");
   TORCH_CHECK(v_cache.dim() == 4 && v_cache.size(1) == KV && v_cache.size(2) == 128,
               "v_cache must be [blocks, KV, 128, block]");
   TORCH_CHECK(cos_sin.size(1) == 128, "cos_sin must be [max_pos, 128]");
-  const int block = k_cache.size(2);
+  const int block = k_cache.size(3);
   check_rc(pa_rope_cache(q_out.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(), qkv.data_ptr(),
                          positions.data_ptr<int>(), slot_mapping.data_ptr<int>(),
                          cos_sin.data_ptr<float>(), T, H, KV, qkv.stride(0), block,
@@ -111,35 +111,34 @@ void silu_mul(at::Tensor out, at::Tensor in) {
 
 void paged_attention(at::Tensor out, at::Tensor part_o, at::Tensor part_ml, at::Tensor q,
                      at::Tensor k_cache, at::Tensor v_cache, at::Tensor items, at::Tensor n_items,
-                     at::Tensor ritems, at::Tensor n_ritems, at::Tensor q_start, at::Tensor q_len,
+                     at::Tensor counters, at::Tensor q_start, at::Tensor q_len,
                      at::Tensor ctx_len, at::Tensor block_table, double scale) {
-  for (auto* t : {&out, &part_o, &part_ml, &q, &k_cache, &v_cache, &items, &n_items, &ritems,
-                  &n_ritems, &q_start, &q_len, &ctx_len, &block_table})
+  for (auto* t : {&out, &part_o, &part_ml, &q, &k_cache, &v_cache, &items, &n_items, &counters,
+                  &q_start, &q_len, &ctx_len, &block_table})
     check_gpu(*t, "paged_attention arg");
   check_dtype(q, at::kBFloat16, "q"); check_dtype(out, at::kBFloat16, "out");
   check_dtype(k_cache, at::kBFloat16, "k_cache"); check_dtype(v_cache, at::kBFloat16, "v_cache");
   check_dtype(part_o, at::kFloat, "part_o"); check_dtype(part_ml, at::kFloat, "part_ml");
-  for (auto* t : {&items, &n_items, &ritems, &n_ritems, &q_start, &q_len, &ctx_len, &block_table})
+  for (auto* t : {&items, &n_items, &counters, &q_start, &q_len, &ctx_len, &block_table})
     check_dtype(*t, at::kInt, "paged_attention int arg");
   TORCH_CHECK(q.dim() == 3 && q.size(2) == 128, "q must be [T, H, 128]");
-  TORCH_CHECK(k_cache.dim() == 4 && k_cache.size(2) == 16 && k_cache.size(3) == 128,
-              "k_cache must be [blocks, KV, 16, 128]");
+  TORCH_CHECK(k_cache.dim() == 5 && k_cache.size(2) == 16 && k_cache.size(3) == 16 && k_cache.size(4) == 8,
+              "k_cache must be [blocks, KV, 16, 16, 8]");
   TORCH_CHECK(v_cache.dim() == 4 && v_cache.size(2) == 128 && v_cache.size(3) == 16,
               "v_cache must be [blocks, KV, 128, 16]");
   const int H = q.size(1), KV = k_cache.size(1);
   TORCH_CHECK(items.dim() == 2 && items.size(1) == 4, "items must be [max_items, 4]");
-  TORCH_CHECK(ritems.dim() == 2 && ritems.size(1) == 4, "ritems must be [max_ritems, 4]");
   TORCH_CHECK(block_table.dim() == 2, "block_table must be [seqs, max_blocks]");
-  const int max_items = items.size(0), max_ritems = ritems.size(0);
-  TORCH_CHECK(part_o.numel() >= (int64_t)max_items * KV * 16 * 128 || max_ritems == 0,
-              "part_o workspace too small");
-  TORCH_CHECK(part_ml.numel() >= (int64_t)max_items * KV * 16 * 2 || max_ritems == 0,
-              "part_ml workspace too small");
+  const int max_items = items.size(0);
+  TORCH_CHECK(part_o.numel() >= (int64_t)max_items * KV * 16 * 128, "part_o workspace too small");
+  TORCH_CHECK(part_ml.numel() >= (int64_t)max_items * KV * 16 * 2, "part_ml workspace too small");
+  TORCH_CHECK(counters.numel() >= block_table.size(0) * KV,
+              "counters must hold one zero-initialised int per (sequence, KV head)");
   const float scale_log2 = (float)(scale * 1.4426950408889634);
   check_rc(pa_paged_attention(out.data_ptr(), part_o.data_ptr<float>(), part_ml.data_ptr<float>(),
                               q.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(),
                               items.data_ptr<int>(), n_items.data_ptr<int>(), max_items,
-                              ritems.data_ptr<int>(), n_ritems.data_ptr<int>(), max_ritems,
+                              counters.data_ptr<int>(),
                               q_start.data_ptr<int>(), q_len.data_ptr<int>(),
                               ctx_len.data_ptr<int>(), block_table.data_ptr<int>(),
                               block_table.size(1), H, KV, scale_log2, cur_stream()),

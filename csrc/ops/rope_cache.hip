@@ -2,11 +2,12 @@
 //
 // Input is the fused QKV GEMM output [T, (H + 2*KV) * 128]. For every token:
 //   q  -> rotate-half RoPE -> q_out[T, H, 128]
-//   k  -> rotate-half RoPE -> k_cache[block][kv][slot][128]      (row-major keys)
+//   k  -> rotate-half RoPE -> k_cache[block][kv][128/8][slot][8]  (fragment-major keys)
 //   v  ->                     v_cache[block][kv][128][slot]      (transposed values)
-// The V^T page layout is what lets the attention kernel feed V straight from
-// HBM into the A operand of v_mfma_f32_16x16x32_bf16 (8 consecutive keys of one
-// head-dim = one 16-byte load), see attention.hip.
+// Both page layouts are chosen for the attention kernel's MFMA operand loads
+// (attention.hip): a K A-fragment (8 dims of 16 keys) and a V^T A-fragment
+// (8 keys of 16 dims) are each ONE contiguous 256-B run of a page, so every
+// fragment load instruction reads whole 128-B lines.
 // cos/sin come from a host-precomputed fp32 table [max_pos, 128] (cos | sin),
 // so no transcendental work runs on the GPU (guide App. B, element-wise/RoPE).
 #include "common.h"
@@ -57,9 +58,9 @@ __global__ __launch_bounds__(256) void rope_cache_kernel(
         *reinterpret_cast<bf16x4*>(dst + i + 64) = o2;
       } else if (slot >= 0) {
         const int blk = slot / BLK, off = slot % BLK;
-        bf16* dst = k_cache + (((size_t)blk * KV + hh) * BLK + off) * HD;
-        *reinterpret_cast<bf16x4*>(dst + i) = o1;
-        *reinterpret_cast<bf16x4*>(dst + i + 64) = o2;
+        bf16* page = k_cache + ((size_t)blk * KV + hh) * HD * BLK;  // [16 chunks][BLK][8]
+        *reinterpret_cast<bf16x4*>(page + ((size_t)(i >> 3) * BLK + off) * 8 + (i & 7)) = o1;
+        *reinterpret_cast<bf16x4*>(page + ((size_t)((i + 64) >> 3) * BLK + off) * 8 + (i & 7)) = o2;
       }
     } else if (slot >= 0) {
       const int uu = u - nq - nk;

@@ -103,13 +103,13 @@ PYBIND11_MODULE(_runtime, m) {
         const StepLayout& L = s.layout();
         py::dict d;
         d["max_tokens"] = L.max_tokens; d["max_seqs"] = L.max_seqs; d["max_blocks"] = L.max_blocks;
-        d["max_items"] = L.max_items; d["max_ritems"] = L.max_ritems;
+        d["max_items"] = L.max_items;
         d["input_ids"] = L.input_ids; d["positions"] = L.positions; d["slots"] = L.slots;
         d["q_start"] = L.q_start; d["q_len"] = L.q_len; d["ctx_len"] = L.ctx_len;
         d["logit_rows"] = L.logit_rows; d["mask_class"] = L.mask_class; d["forced"] = L.forced;
         d["offsets"] = L.offsets; d["temperature"] = L.temperature; d["seeds"] = L.seeds;
-        d["items"] = L.items; d["n_items"] = L.n_items; d["ritems"] = L.ritems;
-        d["n_ritems"] = L.n_ritems; d["counts"] = L.counts; d["block_table"] = L.block_table;
+        d["items"] = L.items; d["n_items"] = L.n_items;
+        d["counts"] = L.counts; d["block_table"] = L.block_table;
         d["total"] = L.total;
         return d;
       })

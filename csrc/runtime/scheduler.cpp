@@ -21,8 +21,7 @@ Scheduler::Scheduler(const SchedulerConfig& cfg)
   L.max_blocks = (cfg.max_model_len + cfg.block_size - 1) / cfg.block_size;
   const int32_t tpw = 16 / std::max(1, cfg.gqa_group);
   const int32_t max_parts = (cfg.max_model_len + 511) / 512;
-  L.max_items = L.max_tokens / (4 * tpw) + L.max_seqs * (max_parts + 1) + 4;
-  L.max_ritems = L.max_seqs + 4;
+  L.max_items = L.max_tokens / (2 * tpw) + L.max_seqs * (max_parts + 1) + 4;
   int32_t o = 0;
   auto take = [&](int32_t n) {
     const int32_t at = o;
@@ -31,7 +30,6 @@ Scheduler::Scheduler(const SchedulerConfig& cfg)
   };
   L.counts = take(8);
   L.n_items = take(1);
-  L.n_ritems = take(1);
   L.input_ids = take(L.max_tokens);
   L.positions = take(L.max_tokens);
   L.slots = take(L.max_tokens);
@@ -45,7 +43,6 @@ Scheduler::Scheduler(const SchedulerConfig& cfg)
   L.temperature = take(L.max_seqs);
   L.seeds = take(2 * L.max_seqs);
   L.items = take(4 * L.max_items);
-  L.ritems = take(4 * L.max_ritems);
   L.block_table = take(L.max_seqs * L.max_blocks);
   L.total = o;
 }
@@ -210,11 +207,21 @@ int32_t Scheduler::schedule(int32_t* buf) {
   float* temp = reinterpret_cast<float*>(buf + L.temperature);
   int64_t* seeds = reinterpret_cast<int64_t*>(buf + L.seeds);
   int32_t* items = buf + L.items;
-  int32_t* ritems = buf + L.ritems;
   int32_t* bt = buf + L.block_table;
   const int32_t tpw = 16 / std::max(1, cfg_.gqa_group);
 
-  int32_t T = 0, ns = 0, nsamp = 0, nit = 0, nrit = 0, pslot = 0;
+  int32_t T = 0, ns = 0, nsamp = 0, nit = 0, nparted = 0, pslot = 0;
+  // prefill (q-split) tiles go first in the item list, heaviest (last) tile of a
+  // chunk first, so the long-running workgroups start before the decode items
+  const int32_t qtile = 32 / std::max(1, cfg_.gqa_group);
+  for (size_t si = 0; si < last_plan_.size(); ++si) {
+    const int32_t n = last_plan_[si].n;
+    if (n <= tpw) continue;
+    for (int32_t qb = ((n - 1) / qtile) * qtile; qb >= 0; qb -= qtile) {
+      int32_t* it = items + 4 * nit++;
+      it[0] = (int32_t)si; it[1] = qb; it[2] = std::min(qtile, n - qb) | (1 << 20); it[3] = 0;
+    }
+  }
   for (const Planned& p : last_plan_) {
     Sequence* s = p.s;
     const int32_t n = p.n, c0 = s->num_computed, ctx = c0 + n;
@@ -248,18 +255,11 @@ int32_t Scheduler::schedule(int32_t* buf) {
           int32_t* it = items + 4 * nit++;
           it[0] = ns; it[1] = 0; it[2] = n | (q << 8) | (nparts << 20); it[3] = pslot + q;
         }
-        int32_t* r = ritems + 4 * nrit++;
-        r[0] = ns; r[1] = pslot; r[2] = nparts; r[3] = 0 | (n << 16);
+        ++nparted;  // merged in-kernel by the last partition (attention.hip)
         pslot += nparts;
       } else {
         int32_t* it = items + 4 * nit++;
         it[0] = ns; it[1] = 0; it[2] = n | (1 << 20); it[3] = 0;
-      }
-    } else {
-      const int32_t tile = 4 * tpw;
-      for (int32_t qb = 0; qb < n; qb += tile) {
-        int32_t* it = items + 4 * nit++;
-        it[0] = ns; it[1] = qb; it[2] = std::min(tile, n - qb) | (1 << 20); it[3] = 0;
       }
     }
     s->num_computed = ctx;
@@ -289,10 +289,9 @@ int32_t Scheduler::schedule(int32_t* buf) {
   counts[1] = ns;
   counts[2] = nsamp;
   counts[3] = nit;
-  counts[4] = nrit;
+  counts[4] = nparted;
   counts[5] = pslot;
   buf[L.n_items] = nit;
-  buf[L.n_ritems] = nrit;
   if (T > 0) ++stat_steps_;
   return T;
 }

@@ -38,9 +38,9 @@ struct SchedulerConfig {
 };
 
 struct StepLayout {
-  int32_t max_tokens, max_seqs, max_blocks, max_items, max_ritems;
+  int32_t max_tokens, max_seqs, max_blocks, max_items;
   int32_t input_ids, positions, slots, q_start, q_len, ctx_len, logit_rows, mask_class, forced,
-      offsets, temperature, seeds, items, n_items, ritems, n_ritems, counts, block_table, total;
+      offsets, temperature, seeds, items, n_items, counts, block_table, total;
 };
 
 enum FinishReason : int32_t { NOT_FINISHED = -1, FINISH_STOP = 0, FINISH_LENGTH = 1, FINISH_ABORT = 2 };

@@ -378,11 +378,26 @@ class BaseAgent:
             raise ValueError("Task deadline has passed")
 
     # ------------------------------------------------------------------ LLM calls
+    def _compose_messages(self, system: str, prompt: str) -> List[Dict[str, str]]:
+        """Chat messages for one agent call.
+
+        Against the on-node engine (LLMs with `prefix_cache_layout`), the task
+        text goes FIRST and the agent's identity block after it: every call of a
+        task — the orchestrator's and every agent's — then starts with the same
+        "Task: ..." tokens, so its KV blocks are prefilled once per task and
+        reused by the prefix cache (the reference sends system-then-user to a
+        remote API, pilott/core/agent.py; same content, different order)."""
+        if getattr(self.llm, "prefix_cache_layout", False) and prompt.startswith("Task:"):
+            head, sep, tail = prompt.partition("\n\n")
+            if sep:
+                return [{"role": "user", "content": f"{head}\n\n{system.rstrip()}\n\n{tail}"}]
+        return [{"role": "system", "content": system}, {"role": "user", "content": prompt}]
+
     async def _llm_json(self, kind: str, fixed: Optional[Dict[str, Any]] = None, **kw) -> Dict[str, Any]:
         prompt = self.prompts.format_prompt(kind, **kw)
         system = self.prompts.format_prompt("system_base", role=self.config.role, goal=self.config.goal,
                                             backstory=self.config.backstory or "No specific backstory.")
-        messages = [{"role": "system", "content": system}, {"role": "user", "content": prompt}]
+        messages = self._compose_messages(system, prompt)
         rf = {"schema": f"agent.{kind}", "fixed": fixed or {}}
         try:
             resp = await self.llm.generate_response(messages, response_format=rf)

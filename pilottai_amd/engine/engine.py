@@ -47,8 +47,11 @@ from .tokenizer import Tokenizer, get_tokenizer
 
 log = logging.getLogger("pilottai_amd.engine")
 
-DEFAULT_BUCKETS = [8, 16, 32, 48, 64, 80, 96, 112, 128, 160, 192, 224, 256, 320, 384, 448, 512,
-                   640, 768, 1024, 1280, 1536, 2048, 3072, 4096, 6144, 8192]
+# hipGraph token buckets: a step of T tokens replays the smallest bucket >= T, so
+# the spacing bounds the padded (wasted) work: 32-token steps up to 512, 64 up to
+# 2048 (prefill-heavy agent steps sit at 400-1000 tokens).
+DEFAULT_BUCKETS = ([8, 16, 32, 48, 64] + list(range(96, 513, 32)) + list(range(576, 2049, 64))
+                   + [3072, 4096, 6144, 8192])
 
 
 @dataclass
@@ -179,6 +182,7 @@ class LLMEngine:
         self._host_np = self._host_meta.numpy()
         self._dev_meta = torch.zeros(L["total"], dtype=torch.int32, device=self.device) if self.on_gpu \
             else self._host_meta
+        self._att_counters = torch.zeros(L["max_seqs"] * kv_local, dtype=torch.int32, device=self.device)
         self._init_views()
         V = mc.vocab_size
         self._mask_words = (V + 31) // 32
@@ -239,8 +243,7 @@ class LLMEngine:
             block_table=sl("block_table", ms * mb).view(ms, mb),
             items=sl("items", 4 * L["max_items"]).view(L["max_items"], 4),
             n_items=sl("n_items", 1),
-            ritems=sl("ritems", 4 * L["max_ritems"]).view(L["max_ritems"], 4),
-            n_ritems=sl("n_ritems", 1),
+            att_counters=self._att_counters,
             logit_rows=sl("logit_rows", ms))
         self._temp = sl("temperature", ms).view(torch.float32)
         self._mask_cls = sl("mask_class", ms)
@@ -258,14 +261,13 @@ class LLMEngine:
         return True
 
     def _items_for_bucket(self, bucket: int, s_b: int) -> int:
-        return min(self.L["max_items"], bucket // (4 * self._tpw) + s_b * (self._max_parts + 1) + 4)
+        return min(self.L["max_items"], bucket // (2 * self._tpw) + s_b * (self._max_parts + 1) + 4)
 
     def _meta_for(self, bucket: int, s_b: int, ns: int) -> StepMeta:
         m = self.meta
         n_it = self._items_for_bucket(bucket, s_b)
         return StepMeta(m.input_ids, m.positions, m.slots, m.q_start, m.q_len, m.ctx_len,
-                        m.block_table, m.items[:n_it], m.n_items, m.ritems[:min(s_b + 4, m.ritems.shape[0])],
-                        m.n_ritems, m.logit_rows, num_seqs=ns)
+                        m.block_table, m.items[:n_it], m.n_items, m.att_counters, m.logit_rows, num_seqs=ns)
 
     def _forward_and_sample(self, bucket: int, s_b: int, ns: int):
         meta = self._meta_for(bucket, s_b, ns)

@@ -161,6 +161,7 @@ class LocalLLM(BaseLLM):
     """Reference LLMHandler contract backed by the local MI355X engine."""
 
     provider = "local"
+    prefix_cache_layout = True  # agents put the shared task text first (core/agent.py)
 
     def __init__(self, config: Any = None, engine=None):
         super().__init__(config)

@@ -95,20 +95,20 @@ class StepMeta:
     block_table: torch.Tensor
     items: torch.Tensor
     n_items: torch.Tensor
-    ritems: torch.Tensor
-    n_ritems: torch.Tensor
+    att_counters: torch.Tensor  # persistent zeroed workspace (partition tickets), not step data
     logit_rows: torch.Tensor
     num_seqs: int = 0  # host-side count, used only by the CPU reference path
 
 
 class KVCache:
-    """Per-layer paged pools: K [NB, KV, 16, 128], V^T [NB, KV, 128, 16] (bf16)."""
+    """Per-layer paged pools (bf16): K [NB, KV, 128/8, 16, 8] fragment-major,
+    V^T [NB, KV, 128, 16] (layouts: csrc/ops/rope_cache.hip)."""
 
     def __init__(self, num_layers: int, num_blocks: int, kv_heads: int, device, dtype=torch.bfloat16,
                  block_size: int = 16):
         self.num_blocks = num_blocks
         self.block_size = block_size
-        self.k = torch.zeros(num_layers, num_blocks, kv_heads, block_size, 128, dtype=dtype, device=device)
+        self.k = torch.zeros(num_layers, num_blocks, kv_heads, 16, block_size, 8, dtype=dtype, device=device)
         self.v = torch.zeros(num_layers, num_blocks, kv_heads, 128, block_size, dtype=dtype, device=device)
 
     @staticmethod
@@ -269,7 +269,7 @@ class LlamaModel:
             ops.rope_cache(q, kv.k[li], kv.v[li], qkv, meta.positions, meta.slots, self.cos_sin, H, KVh)
             attn = torch.empty(T, H, hd, dtype=self.dtype, device=self.device)
             ops.paged_attention(attn, part_o, part_ml, q, kv.k[li], kv.v[li], meta.items, meta.n_items,
-                                meta.ritems, meta.n_ritems, meta.q_start, meta.q_len, meta.ctx_len,
+                                meta.att_counters, meta.q_start, meta.q_len, meta.ctx_len,
                                 meta.block_table, self.scale, num_seqs=meta.num_seqs)
             o = ops.linear(attn.view(T, H * hd), L["wo"], "o")
             if self.tp.size > 1:

@@ -12,16 +12,20 @@ ATT_PART = 512  # keys per decode partition (must match csrc/ops/attention.hip)
 
 
 def build_attention_items(q_lens: Sequence[int], ctx_lens: Sequence[int], group: int,
-                          split: bool = True) -> Tuple[List[Tuple[int, int, int, int]],
-                                                       List[Tuple[int, int, int, int]], int]:
-    """Return (items, reduce_items, n_partial_slots).
+                          split: bool = True) -> Tuple[List[Tuple[int, int, int, int]], int]:
+    """Return (items, n_partial_slots).
 
-    item        = (seq, q_begin, nq | part << 8 | nparts << 20, partial_slot)
-    reduce_item = (seq, first_partial_slot, nparts, q_begin | nq << 16)
+    item = (seq, q_begin, nq | part << 8 | nparts << 20, partial_slot); the
+    partitions of a split decode row are merged in-kernel by the last to finish.
     """
-    tpw = 16 // group  # query tokens per wave
+    tpw = 16 // group  # query tokens per wave (kv-split path)
+    qtile = 32 // group  # tokens per prefill item (32 MFMA columns)
     items: List[Tuple[int, int, int, int]] = []
-    ritems: List[Tuple[int, int, int, int]] = []
+    # prefill tiles first, heaviest tile of each chunk first (as the scheduler)
+    for s, (ql, ctx) in enumerate(zip(q_lens, ctx_lens)):
+        if ql > tpw:
+            for qb in range(((ql - 1) // qtile) * qtile, -1, -qtile):
+                items.append((s, qb, min(qtile, ql - qb) | (1 << 20), 0))
     slot = 0
     for s, (ql, ctx) in enumerate(zip(q_lens, ctx_lens)):
         if ql <= 0:
@@ -32,13 +36,7 @@ def build_attention_items(q_lens: Sequence[int], ctx_lens: Sequence[int], group:
             if nparts > 1:
                 for p in range(nparts):
                     items.append((s, 0, ql | (p << 8) | (nparts << 20), slot + p))
-                ritems.append((s, slot, nparts, 0 | (ql << 16)))
                 slot += nparts
             else:
                 items.append((s, 0, ql | (1 << 20), 0))
-        else:
-            tile = 4 * tpw
-            for qb in range(0, ql, tile):
-                nq = min(tile, ql - qb)
-                items.append((s, qb, nq | (1 << 20), 0))
-    return items, ritems, slot
+    return items, slot

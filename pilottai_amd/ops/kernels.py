@@ -107,14 +107,15 @@ def rope_cache(q_out, k_cache, v_cache, qkv, positions, slot_mapping, cos_sin, H
     return q_out
 
 
-def paged_attention(out, part_o, part_ml, q, k_cache, v_cache, items, n_items, ritems, n_ritems,
+def paged_attention(out, part_o, part_ml, q, k_cache, v_cache, items, n_items, counters,
                     q_start, q_len, ctx_len, block_table, scale: float, num_seqs: Optional[int] = None):
-    """Attention over the paged cache. On GPU `items`/`ritems` must be device int32
-    [max, 4] tensors with device counts (graph-capturable); on CPU the reference
-    path ignores the item lists."""
+    """Attention over the paged cache. On GPU `items` must be a device int32
+    [max, 4] tensor with a device count (graph-capturable) and `counters` a
+    zero-initialised int32 tensor of >= seqs * KV entries (partition tickets; the
+    kernel leaves it zeroed); on CPU the reference path ignores both."""
     if _on_gpu(q):
         require_native().paged_attention(out, part_o, part_ml, q, k_cache, v_cache, items, n_items,
-                                         ritems, n_ritems, q_start, q_len, ctx_len, block_table,
+                                         counters, q_start, q_len, ctx_len, block_table,
                                          float(scale))
         return out
     ns = len(q_len) if num_seqs is None else num_seqs

@@ -90,13 +90,13 @@ def rope_cache(q_out, k_cache, v_cache, qkv, positions, slot_mapping, cos_sin, H
         q = apply_rope(q, positions[:T], cos_sin)
         k = apply_rope(k, positions[:T], cos_sin)
     q_out[:T].copy_(q.reshape(q_out[:T].shape))
-    blk = k_cache.shape[2]
+    blk = k_cache.shape[3]  # K page: [KV, 128/8, block, 8] (fragment-major)
     for t in range(T):
         slot = int(slot_mapping[t])
         if slot < 0:
             continue
         b, o = divmod(slot, blk)
-        k_cache[b, :, o, :] = k[t]
+        k_cache[b, :, :, o, :] = k[t].reshape(KV, hd // 8, 8)
         v_cache[b, :, :, o] = v[t]
 
 
@@ -105,7 +105,7 @@ def paged_attention(q, k_cache, v_cache, q_start, q_len, ctx_len, block_table, s
     T, H, hd = q.shape
     KV = k_cache.shape[1]
     G = H // KV
-    blk = k_cache.shape[2]
+    blk = k_cache.shape[3]
     out = torch.zeros_like(q)
     for s in range(len(q_len)):
         ql, ctx, q0 = int(q_len[s]), int(ctx_len[s]), int(q_start[s])
@@ -113,7 +113,7 @@ def paged_attention(q, k_cache, v_cache, q_start, q_len, ctx_len, block_table, s
             continue
         nb = (ctx + blk - 1) // blk
         blocks = block_table[s, :nb].long()
-        K = k_cache[blocks].permute(1, 0, 2, 3).reshape(KV, nb * blk, hd)[:, :ctx].float()
+        K = k_cache[blocks].permute(1, 0, 3, 2, 4).reshape(KV, nb * blk, hd)[:, :ctx].float()
         V = v_cache[blocks].permute(1, 0, 3, 2).reshape(KV, nb * blk, hd)[:, :ctx].float()
         Kh = K.repeat_interleave(G, dim=0)  # [H, ctx, hd]
         Vh = V.repeat_interleave(G, dim=0)

@@ -45,7 +45,7 @@ def test_silu_mul(gpu):
 
 
 def _make_cache(nblocks, KV, dev, blk=16):
-    k = _bf(nblocks, KV, blk, 128, dev=dev)
+    k = _bf(nblocks, KV, 16, blk, 8, dev=dev)
     v = _bf(nblocks, KV, 128, blk, dev=dev)
     return k, v
 
@@ -87,20 +87,20 @@ def _run_attention(gpu, H, KV, q_lens, ctx_lens, seed=0, split=True):
     q_start = np.concatenate([[0], np.cumsum(q_lens)[:-1]]).astype(np.int32)
     T = int(sum(q_lens))
     q = _bf(T, H, 128, dev=gpu)
-    items, ritems, nslots = ops.build_attention_items(q_lens, ctx_lens, G, split=split)
+    items, nslots = ops.build_attention_items(q_lens, ctx_lens, G, split=split)
     it = torch.tensor(items + [(0, 0, 0, 0)], dtype=torch.int32, device=gpu)
-    rit = torch.tensor(ritems + [(0, 0, 0, 0)], dtype=torch.int32, device=gpu)
+    cnt = torch.zeros(ns * KV, dtype=torch.int32, device=gpu)
     n_it = torch.tensor([len(items)], dtype=torch.int32, device=gpu)
-    n_rit = torch.tensor([len(ritems)], dtype=torch.int32, device=gpu)
     maxit = it.shape[0]
     part_o = torch.empty(maxit * KV * 16 * 128, dtype=torch.float32, device=gpu)
     part_ml = torch.empty(maxit * KV * 16 * 2, dtype=torch.float32, device=gpu)
     out = torch.zeros(T, H, 128, dtype=torch.bfloat16, device=gpu)
     scale = 1.0 / math.sqrt(128)
     dev_i = lambda a: torch.tensor(a, dtype=torch.int32, device=gpu)  # noqa: E731
-    ops.paged_attention(out, part_o, part_ml, q, kc, vc, it, n_it, rit, n_rit, dev_i(q_start),
+    ops.paged_attention(out, part_o, part_ml, q, kc, vc, it, n_it, cnt, dev_i(q_start),
                         dev_i(q_lens), dev_i(ctx_lens), bt.to(gpu), scale)
     torch.cuda.synchronize()
+    assert int(cnt.abs().sum()) == 0, "partition tickets must be left zeroed"
     r = ref.paged_attention(q.cpu(), kc.cpu(), vc.cpu(), q_start, q_lens, ctx_lens, bt, scale)
     return out.cpu().float(), r.float()
 
@@ -117,6 +117,16 @@ def test_attention_prefill_and_mixed(gpu, H, KV):
     q_lens = [37, 1, 100, 3, 16, 5, 250]
     ctx = [37, 700, 164, 40, 16, 1029, 260]
     o, r = _run_attention(gpu, H, KV, q_lens, ctx, seed=5)
+    torch.testing.assert_close(o, r, atol=2e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("H,KV", [(16, 16), (16, 8), (64, 8), (32, 8)])
+def test_attention_prefill_tiles(gpu, H, KV):
+    """q-split path: chunks spanning several 4 x 32/G-token tiles, cached prefixes,
+    partial last tiles, plus decode rows in the same launch."""
+    q_lens = [300, 129, 33, 1, 2, 77]
+    ctx = [300, 1129, 65, 900, 18, 77 + 512]
+    o, r = _run_attention(gpu, H, KV, q_lens, ctx, seed=11)
     torch.testing.assert_close(o, r, atol=2e-2, rtol=2e-2)
 
 

@@ -85,7 +85,7 @@ def test_scheduler_prefix_cache_preemption_and_layout():
     assert list(buf[L["positions"]:L["positions"] + 3]) == [0, 1, 2]
     assert buf[L["logit_rows"]] == 49
     items = buf[L["items"]:L["items"] + 4 * c[3]].reshape(-1, 4)
-    ref_items, _, _ = build_attention_items([50], [50], 4)
+    ref_items, _ = build_attention_items([50], [50], 4)
     assert [tuple(x) for x in items] == ref_items
     for _ in range(3):
         outs = s.commit(np.array([5], np.int32).ctypes.data, 1)

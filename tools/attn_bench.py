@@ -1,0 +1,101 @@
+#!/usr/bin/env python3
+"""Paged-attention microbenchmark (Llama-3-8B heads: H=32, KV=8, head_dim 128).
+
+Cases mirror the agent-serving steps seen in bench.py profiles:
+  decode64   64 decode tokens, ctx 512            (pure KV streaming)
+  prefill    2 prompts x 320 new tokens, ctx 480  (prefix-cached task text)
+  mix        decode64 + prefill in one launch     (a typical bench step)
+Each case is timed with the exact item count and with the grid padded to what
+the engine's hipGraph bucket reserves (`--pad`), to expose empty-workgroup cost.
+
+    python tools/attn_bench.py [--iters 50]
+"""
+import argparse
+import json
+import math
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from pilottai_amd import ops  # noqa: E402
+
+
+def setup(q_lens, ctx_lens, H=32, KV=8, pad_items=0, dev="cuda"):
+    G = H // KV
+    blk = 16
+    ns = len(q_lens)
+    nbs = [(c + blk - 1) // blk for c in ctx_lens]
+    total = sum(nbs) + 4
+    mb = max(nbs)
+    kc = (torch.randn(total, KV, 16, blk, 8, device=dev) * 0.5).to(torch.bfloat16)
+    vc = (torch.randn(total, KV, 128, blk, device=dev) * 0.5).to(torch.bfloat16)
+    perm = torch.randperm(total).tolist()
+    bt = torch.zeros(ns, mb, dtype=torch.int32)
+    c = 0
+    for s, nb in enumerate(nbs):
+        bt[s, :nb] = torch.tensor(perm[c:c + nb], dtype=torch.int32)
+        c += nb
+    q_start = np.concatenate([[0], np.cumsum(q_lens)[:-1]]).astype(np.int32)
+    T = int(sum(q_lens))
+    q = (torch.randn(T, H, 128, device=dev) * 0.5).to(torch.bfloat16)
+    items, _ = ops.build_attention_items(q_lens, ctx_lens, G)
+    n_items = len(items)
+    items = items + [(0, 0, 0, 0)] * max(1, pad_items - len(items))
+    it = torch.tensor(items, dtype=torch.int32, device=dev)
+    cnt = torch.zeros(ns * KV, dtype=torch.int32, device=dev)
+    di = lambda a: torch.tensor(a, dtype=torch.int32, device=dev)  # noqa: E731
+    n_it = di([n_items])
+    part_o = torch.empty(it.shape[0] * KV * 16 * 128, dtype=torch.float32, device=dev)
+    part_ml = torch.empty(it.shape[0] * KV * 16 * 2, dtype=torch.float32, device=dev)
+    out = torch.zeros(T, H, 128, dtype=torch.bfloat16, device=dev)
+    args = (out, part_o, part_ml, q, kc, vc, it, n_it, cnt, di(q_start), di(q_lens), di(ctx_lens),
+            bt.to(dev), 1.0 / math.sqrt(128))
+    kv_bytes = sum(ctx_lens) * KV * 128 * 2 * 2
+    flops = sum(4 * ql * (c - ql + (ql + 1) / 2) * H * 128 for ql, c in zip(q_lens, ctx_lens))
+    return args, kv_bytes, flops, n_items
+
+
+def timeit(args, iters):
+    for _ in range(3):
+        ops.paged_attention(*args)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        ops.paged_attention(*args)
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) * 1000 / iters
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--iters", type=int, default=50)
+    ap.add_argument("--pad", type=int, default=2228, help="items reserved by the 768-token bucket")
+    ap.add_argument("--scan", action="store_true", help="prefill length scan instead of the step cases")
+    a = ap.parse_args()
+    torch.manual_seed(0)
+    cases = {
+        "decode64": ([1] * 64, [512] * 64),
+        "decode64_long": ([1] * 64, [2048] * 64),
+        "prefill": ([320, 320], [480, 480]),
+        "prefill_cold": ([480], [480]),
+        "mix": ([1] * 64 + [320, 320], [512] * 64 + [480, 480]),
+    }
+    if a.scan:
+        cases = {f"pf{n}": ([n], [n]) for n in (8, 32, 128, 256, 512, 1024, 2048, 4096)}
+        cases.update({f"pf8x{n}": ([n] * 8, [n] * 8) for n in (128, 512)})
+    for name, (ql, cl) in cases.items():
+        for pad in ((0,) if a.scan else (0, a.pad)):
+            args, kvb, fl, n = setup(ql, cl, pad_items=pad)
+            us = timeit(args, a.iters)
+            print(json.dumps({"case": name, "items": n, "grid_items": args[6].shape[0], "us": round(us, 1),
+                              "kv_TBps": round(kvb / us / 1e6, 2), "TFLOPs": round(fl / us / 1e6, 1)}),
+                  flush=True)
+
+
+if __name__ == "__main__":
+    main()
