@@ -23,7 +23,11 @@ int pa_sample_workspace_floats(int rows, int V);
 int pa_sample(int* out_tokens, float* out_keys, float* workspace, const void* logits, int rows,
               int V, int ld, int vocab_offset, const float* temperature, const int* mask_class,
               const uint32_t* class_masks, int mask_words, const int64_t* seeds,
-              const int* offsets, const int* forced, hipStream_t st);
+              const int* offsets, const int* forced, const float* tau, hipStream_t st);
+int pa_topkp_threshold(float* tau, const void* logits, int rows, int V, int ld, int shards,
+                       long long shard_stride, const float* temperature, const int* top_k,
+                       const float* top_p, const int* mask_class, const uint32_t* class_masks,
+                       int mask_words, hipStream_t st);
 void pa_skinny_set_variant(int v);
 int pa_skinny_gemm(void* y, const void* x, const void* w, int M, int N, int K, int ldy, hipStream_t st);
 int pa_cosine_topk_workspace_bytes(int Q, int N, int K);
@@ -165,7 +169,7 @@ int64_t sample_workspace_floats(int64_t rows, int64_t V) {
 void sample(at::Tensor out_tokens, c10::optional<at::Tensor> out_keys, at::Tensor workspace,
             at::Tensor logits, int64_t vocab_offset, at::Tensor temperature, at::Tensor mask_class,
             at::Tensor class_masks, at::Tensor seeds, at::Tensor offsets,
-            c10::optional<at::Tensor> forced) {
+            c10::optional<at::Tensor> forced, c10::optional<at::Tensor> tau) {
   check_gpu(out_tokens, "out_tokens"); check_gpu(workspace, "workspace");
   check_gpu(temperature, "temperature"); check_gpu(mask_class, "mask_class");
   check_gpu(class_masks, "class_masks"); check_gpu(seeds, "seeds"); check_gpu(offsets, "offsets");
@@ -192,12 +196,18 @@ void sample(at::Tensor out_tokens, c10::optional<at::Tensor> out_keys, at::Tenso
     check_gpu(*forced, "forced"); check_dtype(*forced, at::kInt, "forced");
     fp = forced->data_ptr<int>();
   }
+  const float* tp = nullptr;
+  if (tau.has_value()) {
+    check_gpu(*tau, "tau"); check_dtype(*tau, at::kFloat, "tau");
+    TORCH_CHECK(tau->numel() >= rows, "tau too short");
+    tp = tau->data_ptr<float>();
+  }
   check_rc(pa_sample(out_tokens.data_ptr<int>(), keys, workspace.data_ptr<float>(),
                      logits.data_ptr(), rows, V, logits.stride(0), vocab_offset,
                      temperature.data_ptr<float>(), mask_class.data_ptr<int>(),
                      reinterpret_cast<const uint32_t*>(class_masks.data_ptr<int>()),
                      class_masks.size(1), seeds.data_ptr<int64_t>(), offsets.data_ptr<int>(), fp,
-                     cur_stream()),
+                     tp, cur_stream()),
            "sample");
 }
 
@@ -238,6 +248,37 @@ void cosine_topk(at::Tensor out_scores, at::Tensor out_rows, at::Tensor workspac
 
 }  // namespace
 
+// tau[r] = top-k / top-p logit threshold of row r. `logits` is [rows, V] or a TP
+// all-gather [shards, rows, V/shards] (then V is the full vocabulary).
+void topkp_threshold(at::Tensor tau, at::Tensor logits, int64_t V, at::Tensor temperature,
+                     at::Tensor top_k, at::Tensor top_p, at::Tensor mask_class, at::Tensor class_masks) {
+  for (auto* t : {&tau, &logits, &temperature, &top_k, &top_p, &mask_class, &class_masks})
+    check_gpu(*t, "topkp_threshold arg");
+  check_dtype(tau, at::kFloat, "tau"); check_dtype(logits, at::kBFloat16, "logits");
+  check_dtype(temperature, at::kFloat, "temperature"); check_dtype(top_k, at::kInt, "top_k");
+  check_dtype(top_p, at::kFloat, "top_p"); check_dtype(mask_class, at::kInt, "mask_class");
+  check_dtype(class_masks, at::kInt, "class_masks");
+  int shards = 1, rows, ld;
+  long long sstride = 0;
+  if (logits.dim() == 3) {
+    shards = logits.size(0); rows = logits.size(1); ld = logits.stride(1); sstride = logits.stride(0);
+    TORCH_CHECK(logits.size(2) * shards == V, "gathered logits do not cover the vocabulary");
+  } else {
+    TORCH_CHECK(logits.dim() == 2 && logits.size(1) == V, "logits must be [rows, V]");
+    rows = logits.size(0); ld = logits.stride(0);
+  }
+  TORCH_CHECK(logits.stride(-1) == 1, "logits need unit inner stride");
+  TORCH_CHECK(tau.numel() >= rows && temperature.numel() >= rows && top_k.numel() >= rows &&
+                  top_p.numel() >= rows && mask_class.numel() >= rows, "per-row tensors too short");
+  TORCH_CHECK(class_masks.dim() == 2 && class_masks.size(1) * 32 >= V, "class_masks too narrow");
+  check_rc(pa_topkp_threshold(tau.data_ptr<float>(), logits.data_ptr(), rows, V, ld, shards, sstride,
+                              temperature.data_ptr<float>(), top_k.data_ptr<int>(), top_p.data_ptr<float>(),
+                              mask_class.data_ptr<int>(),
+                              reinterpret_cast<const uint32_t*>(class_masks.data_ptr<int>()),
+                              class_masks.size(1), cur_stream()),
+           "topkp_threshold");
+}
+
 PYBIND11_MODULE(_C, m) {
   m.doc() = "pilottai_amd CDNA4 (gfx950) HIP kernels";
   m.def("rmsnorm", &rmsnorm);
@@ -250,7 +291,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("sample_workspace_floats", &sample_workspace_floats);
   m.def("sample", &sample, py::arg("out_tokens"), py::arg("out_keys"), py::arg("workspace"),
         py::arg("logits"), py::arg("vocab_offset"), py::arg("temperature"), py::arg("mask_class"),
-        py::arg("class_masks"), py::arg("seeds"), py::arg("offsets"), py::arg("forced"));
+        py::arg("class_masks"), py::arg("seeds"), py::arg("offsets"), py::arg("forced"),
+        py::arg("tau") = py::none());
+  m.def("topkp_threshold", &topkp_threshold);
   m.def("cosine_topk_workspace_bytes", &cosine_topk_workspace_bytes);
   m.def("cosine_topk", &cosine_topk);
   m.attr("ATT_PART") = 512;

@@ -5,8 +5,10 @@
 // so one streaming pass over the vocabulary replaces softmax + cumsum + search,
 // and the vocabulary can be split over many workgroups (a 128K-entry row is
 // 32 workgroups of 4096 entries; a decode batch of 64 rows fills 2048 WGs).
-// T == 0 selects greedy argmax. top-k (k <= 64) runs a per-row threshold search
-// on the chunk winners' candidate lists (see topk pass below).
+// T == 0 selects greedy argmax. top-k / top-p truncation is a per-row logit
+// threshold tau computed exactly by topkp_threshold_kernel (radix select on the
+// bf16 order key, below); the sampler then keeps logit >= tau, and Gumbel-max
+// over the kept set samples the renormalised truncated distribution.
 // U_i comes from a counter-based hash of (row seed, row offset, vocab index),
 // so a request samples the same token regardless of how it was batched, and the
 // vocab-parallel (TP) variant produces the identical token after an all-gather
@@ -35,9 +37,11 @@ __global__ __launch_bounds__(256) void sample_chunk_kernel(
     float* __restrict__ part_k, int* __restrict__ part_i, const bf16* __restrict__ logits,
     int V, int ld, int vocab_offset, const float* __restrict__ temperature,
     const int* __restrict__ mask_class, const uint32_t* __restrict__ class_masks, int mask_words,
-    const int64_t* __restrict__ seeds, const int* __restrict__ offsets, int nchunk) {
+    const int64_t* __restrict__ seeds, const int* __restrict__ offsets, int nchunk,
+    const float* __restrict__ tau) {
   const int row = blockIdx.y, chunk = blockIdx.x;
   const float T = temperature[row];
+  const float thr = tau ? tau[row] : -INFINITY;
   const bool greedy = T <= 0.f;
   const float invT = greedy ? 1.f : 1.f / T;
   const int mc = mask_class[row];
@@ -60,7 +64,9 @@ __global__ __launch_bounds__(256) void sample_chunk_kernel(
     for (int j = 0; j < 8; ++j) {
       const int i = i0 + j;
       if (i >= V || !((bits >> j) & 1u)) continue;
-      float key = bf2f(v[j]) * invT;
+      const float lv = bf2f(v[j]);
+      if (lv < thr) continue;
+      float key = lv * invT;
       if (!greedy) {
         const float u = uniform01(seed, off, (uint32_t)(vocab_offset + i));
         key += -__logf(-__logf(u));
@@ -113,7 +119,127 @@ __global__ __launch_bounds__(64) void sample_final_kernel(int* __restrict__ out_
   }
 }
 
+// ---------------------------------------------------------------------------
+// top-k / top-p threshold. One 1024-thread workgroup per row; the row is read
+// from L2 once per pass (4 passes). bf16 values map to a monotone 16-bit order
+// key; the threshold key is found byte by byte from 256-bin histograms of
+// (count, softmax mass at the row's temperature) in LDS, so the kept set is
+// exactly {allowed i : logit_i >= tau} with
+//   top-k: the k-th largest allowed logit, top-p: the smallest top set whose
+//   mass reaches p (ties at the boundary value are kept), tau = the larger.
+// The logits may be a TP all-gather: `shards` slices of V/shards columns
+// each, `shard_stride` elements apart.
+__device__ __forceinline__ uint32_t bf16_order_key(uint16_t b) {
+  return (b & 0x8000u) ? (~(uint32_t)b & 0xffffu) : ((uint32_t)b | 0x8000u);
+}
+__device__ __forceinline__ float order_key_value(uint32_t k) {
+  const uint16_t b = (k & 0x8000u) ? (uint16_t)(k & 0x7fffu) : (uint16_t)(~k & 0xffffu);
+  return __uint_as_float((uint32_t)b << 16);
+}
+
+constexpr int TKP_THREADS = 1024;
+
+__global__ __launch_bounds__(TKP_THREADS) void topkp_threshold_kernel(
+    float* __restrict__ tau, const uint16_t* __restrict__ logits, int V, int ld, int shards,
+    size_t shard_stride, const float* __restrict__ temperature, const int* __restrict__ top_k,
+    const float* __restrict__ top_p, const int* __restrict__ mask_class,
+    const uint32_t* __restrict__ class_masks, int mask_words) {
+  const int row = blockIdx.x;
+  const int k = top_k[row];
+  const float p = top_p[row];
+  const float T = temperature[row];
+  if (T <= 0.f || ((k <= 0 || k >= V) && !(p < 1.f))) {  // nothing to truncate
+    if (threadIdx.x == 0) tau[row] = -INFINITY;
+    return;
+  }
+  const int vs = V / shards;
+  const int mc = mask_class[row];
+  const float invT_log2 = 1.4426950408889634f / T;
+  __shared__ float s_cnt[256], s_mass[256];
+  __shared__ float red[TKP_THREADS / 64];
+  __shared__ uint32_t s_sel[2];
+  __shared__ float s_carry[2];
+  auto value_at = [&](int g, uint32_t* key) -> bool {
+    if (mc >= 0 && !((class_masks[(size_t)mc * mask_words + (g >> 5)] >> (g & 31)) & 1u)) return false;
+    const int sh = g / vs, li = g - sh * vs;
+    *key = bf16_order_key(logits[sh * shard_stride + (size_t)row * ld + li]);
+    return true;
+  };
+  // pass 1: max allowed logit
+  float mx = -INFINITY;
+  for (int g = threadIdx.x; g < V; g += TKP_THREADS) {
+    uint32_t kk;
+    if (value_at(g, &kk)) mx = fmaxf(mx, order_key_value(kk));
+  }
+  mx = wave_max(mx);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mx;
+  __syncthreads();
+  mx = red[0];
+#pragma unroll
+  for (int w = 1; w < TKP_THREADS / 64; ++w) mx = fmaxf(mx, red[w]);
+  if (mx == -INFINITY) {  // no allowed token: leave the row to the sampler's fallback
+    if (threadIdx.x == 0) tau[row] = -INFINITY;
+    return;
+  }
+  // passes 2/3: histogram of the high byte, then of the low byte inside the
+  // selected high bin; each followed by a top-down scan of the 256 bins
+  uint32_t prefix = 0;
+  float above_cnt = 0.f, above_mass = 0.f, total_mass = 0.f;
+  for (int level = 0; level < 2; ++level) {
+    if (threadIdx.x < 256) { s_cnt[threadIdx.x] = 0.f; s_mass[threadIdx.x] = 0.f; }
+    __syncthreads();
+    for (int g = threadIdx.x; g < V; g += TKP_THREADS) {
+      uint32_t kk;
+      if (!value_at(g, &kk)) continue;
+      if (level == 1 && (kk >> 8) != prefix) continue;
+      const int bin = level == 0 ? (int)(kk >> 8) : (int)(kk & 0xff);
+      atomicAdd(&s_cnt[bin], 1.f);
+      atomicAdd(&s_mass[bin], exp2f((order_key_value(kk) - mx) * invT_log2));
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      if (level == 0) {
+        for (int b = 0; b < 256; ++b) total_mass += s_mass[b];
+        s_carry[0] = total_mass;
+      }
+      const float tm = level == 0 ? total_mass : s_carry[0];
+      const float need_mass = p < 1.f ? p * tm : INFINITY;
+      const float need_cnt = (k > 0 && k < V) ? (float)k : INFINITY;
+      float c = above_cnt, m = above_mass;
+      int sel = 0;
+      for (int b = 255; b >= 0; --b) {
+        const float c2 = c + s_cnt[b], m2 = m + s_mass[b];
+        if (c2 >= need_cnt || m2 >= need_mass) { sel = b; break; }
+        c = c2; m = m2;
+        sel = b;
+      }
+      s_sel[0] = (uint32_t)sel;
+      s_carry[1] = c;  // count strictly above the selected bin
+      red[0] = m;      // mass strictly above the selected bin
+    }
+    __syncthreads();
+    const uint32_t sel = s_sel[0];
+    above_cnt = s_carry[1];
+    above_mass = red[0];
+    prefix = level == 0 ? sel : ((prefix << 8) | sel);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) tau[row] = order_key_value(prefix);
+}
+
 }  // namespace pa
+
+extern "C" int pa_topkp_threshold(float* tau, const void* logits, int rows, int V, int ld, int shards,
+                                  long long shard_stride, const float* temperature, const int* top_k,
+                                  const float* top_p, const int* mask_class, const uint32_t* class_masks,
+                                  int mask_words, hipStream_t st) {
+  if (rows <= 0) return 0;
+  if (shards <= 0 || V % shards != 0) return -1;
+  hipLaunchKernelGGL(pa::topkp_threshold_kernel, dim3(rows), dim3(pa::TKP_THREADS), 0, st, tau,
+                     (const uint16_t*)logits, V, ld, shards, (size_t)shard_stride, temperature, top_k,
+                     top_p, mask_class, class_masks, mask_words);
+  return (int)hipGetLastError();
+}
 
 extern "C" int pa_sample_workspace_floats(int rows, int V) {
   const int nchunk = (V + pa::SMP_CHUNK - 1) / pa::SMP_CHUNK;
@@ -127,7 +253,7 @@ extern "C" int pa_sample(int* out_tokens, float* out_keys, float* workspace, con
                          int rows, int V, int ld, int vocab_offset, const float* temperature,
                          const int* mask_class, const uint32_t* class_masks, int mask_words,
                          const int64_t* seeds, const int* offsets, const int* forced,
-                         hipStream_t st) {
+                         const float* tau, hipStream_t st) {
   if (rows <= 0) return 0;
   if (V % 8 != 0 || ld % 8 != 0) return -1;
   const int nchunk = (V + pa::SMP_CHUNK - 1) / pa::SMP_CHUNK;
@@ -135,7 +261,7 @@ extern "C" int pa_sample(int* out_tokens, float* out_keys, float* workspace, con
   int* pi = reinterpret_cast<int*>(workspace + (size_t)rows * nchunk);
   hipLaunchKernelGGL(pa::sample_chunk_kernel, dim3(nchunk, rows), dim3(256), 0, st, pk, pi,
                      (const pa::bf16*)logits, V, ld, vocab_offset, temperature, mask_class,
-                     class_masks, mask_words, seeds, offsets, nchunk);
+                     class_masks, mask_words, seeds, offsets, nchunk, tau);
   hipLaunchKernelGGL(pa::sample_final_kernel, dim3(rows), dim3(64), 0, st, out_tokens, out_keys,
                      pk, pi, forced, nchunk);
   return (int)hipGetLastError();

@@ -108,6 +108,7 @@ PYBIND11_MODULE(_runtime, m) {
         d["q_start"] = L.q_start; d["q_len"] = L.q_len; d["ctx_len"] = L.ctx_len;
         d["logit_rows"] = L.logit_rows; d["mask_class"] = L.mask_class; d["forced"] = L.forced;
         d["offsets"] = L.offsets; d["temperature"] = L.temperature; d["seeds"] = L.seeds;
+        d["top_k"] = L.top_k; d["top_p"] = L.top_p;
         d["items"] = L.items; d["n_items"] = L.n_items;
         d["counts"] = L.counts; d["block_table"] = L.block_table;
         d["total"] = L.total;
@@ -116,10 +117,14 @@ PYBIND11_MODULE(_runtime, m) {
       .def("add_request",
            [](Scheduler& s, int64_t id, const std::vector<int32_t>& prompt, float temperature,
               int32_t max_tokens, int64_t seed, bool ignore_eos,
-              const std::vector<int32_t>& stop_ids, const py::object& grammar) {
+              const std::vector<int32_t>& stop_ids, const py::object& grammar, int32_t top_k,
+              float top_p) {
              s.add_request(id, prompt, temperature, max_tokens, seed, ignore_eos, stop_ids,
-                           make_grammar(grammar));
-           })
+                           make_grammar(grammar), top_k, top_p);
+           },
+           py::arg("id"), py::arg("prompt"), py::arg("temperature"), py::arg("max_tokens"),
+           py::arg("seed"), py::arg("ignore_eos"), py::arg("stop_ids"), py::arg("grammar"),
+           py::arg("top_k") = 0, py::arg("top_p") = 1.0f)
       .def("schedule", [](Scheduler& s, uintptr_t buf) {
         py::gil_scoped_release nogil;
         return s.schedule(reinterpret_cast<int32_t*>(buf));

@@ -41,6 +41,8 @@ Scheduler::Scheduler(const SchedulerConfig& cfg)
   L.forced = take(L.max_seqs);
   L.offsets = take(L.max_seqs);
   L.temperature = take(L.max_seqs);
+  L.top_k = take(L.max_seqs);
+  L.top_p = take(L.max_seqs);
   L.seeds = take(2 * L.max_seqs);
   L.items = take(4 * L.max_items);
   L.block_table = take(L.max_seqs * L.max_blocks);
@@ -49,7 +51,8 @@ Scheduler::Scheduler(const SchedulerConfig& cfg)
 
 void Scheduler::add_request(int64_t id, std::vector<int32_t> prompt, float temperature,
                             int32_t max_tokens, int64_t seed, bool ignore_eos,
-                            std::vector<int32_t> stop_ids, std::unique_ptr<Grammar> grammar) {
+                            std::vector<int32_t> stop_ids, std::unique_ptr<Grammar> grammar,
+                            int32_t top_k, float top_p) {
   auto s = std::make_unique<Sequence>();
   s->id = id;
   if ((int32_t)prompt.size() >= cfg_.max_model_len)
@@ -58,6 +61,8 @@ void Scheduler::add_request(int64_t id, std::vector<int32_t> prompt, float tempe
   s->tokens = std::move(prompt);
   s->prompt_len = (int32_t)s->tokens.size();
   s->temperature = temperature;
+  s->top_k = std::max(0, top_k);
+  s->top_p = (top_p > 0.f && top_p < 1.f) ? top_p : 1.f;
   s->max_tokens = std::max(1, max_tokens);
   s->seed = seed;
   s->ignore_eos = ignore_eos;
@@ -205,6 +210,9 @@ int32_t Scheduler::schedule(int32_t* buf) {
   int32_t* fc = buf + L.forced;
   int32_t* off = buf + L.offsets;
   float* temp = reinterpret_cast<float*>(buf + L.temperature);
+  int32_t* tk = buf + L.top_k;
+  float* tp = reinterpret_cast<float*>(buf + L.top_p);
+  int32_t ntrunc = 0;
   int64_t* seeds = reinterpret_cast<int64_t*>(buf + L.seeds);
   int32_t* items = buf + L.items;
   int32_t* bt = buf + L.block_table;
@@ -244,6 +252,9 @@ int32_t Scheduler::schedule(int32_t* buf) {
       fc[nsamp] = forced;
       off[nsamp] = (int32_t)s->tokens.size();
       temp[nsamp] = s->temperature;
+      tk[nsamp] = s->top_k;
+      tp[nsamp] = s->top_p;
+      if (s->temperature > 0.f && (s->top_k > 0 || s->top_p < 1.f) && forced < 0) ++ntrunc;
       seeds[nsamp] = s->seed;
       ++nsamp;
     }
@@ -278,6 +289,8 @@ int32_t Scheduler::schedule(int32_t* buf) {
     fc[r] = -1;
     off[r] = 0;
     temp[r] = 0.f;
+    tk[r] = 0;
+    tp[r] = 1.f;
     seeds[r] = 0;
   }
   for (int32_t r = ns; r < L.max_seqs; ++r) {
@@ -291,6 +304,7 @@ int32_t Scheduler::schedule(int32_t* buf) {
   counts[3] = nit;
   counts[4] = nparted;
   counts[5] = pslot;
+  counts[6] = ntrunc;  // rows that need the top-k / top-p threshold pass
   buf[L.n_items] = nit;
   if (T > 0) ++stat_steps_;
   return T;

@@ -40,7 +40,7 @@ struct SchedulerConfig {
 struct StepLayout {
   int32_t max_tokens, max_seqs, max_blocks, max_items;
   int32_t input_ids, positions, slots, q_start, q_len, ctx_len, logit_rows, mask_class, forced,
-      offsets, temperature, seeds, items, n_items, counts, block_table, total;
+      offsets, temperature, top_k, top_p, seeds, items, n_items, counts, block_table, total;
 };
 
 enum FinishReason : int32_t { NOT_FINISHED = -1, FINISH_STOP = 0, FINISH_LENGTH = 1, FINISH_ABORT = 2 };
@@ -70,6 +70,8 @@ struct Sequence {
   std::vector<uint64_t> block_hashes;  // hash chain of registered leading blocks
   std::unique_ptr<Grammar> grammar;
   float temperature = 0.7f;
+  int32_t top_k = 0;    // 0 = no top-k truncation
+  float top_p = 1.0f;   // 1 = no nucleus truncation
   int32_t max_tokens = 256;
   int64_t seed = 0;
   bool ignore_eos = false;
@@ -87,7 +89,7 @@ class Scheduler {
 
   void add_request(int64_t id, std::vector<int32_t> prompt, float temperature, int32_t max_tokens,
                    int64_t seed, bool ignore_eos, std::vector<int32_t> stop_ids,
-                   std::unique_ptr<Grammar> grammar);
+                   std::unique_ptr<Grammar> grammar, int32_t top_k = 0, float top_p = 1.0f);
   bool abort(int64_t id);
   // Fill `buf` (layout()) for the next step. Returns the number of tokens in the
   // step (0 = nothing to run).

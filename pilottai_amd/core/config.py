@@ -84,6 +84,8 @@ class LLMConfig(BaseModel):
     provider: str = "local"
     api_key: SecretStr = SecretStr("")
     temperature: float = Field(default=0.7, ge=0.0, le=2.0)
+    top_p: float = Field(default=1.0, gt=0.0, le=1.0)   # nucleus truncation (1 = off)
+    top_k: int = Field(default=0, ge=0)                 # top-k truncation (0 = off)
     max_tokens: int = Field(default=2000, gt=0)
     function_calling_model: Optional[str] = None
     system_template: Optional[str] = None
@@ -101,7 +103,8 @@ class LLMConfig(BaseModel):
 
     def to_dict(self) -> Dict[str, Any]:
         return {"model_name": self.model_name, "provider": self.provider, "temperature": self.temperature,
-                "max_tokens": self.max_tokens, "function_calling_model": self.function_calling_model}
+                "top_p": self.top_p, "top_k": self.top_k, "max_tokens": self.max_tokens,
+                "function_calling_model": self.function_calling_model}
 
     def handler_config(self) -> Dict[str, Any]:
         d = self.model_dump()

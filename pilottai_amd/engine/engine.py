@@ -74,7 +74,7 @@ class EngineConfig:
     capture_on_start: bool = True
 
 
-# TP step header: [op, T, ns, nsamp, bucket, masks_changed, n_copy]
+# TP step header: [op, T, ns, nsamp, bucket, masks_changed, n_copy, truncate]
 _OP_STOP, _OP_STEP = 0, 1
 
 
@@ -121,6 +121,8 @@ class _Request:
     grammar: Optional[list]
     callback: Callable[[GenerationOutput], None]
     t_arrival: float
+    top_k: int = 0
+    top_p: float = 1.0
 
 
 class LLMEngine:
@@ -203,11 +205,14 @@ class LLMEngine:
         buckets = cfg.token_buckets or DEFAULT_BUCKETS
         self.buckets = sorted({b for b in buckets if b <= cfg.max_num_batched_tokens} |
                               {cfg.max_num_batched_tokens})
-        self._graphs: Dict[int, "torch.cuda.CUDAGraph"] = {}
+        # one graph per (token bucket, top-k/top-p pass); truncating variants are
+        # captured on first use, so steps without truncation pay nothing for it
+        self._graphs: Dict[tuple, "torch.cuda.CUDAGraph"] = {}
+        self._tau = torch.empty(S, dtype=torch.float32, device=self.device)
         self._graph_pool = None
         self.use_graphs = cfg.use_graphs and self.on_gpu
         self.is_driver = self.tp.rank == 0
-        self._tp_header = torch.zeros(7, dtype=torch.int64)
+        self._tp_header = torch.zeros(8, dtype=torch.int64)
         self._tp_closed = False
         # ---- request plumbing
         self._inbox: "queue.SimpleQueue" = queue.SimpleQueue()
@@ -246,6 +251,8 @@ class LLMEngine:
             att_counters=self._att_counters,
             logit_rows=sl("logit_rows", ms))
         self._temp = sl("temperature", ms).view(torch.float32)
+        self._top_k = sl("top_k", ms)
+        self._top_p = sl("top_p", ms).view(torch.float32)
         self._mask_cls = sl("mask_class", ms)
         self._forced = sl("forced", ms)
         self._offsets = sl("offsets", ms)
@@ -269,24 +276,45 @@ class LLMEngine:
         return StepMeta(m.input_ids, m.positions, m.slots, m.q_start, m.q_len, m.ctx_len,
                         m.block_table, m.items[:n_it], m.n_items, m.att_counters, m.logit_rows, num_seqs=ns)
 
-    def _forward_and_sample(self, bucket: int, s_b: int, ns: int):
+    def _forward_and_sample(self, bucket: int, s_b: int, ns: int, trunc: bool = False):
         meta = self._meta_for(bucket, s_b, ns)
         logits = self.model.forward(meta, self.kv, bucket, s_b, self._part_o, self._part_ml)
+        tau = None
+        if trunc:
+            # exact top-k / top-p threshold on the full vocabulary (TP: all-gathered)
+            full = logits if self.tp.size == 1 else self.tp.all_gather(logits)
+            tau = ops.topkp_threshold(full, self.model_cfg.vocab_size, self._temp[:s_b], self._top_k[:s_b],
+                                      self._top_p[:s_b], self._mask_cls[:s_b], self._class_masks,
+                                      out=self._tau[:s_b])
         if self.tp.size == 1:
             ops.sample(logits, self._temp[:s_b], self._mask_cls[:s_b], self._class_masks,
                        self._seeds[:s_b], self._offsets[:s_b], self._forced[:s_b],
-                       out=self._sampled_dev[:s_b], workspace=self._sample_ws)
+                       out=self._sampled_dev[:s_b], workspace=self._sample_ws, tau=tau)
         else:
             # vocab-parallel: local winners + keys, all-gather, global argmax (identical
             # to the TP=1 token because the Gumbel noise is keyed on the global index)
             ops.sample(logits, self._temp[:s_b], self._mask_cls[:s_b], self._class_masks,
                        self._seeds[:s_b], self._offsets[:s_b], self._forced[:s_b],
                        out=self._sampled_dev[:s_b], workspace=self._sample_ws,
-                       vocab_offset=self.model.vocab_offset, out_keys=self._keys_dev[:s_b])
+                       vocab_offset=self.model.vocab_offset, out_keys=self._keys_dev[:s_b], tau=tau)
             keys = self.tp.all_gather(self._keys_dev[:s_b])        # [tp, s_b]
             toks = self.tp.all_gather(self._sampled_dev[:s_b])     # [tp, s_b]
             best = keys.argmax(0, keepdim=True)
             self._sampled_dev[:s_b].copy_(toks.gather(0, best).squeeze(0))
+
+    def _run(self, bucket: int, ns: int, trunc: bool, n_copy: int):
+        """Replay the (bucket, trunc) graph — capturing it first if needed — or run eagerly."""
+        if not self.use_graphs:
+            self._forward_and_sample(bucket, self._seq_bucket(bucket), ns, trunc)
+            return
+        g = self._graphs.get((bucket, trunc))
+        if g is None:
+            saved = self._dev_meta[:n_copy].clone()
+            self.capture_graphs([bucket], trunc=trunc)  # clobbers the device metadata
+            self._dev_meta[:n_copy].copy_(saved)
+            g = self._graphs[(bucket, trunc)]
+        g.replay()
+        self.stats["graph_replays"] += 1
 
     def _seq_bucket(self, bucket: int) -> int:
         return min(bucket, self.cfg.max_num_seqs)
@@ -298,7 +326,7 @@ class LLMEngine:
         d[L["slots"]:L["slots"] + L["max_tokens"]] = -1
         self._dev_meta.copy_(d.to(self.device))
 
-    def capture_graphs(self, buckets: Optional[Sequence[int]] = None):
+    def capture_graphs(self, buckets: Optional[Sequence[int]] = None, trunc: bool = False):
         """Capture one hipGraph per token bucket (shared memory pool)."""
         if not self.use_graphs:
             return
@@ -307,19 +335,19 @@ class LLMEngine:
             self._graph_pool = torch.cuda.graph_pool_handle()
         t0 = time.time()
         for b in sorted(buckets or self.buckets, reverse=True):
-            if b in self._graphs:
+            if (b, trunc) in self._graphs:
                 continue
             s_b = self._seq_bucket(b)
             st = torch.cuda.Stream(device=self.device)
             st.wait_stream(torch.cuda.current_stream())
             with torch.cuda.stream(st):
                 for _ in range(2):
-                    self._forward_and_sample(b, s_b, 0)
+                    self._forward_and_sample(b, s_b, 0, trunc)
             torch.cuda.current_stream().wait_stream(st)
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, pool=self._graph_pool):
-                self._forward_and_sample(b, s_b, 0)
-            self._graphs[b] = g
+                self._forward_and_sample(b, s_b, 0, trunc)
+            self._graphs[(b, trunc)] = g
         torch.cuda.synchronize()
         log.info("captured %d hipGraphs in %.1fs", len(self._graphs), time.time() - t0)
 
@@ -333,15 +361,19 @@ class LLMEngine:
     def submit(self, prompt_ids: Sequence[int], callback: Callable[[GenerationOutput], None], *,
                temperature: float = 0.7, max_tokens: int = 256, seed: Optional[int] = None,
                ignore_eos: bool = False, stop_ids: Sequence[int] = (), grammar: Optional[list] = None,
-               request_id: Optional[int] = None) -> int:
-        """Thread-safe; `callback` runs on the engine thread when the request finishes."""
+               request_id: Optional[int] = None, top_k: int = 0, top_p: float = 1.0) -> int:
+        """Thread-safe; `callback` runs on the engine thread when the request finishes.
+
+        top_k > 0 / top_p < 1 truncate the (grammar-masked) distribution before
+        sampling (exact threshold kernel, csrc/ops/sampling.hip)."""
         if self._err is not None:
             raise RuntimeError(f"engine failed: {self._err!r}")
         rid = request_id if request_id is not None else self.new_request_id()
         if seed is None:
             seed = (self.cfg.seed * 0x9E3779B1 + rid * 0x85EBCA77) & 0x7FFFFFFFFFFFFFFF
         req = _Request(rid, list(prompt_ids), float(temperature), int(max_tokens), int(seed),
-                       bool(ignore_eos), list(stop_ids), grammar, callback, self._rt.now())
+                       bool(ignore_eos), list(stop_ids), grammar, callback, self._rt.now(),
+                       int(top_k or 0), float(1.0 if top_p is None else top_p))
         self._inbox.put(req)
         self._wake.set()
         return rid
@@ -419,17 +451,13 @@ class LLMEngine:
         with torch.inference_mode():
             while True:
                 self.tp.broadcast(h, cpu=True)
-                op, T, ns, nsamp, bucket, masks_changed, n_copy = (int(v) for v in h.tolist())
+                op, T, ns, nsamp, bucket, masks_changed, n_copy, trunc = (int(v) for v in h.tolist())
                 if op == _OP_STOP:
                     break
                 if masks_changed:
                     self.tp.broadcast(self._class_masks)
                 self.tp.broadcast(self._dev_meta[:n_copy])
-                g = self._graphs.get(bucket) if self.use_graphs else None
-                if g is not None:
-                    g.replay()
-                else:
-                    self._forward_and_sample(bucket, self._seq_bucket(bucket), ns)
+                self._run(bucket, ns, bool(trunc), n_copy)
                 if self.on_gpu:
                     torch.cuda.current_stream().synchronize()
                 n += 1
@@ -449,7 +477,7 @@ class LLMEngine:
                 break
             self._reqs[req.rid] = req
             self.sched.add_request(req.rid, req.prompt_ids, req.temperature, req.max_tokens, req.seed,
-                                   req.ignore_eos, req.stop_ids, req.grammar)
+                                   req.ignore_eos, req.stop_ids, req.grammar, req.top_k, req.top_p)
             self.stats["requests"] += 1
         while True:
             try:
@@ -486,7 +514,7 @@ class LLMEngine:
                 raise RuntimeError("KV cache too small for the head request")
             return False
         c = self._host_np[L["counts"]:L["counts"] + 8]
-        ns, nsamp = int(c[1]), int(c[2])
+        ns, nsamp, trunc = int(c[1]), int(c[2]), int(c[6]) > 0
         bucket = next(b for b in self.buckets if b >= T)
         s_b = self._seq_bucket(bucket)
         masks_changed = self._sync_masks()
@@ -494,21 +522,12 @@ class LLMEngine:
         if self.on_gpu:
             self._dev_meta[:n_copy].copy_(self._host_meta[:n_copy], non_blocking=True)
         if self.tp.size > 1:
-            self._tp_send(_OP_STEP, T, ns, nsamp, bucket, int(masks_changed), n_copy)
+            self._tp_send(_OP_STEP, T, ns, nsamp, bucket, int(masks_changed), n_copy, int(trunc))
             if masks_changed:
                 self.tp.broadcast(self._class_masks)
             self.tp.broadcast(self._dev_meta[:n_copy])
         with torch.inference_mode():
-            g = self._graphs.get(bucket) if self.use_graphs else None
-            if g is None and self.use_graphs:
-                self.capture_graphs([bucket])  # clobbers the device metadata: restore it
-                self._dev_meta.copy_(self._host_meta)
-                g = self._graphs[bucket]
-            if g is not None:
-                g.replay()
-                self.stats["graph_replays"] += 1
-            else:
-                self._forward_and_sample(bucket, s_b, ns)
+            self._run(bucket, ns, trunc, n_copy)
         if nsamp:
             self._sampled_host[:nsamp].copy_(self._sampled_dev[:nsamp], non_blocking=self.on_gpu)
         if self.on_gpu:

@@ -90,6 +90,8 @@ class BaseLLM:
         self.config = config
         self.model_name = _cfg_get(config, "model_name", "llama-3-8b")
         self.temperature = float(_cfg_get(config, "temperature", 0.7))
+        self.top_p = float(_cfg_get(config, "top_p", 1.0))
+        self.top_k = int(_cfg_get(config, "top_k", 0))
         self.max_tokens = int(_cfg_get(config, "max_tokens", 2000))
         self.retry_attempts = max(1, int(_cfg_get(config, "retry_attempts", 3)))
         self.retry_delay = float(_cfg_get(config, "retry_delay", 1.0))
@@ -193,11 +195,11 @@ class LocalLLM(BaseLLM):
         def done(out):
             loop.call_soon_threadsafe(lambda: fut.done() or fut.set_result(out))
 
-        temp = self.temperature
-        if response_format and "temperature" in response_format:
-            temp = float(response_format["temperature"])
+        rf = response_format or {}
+        temp = float(rf.get("temperature", self.temperature))
         rid = self.engine.submit(ids, done, temperature=temp, max_tokens=self.max_tokens, grammar=grammar,
-                                 seed=(response_format or {}).get("seed"))
+                                 seed=rf.get("seed"), top_k=int(rf.get("top_k", self.top_k)),
+                                 top_p=float(rf.get("top_p", self.top_p)))
         try:
             out = await fut
         except asyncio.CancelledError:

@@ -11,6 +11,7 @@ from .kernels import (  # noqa: F401
     rope_cache,
     sample,
     sample_workspace,
+    topkp_threshold,
     silu_mul,
     skinny_gemm,
     SKINNY_MAX_M,

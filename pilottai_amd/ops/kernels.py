@@ -131,9 +131,26 @@ def sample_workspace(rows: int, V: int, device) -> torch.Tensor:
     return torch.empty(n, dtype=torch.float32, device=device)
 
 
+def topkp_threshold(logits, V: int, temperature, top_k, top_p, mask_class, class_masks,
+                    out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Per-row logit threshold tau for top-k / top-p (csrc/ops/sampling.hip).
+
+    `logits` is [rows, V] or a TP all-gather [shards, rows, V/shards]."""
+    rows = logits.shape[-2]
+    tau = out if out is not None else torch.empty(rows, dtype=torch.float32, device=logits.device)
+    if _on_gpu(logits):
+        require_native().topkp_threshold(tau, logits, int(V), temperature, top_k, top_p, mask_class,
+                                         class_masks)
+        return tau
+    full = logits if logits.dim() == 2 else logits.permute(1, 0, 2).reshape(rows, V)
+    tau[:rows].copy_(ref.topkp_threshold(full, temperature, top_k, top_p, mask_class, class_masks))
+    return tau
+
+
 def sample(logits, temperature, mask_class, class_masks, seeds, offsets, forced=None,
            out: Optional[torch.Tensor] = None, workspace: Optional[torch.Tensor] = None,
-           vocab_offset: int = 0, out_keys: Optional[torch.Tensor] = None):
+           vocab_offset: int = 0, out_keys: Optional[torch.Tensor] = None,
+           tau: Optional[torch.Tensor] = None):
     rows = logits.shape[0]
     if _on_gpu(logits):
         C = require_native()
@@ -141,10 +158,10 @@ def sample(logits, temperature, mask_class, class_masks, seeds, offsets, forced=
         if workspace is None:
             workspace = sample_workspace(rows, logits.shape[1], logits.device)
         C.sample(out, out_keys, workspace, logits, int(vocab_offset), temperature, mask_class,
-                 class_masks, seeds, offsets, forced)
+                 class_masks, seeds, offsets, forced, tau)
         return out
     toks, keys = ref.sample(logits, temperature, mask_class, class_masks, seeds, offsets, forced,
-                            vocab_offset, return_keys=True)
+                            vocab_offset, return_keys=True, tau=tau)
     if out_keys is not None:
         out_keys[:rows].copy_(keys)
     if out is not None:

@@ -155,9 +155,45 @@ def uniform01(seed: int, row_off: int, cols: np.ndarray) -> np.ndarray:
     return ((h >> np.uint64(8)).astype(np.float64) + 0.5) * (1.0 / 16777216.0)
 
 
+def topkp_threshold(logits: torch.Tensor, temperature, top_k, top_p, mask_class, class_masks):
+    """Exact top-k / top-p logit threshold per row (fp64 math, sort based).
+
+    Kept set = allowed tokens with logit >= tau; tau is the larger of the k-th
+    largest allowed logit and the value at which the descending cumulative
+    softmax(logit / T) mass first reaches p. -inf = no truncation."""
+    rows, V = logits.shape
+    out = torch.full((rows,), float("-inf"), dtype=torch.float32)
+    lg = logits.float().cpu().numpy().astype(np.float64)
+    cm = class_masks.cpu().numpy().view(np.uint32) if class_masks is not None else None
+    for r in range(rows):
+        T, k, p = float(temperature[r]), int(top_k[r]), float(top_p[r])
+        if T <= 0 or ((k <= 0 or k >= V) and not p < 1.0):
+            continue
+        vals = lg[r]
+        mc = int(mask_class[r])
+        if mc >= 0 and cm is not None:
+            idx = np.arange(V)
+            ok = ((cm[mc][idx >> 5] >> (idx & 31).astype(np.uint32)) & 1).astype(bool)
+            vals = vals[ok]
+        if vals.size == 0:
+            continue
+        s = np.sort(vals)[::-1]
+        t = -np.inf
+        if 0 < k < s.size:
+            t = max(t, s[k - 1])
+        if p < 1.0:
+            w = np.exp((s - s[0]) / T)
+            c = np.cumsum(w)
+            j = int(np.searchsorted(c, p * c[-1] * (1 - 1e-6)))
+            t = max(t, s[min(j, s.size - 1)])
+        out[r] = t
+    return out
+
+
 def sample(logits: torch.Tensor, temperature, mask_class, class_masks, seeds, offsets,
-           forced=None, vocab_offset: int = 0, return_keys: bool = False):
-    """Gumbel-max sampling with grammar masks; returns int32 tokens [rows]."""
+           forced=None, vocab_offset: int = 0, return_keys: bool = False, tau=None):
+    """Gumbel-max sampling with grammar masks (and optional top-k/p threshold
+    tau: logits below it are excluded); returns int32 tokens [rows]."""
     rows, V = logits.shape
     toks = torch.zeros(rows, dtype=torch.int32)
     keys_out = torch.zeros(rows, dtype=torch.float32)
@@ -178,6 +214,8 @@ def sample(logits: torch.Tensor, temperature, mask_class, class_masks, seeds, of
             key = lg[r] / T
             u = uniform01(int(seeds[r]), int(offsets[r]), idx)
             key = key + (-np.log(-np.log(u)))
+        if tau is not None:
+            valid &= lg[r] >= float(tau[r])
         key[~valid] = -np.inf
         best = int(np.argmax(key)) if valid.any() else 0
         keys_out[r] = float(key[best]) if valid.any() else float("-inf")

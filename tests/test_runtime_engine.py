@@ -147,3 +147,23 @@ def test_reference_sampler_masks_and_forced():
     masks = torch.stack([ref.pack_mask(np.ones(V, bool)), ref.pack_mask(allowed)])
     t = ref.sample(logits, [0.0, 0.7, 0.0], [0, 1, -1], masks, [1, 2, 3], [0, 0, 0], [-1, -1, 77])
     assert int(t[0]) == int(logits[0].float().argmax()) and int(t[1]) in (3, 200) and int(t[2]) == 77
+
+
+def test_engine_cpu_top_k_top_p(tok):
+    """top-k = 1 is greedy; top-p/top-k rows only emit tokens inside the kept set
+    (reference threshold), also under a grammar."""
+    from pilottai_amd.engine.engine import EngineConfig, LLMEngine
+
+    e = LLMEngine(EngineConfig(model="tiny", max_num_seqs=8, max_num_batched_tokens=128, max_model_len=512,
+                               num_kv_blocks=128), device="cpu")
+    p = tok.encode("Task: evaluate. Result: ok")
+    g = e.generate([p], temperature=0.0, max_tokens=5, ignore_eos=True)[0]
+    k1 = e.generate([p], temperature=1.3, max_tokens=5, ignore_eos=True, top_k=1, seed=3)[0]
+    assert k1.token_ids == g.token_ids
+    # top-p = tiny keeps only the argmax too
+    p1 = e.generate([p], temperature=0.9, max_tokens=5, ignore_eos=True, top_p=1e-6, seed=5)[0]
+    assert p1.token_ids == g.token_ids
+    segs = e.grammar.compile("orchestrator.result_evaluation")
+    out = e.generate([p], temperature=1.0, max_tokens=64, grammar=segs, top_k=3, top_p=0.9)[0]
+    obj = json.loads(out.text)
+    assert set(obj) == {"success", "quality", "requires_retry"}
