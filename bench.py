@@ -57,6 +57,7 @@ def parse():
     ap.add_argument("--max-batched-tokens", type=int, default=2048)
     ap.add_argument("--temperature", type=float, default=0.7)
     ap.add_argument("--steps-per-task", type=int, default=1)
+    ap.add_argument("--token-align", type=int, default=256, help="GEMM-friendly step sizes (0 = off)")
     ap.add_argument("--cpu", action="store_true", help="tiny model on CPU (plumbing smoke only)")
     return ap.parse_args()
 
@@ -80,7 +81,8 @@ async def run_rank(a, rank: int, world: int, device):
     t_init = time.time()
     eng = LLMEngine(EngineConfig(model=a.model if not a.cpu else "tiny", max_num_seqs=max(64, 2 * n_local),
                                  max_num_batched_tokens=a.max_batched_tokens, kv_cache_gb=a.kv_gb if not a.cpu else None,
-                                 num_kv_blocks=4096 if a.cpu else None, seed=1234 + rank), device=device)
+                                 num_kv_blocks=4096 if a.cpu else None, seed=1234 + rank,
+                                 token_align=a.token_align), device=device)
     register_engine(eng.model_cfg.name, eng)
     eng.start()
     llm = LocalLLM(LLMConfig(model_name=eng.model_cfg.name, temperature=a.temperature, max_tokens=1024,

@@ -96,6 +96,8 @@ PYBIND11_MODULE(_runtime, m) {
         if (d.contains("gqa_group")) c.gqa_group = d["gqa_group"].cast<int32_t>();
         if (d.contains("prefix_caching")) c.prefix_caching = d["prefix_caching"].cast<bool>();
         if (d.contains("split_decode")) c.split_decode = d["split_decode"].cast<bool>();
+        if (d.contains("token_align")) c.token_align = d["token_align"].cast<int32_t>();
+        if (d.contains("align_slack")) c.align_slack = d["align_slack"].cast<int32_t>();
         if (d.contains("eos_ids")) c.eos_ids = d["eos_ids"].cast<std::vector<int32_t>>();
         return std::make_unique<Scheduler>(c);
       }))
@@ -148,5 +150,6 @@ PYBIND11_MODULE(_runtime, m) {
       .def_property_readonly("total_prompt_tokens", &Scheduler::total_prompt_tokens)
       .def_property_readonly("total_cached_tokens", &Scheduler::total_cached_tokens)
       .def_property_readonly("total_preemptions", &Scheduler::total_preemptions)
-      .def_property_readonly("steps", &Scheduler::steps);
+      .def_property_readonly("steps", &Scheduler::steps)
+      .def_property_readonly("aligned_steps", &Scheduler::aligned_steps);
 }

@@ -197,6 +197,29 @@ int32_t Scheduler::schedule(int32_t* buf) {
     prefill_budget -= n;
   }
 
+  // 2b) align the step size (see SchedulerConfig::token_align): trim chunk tails,
+  //     newest entries first, never below one token per entry
+  if (cfg_.token_align > 0) {
+    int32_t T = 0;
+    for (const Planned& p : last_plan_) T += p.n;
+    const int32_t r = T % cfg_.token_align;
+    if (T > cfg_.token_align && r > 0 && r <= cfg_.align_slack) {
+      int32_t cap = 0;
+      for (const Planned& p : last_plan_) cap += p.n - 1;
+      if (cap >= r) {
+        int32_t left = r;
+        for (size_t i = last_plan_.size(); i-- > 0 && left > 0;) {
+          Planned& p = last_plan_[i];
+          const int32_t cut = std::min(left, p.n - 1);
+          p.n -= cut;
+          left -= cut;
+          p.sample = p.s->num_computed + p.n == (int32_t)p.s->tokens.size();
+        }
+        ++stat_aligned_steps_;
+      }
+    }
+  }
+
   // 3) emit the step description
   int32_t* counts = buf + L.counts;
   int32_t* ids = buf + L.input_ids;

@@ -34,6 +34,12 @@ struct SchedulerConfig {
   int32_t gqa_group = 4;               // query heads per KV head (attention work items)
   bool prefix_caching = true;
   bool split_decode = true;            // flash-decoding partitions for long contexts
+  // GEMM-friendly step sizes: when a step has T > token_align tokens and
+  // T % token_align <= align_slack, the tail of the multi-token chunks (prefill /
+  // jump-forward) is deferred so that T is a multiple of token_align (library
+  // GEMM cost jumps at each 256-row tile boundary). 0 disables.
+  int32_t token_align = 0;
+  int32_t align_slack = 96;
   std::vector<int32_t> eos_ids;
 };
 
@@ -107,6 +113,7 @@ class Scheduler {
   int64_t total_cached_tokens() const { return stat_cached_tokens_; }
   int64_t total_preemptions() const { return stat_preemptions_; }
   int64_t steps() const { return stat_steps_; }
+  int64_t aligned_steps() const { return stat_aligned_steps_; }
   bool has_work() const { return !running_.empty() || !waiting_.empty(); }
   void reset_prefix_cache();
 
@@ -133,6 +140,7 @@ class Scheduler {
   std::vector<SeqOutput> aborted_;
   int64_t arrival_counter_ = 0;
   int64_t stat_prompt_tokens_ = 0, stat_cached_tokens_ = 0, stat_preemptions_ = 0, stat_steps_ = 0;
+  int64_t stat_aligned_steps_ = 0;
 };
 
 double now_seconds();

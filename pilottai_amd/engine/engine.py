@@ -72,6 +72,8 @@ class EngineConfig:
     seed: int = 0
     weights_path: Optional[str] = None
     capture_on_start: bool = True
+    token_align: int = 256   # GEMM-friendly step sizes (runtime/scheduler.h); 0 = off
+    align_slack: int = 96
 
 
 # TP step header: [op, T, ns, nsamp, bucket, masks_changed, n_copy, truncate]
@@ -145,6 +147,10 @@ class LLMEngine:
         self.grammar = GrammarCompiler(self.tok)
         self.model_cfg = get_config(cfg.model)
         mc = self.model_cfg
+        if self.on_gpu:
+            from .gemm_tuning import load_tuned_gemms
+
+            self.tuned_gemms = load_tuned_gemms(mc.name, self.tp.size)
         t0 = time.time()
         self.model = LlamaModel(mc, self.device, tp=self.tp, seed=cfg.seed, weights_path=cfg.weights_path)
         self.load_time = time.time() - t0
@@ -176,6 +182,7 @@ class LLMEngine:
             "max_prefill_tokens": cfg.max_prefill_tokens, "max_model_len": self.max_model_len,
             "gqa_group": self.model.h_local // self.model.kv_local,
             "prefix_caching": cfg.prefix_caching, "split_decode": cfg.split_decode,
+            "token_align": cfg.token_align, "align_slack": cfg.align_slack,
             "eos_ids": list(self.tok.eos_ids)})
         L = self.L = self.sched.layout()
         pin = self.on_gpu
@@ -571,7 +578,7 @@ class LLMEngine:
             "running": s.num_running, "waiting": s.num_waiting, "free_kv_blocks": s.num_free_blocks,
             "total_kv_blocks": self.num_kv_blocks, "cached_kv_blocks": s.num_cached_blocks,
             "prompt_tokens": s.total_prompt_tokens, "prefix_cache_hit_tokens": s.total_cached_tokens,
-            "preemptions": s.total_preemptions, "graphs": len(self._graphs),
+            "preemptions": s.total_preemptions, "graphs": len(self._graphs), "aligned_steps": s.aligned_steps,
             "kv_cache_gb": self.kv.k.numel() * 2 * 2 / 2**30,
             "weights_gb": self.model.weight_bytes() / 2**30,
         })

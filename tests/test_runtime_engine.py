@@ -167,3 +167,31 @@ def test_engine_cpu_top_k_top_p(tok):
     out = e.generate([p], temperature=1.0, max_tokens=64, grammar=segs, top_k=3, top_p=0.9)[0]
     obj = json.loads(out.text)
     assert set(obj) == {"success", "quality", "requires_retry"}
+
+
+def test_scheduler_token_alignment():
+    """Steps just above a multiple of token_align are trimmed to it; the deferred
+    prompt tail is computed next step and the generated tokens are unchanged."""
+    from pilottai_amd import _runtime
+
+    def run(align):
+        s = _runtime.Scheduler({"num_blocks": 256, "block_size": 16, "max_num_seqs": 8,
+                                "max_num_batched_tokens": 2048, "max_prefill_tokens": 2048,
+                                "max_model_len": 2048, "gqa_group": 4, "eos_ids": [128009],
+                                "token_align": align, "align_slack": 96})
+        L = s.layout()
+        buf = np.zeros(L["total"], dtype=np.int32)
+        s.add_request(1, list(range(300)), 0.0, 3, 1, True, [], None)
+        s.add_request(2, list(range(1000, 1250)), 0.0, 3, 2, True, [], None)
+        sizes = []
+        while s.has_work():
+            T = s.schedule(buf.ctypes.data)
+            sizes.append(T)
+            nsamp = int(buf[L["counts"] + 2])
+            s.commit(np.full(max(1, nsamp), 7, dtype=np.int32).ctypes.data, nsamp)
+        return sizes, s.aligned_steps
+
+    plain, _ = run(0)
+    aligned, n_al = run(256)
+    assert plain[0] == 550 and aligned[0] == 512 and n_al >= 1
+    assert sum(plain) == sum(aligned)
