@@ -30,7 +30,7 @@ int pa_topkp_threshold(float* tau, const void* logits, int rows, int V, int ld, 
                        int mask_words, hipStream_t st);
 void pa_skinny_set_variant(int v);
 int pa_skinny_gemm(void* y, const void* x, const void* w, int M, int N, int K, int ldy, hipStream_t st);
-int pa_cosine_topk_workspace_bytes(int Q, int N, int K);
+long long pa_cosine_topk_workspace_bytes(int Q, int N, int K);
 int pa_cosine_topk(float* out_scores, int* out_rows, void* workspace, const void* queries,
                    const void* index, int Q, int N, int D, int K, const int* row_priority,
                    const uint64_t* row_tags, const float* row_expiry, const int* q_min_priority,
@@ -230,7 +230,10 @@ void cosine_topk(at::Tensor out_scores, at::Tensor out_rows, at::Tensor workspac
   TORCH_CHECK(queries.dim() == 2 && index.dim() == 2 && queries.size(1) == index.size(1),
               "queries [Q, D] and index [N, D] must agree on D");
   const int Q = queries.size(0), N = index.size(0), D = index.size(1);
+  TORCH_CHECK(Q <= 64, "cosine_topk takes at most 64 queries per call (ops.cosine_topk chunks larger batches)");
   TORCH_CHECK(n_valid <= N, "n_valid exceeds index rows");
+  TORCH_CHECK(queries.is_contiguous() && index.stride(1) == 1 && index.stride(0) == D,
+              "queries and index must be contiguous row-major");
   TORCH_CHECK(out_scores.numel() >= (int64_t)Q * K && out_rows.numel() >= (int64_t)Q * K,
               "output too small");
   TORCH_CHECK(workspace.numel() * workspace.element_size() >=

@@ -10,26 +10,29 @@
 // && (expiry == 0 || expiry > now) — the reference's candidate-index semantics
 // (priority index range, tag-set intersection, is_expired) evaluated in-kernel.
 //
-// Stage 1 (grid = row-slices x query-tiles of 16): each wave multiplies 16 index
-// rows by the 16-query tile with v_mfma_f32_16x16x32_bf16 (rows stream from HBM
-// straight into the A operand, the query tile sits in LDS as the B operand), so
-// a [Q<=16, 1024] x [1024, N] scan is one pass over the index at HBM rate.
-// Scores above the per-query running threshold are appended to an LDS candidate
-// buffer; when a buffer nears capacity the workgroup sorts it (bitonic) and
-// raises the threshold to the current k-th best. Each slice writes its top-k.
-// Stage 2 (one WG per query) merges the slices' top-k lists the same way.
+// Stage 1 (one pass over the index for up to 64 queries): each workgroup owns a
+// slice of rows; its 8 waves take 16-row groups and multiply them by EVERY query
+// tile with v_mfma_f32_16x16x32_bf16 — index rows stream from HBM straight into
+// the A operand once, the (<= 64) queries sit in LDS as B operands, so a 205 GB
+// 100M x 1024 index is read exactly once per batch of agent queries. Scores
+// above a query's running threshold (and passing the filters) are appended to
+// that query's candidate buffer (global workspace, per workgroup); a full buffer
+// is sorted (bitonic, in LDS) and the threshold raised to its k-th best. Each
+// slice writes its top-k. Stage 2 (one WG per query) merges the slices' lists.
 #include "common.h"
 
 namespace pa {
 
-constexpr int SIM_CAND = 256;     // candidate buffer per query (power of two)
+constexpr int SIM_CAND = 256;     // candidate buffer per (slice, query), power of two
 constexpr int SIM_MAXK = 64;
-constexpr int SIM_QT = 16;        // queries per tile (MFMA N)
-constexpr int SIM_MAXD = 1024;    // LDS query tile capacity (bf16)
-constexpr int SIM_MIN_ROWS_PER_WG = 1024;
-constexpr int SIM_MAX_WG = 1024;
+constexpr int SIM_QT = 16;        // queries per MFMA tile (N = 16)
+constexpr int SIM_MAXQ = 64;      // queries per pass (4 tiles resident in LDS)
+constexpr int SIM_MAXD = 1024;    // LDS query capacity per query (bf16)
+constexpr int SIM_THREADS = 512;  // 8 waves
+constexpr int SIM_MIN_ROWS_PER_WG = 2048;
+constexpr int SIM_MAX_WG = 256;    // one resident workgroup per CU: the threshold warm-up is paid once per CU
 
-__device__ __forceinline__ int sim_num_wg(int N) {
+__host__ __device__ inline int sim_num_wg(int N) {
   int nwg = (N + SIM_MIN_ROWS_PER_WG - 1) / SIM_MIN_ROWS_PER_WG;
   if (nwg > SIM_MAX_WG) nwg = SIM_MAX_WG;
   if (nwg < 1) nwg = 1;
@@ -41,9 +44,9 @@ __device__ void bitonic_desc(float* cs, int* cr) {
   for (int k = 2; k <= SIM_CAND; k <<= 1) {
     for (int j = k >> 1; j > 0; j >>= 1) {
       __syncthreads();
-      const int i = threadIdx.x;  // SIM_CAND == 256 threads
+      const int i = threadIdx.x;
       const int p = i ^ j;
-      if (p > i) {
+      if (i < SIM_CAND && p > i) {
         const bool desc = (i & k) == 0;
         const float a = cs[i], b = cs[p];
         const bool swap = desc ? (a < b) : (a > b);
@@ -60,7 +63,7 @@ __device__ void bitonic_desc(float* cs, int* cr) {
 // Compact query c's buffer to its best K entries and update its threshold.
 __device__ void compact_query(float* cs, int* cr, int* cnt, float* theta, int K) {
   const int n = min(*cnt, SIM_CAND);
-  if (threadIdx.x >= n) { cs[threadIdx.x] = -INFINITY; cr[threadIdx.x] = -1; }
+  if (threadIdx.x < SIM_CAND && threadIdx.x >= n) { cs[threadIdx.x] = -INFINITY; cr[threadIdx.x] = -1; }
   bitonic_desc(cs, cr);
   if (threadIdx.x == 0) {
     const int keep = min(n, K);
@@ -70,103 +73,133 @@ __device__ void compact_query(float* cs, int* cr, int* cnt, float* theta, int K)
   __syncthreads();
 }
 
-__global__ __launch_bounds__(256) void cosine_stage1_kernel(
-    float* __restrict__ ws_s, int* __restrict__ ws_r, const bf16* __restrict__ queries,
-    const bf16* __restrict__ index, int Q, int N, int D, int K, const int* __restrict__ row_prio,
-    const uint64_t* __restrict__ row_tags, const float* __restrict__ row_exp,
-    const int* __restrict__ q_minp, const uint64_t* __restrict__ q_tags, float now) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  bf16* qt = reinterpret_cast<bf16*>(smem);                                  // [16][D]
-  float* cand_s = reinterpret_cast<float*>(smem + SIM_QT * SIM_MAXD * 2);    // [16][CAND]
-  int* cand_r = reinterpret_cast<int*>(cand_s + SIM_QT * SIM_CAND);          // [16][CAND]
-  int* cnt = cand_r + SIM_QT * SIM_CAND;                                     // [16]
-  float* theta = reinterpret_cast<float*>(cnt + SIM_QT);                     // [16]
-  int* flag = reinterpret_cast<int*>(theta + SIM_QT);                        // [1]
+// Sort the global candidate buffer `gs/gr` of one query through the LDS scratch,
+// keep the best K, raise the threshold.
+__device__ void compact_global(float* gs, int* gr, float* cs, int* cr, int* cnt, float* theta, int K) {
+  const int n = min(*cnt, SIM_CAND);
+  if (threadIdx.x < SIM_CAND) {
+    cs[threadIdx.x] = threadIdx.x < n ? gs[threadIdx.x] : -INFINITY;
+    cr[threadIdx.x] = threadIdx.x < n ? gr[threadIdx.x] : -1;
+  }
+  bitonic_desc(cs, cr);  // begins and ends with a barrier
+  if (threadIdx.x < K) {
+    gs[threadIdx.x] = cs[threadIdx.x];
+    gr[threadIdx.x] = cr[threadIdx.x];
+  }
+  if (threadIdx.x == 0) {
+    const int keep = min(n, K);
+    *cnt = keep;
+    if (keep == K) *theta = cs[K - 1];
+  }
+  __syncthreads();
+}
 
-  const int nwg = gridDim.x, wg = blockIdx.x, qtile = blockIdx.y;
+__global__ __launch_bounds__(SIM_THREADS) void cosine_stage1_kernel(
+    float* __restrict__ ws_s, int* __restrict__ ws_r, float* __restrict__ cand_s, int* __restrict__ cand_r,
+    const bf16* __restrict__ queries, const bf16* __restrict__ index, int Q, int N, int D, int K,
+    const int* __restrict__ row_prio, const uint64_t* __restrict__ row_tags,
+    const float* __restrict__ row_exp, const int* __restrict__ q_minp, const uint64_t* __restrict__ q_tags,
+    float now) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int NQT = (Q + SIM_QT - 1) / SIM_QT;
+  const int QLD = D + 8;  // padded LDS row: the 16 query rows of a B fragment hit distinct bank slots
+  bf16* qt = reinterpret_cast<bf16*>(smem);                                     // [NQT*16][QLD]
+  float* cs = reinterpret_cast<float*>(smem + (size_t)NQT * SIM_QT * QLD * 2);  // sort scratch [CAND]
+  int* cr = reinterpret_cast<int*>(cs + SIM_CAND);                            // [CAND]
+  int* cnt = cr + SIM_CAND;                                                   // [MAXQ]
+  float* theta = reinterpret_cast<float*>(cnt + SIM_MAXQ);                    // [MAXQ]
+  int* minp = reinterpret_cast<int*>(theta + SIM_MAXQ);                       // [MAXQ]
+  uint64_t* qtag = reinterpret_cast<uint64_t*>(minp + SIM_MAXQ);              // [MAXQ]
+
+  const int nwg = gridDim.x, wg = blockIdx.x;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int g = lane >> 4, col = lane & 15;
-  const int qi = qtile * SIM_QT + col;
-  const bool qvalid = qi < Q;
-  // stage the query tile into LDS (zero rows for missing queries)
-  for (int v = threadIdx.x; v < SIM_QT * D / 8; v += 256) {
+  for (int v = threadIdx.x; v < NQT * SIM_QT * D / 8; v += SIM_THREADS) {
     const int r = (v * 8) / D, c = (v * 8) % D;
-    const int qq = qtile * SIM_QT + r;
     bf16x8 x;
-    if (qq < Q) x = *reinterpret_cast<const bf16x8*>(queries + (size_t)qq * D + c);
+    if (r < Q) x = *reinterpret_cast<const bf16x8*>(queries + (size_t)r * D + c);
     else {
 #pragma unroll
       for (int j = 0; j < 8; ++j) x[j] = (bf16)0.f;
     }
-    *reinterpret_cast<bf16x8*>(qt + r * D + c) = x;
+    *reinterpret_cast<bf16x8*>(qt + (size_t)r * QLD + c) = x;
   }
-  if (threadIdx.x < SIM_QT) { cnt[threadIdx.x] = 0; theta[threadIdx.x] = -INFINITY; }
+  if (threadIdx.x < SIM_MAXQ) {
+    const int q = threadIdx.x;
+    cnt[q] = 0;
+    theta[q] = -INFINITY;
+    minp[q] = q < Q ? q_minp[q] : 0x7fffffff;
+    qtag[q] = q < Q ? q_tags[q] : 0ull;
+  }
   __syncthreads();
 
-  const int minp = qvalid ? q_minp[qi] : 0x7fffffff;
-  const uint64_t qtag = qvalid ? q_tags[qi] : 0ull;
-  // rows of this slice
+  float* my_s = cand_s + (size_t)wg * SIM_MAXQ * SIM_CAND;
+  int* my_r = cand_r + (size_t)wg * SIM_MAXQ * SIM_CAND;
   const int per = (N + nwg - 1) / nwg;
   const int r0 = wg * per, r1 = min(N, r0 + per);
   const int ngroups = (max(0, r1 - r0) + 15) / 16;
-  const int nrounds = (ngroups + 3) / 4;
+  const int nrounds = (ngroups + 7) / 8;
   const int ksteps = D / 32;
 
   for (int round = 0; round < nrounds; ++round) {
-    const int grp = round * 4 + wid;
+    const int grp = round * 8 + wid;
     if (grp < ngroups) {
       const int gbase = r0 + grp * 16;
-      // A operand: row gbase + col (clamped), dims 32m + 8g
       const int arow = min(gbase + col, N - 1);
       const bf16* ap = index + (size_t)arow * D + 8 * g;
-      const bf16* bp = qt + col * D + 8 * g;
-      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll 8
+      f32x4 acc[SIM_MAXQ / SIM_QT];
+#pragma unroll
+      for (int t = 0; t < SIM_MAXQ / SIM_QT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 16
       for (int m = 0; m < ksteps; ++m) {
         const bf16x8 a = *reinterpret_cast<const bf16x8*>(ap + 32 * m);
-        const bf16x8 b = *reinterpret_cast<const bf16x8*>(bp + 32 * m);
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc, 0, 0, 0);
-      }
-      // lane holds rows gbase + 4g + r for query col
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = gbase + 4 * g + r;
-        if (!qvalid || row >= r1) continue;
-        const float sc = acc[r];
-        if (!(sc > theta[col])) continue;
-        if (row_prio[row] < minp) continue;
-        if ((row_tags[row] & qtag) != qtag) continue;
-        const float ex = row_exp[row];
-        if (ex != 0.f && !(ex > now)) continue;
-        const int pos = atomicAdd(&cnt[col], 1);
-        if (pos < SIM_CAND) {
-          cand_s[col * SIM_CAND + pos] = sc;
-          cand_r[col * SIM_CAND + pos] = row;
+        for (int t = 0; t < SIM_MAXQ / SIM_QT; ++t) {
+          if (t < NQT) {
+            const bf16x8 b = *reinterpret_cast<const bf16x8*>(qt + (size_t)(t * SIM_QT + col) * QLD + 32 * m + 8 * g);
+            acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc[t], 0, 0, 0);
+          }
+        }
+      }
+      // lane holds rows gbase + 4g + r for queries t*16 + col
+#pragma unroll
+      for (int t = 0; t < SIM_MAXQ / SIM_QT; ++t) {
+        const int q = t * SIM_QT + col;
+        if (t >= NQT || q >= Q) continue;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = gbase + 4 * g + r;
+          const float sc = acc[t][r];
+          if (row >= r1 || !(sc > theta[q])) continue;
+          if (row_prio[row] < minp[q]) continue;
+          if ((row_tags[row] & qtag[q]) != qtag[q]) continue;
+          const float ex = row_exp[row];
+          if (ex != 0.f && !(ex > now)) continue;
+          const int pos = atomicAdd(&cnt[q], 1);
+          if (pos < SIM_CAND) {
+            my_s[q * SIM_CAND + pos] = sc;
+            my_r[q * SIM_CAND + pos] = row;
+          }
         }
       }
     }
     __syncthreads();
-    // compaction when a buffer cannot absorb another round (64 rows)
-    for (int c = 0; c < SIM_QT; ++c) {
-      if (cnt[c] > SIM_CAND - 64)
-        compact_query(cand_s + c * SIM_CAND, cand_r + c * SIM_CAND, &cnt[c], &theta[c], K);
-    }
+    // a buffer must absorb the next round (8 waves x 16 rows)
+    for (int q = 0; q < Q; ++q)
+      if (cnt[q] > SIM_CAND - 128)
+        compact_global(my_s + q * SIM_CAND, my_r + q * SIM_CAND, cs, cr, &cnt[q], &theta[q], K);
   }
   __syncthreads();
-  // final: sort every valid query's buffer and emit its top-K
-  for (int c = 0; c < SIM_QT; ++c) {
-    const int qq = qtile * SIM_QT + c;
-    if (qq >= Q) break;
-    compact_query(cand_s + c * SIM_CAND, cand_r + c * SIM_CAND, &cnt[c], &theta[c], K);
-    const int n = cnt[c];
+  for (int q = 0; q < Q; ++q) {
+    compact_global(my_s + q * SIM_CAND, my_r + q * SIM_CAND, cs, cr, &cnt[q], &theta[q], K);
+    const int n = cnt[q];
     if (threadIdx.x < K) {
-      const size_t o = ((size_t)qq * nwg + wg) * K + threadIdx.x;
-      ws_s[o] = threadIdx.x < n ? cand_s[c * SIM_CAND + threadIdx.x] : -INFINITY;
-      ws_r[o] = threadIdx.x < n ? cand_r[c * SIM_CAND + threadIdx.x] : -1;
+      const size_t o = ((size_t)q * nwg + wg) * K + threadIdx.x;
+      ws_s[o] = threadIdx.x < n ? cs[threadIdx.x] : -INFINITY;
+      ws_r[o] = threadIdx.x < n ? cr[threadIdx.x] : -1;
     }
     __syncthreads();
   }
-  (void)flag;
 }
 
 __global__ __launch_bounds__(256) void cosine_stage2_kernel(float* __restrict__ out_s,
@@ -204,10 +237,11 @@ __global__ __launch_bounds__(256) void cosine_stage2_kernel(float* __restrict__ 
 
 }  // namespace pa
 
-extern "C" int pa_cosine_topk_workspace_bytes(int Q, int N, int K) {
-  const int nwg = (N + pa::SIM_MIN_ROWS_PER_WG - 1) / pa::SIM_MIN_ROWS_PER_WG;
-  const int w = nwg > pa::SIM_MAX_WG ? pa::SIM_MAX_WG : (nwg < 1 ? 1 : nwg);
-  return Q * w * K * 8;
+// workspace = stage-1 top-k lists [Q][nwg][K] (score, row) + per-(slice, query)
+// candidate buffers [nwg][64][CAND] (score, row)
+extern "C" long long pa_cosine_topk_workspace_bytes(int Q, int N, int K) {
+  const long long w = pa::sim_num_wg(N);
+  return (long long)Q * w * K * 8 + w * pa::SIM_MAXQ * pa::SIM_CAND * 8;
 }
 
 extern "C" int pa_cosine_topk(float* out_scores, int* out_rows, void* workspace,
@@ -217,29 +251,29 @@ extern "C" int pa_cosine_topk(float* out_scores, int* out_rows, void* workspace,
                               const uint64_t* q_tags, float now, int n_valid, hipStream_t st) {
   (void)n_valid;
   if (Q <= 0) return 0;
-  if (D % 32 != 0 || D > pa::SIM_MAXD || K < 1 || K > pa::SIM_MAXK) return -1;
+  if (D % 32 != 0 || D > pa::SIM_MAXD || K < 1 || K > pa::SIM_MAXK || Q > pa::SIM_MAXQ) return -1;
   if (N <= 0) {
     // empty index: every query gets an empty result (the reference raised here;
     // SURVEY App. A #26)
-    hipMemsetAsync(out_rows, 0xff, (size_t)Q * K * sizeof(int), st);
+    (void)hipMemsetAsync(out_rows, 0xff, (size_t)Q * K * sizeof(int), st);
     return (int)hipGetLastError();
   }
-  int nwg = (N + pa::SIM_MIN_ROWS_PER_WG - 1) / pa::SIM_MIN_ROWS_PER_WG;
-  nwg = nwg > pa::SIM_MAX_WG ? pa::SIM_MAX_WG : (nwg < 1 ? 1 : nwg);
+  const int nwg = pa::sim_num_wg(N);
   float* ws_s = reinterpret_cast<float*>(workspace);
   int* ws_r = reinterpret_cast<int*>(ws_s + (size_t)Q * nwg * K);
-  const size_t lds = pa::SIM_QT * pa::SIM_MAXD * 2 + pa::SIM_QT * pa::SIM_CAND * 8 +
-                     pa::SIM_QT * 8 + 16;
+  float* cand_s = reinterpret_cast<float*>(ws_r + (size_t)Q * nwg * K);
+  int* cand_r = reinterpret_cast<int*>(cand_s + (size_t)nwg * pa::SIM_MAXQ * pa::SIM_CAND);
+  const int nqt = (Q + pa::SIM_QT - 1) / pa::SIM_QT;
+  const size_t lds = (size_t)nqt * pa::SIM_QT * (D + 8) * 2 + pa::SIM_CAND * 8 + pa::SIM_MAXQ * (4 + 4 + 4 + 8);
   static bool attr_set = false;
   if (!attr_set) {
-    hipFuncSetAttribute((const void*)pa::cosine_stage1_kernel,
-                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    (void)hipFuncSetAttribute((const void*)pa::cosine_stage1_kernel,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr_set = true;
   }
-  dim3 g1(nwg, (Q + pa::SIM_QT - 1) / pa::SIM_QT);
-  hipLaunchKernelGGL(pa::cosine_stage1_kernel, g1, dim3(256), lds, st, ws_s, ws_r,
-                     (const pa::bf16*)queries, (const pa::bf16*)index, Q, N, D, K, row_priority,
-                     row_tags, row_expiry, q_min_priority, q_tags, now);
+  hipLaunchKernelGGL(pa::cosine_stage1_kernel, dim3(nwg), dim3(pa::SIM_THREADS), lds, st, ws_s, ws_r,
+                     cand_s, cand_r, (const pa::bf16*)queries, (const pa::bf16*)index, Q, N, D, K,
+                     row_priority, row_tags, row_expiry, q_min_priority, q_tags, now);
   hipLaunchKernelGGL(pa::cosine_stage2_kernel, dim3(Q), dim3(256), 0, st, out_scores, out_rows,
                      ws_s, ws_r, nwg, K);
   return (int)hipGetLastError();

@@ -33,6 +33,7 @@ from .policy import DEFAULT_POLICY, ControlPolicy
 from .prompts import PromptManager, parse_json_response
 from .role import AgentRole, AgentStatus
 from .task import Task, TaskResult, TaskStatus
+from ..utils.timeouts import with_timeout
 
 _DEFAULT_LLM: Dict[str, Any] = {"llm": None, "factory": None}
 
@@ -306,7 +307,7 @@ class BaseAgent:
         try:
             async with lock:
                 try:
-                    result = await asyncio.wait_for(self._execute_task_internal(task), timeout=timeout)
+                    result = await with_timeout(self._execute_task_internal(task), timeout)
                 except asyncio.TimeoutError:
                     self.task_metrics["timeout"] += 1
                     self.task_metrics["failed"] += 1

@@ -99,19 +99,32 @@ class TaskResult(BaseModel):
     output: Any = None
     error: Optional[str] = None
     execution_time: float = 0.0
-    metadata: Dict[str, Any] = Field(default_factory=dict)
+    metadata: Dict[str, Any] = {}
     resources_cleaned: bool = False
-    completion_time: datetime = Field(default_factory=datetime.now)
-    _file_handles: Set[Any] = PrivateAttr(default_factory=set)
-    _temp_files: Set[Path] = PrivateAttr(default_factory=set)
+    completion_time: Optional[datetime] = None  # set at construction (model_post_init)
+    # Hot-path note: no default_factory / PrivateAttr factories here — pydantic
+    # re-inspects every factory's signature per instance, which alone cost ~40 %
+    # of the orchestration plumbing time (benchmarks/plumbing.py).
+    _file_handles: Optional[Set[Any]] = PrivateAttr(default=None)
+    _temp_files: Optional[Set[Path]] = PrivateAttr(default=None)
+
+    def model_post_init(self, __ctx):
+        if self.completion_time is None:
+            self.completion_time = datetime.now()
 
     def register_file_handle(self, h: Any):
+        if self._file_handles is None:
+            self._file_handles = set()
         self._file_handles.add(h)
 
     def register_temp_file(self, p):
+        if self._temp_files is None:
+            self._temp_files = set()
         self._temp_files.add(Path(p))
 
     def cleanup_resources(self):
+        self._file_handles = self._file_handles or set()
+        self._temp_files = self._temp_files or set()
         for h in list(self._file_handles):
             try:
                 h.close()
@@ -130,7 +143,7 @@ class TaskResult(BaseModel):
 class Task(BaseModel):
     model_config = ConfigDict(arbitrary_types_allowed=True, validate_assignment=False)
 
-    id: str = Field(default_factory=lambda: str(uuid.uuid4()))
+    id: str = ""  # a fresh uuid4 when not given (model_post_init)
     description: str
     status: TaskStatus = TaskStatus.PENDING
     priority: TaskPriority = TaskPriority.MEDIUM
@@ -139,29 +152,38 @@ class Task(BaseModel):
     retry_count: int = Field(default=0, ge=0)
     timeout: Optional[float] = None
     deadline: Optional[datetime] = None
-    created_at: datetime = Field(default_factory=datetime.now)
+    created_at: Optional[datetime] = None  # set at construction
     started_at: Optional[datetime] = None
     completed_at: Optional[datetime] = None
-    context: List["Task"] = Field(default_factory=list)
-    tools: List[str] = Field(default_factory=list)
-    config: Dict[str, Any] = Field(default_factory=dict)
-    dependencies: List[str] = Field(default_factory=list)
+    context: List["Task"] = []
+    tools: List[str] = []
+    config: Dict[str, Any] = {}
+    dependencies: List[str] = []
     output_file: Optional[Path] = None
     result: Optional[TaskResult] = None
     complexity: Optional[int] = None
-    metadata: Dict[str, Any] = Field(default_factory=dict)
+    metadata: Dict[str, Any] = {}
     # fields the reference used but never declared (App. A #15)
     parent_task_id: Optional[str] = None
-    subtasks: List[str] = Field(default_factory=list)
-    required_skills: List[str] = Field(default_factory=list)
+    subtasks: List[str] = []
+    required_skills: List[str] = []
     type: Optional[str] = None
 
-    _locks: Dict[str, asyncio.Lock] = PrivateAttr(default_factory=dict)
-    _file_handles: Set[Any] = PrivateAttr(default_factory=set)
-    _temp_files: Set[Path] = PrivateAttr(default_factory=set)
+    _locks: Optional[Dict[str, asyncio.Lock]] = PrivateAttr(default=None)
+    _file_handles: Optional[Set[Any]] = PrivateAttr(default=None)
+    _temp_files: Optional[Set[Path]] = PrivateAttr(default=None)
 
-    def __init__(self, **data):
-        super().__init__(**data)
+    def model_post_init(self, __ctx):
+        if not self.id:
+            self.id = str(uuid.uuid4())
+        if self.created_at is None:
+            self.created_at = datetime.now()
+        if self._locks is None:
+            self._locks = {}
+        if self._file_handles is None:
+            self._file_handles = set()
+        if self._temp_files is None:
+            self._temp_files = set()
         if self.id in self.dependencies:
             raise ValueError(f"Circular dependency: task {self.id} depends on itself")
 

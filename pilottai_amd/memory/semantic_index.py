@@ -125,12 +125,57 @@ class SemanticIndex:
             masks = []
             for r, ts in zip(rows, tags):
                 ts = frozenset(ts or ())
-                self.row_tags_py[r] = ts
-                masks.append(self.tags.mask(ts)[0])
+                m, exact = self.tags.mask(ts)
+                if exact:
+                    self.row_tags_py.pop(r, None)  # recoverable from the bitmask
+                else:
+                    self.row_tags_py[r] = ts       # only rows using the shared overflow bit
+                masks.append(m)
             self.tagbits.index_copy_(0, idx, torch.tensor(masks, dtype=torch.int64, device=self.device))
             exp = [0.0 if e is None else max(1e-3, float(e) - self.epoch) for e in expires_at]
             self.expiry.index_copy_(0, idx, torch.tensor(exp, dtype=torch.float32, device=self.device))
         return rows
+
+    def add_device(self, vectors: torch.Tensor, priorities: torch.Tensor, tag_masks: torch.Tensor,
+                   expiry: Optional[torch.Tensor] = None, normalized: bool = False) -> Tuple[int, int]:
+        """Bulk append from device tensors (no host round trip) — how a 100M-row
+        store is filled. `tag_masks` are bit masks over tags already registered in
+        `self.tags` (bits 0..62); `expiry` is on the index clock (0 = never).
+        Returns (first_row, n); rows wrap around the ring."""
+        n = int(vectors.shape[0])
+        if n == 0:
+            return self.size % self.capacity, 0
+        with self._lock:
+            if self.growable and self.size + n > self.capacity and self.capacity < self.max_capacity:
+                self._grow(self.size + n)
+            start = self.size % self.capacity
+            self.size += n
+            v = vectors.to(self.device)
+            if not normalized:
+                v = torch.nn.functional.normalize(v.float(), dim=1)
+            done = 0
+            while done < n:
+                r0 = (start + done) % self.capacity
+                m = min(n - done, self.capacity - r0)
+                sl = slice(r0, r0 + m)
+                self.vectors[sl].copy_(v[done:done + m])
+                self.priority[sl].copy_(priorities[done:done + m])
+                self.tagbits[sl].copy_(tag_masks[done:done + m])
+                if expiry is None:
+                    self.expiry[sl].zero_()
+                else:
+                    self.expiry[sl].copy_(expiry[done:done + m])
+                for r in [k for k in self.row_tags_py if r0 <= k < r0 + m]:
+                    self.row_tags_py.pop(r)
+                done += m
+        return start, n
+
+    def _row_tags(self, row: int) -> frozenset:
+        ts = self.row_tags_py.get(row)
+        if ts is not None:
+            return ts
+        bits = int(self.tagbits[row].item())
+        return frozenset(t for t, b in self.tags.bits.items() if (bits >> b) & 1)
 
     def delete(self, rows: Sequence[int]):
         with self._lock:
@@ -171,7 +216,7 @@ class SemanticIndex:
             for row, sc in zip(r[i], s[i]):
                 if row < 0:
                     break
-                if not exact[i] and not tag_sets[i] <= self.row_tags_py.get(int(row), frozenset()):
+                if not exact[i] and not tag_sets[i] <= self._row_tags(int(row)):
                     continue
                 res.append((int(row), float(sc)))
                 if len(res) >= k:

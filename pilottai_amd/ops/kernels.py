@@ -170,6 +170,9 @@ def sample(logits, temperature, mask_class, class_masks, seeds, offsets, forced=
     return toks
 
 
+COSINE_MAX_Q = 64  # queries per index pass (LDS-resident query tiles)
+
+
 def cosine_topk(queries, index, n_valid: int, K: int, row_priority, row_tags, row_expiry,
                 q_min_priority, q_tags, now: float, workspace: Optional[torch.Tensor] = None):
     if _on_gpu(index):
@@ -177,11 +180,16 @@ def cosine_topk(queries, index, n_valid: int, K: int, row_priority, row_tags, ro
         Q = queries.shape[0]
         out_s = torch.empty(Q, K, dtype=torch.float32, device=index.device)
         out_r = torch.empty(Q, K, dtype=torch.int32, device=index.device)
-        need = C.cosine_topk_workspace_bytes(Q, max(1, int(n_valid)), K)
+        qc = min(Q, COSINE_MAX_Q)
+        need = C.cosine_topk_workspace_bytes(qc, max(1, int(n_valid)), K)
         if workspace is None or workspace.numel() * workspace.element_size() < need:
             workspace = torch.empty(max(need, 16), dtype=torch.uint8, device=index.device)
-        C.cosine_topk(out_s, out_r, workspace, queries, index, int(n_valid), int(K), row_priority,
-                      row_tags, row_expiry, q_min_priority, q_tags, float(now))
+        # one pass over the index per <= 64 queries (csrc/ops/similarity.hip)
+        for q0 in range(0, Q, COSINE_MAX_Q):
+            q1 = min(Q, q0 + COSINE_MAX_Q)
+            C.cosine_topk(out_s[q0:q1], out_r[q0:q1], workspace, queries[q0:q1].contiguous(), index,
+                          int(n_valid), int(K), row_priority, row_tags, row_expiry,
+                          q_min_priority[q0:q1].contiguous(), q_tags[q0:q1].contiguous(), float(now))
         return out_s, out_r
     return ref.cosine_topk(queries, index, n_valid, K, row_priority, row_tags, row_expiry,
                            q_min_priority, q_tags, now)

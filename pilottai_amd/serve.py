@@ -39,6 +39,7 @@ from .core.prompts import PromptManager, parse_json_response
 from .core.role import AgentStatus
 from .core.router import TaskRouter
 from .core.task import Task, TaskPriority, TaskResult, TaskStatus
+from .utils.timeouts import with_timeout
 
 
 class ServeConfig(BaseModel):
@@ -119,6 +120,7 @@ class Serve:
         self._agent_cv: Optional[asyncio.Condition] = None
         self._waiting_on: Dict[str, List[Task]] = defaultdict(list)
         self._workers: List[asyncio.Task] = []
+        self._active = 0  # tasks executing (worker loop + caller-runs path)
         self._cleanup_task: Optional[asyncio.Task] = None
         self._services: List[Any] = []
         self._shutting_down = False
@@ -280,6 +282,9 @@ class Serve:
 
     # ------------------------------------------------------------------ submit
     async def add_task(self, task: Union[Task, Dict[str, Any], str]) -> str:
+        return await self._submit(task, inline=False)
+
+    async def _submit(self, task: Union[Task, Dict[str, Any], str], inline: bool) -> str:
         if self._shutting_down:
             raise RuntimeError("Orchestrator is shutting down")
         if not self._started:
@@ -302,12 +307,25 @@ class Serve:
                 for st in subtasks:
                     await self._enqueue(st)
                 return task.id
+        if inline and self._queue.empty() and self._active < self.config.max_concurrent_tasks \
+                and not any(d in self.tasks and d not in self.completed_tasks for d in task.dependencies):
+            # caller-runs: a free concurrency slot and nothing queued ahead — run the
+            # task in the caller's coroutine (no queue hop, no worker wake-up); the
+            # slot accounting, timeout, evaluation and callbacks are the worker's
+            self._active += 1
+            try:
+                await self._run(task)
+            except Exception as e:  # noqa: BLE001 — as the worker loop
+                self._finish(task, TaskResult(success=False, error=str(e)))
+            finally:
+                self._active -= 1
+            return task.id
         await self._enqueue(task)
         return task.id
 
     async def execute_task(self, task: Union[Task, Dict[str, Any], str], timeout: Optional[float] = None) -> TaskResult:
         """Documented API: submit and wait for the TaskResult."""
-        tid = await self.add_task(task)
+        tid = await self._submit(task, inline=timeout is None)
         return await self.wait_for(tid, timeout)
 
     async def wait_for(self, task_id: str, timeout: Optional[float] = None) -> TaskResult:
@@ -317,6 +335,8 @@ class Serve:
             if r is None:
                 raise KeyError(task_id)
             return r
+        if timeout is None:
+            return await asyncio.shield(fut)
         return await asyncio.wait_for(asyncio.shield(fut), timeout)
 
     async def _enqueue(self, task: Task):
@@ -351,6 +371,7 @@ class Serve:
     async def _worker(self, idx: int):
         while True:
             _, _, task = await self._queue.get()
+            self._active += 1
             try:
                 if task.id in self.tasks and task.status not in (TaskStatus.CANCELLED,):
                     await self._run(task)
@@ -360,12 +381,13 @@ class Serve:
                 self.logger.error("task %s failed: %s", task.id, e)
                 self._finish(task, TaskResult(success=False, error=str(e)))
             finally:
+                self._active -= 1
                 self._queue.task_done()
 
     async def _run(self, task: Task):
         t_start = time.perf_counter()
         try:
-            result = await asyncio.wait_for(self._execute_task(task), timeout=self.config.task_timeout)
+            result = await with_timeout(self._execute_task(task), self.config.task_timeout)
         except asyncio.TimeoutError:
             self.metrics["timeout_tasks"] += 1
             result = TaskResult(success=False, error="Task execution timed out",

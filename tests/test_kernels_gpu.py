@@ -193,9 +193,9 @@ def test_sample_distribution(gpu):
     assert (emp - exp).abs().max().item() < 0.03
 
 
-def test_cosine_topk(gpu):
+@pytest.mark.parametrize("N,D,Q,K", [(20000, 1024, 5, 8), (150000, 256, 70, 64), (3000, 768, 17, 10)])
+def test_cosine_topk(gpu, N, D, Q, K):
     torch.manual_seed(6)
-    N, D, Q, K = 20000, 1024, 5, 8
     idx = torch.nn.functional.normalize(torch.randn(N, D), dim=1).to(torch.bfloat16)
     qs = torch.nn.functional.normalize(torch.randn(Q, D), dim=1).to(torch.bfloat16)
     qs[1] = idx[1234]  # exact hit
@@ -203,8 +203,8 @@ def test_cosine_topk(gpu):
     tags = torch.randint(0, 8, (N,), dtype=torch.int64)
     exp = torch.zeros(N)
     exp[::7] = 50.0  # expired at now=100
-    qmin = torch.tensor([0, 0, 2, 4, 0], dtype=torch.int32)
-    qt = torch.tensor([0, 0, 1, 2, 3], dtype=torch.int64)
+    qmin = torch.tensor([0, 0, 2, 4, 0] * ((Q + 4) // 5), dtype=torch.int32)[:Q]
+    qt = torch.tensor([0, 0, 1, 2, 3] * ((Q + 4) // 5), dtype=torch.int64)[:Q]
     s, r = ops.cosine_topk(qs.to(gpu), idx.to(gpu), N, K, prio.to(gpu), tags.to(gpu), exp.to(gpu),
                            qmin.to(gpu), qt.to(gpu), 100.0)
     rs, rr = ref.cosine_topk(qs, idx, N, K, prio, tags, exp, qmin, qt, 100.0)
