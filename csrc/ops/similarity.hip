@@ -23,13 +23,14 @@
 
 namespace pa {
 
-constexpr int SIM_CAND = 256;     // candidate buffer per (slice, query), power of two
+constexpr int SIM_CAND = 512;     // candidate buffer per (slice, query), power of two
 constexpr int SIM_MAXK = 64;
 constexpr int SIM_QT = 16;        // queries per MFMA tile (N = 16)
 constexpr int SIM_MAXQ = 64;      // queries per pass (4 tiles resident in LDS)
 constexpr int SIM_MAXD = 1024;    // LDS query capacity per query (bf16)
-constexpr int SIM_THREADS = 512;  // 8 waves
+constexpr int SIM_THREADS = 1024; // 16 waves: 128 KB of row loads in flight per CU
 constexpr int SIM_MIN_ROWS_PER_WG = 2048;
+constexpr int SIM_KB = 4;         // k-steps of row loads issued ahead per batch
 constexpr int SIM_MAX_WG = 256;    // one resident workgroup per CU: the threshold warm-up is paid once per CU
 
 __host__ __device__ inline int sim_num_wg(int N) {
@@ -39,7 +40,7 @@ __host__ __device__ inline int sim_num_wg(int N) {
   return nwg;
 }
 
-// Sort cand_s/cand_r[0..SIM_CAND) descending by score (whole workgroup, 256 threads).
+// Sort cand_s/cand_r[0..SIM_CAND) descending by score (whole workgroup, >= SIM_CAND threads).
 __device__ void bitonic_desc(float* cs, int* cr) {
   for (int k = 2; k <= SIM_CAND; k <<= 1) {
     for (int j = k >> 1; j > 0; j >>= 1) {
@@ -138,11 +139,12 @@ __global__ __launch_bounds__(SIM_THREADS) void cosine_stage1_kernel(
   const int per = (N + nwg - 1) / nwg;
   const int r0 = wg * per, r1 = min(N, r0 + per);
   const int ngroups = (max(0, r1 - r0) + 15) / 16;
-  const int nrounds = (ngroups + 7) / 8;
+  constexpr int NW = SIM_THREADS / 64;
+  const int nrounds = (ngroups + NW - 1) / NW;
   const int ksteps = D / 32;
 
   for (int round = 0; round < nrounds; ++round) {
-    const int grp = round * 8 + wid;
+    const int grp = round * NW + wid;
     if (grp < ngroups) {
       const int gbase = r0 + grp * 16;
       const int arow = min(gbase + col, N - 1);
@@ -150,8 +152,27 @@ __global__ __launch_bounds__(SIM_THREADS) void cosine_stage1_kernel(
       f32x4 acc[SIM_MAXQ / SIM_QT];
 #pragma unroll
       for (int t = 0; t < SIM_MAXQ / SIM_QT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll 16
-      for (int m = 0; m < ksteps; ++m) {
+      // batches of SIM_KB k-steps: independent 16-B row loads in flight per lane
+      // (16 waves x SIM_KB KB per CU) before their MFMAs consume them
+      int m = 0;
+      for (; m + SIM_KB <= ksteps; m += SIM_KB) {
+        bf16x8 av[SIM_KB];
+#pragma unroll
+        for (int u = 0; u < SIM_KB; ++u) av[u] = __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(ap + 32 * (m + u)));
+#pragma unroll
+        for (int u = 0; u < SIM_KB; ++u) {
+#pragma unroll
+          for (int t = 0; t < SIM_MAXQ / SIM_QT; ++t) {
+            if (t < NQT) {
+              const bf16x8 b = *reinterpret_cast<const bf16x8*>(qt + (size_t)(t * SIM_QT + col) * QLD + 32 * (m + u) + 8 * g);
+              acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[u], b, acc[t], 0, 0, 0);
+            }
+          }
+          // one k-step's B reads live at a time (the row loads stay in flight)
+          asm volatile("" ::: "memory");
+        }
+      }
+      for (; m < ksteps; ++m) {
         const bf16x8 a = *reinterpret_cast<const bf16x8*>(ap + 32 * m);
 #pragma unroll
         for (int t = 0; t < SIM_MAXQ / SIM_QT; ++t) {
@@ -184,9 +205,9 @@ __global__ __launch_bounds__(SIM_THREADS) void cosine_stage1_kernel(
       }
     }
     __syncthreads();
-    // a buffer must absorb the next round (8 waves x 16 rows)
+    // a buffer must absorb the next round (NW waves x 16 rows)
     for (int q = 0; q < Q; ++q)
-      if (cnt[q] > SIM_CAND - 128)
+      if (cnt[q] > SIM_CAND - NW * 16)
         compact_global(my_s + q * SIM_CAND, my_r + q * SIM_CAND, cs, cr, &cnt[q], &theta[q], K);
   }
   __syncthreads();
@@ -202,7 +223,7 @@ __global__ __launch_bounds__(SIM_THREADS) void cosine_stage1_kernel(
   }
 }
 
-__global__ __launch_bounds__(256) void cosine_stage2_kernel(float* __restrict__ out_s,
+__global__ __launch_bounds__(SIM_CAND) void cosine_stage2_kernel(float* __restrict__ out_s,
                                                             int* __restrict__ out_r,
                                                             const float* __restrict__ ws_s,
                                                             const int* __restrict__ ws_r,
@@ -274,7 +295,7 @@ extern "C" int pa_cosine_topk(float* out_scores, int* out_rows, void* workspace,
   hipLaunchKernelGGL(pa::cosine_stage1_kernel, dim3(nwg), dim3(pa::SIM_THREADS), lds, st, ws_s, ws_r,
                      cand_s, cand_r, (const pa::bf16*)queries, (const pa::bf16*)index, Q, N, D, K,
                      row_priority, row_tags, row_expiry, q_min_priority, q_tags, now);
-  hipLaunchKernelGGL(pa::cosine_stage2_kernel, dim3(Q), dim3(256), 0, st, out_scores, out_rows,
+  hipLaunchKernelGGL(pa::cosine_stage2_kernel, dim3(Q), dim3(pa::SIM_CAND), 0, st, out_scores, out_rows,
                      ws_s, ws_r, nwg, K);
   return (int)hipGetLastError();
 }
