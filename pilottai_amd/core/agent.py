@@ -28,6 +28,21 @@ from typing import Any, Callable, Deque, Dict, List, Optional, Sequence, Union
 
 import psutil
 
+_PROC = psutil.Process()
+_NCPU = max(1, len(_PROC.cpu_affinity()) if hasattr(_PROC, "cpu_affinity") else (psutil.cpu_count() or 1))
+_CPU_SAMPLE = [0.0, 0.0]  # [monotonic time, value]
+
+
+def _process_cpu_share() -> float:
+    """This process's CPU share in [0, 1], sampled at most every 0.5 s (psutil's
+    interval-free reading is garbage when calls are microseconds apart, which is
+    exactly what many agents reporting metrics back to back produce)."""
+    now = time.monotonic()
+    if now - _CPU_SAMPLE[0] >= 0.5:
+        _CPU_SAMPLE[1] = min(1.0, max(0.0, _PROC.cpu_percent(interval=None) / (100.0 * _NCPU)))
+        _CPU_SAMPLE[0] = now
+    return _CPU_SAMPLE[1]
+
 from .config import AgentConfig, LLMConfig
 from .policy import DEFAULT_POLICY, ControlPolicy
 from .prompts import PromptManager, parse_json_response
@@ -486,7 +501,9 @@ class BaseAgent:
     # ------------------------------------------------------------------ metrics
     async def get_metrics(self) -> Dict[str, Any]:
         done = self.task_metrics["completed"] + self.task_metrics["failed"]
-        cpu = psutil.cpu_percent(interval=None) / 100.0
+        # this process's CPU share, not the whole machine's (the reference used
+        # system-wide psutil, so load from unrelated processes marked agents busy)
+        cpu = _process_cpu_share()
         mem = psutil.virtual_memory().percent / 100.0
         m = {
             "queue_size": len(self.tasks),
@@ -504,6 +521,8 @@ class BaseAgent:
         eng = getattr(getattr(self._llm, "engine", None), "metrics", None)
         if callable(eng):
             em = eng()
+            # a full KV cache throttles delegation (TaskDelegator) but is not a fault:
+            # it stays out of resource_usage, which FaultTolerance acts on
             m["kv_cache_utilization"] = 1.0 - em["free_kv_blocks"] / max(1, em["total_kv_blocks"])
         return m
 

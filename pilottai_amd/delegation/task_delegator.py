@@ -135,6 +135,9 @@ class TaskDelegator:
         best, best_s = None, 0.0
         for aid, a in self._get_available_agents().items():
             try:
+                # an agent that declares it cannot do the task is never chosen
+                if await a.evaluate_task_suitability(t) <= 0.0:
+                    continue
                 if not await self._can_accept_task(a):
                     continue
                 s = await asyncio.wait_for(self._calculate_total_score(a, t), 10)
