@@ -108,6 +108,7 @@ class Serve:
         self.agents: Dict[str, BaseAgent] = {}
         self._started = False
         self._idle: Deque[str] = deque()
+        self._inflight: Dict[str, int] = {}  # tasks running per agent (capacity accounting)
         for a in agents or []:
             self._register_agent(a)
         self.tasks: Dict[str, Task] = {}
@@ -482,6 +483,15 @@ class Serve:
         st = str(getattr(a, "status", "idle"))
         return st == "idle" and getattr(a, "accepting_tasks", True)
 
+    @staticmethod
+    def _capacity(a: BaseAgent) -> int:
+        """Tasks an agent may run at once: 1 (the reference's busy/idle model) unless
+        the agent declares `concurrent_safe` (e.g. a delegating workflow manager,
+        whose work happens in its children), then its config.max_concurrent_tasks."""
+        if getattr(a, "concurrent_safe", False):
+            return max(1, int(getattr(getattr(a, "config", None), "max_concurrent_tasks", 1)))
+        return 1
+
     async def _notify_agents(self):
         if self._agent_cv is not None:
             async with self._agent_cv:
@@ -497,7 +507,10 @@ class Serve:
             while True:
                 agent = self._pick_idle(task, prefer)
                 if agent is not None:
-                    agent.status = AgentStatus.BUSY  # reserved atomically (App. A #12)
+                    n = self._inflight.get(agent.id, 0) + 1
+                    self._inflight[agent.id] = n
+                    if n >= self._capacity(agent):
+                        agent.status = AgentStatus.BUSY  # reserved atomically (App. A #12)
                     return agent
                 left = deadline - time.monotonic()
                 if left <= 0:
@@ -521,12 +534,19 @@ class Serve:
             if a is None:
                 continue
             if self._is_available(a):
+                if self._inflight.get(aid, 0) + 1 < self._capacity(a):
+                    self._idle.append(aid)  # still has free capacity: stays schedulable
                 return a
             if str(a.status) not in ("stopped", "error"):
                 self._idle.append(aid)  # paused (LoadBalancer): keep it, skip it
         return None
 
     async def _release_agent(self, agent: BaseAgent):
+        n = self._inflight.get(agent.id, 1) - 1
+        if n > 0:
+            self._inflight[agent.id] = n
+        else:
+            self._inflight.pop(agent.id, None)
         if agent.id in self.agents:
             if str(agent.status) == "busy" and getattr(agent, "accepting_tasks", True) and not agent.active_tasks:
                 agent.status = AgentStatus.IDLE

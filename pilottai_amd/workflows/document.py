@@ -75,6 +75,8 @@ class StageAgent(BaseAgent):
 
 
 class WorkflowManager(BaseAgent):
+    concurrent_safe = True  # delegates: many workflows may run through one manager
+
     def __init__(self, *a, stage_retries: int = 3, **kw):
         super().__init__(*a, **kw)
         self.delegator = TaskDelegator(self)
@@ -136,7 +138,7 @@ def _stage_agent(stage: str, role: str, llm) -> StageAgent:
 async def build_document_workflow(llm, replicas: int = 2) -> Tuple[WorkflowManager, List[StageAgent]]:
     mgr = WorkflowManager(AgentConfig(role="workflow-manager", role_type=AgentRole.ORCHESTRATOR,
                                       goal="Run extract -> analyze -> summarize", can_delegate=True,
-                                      max_child_agents=64), llm=llm)
+                                      max_child_agents=64, max_concurrent_tasks=1024), llm=llm)
     kids = []
     for stage in STAGES:
         for r in range(replicas):
