@@ -58,6 +58,7 @@ def parse():
     ap.add_argument("--temperature", type=float, default=0.7)
     ap.add_argument("--steps-per-task", type=int, default=1)
     ap.add_argument("--token-align", type=int, default=256, help="GEMM-friendly step sizes (0 = off)")
+    ap.add_argument("--align-slack", type=int, default=96)
     ap.add_argument("--cpu", action="store_true", help="tiny model on CPU (plumbing smoke only)")
     return ap.parse_args()
 
@@ -82,7 +83,7 @@ async def run_rank(a, rank: int, world: int, device):
     eng = LLMEngine(EngineConfig(model=a.model if not a.cpu else "tiny", max_num_seqs=max(64, 2 * n_local),
                                  max_num_batched_tokens=a.max_batched_tokens, kv_cache_gb=a.kv_gb if not a.cpu else None,
                                  num_kv_blocks=4096 if a.cpu else None, seed=1234 + rank,
-                                 token_align=a.token_align), device=device)
+                                 token_align=a.token_align, align_slack=a.align_slack), device=device)
     register_engine(eng.model_cfg.name, eng)
     eng.start()
     llm = LocalLLM(LLMConfig(model_name=eng.model_cfg.name, temperature=a.temperature, max_tokens=1024,
@@ -125,6 +126,7 @@ async def run_rank(a, rank: int, world: int, device):
         await round_(a.warmup, False)
     st0 = dict(eng.stats)
     u0 = dict(llm.usage)
+    n_timed0 = len(eng.timings)
     comm.barrier()
     if device.type == "cuda":
         torch.cuda.synchronize()
@@ -148,6 +150,7 @@ async def run_rank(a, rank: int, world: int, device):
         "busy_s": st1["busy_s"] - st0["busy_s"], "prefix_hit": em["prefix_cache_hit_tokens"],
         "bucket_tokens": st1["bucket_tokens"] - st0["bucket_tokens"],
         "prompt_total": em["prompt_tokens"], "hbm_used_gb": em.get("hbm_used_gb", 0.0),
+        "req_lat": eng.latency_summary(n_timed0),
     }
     return local
 
@@ -181,6 +184,7 @@ def main():
         p50 = lats[len(lats) // 2] if lats else 0.0
         p99 = lats[min(len(lats) - 1, int(0.99 * len(lats)))] if lats else 0.0
         tot = lambda k: sum(g[k] for g in gathered)  # noqa: E731
+        lat0 = gathered[0]["req_lat"]  # rank 0's request timings (per-GPU engines are alike)
         calls = max(1, tot("calls"))
         value = tasks / dt if dt > 0 else 0.0
         out = {
@@ -218,6 +222,8 @@ def main():
             "engine_busy_frac": round(tot("busy_s") / (dt * len(gathered)), 3),
             "prefix_cache_hit_frac": round(tot("prefix_hit") / max(1, tot("prompt_total")), 3),
             "graph_pad_frac": round(1 - tot("tokens") / max(1, tot("bucket_tokens")), 3),
+            "ttft_p50_ms": round(lat0.get("ttft_p50_ms") or 0.0, 1),
+            "tpot_p50_ms": round(lat0.get("tpot_p50_ms") or 0.0, 2),
             "init_s": round(max(g["init_s"] for g in gathered), 1),
             "hbm_used_gb_per_gpu": round(max(g["hbm_used_gb"] for g in gathered), 1),
             "notes": "BASELINE.md publishes no number for this config (vs_baseline null); the reference's "

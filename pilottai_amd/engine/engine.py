@@ -30,6 +30,7 @@ from __future__ import annotations
 
 import logging
 import queue
+from collections import deque
 import threading
 import time
 from dataclasses import dataclass, field
@@ -231,6 +232,7 @@ class LLMEngine:
         self._thread: Optional[threading.Thread] = None
         self._stop = False
         self._err: Optional[BaseException] = None
+        self.timings: "deque" = deque(maxlen=1 << 20)  # (ttft_s, tpot_s, output_tokens) per request
         self.stats = {"steps": 0, "tokens": 0, "sampled": 0, "requests": 0, "finished": 0,
                       "busy_s": 0.0, "prefill_tokens": 0, "decode_steps": 0, "graph_replays": 0,
                       "bucket_tokens": 0}
@@ -415,6 +417,24 @@ class LLMEngine:
             raise RuntimeError(f"engine failed: {self._err!r}")
         return [results[i] for i in ids]
 
+    def prewarm(self, prompt_ids: Sequence[int], timeout: float = 300.0) -> int:
+        """Compute and cache the KV of `prompt_ids` (prefix cache) without keeping
+        the request; returns the number of prompt tokens. Works with or without
+        the engine thread running."""
+        if self._thread is None:
+            return self.generate([list(prompt_ids)], temperature=0.0, max_tokens=1, ignore_eos=True)[0].prompt_tokens
+        done = threading.Event()
+        box = {}
+
+        def cb(o):
+            box["o"] = o
+            done.set()
+
+        self.submit(list(prompt_ids), cb, temperature=0.0, max_tokens=1, ignore_eos=True)
+        if not done.wait(timeout):
+            raise TimeoutError("prewarm did not finish")
+        return box["o"].prompt_tokens
+
     def start(self):
         if self._thread is not None:
             return
@@ -503,6 +523,10 @@ class LLMEngine:
             return
         out = GenerationOutput(rid, list(toks), _REASONS.get(reason, "stop"), plen, cached, len(toks),
                                nsamp, nforced, req.t_arrival, t_first, t_fin, self.tok)
+        # per-request timings: TTFT = arrival -> first token, TPOT = later tokens' mean gap
+        if t_first > 0:
+            n_out = max(1, len(toks))
+            self.timings.append((out.ttft, (t_fin - t_first) / max(1, n_out - 1), n_out))
         try:
             req.callback(out)
         except Exception:  # noqa: BLE001 — a bad callback must not kill the engine
@@ -571,6 +595,17 @@ class LLMEngine:
                     pass
 
     # ------------------------------------------------------------------ info
+    def latency_summary(self, since: int = 0) -> dict:
+        """p50/p99 TTFT and TPOT (ms) over requests finished after index `since`."""
+        tm = list(self.timings)[since:]
+        if not tm:
+            return {}
+        ttft = sorted(t[0] for t in tm)
+        tpot = sorted(t[1] for t in tm if t[2] > 1)
+        pick = lambda v, q: 1000 * v[min(len(v) - 1, int(q * len(v)))] if v else None  # noqa: E731
+        return {"requests": len(tm), "ttft_p50_ms": pick(ttft, 0.5), "ttft_p99_ms": pick(ttft, 0.99),
+                "tpot_p50_ms": pick(tpot, 0.5), "tpot_p99_ms": pick(tpot, 0.99)}
+
     def metrics(self) -> dict:
         s = self.sched
         st = dict(self.stats)

@@ -172,6 +172,9 @@ class LocalLLM(BaseLLM):
 
             engine = get_engine(self.model_name)
         self.engine = engine
+        # node-wide shared context (Serve.broadcast_context): a leading system
+        # message whose KV every GPU pre-warmed into its prefix cache
+        self.shared_context: Optional[str] = None
         self.tok: Tokenizer = engine.tok
         if engine._thread is None:
             engine.start()
@@ -188,6 +191,8 @@ class LocalLLM(BaseLLM):
             fixed = response_format.get("fixed")
             if schema is not None:
                 grammar = self.engine.grammar.compile(schema, fixed)
+        if self.shared_context:
+            messages = [{"role": "system", "content": self.shared_context}] + list(messages)
         ids = encode_chat(self.tok, messages)
         loop = asyncio.get_running_loop()
         fut = loop.create_future()

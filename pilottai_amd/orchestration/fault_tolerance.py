@@ -87,7 +87,8 @@ class GPUHealthProbe:
         if getattr(eng, "failed", None) is not None:
             return f"engine failed: {eng.failed!r}"
         steps = eng.stats.get("steps", 0)
-        busy = eng.sched.has_work() if hasattr(eng, "sched") else False
+        busy = (eng.sched.has_work() if hasattr(eng, "sched") else False) or \
+            not getattr(eng, "_inbox", None) is None and not eng._inbox.empty()
         now = time.monotonic()
         prev = self._last.get(id(eng))
         if prev is None or prev[0] != steps or not busy:

@@ -139,6 +139,21 @@ def broadcast_object(obj, src: int = 0):
     return lst[0]
 
 
+def broadcast_tokens(ids: Optional[List[int]], src: int = 0) -> List[int]:
+    """Shared-context broadcast: token ids from `src` to every rank,
+    as two tensor broadcasts (length, ids) — RCCL over xGMI on GPUs, gloo on CPU."""
+    if not dist.is_initialized():
+        return list(ids or [])
+    dev = _coll_device()
+    n = torch.tensor([len(ids) if dist.get_rank() == src else 0], dtype=torch.int64, device=dev)
+    dist.broadcast(n, src=src)
+    buf = torch.tensor(ids, dtype=torch.int32, device=dev) if dist.get_rank() == src else \
+        torch.empty(int(n.item()), dtype=torch.int32, device=dev)
+    if int(n.item()) > 0:
+        dist.broadcast(buf, src=src)
+    return buf.cpu().tolist()
+
+
 def _coll_device():
     if dist.is_initialized() and dist.get_backend() == "nccl":
         return torch.device("cuda", torch.cuda.current_device())

@@ -642,6 +642,35 @@ class Serve:
     async def get_result(self, task_id: str) -> Optional[TaskResult]:
         return self.completed_tasks.get(task_id) or self.failed_tasks.get(task_id)
 
+    async def broadcast_context(self, text: Optional[str] = None, src: int = 0) -> Dict[str, Any]:
+        """Shared-context broadcast. Collective over the world group:
+        every rank calls it; rank `src` supplies `text`. The text travels as token
+        ids (RCCL over xGMI), each rank's engines pre-compute its KV into their
+        prefix caches, and every LLM of this Serve puts it at the front of its
+        prompts, so all later agent calls on every GPU reuse those blocks."""
+        from .engine.local_llm import encode_chat
+        from .engine.tokenizer import get_tokenizer
+        from .parallel import comm
+
+        llms = [self.manager_llm] + [vars(a).get("_llm") for a in self.agents.values()]
+        llms = list({id(x): x for x in llms if x is not None}.values())
+        engines = list({id(e): e for e in (getattr(x, "engine", None) for x in llms) if e is not None}.values())
+        tok = engines[0].tok if engines else get_tokenizer()
+        rank = comm.env_rank_world()[0] if comm.dist.is_initialized() else 0
+        ids = comm.broadcast_tokens(tok.encode(text or "") if rank == src else None, src=src)
+        ctx = tok.decode(ids)
+        for x in llms:
+            if hasattr(x, "shared_context"):
+                x.shared_context = ctx or None
+        prewarmed = 0
+        if ctx:
+            msg = encode_chat(tok, [{"role": "system", "content": ctx}])
+            for e in engines:
+                await asyncio.to_thread(e.prewarm, msg)
+                prewarmed += 1
+        self.shared_context = ctx
+        return {"tokens": len(ids), "prewarmed_engines": prewarmed}
+
     def get_metrics(self) -> Dict[str, Any]:
         m = {
             "name": self.config.name,
