@@ -42,6 +42,7 @@ import torch
 from pilottai_amd import ops
 from pilottai_amd.models.llama import KVCache, LlamaModel, StepMeta, get_config
 from pilottai_amd.parallel.comm import TPGroup
+from pilottai_amd.utils.tracing import trace_range
 
 from .grammar import MAX_CLASSES, GrammarCompiler
 from .tokenizer import Tokenizer, get_tokenizer
@@ -539,7 +540,8 @@ class LLMEngine:
             return False
         L = self.L
         t0 = time.perf_counter()
-        T = self.sched.schedule(self._host_ptr)
+        with trace_range("engine.schedule"):
+            T = self.sched.schedule(self._host_ptr)
         if T == 0:
             if self.sched.num_running == 0 and self.sched.num_waiting > 0:
                 raise RuntimeError("KV cache too small for the head request")
@@ -557,13 +559,14 @@ class LLMEngine:
             if masks_changed:
                 self.tp.broadcast(self._class_masks)
             self.tp.broadcast(self._dev_meta[:n_copy])
-        with torch.inference_mode():
+        with torch.inference_mode(), trace_range("engine.forward"):
             self._run(bucket, ns, trunc, n_copy)
         if nsamp:
             self._sampled_host[:nsamp].copy_(self._sampled_dev[:nsamp], non_blocking=self.on_gpu)
         if self.on_gpu:
             torch.cuda.current_stream().synchronize()
-        outs = self.sched.commit(self._sampled_host.data_ptr(), nsamp)
+        with trace_range("engine.commit"):
+            outs = self.sched.commit(self._sampled_host.data_ptr(), nsamp)
         st = self.stats
         st["steps"] += 1
         st["tokens"] += T

@@ -34,7 +34,7 @@ from .core.agent import BaseAgent, _content, _resolve_default_llm
 from .core.config import AgentConfig, LLMConfig
 from .core.factory import AgentFactory
 from .core.memory import Memory
-from .core.policy import ControlPolicy
+from .core.policy import DEFAULT_POLICY, ControlPolicy
 from .core.prompts import PromptManager, parse_json_response
 from .core.role import AgentStatus
 from .core.router import TaskRouter
@@ -148,6 +148,9 @@ class Serve:
         return self._manager_llm
 
     def _register_agent(self, agent: BaseAgent):
+        # a Serve-level control policy applies to agents that did not pick one
+        if self.config.policy != "model" and getattr(agent, "policy", None) is DEFAULT_POLICY:
+            agent.policy = self.policy
         self.agents[agent.id] = agent
         if step := self.step_callback:
             if getattr(agent, "step_callback", None) is None:
@@ -167,7 +170,7 @@ class Serve:
         elif self._started and str(getattr(agent, "status", "")) == "stopped":
             await agent.start()
         if getattr(agent, "policy", None) is not None and self.config.policy != "model":
-            agent.policy = self.policy
+            agent.policy = self.policy  # agents created for this Serve follow its policy
         self._register_agent(agent)
         await self._notify_agents()
         return agent
