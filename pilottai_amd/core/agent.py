@@ -81,6 +81,10 @@ def _short(x: Any, n: int = 400) -> Any:
     return x if len(s) <= n else s[:n] + "..."
 
 
+def _is_workflow(task: Task) -> bool:
+    return (task.type or task.metadata.get("type")) == "complex_workflow" and bool(task.metadata.get("steps"))
+
+
 class BaseAgent:
     TASK_TIMEOUT = 300.0
     MAX_HISTORY_SIZE = 100
@@ -322,7 +326,8 @@ class BaseAgent:
         try:
             async with lock:
                 try:
-                    result = await with_timeout(self._execute_task_internal(task), timeout)
+                    body = self._execute_workflow(task) if _is_workflow(task) else self._execute_task_internal(task)
+                    result = await with_timeout(body, timeout)
                 except asyncio.TimeoutError:
                     self.task_metrics["timeout"] += 1
                     self.task_metrics["failed"] += 1
@@ -349,6 +354,34 @@ class BaseAgent:
             if self.status == AgentStatus.BUSY and not self.active_tasks:
                 self.status = AgentStatus.IDLE if self._accepting else AgentStatus.BUSY
             self.last_heartbeat = datetime.now()
+
+    async def _execute_workflow(self, task: Task) -> TaskResult:
+        """Documented orchestration form (reference README.md:143-146):
+        `execute_task({"type": "complex_workflow", "steps": ["extract", "analyze", ...]})`.
+        Steps run in order; each goes to the child agent specialised in it (or the
+        most suitable child), else this agent runs it; a step sees the previous
+        step's output in its metadata. Output: {step: output}."""
+        t0 = time.perf_counter()
+        outputs: Dict[str, Any] = {}
+        prev: Any = None
+        for i, step in enumerate(task.metadata.get("steps") or []):
+            name = step if isinstance(step, str) else str(step.get("type", f"step{i}"))
+            sub = Task(description=f"{name}: {task.description}",
+                       metadata={"type": name, "previous_output": prev, "workflow_id": task.id})
+            child = self._child_for(name)
+            res = await (child.execute_task(sub) if child is not None else self._execute_task_internal(sub))
+            if not res.success:
+                return TaskResult(success=False, output=outputs, error=f"step {name} failed: {res.error}",
+                                  execution_time=time.perf_counter() - t0)
+            outputs[name] = prev = res.output
+        return TaskResult(success=True, output=outputs, execution_time=time.perf_counter() - t0)
+
+    def _child_for(self, step: str) -> Optional["BaseAgent"]:
+        live = [a for a in self.child_agents.values() if str(a.status) not in ("stopped", "error")]
+        for a in live:
+            if step in (a.config.specializations or []) or a.config.role == step:
+                return a
+        return None
 
     async def _execute_task_internal(self, task: Task) -> TaskResult:
         t0 = time.perf_counter()

@@ -298,3 +298,33 @@ async def test_serve_orchestrator_protocol():
     await s.remove_child_agent(n.id)
     assert n.id not in s.child_agents
     await s.stop()
+
+
+def test_complex_workflow_steps_go_to_specialised_children():
+    """README.md:143-146 of the reference: manager.execute_task({"type": "complex_workflow", "steps": [...]})."""
+    import asyncio
+
+    from pilottai_amd.core.agent import BaseAgent
+    from pilottai_amd.core.config import AgentConfig, LLMConfig
+    from pilottai_amd.core.policy import ControlPolicy
+    from pilottai_amd.core.task import TaskResult
+    from pilottai_amd.engine.local_llm import SchemaLLM
+
+    seen = []
+
+    class Worker(BaseAgent):
+        async def _execute_task_internal(self, task):
+            seen.append((self.config.role, task.metadata["type"], task.metadata["previous_output"]))
+            return TaskResult(success=True, output=f"{self.config.role}-out")
+
+    async def main():
+        llm = SchemaLLM(LLMConfig(provider="schema"))
+        mgr = BaseAgent(AgentConfig(role="manager", goal="g", max_child_agents=4), llm=llm, policy=ControlPolicy("fixed"))
+        for s in ("extract", "analyze", "summarize"):
+            await mgr.add_child_agent(Worker(AgentConfig(role=s, goal=s, specializations=[s]), llm=llm))
+        return await mgr.execute_task({"type": "complex_workflow", "steps": ["extract", "analyze", "summarize"]})
+
+    r = asyncio.run(main())
+    assert r.success and r.output == {"extract": "extract-out", "analyze": "analyze-out", "summarize": "summarize-out"}
+    assert seen == [("extract", "extract", None), ("analyze", "analyze", "extract-out"),
+                    ("summarize", "summarize", "analyze-out")]
