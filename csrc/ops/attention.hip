@@ -38,7 +38,7 @@ namespace pa {
 
 constexpr int ATT_HD = 128;
 constexpr int ATT_BLK = 16;
-constexpr int ATT_PART = 512;  // keys per decode partition (multiple of 32)
+constexpr int ATT_PART = 512;  // default keys per decode partition (the step may choose 256/128)
 constexpr float NEG_BIG = -1.0e30f;
 
 // ---------------------------------------------------------------------------
@@ -54,7 +54,7 @@ __device__ __forceinline__ void decode_item(
     float* __restrict__ part_ml, int* __restrict__ counters, const bf16* __restrict__ q, const bf16* __restrict__ k_cache,
     const bf16* __restrict__ v_cache, const int* __restrict__ q_start, const int* __restrict__ q_len,
     const int* __restrict__ ctx_len, const int* __restrict__ block_table, int max_blocks, int H,
-    int KV, int kvh, float scale_log2) {
+    int KV, int kvh, float scale_log2, int psz) {
   const int s = it.x, qb = it.y;
   const int nq = it.z & 0xff, part = (it.z >> 8) & 0xfff, nparts = it.z >> 20;
   const int pidx = it.w;
@@ -68,8 +68,8 @@ __device__ __forceinline__ void decode_item(
   const int key_limit = colvalid ? (ctx - ql + tok + 1) : 0;
   const int head = kvh * G + hg;
   const int causal_end = ctx - ql + qb + nq;
-  const int kv_begin = nparts > 1 ? part * ATT_PART : 0;
-  const int kv_end = nparts > 1 ? min(causal_end, kv_begin + ATT_PART) : causal_end;
+  const int kv_begin = nparts > 1 ? part * psz : 0;
+  const int kv_end = nparts > 1 ? min(causal_end, kv_begin + psz) : causal_end;
   const int t_first = kv_begin >> 5;
   const int t_last = (kv_end + 31) >> 5;
 
@@ -447,18 +447,19 @@ __global__ __launch_bounds__(256, 2) void paged_attn_kernel(
     bf16* __restrict__ out, float* __restrict__ part_o, float* __restrict__ part_ml,
     int* __restrict__ counters, const bf16* __restrict__ q, const bf16* __restrict__ k_cache,
     const bf16* __restrict__ v_cache, const int4* __restrict__ items,
-    const int* __restrict__ n_items, const int* __restrict__ q_start,
+    const int* __restrict__ n_items, const int* __restrict__ part_size, const int* __restrict__ q_start,
     const int* __restrict__ q_len, const int* __restrict__ ctx_len,
     const int* __restrict__ block_table, int max_blocks, int H, int KV, float scale_log2) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int TPW = 16 / G;
   const int n = n_items[0];
+  const int psz = part_size ? part_size[0] : ATT_PART;  // decode partition (keys), per step
   const int kvh = blockIdx.y;
   for (int item = blockIdx.x; item < n; item += gridDim.x) {
     const int4 it = items[item];
     if ((it.z & 0xff) <= TPW)
       decode_item<G>(it, smem, out, part_o, part_ml, counters, q, k_cache, v_cache, q_start, q_len, ctx_len,
-                     block_table, max_blocks, H, KV, kvh, scale_log2);
+                     block_table, max_blocks, H, KV, kvh, scale_log2, psz);
     else
       prefill_item<G>(it, smem, out, q, k_cache, v_cache, q_start, q_len, ctx_len, block_table,
                       max_blocks, H, KV, kvh, scale_log2);
@@ -470,7 +471,8 @@ __global__ __launch_bounds__(256, 2) void paged_attn_kernel(
 
 extern "C" int pa_paged_attention(void* out, float* part_o, float* part_ml, const void* q,
                                   const void* k_cache, const void* v_cache, const int* items,
-                                  const int* n_items, int max_items, int* counters, const int* q_start,
+                                  const int* n_items, int max_items, const int* part_size, int* counters,
+                                  const int* q_start,
                                   const int* q_len, const int* ctx_len, const int* block_table,
                                   int max_blocks, int H, int KV, float scale_log2,
                                   hipStream_t st) {
@@ -492,7 +494,8 @@ extern "C" int pa_paged_attention(void* out, float* part_o, float* part_ml, cons
                          (pa::bf16*)out,                                                    \
                          part_o, part_ml, counters, (const pa::bf16*)q,                      \
                          (const pa::bf16*)k_cache, (const pa::bf16*)v_cache,                \
-                         (const int4*)items, n_items, q_start, q_len, ctx_len, block_table, \
+                         (const int4*)items, n_items, part_size, q_start, q_len, ctx_len,    \
+                         block_table,                                                       \
                          max_blocks, H, KV, scale_log2);                                    \
   } while (0)
   switch (G) {

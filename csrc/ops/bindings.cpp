@@ -16,7 +16,7 @@ int pa_rope_cache(void* q_out, void* k_cache, void* v_cache, const void* qkv, co
 int pa_silu_mul(void* out, const void* in, int T, int F, hipStream_t st);
 int pa_paged_attention(void* out, float* part_o, float* part_ml, const void* q, const void* k_cache,
                        const void* v_cache, const int* items, const int* n_items, int max_items,
-                       int* counters, const int* q_start,
+                       const int* part_size, int* counters, const int* q_start,
                        const int* q_len, const int* ctx_len, const int* block_table,
                        int max_blocks, int H, int KV, float scale_log2, hipStream_t st);
 int pa_sample_workspace_floats(int rows, int V);
@@ -116,7 +116,8 @@ void silu_mul(at::Tensor out, at::Tensor in) {
 void paged_attention(at::Tensor out, at::Tensor part_o, at::Tensor part_ml, at::Tensor q,
                      at::Tensor k_cache, at::Tensor v_cache, at::Tensor items, at::Tensor n_items,
                      at::Tensor counters, at::Tensor q_start, at::Tensor q_len,
-                     at::Tensor ctx_len, at::Tensor block_table, double scale) {
+                     at::Tensor ctx_len, at::Tensor block_table, double scale,
+                     c10::optional<at::Tensor> part_size) {
   for (auto* t : {&out, &part_o, &part_ml, &q, &k_cache, &v_cache, &items, &n_items, &counters,
                   &q_start, &q_len, &ctx_len, &block_table})
     check_gpu(*t, "paged_attention arg");
@@ -142,6 +143,7 @@ void paged_attention(at::Tensor out, at::Tensor part_o, at::Tensor part_ml, at::
   check_rc(pa_paged_attention(out.data_ptr(), part_o.data_ptr<float>(), part_ml.data_ptr<float>(),
                               q.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(),
                               items.data_ptr<int>(), n_items.data_ptr<int>(), max_items,
+                              part_size.has_value() ? part_size->data_ptr<int>() : nullptr,
                               counters.data_ptr<int>(),
                               q_start.data_ptr<int>(), q_len.data_ptr<int>(),
                               ctx_len.data_ptr<int>(), block_table.data_ptr<int>(),
@@ -290,7 +292,10 @@ PYBIND11_MODULE(_C, m) {
   m.def("silu_mul", &silu_mul);
   m.def("skinny_gemm", &skinny_gemm);
   m.def("skinny_set_variant", [](int v) { pa_skinny_set_variant(v); });
-  m.def("paged_attention", &paged_attention);
+  m.def("paged_attention", &paged_attention, py::arg("out"), py::arg("part_o"), py::arg("part_ml"), py::arg("q"),
+        py::arg("k_cache"), py::arg("v_cache"), py::arg("items"), py::arg("n_items"), py::arg("counters"),
+        py::arg("q_start"), py::arg("q_len"), py::arg("ctx_len"), py::arg("block_table"), py::arg("scale"),
+        py::arg("part_size") = py::none());
   m.def("sample_workspace_floats", &sample_workspace_floats);
   m.def("sample", &sample, py::arg("out_tokens"), py::arg("out_keys"), py::arg("workspace"),
         py::arg("logits"), py::arg("vocab_offset"), py::arg("temperature"), py::arg("mask_class"),

@@ -97,6 +97,7 @@ PYBIND11_MODULE(_runtime, m) {
         if (d.contains("prefix_caching")) c.prefix_caching = d["prefix_caching"].cast<bool>();
         if (d.contains("split_decode")) c.split_decode = d["split_decode"].cast<bool>();
         if (d.contains("token_align")) c.token_align = d["token_align"].cast<int32_t>();
+        if (d.contains("kv_heads")) c.kv_heads = d["kv_heads"].cast<int32_t>();
         if (d.contains("align_slack")) c.align_slack = d["align_slack"].cast<int32_t>();
         if (d.contains("eos_ids")) c.eos_ids = d["eos_ids"].cast<std::vector<int32_t>>();
         return std::make_unique<Scheduler>(c);
@@ -111,7 +112,7 @@ PYBIND11_MODULE(_runtime, m) {
         d["logit_rows"] = L.logit_rows; d["mask_class"] = L.mask_class; d["forced"] = L.forced;
         d["offsets"] = L.offsets; d["temperature"] = L.temperature; d["seeds"] = L.seeds;
         d["top_k"] = L.top_k; d["top_p"] = L.top_p;
-        d["items"] = L.items; d["n_items"] = L.n_items;
+        d["items"] = L.items; d["n_items"] = L.n_items; d["part_size"] = L.part_size;
         d["counts"] = L.counts; d["block_table"] = L.block_table;
         d["total"] = L.total;
         return d;

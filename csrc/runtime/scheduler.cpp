@@ -30,6 +30,7 @@ Scheduler::Scheduler(const SchedulerConfig& cfg)
   };
   L.counts = take(8);
   L.n_items = take(1);
+  L.part_size = take(1);
   L.input_ids = take(L.max_tokens);
   L.positions = take(L.max_tokens);
   L.slots = take(L.max_tokens);
@@ -242,6 +243,32 @@ int32_t Scheduler::schedule(int32_t* buf) {
   const int32_t tpw = 16 / std::max(1, cfg_.gqa_group);
 
   int32_t T = 0, ns = 0, nsamp = 0, nit = 0, nparted = 0, pslot = 0;
+  // decode partition size: with few decode rows, smaller flash-decoding
+  // partitions give the attention launch enough workgroups to fill the chip
+  // (>= ~512 across the KV heads); the item list must still fit max_items
+  int32_t psz = 512;
+  if (cfg_.split_decode) {
+    int64_t parts[3] = {0, 0, 0};  // partition sizes 512, 256, 128
+    int64_t nprefill = 0;
+    for (const Planned& p : last_plan_) {
+      const int32_t c = p.s->num_computed + p.n;
+      if (p.n <= tpw) {
+        parts[0] += std::max(1, (c + 511) / 512);
+        parts[1] += std::max(1, (c + 255) / 256);
+        parts[2] += std::max(1, (c + 127) / 128);
+      } else {
+        nprefill += (p.n + 31) / 32 + 1;
+      }
+    }
+    const int64_t kv = std::max(1, cfg_.kv_heads), target = 512;
+    if (parts[0] * kv < target) {
+      psz = parts[1] * kv < target ? 128 : 256;
+      const int64_t need = nprefill + (psz == 128 ? parts[2] : parts[1]);
+      if (need > L.max_items) psz = 512;
+    }
+  }
+  buf[L.part_size] = psz;
+
   // prefill (q-split) tiles go first in the item list, heaviest (last) tile of a
   // chunk first, so the long-running workgroups start before the decode items
   const int32_t qtile = 32 / std::max(1, cfg_.gqa_group);
@@ -283,7 +310,7 @@ int32_t Scheduler::schedule(int32_t* buf) {
     }
     // attention work items (mirrors pilottai_amd/ops/attn_meta.py)
     if (n <= tpw) {
-      const int32_t nparts = cfg_.split_decode ? std::max(1, (ctx + 511) / 512) : 1;
+      const int32_t nparts = cfg_.split_decode ? std::max(1, (ctx + psz - 1) / psz) : 1;
       if (nparts > 1) {
         for (int32_t q = 0; q < nparts; ++q) {
           int32_t* it = items + 4 * nit++;

@@ -39,6 +39,7 @@ struct SchedulerConfig {
   // jump-forward) is deferred so that T is a multiple of token_align (library
   // GEMM cost jumps at each 256-row tile boundary). 0 disables.
   int32_t token_align = 0;
+  int32_t kv_heads = 8;                // KV heads per rank (sizes the decode partitioning)
   int32_t align_slack = 96;
   std::vector<int32_t> eos_ids;
 };
@@ -46,7 +47,7 @@ struct SchedulerConfig {
 struct StepLayout {
   int32_t max_tokens, max_seqs, max_blocks, max_items;
   int32_t input_ids, positions, slots, q_start, q_len, ctx_len, logit_rows, mask_class, forced,
-      offsets, temperature, top_k, top_p, seeds, items, n_items, counts, block_table, total;
+      offsets, temperature, top_k, top_p, seeds, items, n_items, part_size, counts, block_table, total;
 };
 
 enum FinishReason : int32_t { NOT_FINISHED = -1, FINISH_STOP = 0, FINISH_LENGTH = 1, FINISH_ABORT = 2 };

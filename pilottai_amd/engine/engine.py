@@ -185,6 +185,7 @@ class LLMEngine:
             "gqa_group": self.model.h_local // self.model.kv_local,
             "prefix_caching": cfg.prefix_caching, "split_decode": cfg.split_decode,
             "token_align": cfg.token_align, "align_slack": cfg.align_slack,
+            "kv_heads": self.model.kv_local,
             "eos_ids": list(self.tok.eos_ids)})
         L = self.L = self.sched.layout()
         pin = self.on_gpu
@@ -259,6 +260,7 @@ class LLMEngine:
             items=sl("items", 4 * L["max_items"]).view(L["max_items"], 4),
             n_items=sl("n_items", 1),
             att_counters=self._att_counters,
+            part_size=sl("part_size", 1),
             logit_rows=sl("logit_rows", ms))
         self._temp = sl("temperature", ms).view(torch.float32)
         self._top_k = sl("top_k", ms)
@@ -284,7 +286,8 @@ class LLMEngine:
         m = self.meta
         n_it = self._items_for_bucket(bucket, s_b)
         return StepMeta(m.input_ids, m.positions, m.slots, m.q_start, m.q_len, m.ctx_len,
-                        m.block_table, m.items[:n_it], m.n_items, m.att_counters, m.logit_rows, num_seqs=ns)
+                        m.block_table, m.items[:n_it], m.n_items, m.att_counters, m.logit_rows, num_seqs=ns,
+                        part_size=m.part_size)
 
     def _forward_and_sample(self, bucket: int, s_b: int, ns: int, trunc: bool = False):
         meta = self._meta_for(bucket, s_b, ns)

@@ -98,6 +98,7 @@ class StepMeta:
     att_counters: torch.Tensor  # persistent zeroed workspace (partition tickets), not step data
     logit_rows: torch.Tensor
     num_seqs: int = 0  # host-side count, used only by the CPU reference path
+    part_size: Optional[torch.Tensor] = None  # device int[1]: decode partition size of the step
 
 
 class KVCache:
@@ -270,7 +271,7 @@ class LlamaModel:
             attn = torch.empty(T, H, hd, dtype=self.dtype, device=self.device)
             ops.paged_attention(attn, part_o, part_ml, q, kv.k[li], kv.v[li], meta.items, meta.n_items,
                                 meta.att_counters, meta.q_start, meta.q_len, meta.ctx_len,
-                                meta.block_table, self.scale, num_seqs=meta.num_seqs)
+                                meta.block_table, self.scale, num_seqs=meta.num_seqs, part_size=meta.part_size)
             o = ops.linear(attn.view(T, H * hd), L["wo"], "o")
             if self.tp.size > 1:
                 self.tp.all_reduce(o)

@@ -12,7 +12,7 @@ ATT_PART = 512  # keys per decode partition (must match csrc/ops/attention.hip)
 
 
 def build_attention_items(q_lens: Sequence[int], ctx_lens: Sequence[int], group: int,
-                          split: bool = True) -> Tuple[List[Tuple[int, int, int, int]], int]:
+                          split: bool = True, part: int = ATT_PART) -> Tuple[List[Tuple[int, int, int, int]], int]:
     """Return (items, n_partial_slots).
 
     item = (seq, q_begin, nq | part << 8 | nparts << 20, partial_slot); the
@@ -31,7 +31,7 @@ def build_attention_items(q_lens: Sequence[int], ctx_lens: Sequence[int], group:
         if ql <= 0:
             continue
         if ql <= tpw:
-            nparts = (ctx + ATT_PART - 1) // ATT_PART if split else 1
+            nparts = (ctx + part - 1) // part if split else 1
             nparts = max(1, nparts)
             if nparts > 1:
                 for p in range(nparts):

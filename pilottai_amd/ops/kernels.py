@@ -108,7 +108,8 @@ def rope_cache(q_out, k_cache, v_cache, qkv, positions, slot_mapping, cos_sin, H
 
 
 def paged_attention(out, part_o, part_ml, q, k_cache, v_cache, items, n_items, counters,
-                    q_start, q_len, ctx_len, block_table, scale: float, num_seqs: Optional[int] = None):
+                    q_start, q_len, ctx_len, block_table, scale: float, num_seqs: Optional[int] = None,
+                    part_size: Optional[torch.Tensor] = None):
     """Attention over the paged cache. On GPU `items` must be a device int32
     [max, 4] tensor with a device count (graph-capturable) and `counters` a
     zero-initialised int32 tensor of >= seqs * KV entries (partition tickets; the
@@ -116,7 +117,7 @@ def paged_attention(out, part_o, part_ml, q, k_cache, v_cache, items, n_items, c
     if _on_gpu(q):
         require_native().paged_attention(out, part_o, part_ml, q, k_cache, v_cache, items, n_items,
                                          counters, q_start, q_len, ctx_len, block_table,
-                                         float(scale))
+                                         float(scale), part_size)
         return out
     ns = len(q_len) if num_seqs is None else num_seqs
     r = ref.paged_attention(q, k_cache, v_cache, q_start[:ns], q_len[:ns], ctx_len[:ns],

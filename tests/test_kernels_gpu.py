@@ -69,7 +69,7 @@ def test_rope_cache(gpu):
     torch.testing.assert_close(vc.cpu().float(), vc_r.float(), atol=0, rtol=0)
 
 
-def _run_attention(gpu, H, KV, q_lens, ctx_lens, seed=0, split=True):
+def _run_attention(gpu, H, KV, q_lens, ctx_lens, seed=0, split=True, part=512):
     torch.manual_seed(seed)
     G = H // KV
     blk = 16
@@ -87,7 +87,7 @@ def _run_attention(gpu, H, KV, q_lens, ctx_lens, seed=0, split=True):
     q_start = np.concatenate([[0], np.cumsum(q_lens)[:-1]]).astype(np.int32)
     T = int(sum(q_lens))
     q = _bf(T, H, 128, dev=gpu)
-    items, nslots = ops.build_attention_items(q_lens, ctx_lens, G, split=split)
+    items, nslots = ops.build_attention_items(q_lens, ctx_lens, G, split=split, part=part)
     it = torch.tensor(items + [(0, 0, 0, 0)], dtype=torch.int32, device=gpu)
     cnt = torch.zeros(ns * KV, dtype=torch.int32, device=gpu)
     n_it = torch.tensor([len(items)], dtype=torch.int32, device=gpu)
@@ -98,7 +98,7 @@ def _run_attention(gpu, H, KV, q_lens, ctx_lens, seed=0, split=True):
     scale = 1.0 / math.sqrt(128)
     dev_i = lambda a: torch.tensor(a, dtype=torch.int32, device=gpu)  # noqa: E731
     ops.paged_attention(out, part_o, part_ml, q, kc, vc, it, n_it, cnt, dev_i(q_start),
-                        dev_i(q_lens), dev_i(ctx_lens), bt.to(gpu), scale)
+                        dev_i(q_lens), dev_i(ctx_lens), bt.to(gpu), scale, part_size=dev_i([part]))
     torch.cuda.synchronize()
     assert int(cnt.abs().sum()) == 0, "partition tickets must be left zeroed"
     r = ref.paged_attention(q.cpu(), kc.cpu(), vc.cpu(), q_start, q_lens, ctx_lens, bt, scale)
@@ -127,6 +127,14 @@ def test_attention_prefill_tiles(gpu, H, KV):
     q_lens = [300, 129, 33, 1, 2, 77]
     ctx = [300, 1129, 65, 900, 18, 77 + 512]
     o, r = _run_attention(gpu, H, KV, q_lens, ctx, seed=11)
+    torch.testing.assert_close(o, r, atol=2e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("part", [128, 256])
+def test_attention_small_partitions(gpu, part):
+    """Per-step decode partition sizes chosen by the scheduler for small batches."""
+    ctx = [1, 100, 127, 128, 129, 700, 2049, 64]
+    o, r = _run_attention(gpu, 32, 8, [1, 1, 2, 1, 4, 1, 1, 3], ctx, seed=13, part=part)
     torch.testing.assert_close(o, r, atol=2e-2, rtol=2e-2)
 
 
