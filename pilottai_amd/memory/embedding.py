@@ -55,9 +55,14 @@ class HashingEmbedder:
 
 
 class EngineEmbedder:
-    """Mean-pooled token embeddings of the local engine's model, projected to `dim`."""
+    """Embeddings from the serving model itself: final hidden states of
+    a dense forward (LlamaModel.hidden_states) mean-pooled over the text's tokens,
+    projected to `dim` by a fixed orthonormal matrix and L2-normalised. Texts are
+    embedded in batches of up to `batch_size`, truncated to `max_tokens`. With
+    `pool="tokens"` the (much cheaper) mean of input token embeddings is used."""
 
-    def __init__(self, engine, dim: int = 1024, seed: int = 0):
+    def __init__(self, engine, dim: int = 1024, seed: int = 0, pool: str = "hidden", batch_size: int = 16,
+                 max_tokens: int = 512):
         import torch
 
         self.engine = engine
@@ -66,6 +71,9 @@ class EngineEmbedder:
         g = torch.Generator().manual_seed(seed)
         q, _ = torch.linalg.qr(torch.randn(d, max(d, dim), generator=g))
         self.proj = q[:, :dim].contiguous().to(engine.device, torch.float32)
+        self.pool = pool if getattr(engine.model.tp, "size", 1) == 1 else "tokens"
+        self.batch_size = batch_size
+        self.max_tokens = max_tokens
 
     def embed(self, texts: Sequence[str]) -> np.ndarray:
         import torch
@@ -74,11 +82,16 @@ class EngineEmbedder:
         m = self.engine.model
         rows: List[np.ndarray] = []
         with torch.inference_mode():
-            for t in texts:
-                ids = torch.tensor(self.engine.tok.encode(t)[:512] or [0], device=self.engine.device)
-                h = F.embedding(ids, m.embed).float().mean(0)
-                v = (h @ self.proj)
-                rows.append(torch.nn.functional.normalize(v, dim=0).cpu().numpy())
+            if self.pool == "hidden":
+                for i in range(0, len(texts), self.batch_size):
+                    ids = [self.engine.tok.encode(t)[: self.max_tokens] or [0] for t in texts[i:i + self.batch_size]]
+                    v = F.normalize(m.hidden_states(ids) @ self.proj, dim=1)
+                    rows.extend(v.cpu().numpy())
+            else:
+                for t in texts:
+                    ids = torch.tensor(self.engine.tok.encode(t)[: self.max_tokens] or [0], device=self.engine.device)
+                    h = F.embedding(ids, m.embed).float().mean(0)
+                    rows.append(F.normalize(h @ self.proj, dim=0).cpu().numpy())
         return np.stack(rows) if rows else np.zeros((0, self.dim), np.float32)
 
     def __call__(self, texts):

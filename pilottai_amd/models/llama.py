@@ -318,3 +318,49 @@ class LlamaModel:
             h = (h.to(self.dtype).float() + (a.float() @ L["w2"].float().T).to(self.dtype).float())
         x = ref.rmsnorm(h.to(self.dtype), self.norm, cfg.rms_eps)
         return (x.float() @ self.lm_head.float().T)
+
+    # -- dense batched encoder forward (semantic-memory embeddings) ----
+    @torch.no_grad()
+    def hidden_states(self, batch: List[List[int]]) -> torch.Tensor:
+        """Final-norm hidden states mean-pooled over each sequence's tokens: [B, d].
+
+        A dense bf16 causal forward (library GEMMs + SDPA attention, no KV cache),
+        right-padded to the longest sequence; used by EngineEmbedder to embed
+        memory items with the serving model itself. TP=1 only."""
+        assert self.tp.size == 1, "hidden_states runs on a TP=1 model"
+        cfg, dev, dt = self.cfg, self.device, self.dtype
+        B = len(batch)
+        T = max(1, max(len(s) for s in batch))
+        ids = torch.zeros(B, T, dtype=torch.long, device=dev)
+        valid = torch.zeros(B, T, dtype=torch.bool, device=dev)
+        for i, s in enumerate(batch):
+            if s:
+                ids[i, :len(s)] = torch.tensor(s, device=dev)
+                valid[i, :len(s)] = True
+        H, KVh, hd = self.h_local, self.kv_local, cfg.head_dim
+        pos = torch.arange(T, device=dev)
+        cs = self.cos_sin[:T]
+        cos, sin = cs[:, : hd // 2].to(dt), cs[:, hd // 2:].to(dt)
+
+        def rope(x):  # [B, T, h, hd], rotate-half
+            x1, x2 = x[..., : hd // 2], x[..., hd // 2:]
+            c, s = cos[None, :, None, :], sin[None, :, None, :]
+            return torch.cat([x1 * c - x2 * s, x2 * c + x1 * s], dim=-1)
+
+        h = F.embedding(ids, self.embed)                      # [B, T, d]
+        for L in self.layers:
+            x = F.rms_norm(h, (cfg.hidden_size,), L["ln1"], cfg.rms_eps)
+            qkv = F.linear(x, L["wqkv"])
+            q = rope(qkv[..., : H * hd].view(B, T, H, hd))
+            k = rope(qkv[..., H * hd:(H + KVh) * hd].view(B, T, KVh, hd))
+            v = qkv[..., (H + KVh) * hd:].view(B, T, KVh, hd)
+            o = F.scaled_dot_product_attention(q.transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2),
+                                               is_causal=True, enable_gqa=True, scale=self.scale)
+            h = h + F.linear(o.transpose(1, 2).reshape(B, T, H * hd), L["wo"])
+            x = F.rms_norm(h, (cfg.hidden_size,), L["ln2"], cfg.rms_eps)
+            gu = F.linear(x, L["w13"])
+            g, u = gu.chunk(2, dim=-1)
+            h = h + F.linear(F.silu(g) * u, L["w2"])
+        x = F.rms_norm(h, (cfg.hidden_size,), self.norm, cfg.rms_eps).float()
+        w = valid.unsqueeze(-1).float()
+        return (x * w).sum(1) / w.sum(1).clamp_min(1.0)

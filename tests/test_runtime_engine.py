@@ -195,3 +195,32 @@ def test_scheduler_token_alignment():
     aligned, n_al = run(256)
     assert plain[0] == 550 and aligned[0] == 512 and n_al >= 1
     assert sum(plain) == sum(aligned)
+
+
+def test_hidden_states_match_reference_forward():
+    """The dense encoder forward (EngineEmbedder): right padding does not leak into
+    shorter sequences, identical texts embed identically, vectors are unit norm."""
+    import torch
+
+    from pilottai_amd.memory.embedding import EngineEmbedder
+    from pilottai_amd.models.llama import LlamaModel, get_config
+
+    m = LlamaModel(get_config("tiny"), "cpu", seed=2)
+    a, b = [5, 17, 300, 4000, 9], [77, 78]
+    hs = m.hidden_states([a, b])
+    assert hs.shape == (2, 512)
+    # padding does not leak into the shorter sequence
+    torch.testing.assert_close(hs[1], m.hidden_states([b])[0], atol=2e-2, rtol=2e-2)
+
+    class _E:  # minimal engine facade
+        model, device = m, torch.device("cpu")
+        model_cfg = m.cfg
+
+        class tok:
+            @staticmethod
+            def encode(t):
+                return [ord(c) % 1000 for c in t]
+
+    emb = EngineEmbedder(_E(), dim=64)
+    v = emb.embed(["alpha beta", "alpha beta", "unrelated text here"])
+    assert v.shape == (3, 64) and abs(float((v[0] * v[1]).sum()) - 1.0) < 1e-4
