@@ -78,7 +78,9 @@ async def run_rank(a, rank: int, world: int, device):
     from pilottai_amd.tools.tool import Tool, echo_tool
 
     # workers of this rank (agent-DP sharding)
-    n_local = a.workers // world + (1 if rank < a.workers % world else 0)
+    from pilottai_amd.parallel.agent_dp import shard_workers
+
+    n_local = len(shard_workers(a.workers, world, rank))
     t_init = time.time()
     eng = LLMEngine(EngineConfig(model=a.model if not a.cpu else "tiny", max_num_seqs=max(64, 2 * n_local),
                                  max_num_batched_tokens=a.max_batched_tokens, kv_cache_gb=a.kv_gb if not a.cpu else None,

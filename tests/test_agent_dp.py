@@ -1,0 +1,47 @@
+"""Agent-DP global load view over 2 gloo ranks."""
+import json
+import os
+import socket
+
+import torch.multiprocessing as mp
+
+from pilottai_amd.parallel.agent_dp import shard_workers
+
+
+def test_shard_workers_covers_all():
+    for n, w in ((64, 8), (64, 3), (5, 8)):
+        shards = [list(shard_workers(n, w, r)) for r in range(w)]
+        assert sum(shards, []) == list(range(n))
+        assert max(map(len, shards)) - min(map(len, shards)) <= 1
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    import torch
+
+    from pilottai_amd.parallel.agent_dp import GlobalLoadView
+    from pilottai_amd.parallel.comm import init_distributed
+
+    init_distributed("gloo")
+    view = GlobalLoadView()
+    view.update([5.0 - 4 * rank, 2.0, 1.0, 0.1 * rank, 1000.0])
+    with open(f"{out}.{rank}", "w") as f:
+        json.dump({"table": view.table, "least": view.least_loaded_rank(), "totals": view.totals()}, f)
+    torch.distributed.destroy_process_group()
+
+
+def test_global_load_view_two_ranks(tmp_path):
+    out = str(tmp_path / "load")
+    mp.start_processes(_worker, args=(2, _port(), out), nprocs=2, join=True, start_method="spawn")
+    r0, r1 = (json.load(open(f"{out}.{r}")) for r in range(2))
+    assert r0 == r1
+    assert r0["least"] == 1 and r0["totals"]["queue_size"] == 6.0 and len(r0["table"]) == 2
