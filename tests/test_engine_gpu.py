@@ -80,3 +80,18 @@ def test_top_k_top_p_graph_variant(engine):
     assert again.token_ids == plain.token_ids
     assert all(len(o.token_ids) == 8 for o in both)
     assert any(key[1] for key in engine._graphs)  # the truncating variant was captured
+
+
+def test_hidden_states_match_reference_forward(engine):
+    """Dense encoder forward on the GPU (SDPA + hipBLASLt): pooled hidden states
+    projected by the LM head equal the mean of the fp32 reference logits."""
+    m = engine.model
+    tok = engine.tok
+    seqs = [tok.encode("semantic memory item about quarterly revenue"), tok.encode("short one")]
+    hs = m.hidden_states(seqs)
+    assert hs.shape == (2, m.cfg.hidden_size) and hs.device.type == "cuda"
+    for i, s in enumerate(seqs):
+        want = m.reference_logits(s).mean(0)
+        got = hs[i] @ m.lm_head.float().T
+        err = (got - want).abs().max() / want.abs().max()
+        assert err < 0.05, float(err)
