@@ -30,6 +30,9 @@ int pa_topkp_threshold(float* tau, const void* logits, int rows, int V, int ld, 
                        int mask_words, hipStream_t st);
 void pa_skinny_set_variant(int v);
 int pa_skinny_gemm(void* y, const void* x, const void* w, int M, int N, int K, int ldy, hipStream_t st);
+int pa_decode_gemm(void* y, const void* x, const void* wp, const void* resid, int M, int N, int K,
+                   int ldx, int ldy, int ldr, int epi, int norm, float eps, int nt, int waves,
+                   hipStream_t st);
 long long pa_cosine_topk_workspace_bytes(int Q, int N, int K);
 int pa_cosine_topk(float* out_scores, int* out_rows, void* workspace, const void* queries,
                    const void* index, int Q, int N, int D, int K, const int* row_priority,
@@ -164,6 +167,38 @@ bool skinny_gemm(at::Tensor y, at::Tensor x, at::Tensor w) {
   return rc == 0;
 }
 
+// y = epi(rownorm(x) . W^T) on fragment-major packed weights wp [N/16, K/32, 64, 8]
+// (csrc/ops/gemm_decode.hip). epi 0 plain, 1 silu(gate)*up (y has N/2 columns),
+// 2 y = resid + acc. Returns false if the shape is not handled.
+bool decode_gemm(at::Tensor y, at::Tensor x, at::Tensor wp, c10::optional<at::Tensor> resid, int64_t epi,
+                 bool norm, double eps, int64_t nt, int64_t waves) {
+  check_gpu(wp, "wp");
+  TORCH_CHECK(x.is_cuda() && x.dim() == 2 && x.stride(1) == 1, "x must be a 2-D GPU tensor, unit inner stride");
+  TORCH_CHECK(y.is_cuda() && y.dim() == 2 && y.stride(1) == 1, "y must be a 2-D GPU tensor, unit inner stride");
+  check_dtype(x, at::kBFloat16, "x"); check_dtype(wp, at::kBFloat16, "wp"); check_dtype(y, at::kBFloat16, "y");
+  TORCH_CHECK(wp.dim() == 4 && wp.size(2) == 64 && wp.size(3) == 8, "wp must be packed [N/16, K/32, 64, 8]");
+  const int M = x.size(0), K = x.size(1), N = wp.size(0) * 16;
+  TORCH_CHECK(wp.size(1) * 32 == K, "packed weight K ", wp.size(1) * 32, " != x K ", K);
+  TORCH_CHECK(x.stride(0) % 8 == 0 && K % 8 == 0, "x rows must be 16-byte aligned");
+  const int NO = epi == 1 ? N / 2 : N;
+  TORCH_CHECK(y.size(0) == M && y.size(1) == NO, "y shape [", y.size(0), ", ", y.size(1), "] != [", M, ", ", NO, "]");
+  const void* rp = nullptr;
+  int ldr = 0;
+  if (epi == 2) {
+    TORCH_CHECK(resid.has_value(), "epi=2 needs resid");
+    const auto& r = *resid;
+    TORCH_CHECK(r.is_cuda() && r.dim() == 2 && r.stride(1) == 1 && r.size(0) == M && r.size(1) == N,
+                "resid must be [M, N] with unit inner stride");
+    check_dtype(r, at::kBFloat16, "resid");
+    rp = r.data_ptr();
+    ldr = r.stride(0);
+  }
+  const int rc = pa_decode_gemm(y.data_ptr(), x.data_ptr(), wp.data_ptr(), rp, M, N, K, x.stride(0), y.stride(0),
+                                ldr, (int)epi, norm ? 1 : 0, (float)eps, (int)nt, (int)waves, cur_stream());
+  TORCH_CHECK(rc >= 0, "decode_gemm launch failed");
+  return rc == 0;
+}
+
 int64_t sample_workspace_floats(int64_t rows, int64_t V) {
   return pa_sample_workspace_floats(rows, V);
 }
@@ -292,6 +327,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("silu_mul", &silu_mul);
   m.def("skinny_gemm", &skinny_gemm);
   m.def("skinny_set_variant", [](int v) { pa_skinny_set_variant(v); });
+  m.def("decode_gemm", &decode_gemm, py::arg("y"), py::arg("x"), py::arg("wp"), py::arg("resid") = py::none(),
+        py::arg("epi") = 0, py::arg("norm") = false, py::arg("eps") = 1e-5, py::arg("nt") = 0,
+        py::arg("waves") = 0);
   m.def("paged_attention", &paged_attention, py::arg("out"), py::arg("part_o"), py::arg("part_ml"), py::arg("q"),
         py::arg("k_cache"), py::arg("v_cache"), py::arg("items"), py::arg("n_items"), py::arg("counters"),
         py::arg("q_start"), py::arg("q_len"), py::arg("ctx_len"), py::arg("block_table"), py::arg("scale"),

@@ -1,0 +1,251 @@
+// Decode-step projections on pre-packed weights (fused):
+//
+//     y[M, N] = epi( r[m] * x[M, K] · W[N, K]^T )        bf16 in/out, fp32 accumulate, M <= 64
+//
+// At decode batch sizes every projection is bound by streaming W from HBM once
+// (Llama-3-8B: 14 GB of layer weights per step), so this kernel is organised
+// around the W stream and fuses the small per-layer kernels that would
+// otherwise each cost a launch + a few microseconds at M <= 16:
+//
+//   * W is stored "fragment-major" (packed once at model load, pa_decode_pack):
+//     Wp[N/16][K/32][64 lanes][8] with lane l = 16*g + c holding
+//     W[16t + c][32s + 8g .. 8g+7] — exactly the B operand of
+//     v_mfma_f32_16x16x32_bf16. One wave load is 1 KiB of CONTIGUOUS memory
+//     (8 full 128-B lines) instead of 16 rows x 64 B (16 half lines), which
+//     halves the texture-path work per streamed byte (guide §5: fragment-shaped
+//     loads cost 2x TA at identical HBM traffic);
+//   * a workgroup owns NT column tiles (16*NT outputs) and ALL rows; its WAVES
+//     waves split K, each streaming a contiguous run of its tiles' fragments;
+//     x (<= 512 KB, L2-resident) feeds the A operand and is re-used across the
+//     NT tiles; per-wave partials are summed through LDS;
+//   * NORM: RMSNorm folded in — the norm weight is pre-multiplied into W's
+//     columns at load time, the kernel accumulates sum(x^2) from the same x
+//     fragments it feeds to the MFMAs and scales each output row by
+//     rsqrt(mean + eps) (no separate norm kernel, no normalised-x round trip);
+//   * EPI_SILU: gate/up tiles are interleaved in the packed layout, so the
+//     workgroup holds gate and up for the same 16 outputs and writes
+//     silu(gate) * up directly (no [M, 2F] intermediate, no SwiGLU kernel);
+//   * EPI_RESID: y = resid + acc (in place on the residual stream).
+//   * grid = N / (16*NT) workgroups, XCD-aware bijective remap so consecutive
+//     column groups share one XCD's L2 copy of x.
+//
+// Replaces the norm -> GEMM -> SwiGLU -> GEMM -> add chain of the reference
+// model path (models/llama.py forward) for decode-sized steps.
+#include "common.h"
+
+namespace pa {
+
+enum { EPI_PLAIN = 0, EPI_SILU = 1, EPI_RESID = 2 };
+
+template <int MT, int NT, int WAVES, int U, int EPI, bool NORM>
+__global__ __launch_bounds__(WAVES * 64) void decode_gemm_kernel(
+    bf16* __restrict__ y, const bf16* __restrict__ x, const bf16* __restrict__ wp,
+    const bf16* resid, int M, int N, int K, int ldx, int ldy, int ldr, float eps) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int TM = MT * 16, TN = NT * 16;
+  float* red = reinterpret_cast<float*>(smem);  // [WAVES][TM][TN]
+  float* ssq = red + WAVES * TM * TN;            // [WAVES][TM]
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int g = lane >> 4, c = lane & 15;
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int q = nwg / 8, rr = nwg % 8, xcd = bid % 8;
+  const int grp = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + bid / 8;
+  const int tile0 = grp * NT;
+
+  const int KS = K / 32;
+  const int per = (KS + WAVES - 1) / WAVES;
+  const int ks0 = min(KS, wid * per);
+  const int ks1 = min(KS, ks0 + per);
+
+  f32x4 acc[MT][NT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float ss[MT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i) ss[i] = 0.f;
+
+  const bf16x8* wt[NT];
+#pragma unroll
+  for (int j = 0; j < NT; ++j)
+    wt[j] = reinterpret_cast<const bf16x8*>(wp + ((size_t)(tile0 + j) * KS) * 512) + lane;
+  const bf16* xr[MT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i) {
+    const int m = 16 * i + c;
+    xr[i] = x + (size_t)(m < M ? m : 0) * ldx + 8 * g;
+  }
+
+  auto step = [&](const bf16x8 (&bw)[NT], int ks) {
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+      const bf16x8 a = *reinterpret_cast<const bf16x8*>(xr[i] + 32 * ks);
+      if constexpr (NORM) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float v = (float)a[e];
+          ss[i] = fmaf(v, v, ss[i]);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < NT; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bw[j], acc[i][j], 0, 0, 0);
+    }
+  };
+
+  int ks = ks0;
+  for (; ks + U <= ks1; ks += U) {
+    bf16x8 bw[U][NT];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int j = 0; j < NT; ++j) bw[u][j] = wt[j][(size_t)(ks + u) * 64];
+#pragma unroll
+    for (int u = 0; u < U; ++u) step(bw[u], ks + u);
+  }
+  for (; ks < ks1; ++ks) {
+    bf16x8 bw[NT];
+#pragma unroll
+    for (int j = 0; j < NT; ++j) bw[j] = wt[j][(size_t)ks * 64];
+    step(bw, ks);
+  }
+
+  // C layout of a 16x16 tile: lane (g, c) holds rows 4g + r, column c.
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        red[(wid * TM + 16 * i + 4 * g + r) * TN + 16 * j + c] = acc[i][j][r];
+  if constexpr (NORM) {
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+      float v = ss[i];
+      v += __shfl_xor(v, 16, 64);
+      v += __shfl_xor(v, 32, 64);
+      if (g == 0) ssq[wid * TM + 16 * i + c] = v;
+    }
+  }
+  __syncthreads();
+  constexpr int TNO = EPI == EPI_SILU ? TN / 2 : TN;
+  const int n0 = (EPI == EPI_SILU ? tile0 / 2 : tile0) * 16;
+  const float inv_k = 1.f / (float)K;
+  for (int e = threadIdx.x; e < TM * TNO; e += WAVES * 64) {
+    const int m = e / TNO, n = e % TNO;
+    if (m >= M) continue;
+    float rs = 1.f;
+    if constexpr (NORM) {
+      float t = 0.f;
+#pragma unroll
+      for (int wv = 0; wv < WAVES; ++wv) t += ssq[wv * TM + m];
+      rs = rsqrtf(t * inv_k + eps);
+    }
+    if constexpr (EPI == EPI_SILU) {
+      const int p = n >> 4, cc = n & 15;
+      float gs = 0.f, us = 0.f;
+#pragma unroll
+      for (int wv = 0; wv < WAVES; ++wv) {
+        gs += red[(wv * TM + m) * TN + 32 * p + cc];
+        us += red[(wv * TM + m) * TN + 32 * p + 16 + cc];
+      }
+      gs *= rs;
+      us *= rs;
+      y[(size_t)m * ldy + n0 + n] = (bf16)(gs / (1.f + __expf(-gs)) * us);
+    } else {
+      float s = 0.f;
+#pragma unroll
+      for (int wv = 0; wv < WAVES; ++wv) s += red[(wv * TM + m) * TN + n];
+      s *= rs;
+      if constexpr (EPI == EPI_RESID) s += (float)resid[(size_t)m * ldr + n0 + n];
+      y[(size_t)m * ldy + n0 + n] = (bf16)s;
+    }
+  }
+}
+
+template <int MT, int NT, int WAVES, int EPI, bool NORM>
+static int launch_dg(bf16* y, const bf16* x, const bf16* wp, const bf16* resid, int M, int N, int K,
+                     int ldx, int ldy, int ldr, float eps, hipStream_t st) {
+  constexpr int U = MT == 1 ? 8 : (MT == 2 ? 4 : 2);
+  const size_t lds = (size_t)WAVES * MT * 16 * (NT * 16 + 1) * sizeof(float);
+  auto kern = decode_gemm_kernel<MT, NT, WAVES, U, EPI, NORM>;
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr = true;
+  }
+  hipLaunchKernelGGL(kern, dim3(N / (16 * NT)), dim3(WAVES * 64), lds, st, y, x, wp, resid, M, N, K, ldx,
+                     ldy, ldr, eps);
+  return 0;
+}
+
+template <int MT, int EPI, bool NORM>
+static int pick_nw(int nt, int waves, bf16* y, const bf16* x, const bf16* wp, const bf16* resid, int M,
+                   int N, int K, int ldx, int ldy, int ldr, float eps, hipStream_t st) {
+#define PA_DG(NT_, W_)                                                                                 \
+  if (nt == NT_ && waves == W_)                                                                        \
+    return launch_dg<MT, NT_, W_, EPI, NORM>(y, x, wp, resid, M, N, K, ldx, ldy, ldr, eps, st);
+  if constexpr (EPI != EPI_SILU) {
+    PA_DG(1, 8) PA_DG(1, 16)
+  }
+  PA_DG(2, 8) PA_DG(2, 16)
+  if constexpr (MT <= 2) {
+    PA_DG(4, 8) PA_DG(4, 16)
+  } else {
+    PA_DG(4, 8)
+  }
+#undef PA_DG
+  return 1;
+}
+
+// Default (tile width, waves) per shape — chosen from tools/gemm_bench.py --decode
+// (profiles/r1_decode_gemm.md): enough workgroups to cover 256 CUs, K split over
+// 16 waves when there is only ~one workgroup per CU.
+static void default_cfg(int MT, int N, int K, int epi, int& nt, int& waves) {
+  const int tiles = N / 16;
+  nt = (epi == EPI_SILU) ? 2 : (tiles >= 2048 ? 2 : 1);
+  if (MT >= 4 && nt == 1 && epi != EPI_SILU) nt = 1;
+  const int wgs = tiles / nt;
+  waves = wgs <= 512 ? 16 : 8;
+  if (MT >= 4) waves = 8;
+  (void)K;
+}
+
+}  // namespace pa
+
+// Returns 1 if the shape/config is not handled, 0 on success, -2 on a launch error.
+// epi: 0 plain, 1 silu(gate)*up over interleaved tile pairs, 2 residual add.
+extern "C" int pa_decode_gemm(void* y, const void* x, const void* wp, const void* resid, int M, int N, int K,
+                              int ldx, int ldy, int ldr, int epi, int norm, float eps, int nt, int waves,
+                              hipStream_t st) {
+  using namespace pa;
+  if (M <= 0) return 0;
+  if (M > 64 || K % 32 != 0 || N % 16 != 0 || epi < 0 || epi > 2) return 1;
+  if (epi == EPI_SILU && (N / 16) % 2) return 1;
+  if (epi == EPI_RESID && !resid) return 1;
+  const int MT = M <= 16 ? 1 : (M <= 32 ? 2 : 4);
+  if (nt <= 0 || waves <= 0) default_cfg(MT, N, K, epi, nt, waves);
+  if ((N / 16) % nt) return 1;
+  bf16* Y = (bf16*)y;
+  const bf16* X = (const bf16*)x;
+  const bf16* W = (const bf16*)wp;
+  const bf16* R = (const bf16*)resid;
+  int rc = 1;
+#define PA_DGE(MT_)                                                                                         \
+  switch (epi * 2 + (norm ? 1 : 0)) {                                                                       \
+    case 0: rc = pick_nw<MT_, EPI_PLAIN, false>(nt, waves, Y, X, W, R, M, N, K, ldx, ldy, ldr, eps, st); break; \
+    case 1: rc = pick_nw<MT_, EPI_PLAIN, true>(nt, waves, Y, X, W, R, M, N, K, ldx, ldy, ldr, eps, st); break;  \
+    case 3: rc = pick_nw<MT_, EPI_SILU, true>(nt, waves, Y, X, W, R, M, N, K, ldx, ldy, ldr, eps, st); break;   \
+    case 4: rc = pick_nw<MT_, EPI_RESID, false>(nt, waves, Y, X, W, R, M, N, K, ldx, ldy, ldr, eps, st); break; \
+    default: rc = 1;                                                                                        \
+  }
+  switch (MT) {
+    case 1: PA_DGE(1) break;
+    case 2: PA_DGE(2) break;
+    default: PA_DGE(4) break;
+  }
+#undef PA_DGE
+  if (rc != 0) return rc;
+  return (int)hipGetLastError() == 0 ? 0 : -2;
+}

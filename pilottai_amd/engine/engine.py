@@ -76,6 +76,7 @@ class EngineConfig:
     capture_on_start: bool = True
     token_align: int = 256   # GEMM-friendly step sizes (runtime/scheduler.h); 0 = off
     align_slack: int = 96
+    decode_fused: Optional[bool] = None  # packed-weight fused decode path; None = when it fits in HBM
 
 
 # TP step header: [op, T, ns, nsamp, bucket, masks_changed, n_copy, truncate]
@@ -154,7 +155,8 @@ class LLMEngine:
 
             self.tuned_gemms = load_tuned_gemms(mc.name, self.tp.size)
         t0 = time.time()
-        self.model = LlamaModel(mc, self.device, tp=self.tp, seed=cfg.seed, weights_path=cfg.weights_path)
+        self.model = LlamaModel(mc, self.device, tp=self.tp, seed=cfg.seed, weights_path=cfg.weights_path,
+                                decode_pack=cfg.decode_fused)
         self.load_time = time.time() - t0
         self.max_model_len = min(cfg.max_model_len, mc.max_position)
         # ---- KV cache sizing (288 GB HBM: the default leaves room for graphs/activations)

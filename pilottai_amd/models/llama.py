@@ -118,8 +118,12 @@ class KVCache:
 
 
 class LlamaModel:
+    # decode steps of at most this many tokens run the fused packed-weight path
+    # (csrc/ops/gemm_decode.hip; tools/decode_gemm_bench.py, profiles/r1_decode_gemm.md)
+    DECODE_FUSED_MAX_T = 16
+
     def __init__(self, cfg: LlamaConfig, device, dtype=torch.bfloat16, tp: Optional[TPGroup] = None,
-                 seed: int = 0, weights_path: Optional[str] = None):
+                 seed: int = 0, weights_path: Optional[str] = None, decode_pack: Optional[bool] = None):
         self.cfg = cfg
         self.device = torch.device(device)
         self.dtype = dtype
@@ -139,6 +143,34 @@ class LlamaModel:
             self._load_hf(weights_path)
         else:
             self._init_random(seed)
+        self.decode_packed = False
+        if decode_pack is None:
+            decode_pack = self._pack_fits()
+        if decode_pack:
+            self._pack_decode_weights()
+
+    # -- decode weight copies ------------------------------------------------------
+    def _pack_fits(self) -> bool:
+        """A second, fragment-major copy of every projection is kept for decode
+        steps (hipBLASLt keeps the row-major one for prefill). It is worth its HBM
+        whenever both copies leave most of the card to the KV cache: Llama-3-8B
+        (2 x 15 GB), 70B at TP=8 (2 x 17.6 GB/GPU); not 70B at TP=1 (141 GB)."""
+        if self.device.type != "cuda":
+            return True
+        total = torch.cuda.get_device_properties(self.device).total_memory
+        return 2 * self.weight_bytes() <= 0.45 * total
+
+    def _pack_decode_weights(self):
+        """Fragment-major copies for ops.decode_gemm, with the RMSNorm weights
+        folded into the columns of the matrices they feed (QKV <- ln1, gate_up <-
+        ln2), so the decode path needs no separate norm kernel."""
+        for L in self.layers:
+            L["wqkv_p"] = ops.pack_decode_weight(L["wqkv"] * L["ln1"][None, :])
+            L["wo_p"] = ops.pack_decode_weight(L["wo"])
+            L["w13_p"] = ops.pack_decode_gate_up(L["w13"] * L["ln2"][None, :])
+            L["w2_p"] = ops.pack_decode_weight(L["w2"])
+        self.lm_head_p = ops.pack_decode_weight(self.lm_head)
+        self.decode_packed = True
 
     # -- weights -----------------------------------------------------------------
     def _init_random(self, seed: int):
@@ -240,6 +272,8 @@ class LlamaModel:
         n = self.embed.numel() + self.norm.numel()
         if self.lm_head is not self.embed:
             n += self.lm_head.numel()
+        if getattr(self, "lm_head_p", None) is not None:
+            n += self.lm_head_p.numel()
         for L in self.layers:
             n += sum(t.numel() for t in L.values())
         return n * self.embed.element_size()
@@ -259,6 +293,8 @@ class LlamaModel:
         """Returns local-vocab logits [num_logit_rows, V/tp] (bf16)."""
         cfg = self.cfg
         T = num_tokens
+        if self.decode_packed and T <= self.DECODE_FUSED_MAX_T:
+            return self._forward_decode(meta, kv, T, num_logit_rows, part_o, part_ml)
         H, KVh, hd = self.h_local, self.kv_local, cfg.head_dim
         ids = meta.input_ids[:T].long() if self.device.type == "cpu" else meta.input_ids[:T]
         h = self._embed(ids)
@@ -287,6 +323,46 @@ class LlamaModel:
         rows = rows.long() if self.device.type == "cpu" else rows
         xs = x.index_select(0, rows)
         return ops.linear(xs, self.lm_head, "lm_head")
+
+    def _forward_decode(self, meta: StepMeta, kv: KVCache, T: int, num_logit_rows: int,
+                        part_o: torch.Tensor, part_ml: torch.Tensor) -> torch.Tensor:
+        """Decode-sized step on the packed weights: 6 launches per layer
+        (QKV+norm, RoPE/KV write, attention, O+residual, gate_up+norm+SwiGLU,
+        down+residual) instead of 9; the residual stream h is updated in place."""
+        cfg = self.cfg
+        H, KVh, hd = self.h_local, self.kv_local, cfg.head_dim
+        eps = cfg.rms_eps
+        tp = self.tp.size > 1
+        ids = meta.input_ids[:T].long() if self.device.type == "cpu" else meta.input_ids[:T]
+        h = self._embed(ids)
+        if not h.is_contiguous():
+            h = h.contiguous()
+        for li, L in enumerate(self.layers):
+            qkv = ops.decode_gemm(h, L["wqkv_p"], "plain", norm=True, eps=eps)
+            q = torch.empty(T, H, hd, dtype=self.dtype, device=self.device)
+            ops.rope_cache(q, kv.k[li], kv.v[li], qkv, meta.positions, meta.slots, self.cos_sin, H, KVh)
+            attn = torch.empty(T, H, hd, dtype=self.dtype, device=self.device)
+            ops.paged_attention(attn, part_o, part_ml, q, kv.k[li], kv.v[li], meta.items, meta.n_items,
+                                meta.att_counters, meta.q_start, meta.q_len, meta.ctx_len,
+                                meta.block_table, self.scale, num_seqs=meta.num_seqs, part_size=meta.part_size)
+            a2 = attn.view(T, H * hd)
+            if tp:
+                o = ops.decode_gemm(a2, L["wo_p"], "plain")
+                self.tp.all_reduce(o)
+                h.add_(o)
+            else:
+                ops.decode_gemm(a2, L["wo_p"], "resid", resid=h, out=h)
+            a = ops.decode_gemm(h, L["w13_p"], "silu", norm=True, eps=eps)
+            if tp:
+                d = ops.decode_gemm(a, L["w2_p"], "plain")
+                self.tp.all_reduce(d)
+                h.add_(d)
+            else:
+                ops.decode_gemm(a, L["w2_p"], "resid", resid=h, out=h)
+        rows = meta.logit_rows[:num_logit_rows]
+        rows = rows.long() if self.device.type == "cpu" else rows
+        xs = ops.rmsnorm(h.index_select(0, rows), self.norm, eps)
+        return ops.decode_gemm(xs, self.lm_head_p, "plain")
 
     # -- reference (dense, no cache) forward used by numerics tests ----------------
     @torch.no_grad()

@@ -1,6 +1,9 @@
 """CDNA4 kernels (HIP, gfx950) and their fp32 PyTorch references."""
 from .kernels import (  # noqa: F401
     cosine_topk,
+    decode_gemm,
+    pack_decode_gate_up,
+    pack_decode_weight,
     fused_add_rmsnorm,
     linear,
     native_available,

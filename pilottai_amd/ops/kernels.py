@@ -223,3 +223,70 @@ def linear(x: torch.Tensor, w: torch.Tensor, kind: str) -> torch.Tensor:
             and x.is_contiguous()):
         return skinny_gemm(x, w)
     return torch.nn.functional.linear(x, w)
+
+
+# ---------------------------------------------------------------------------
+# Decode-step projections on fragment-major packed weights (csrc/ops/gemm_decode.hip)
+
+DECODE_EPI = {"plain": 0, "silu": 1, "resid": 2}
+
+
+def pack_decode_weight(w: torch.Tensor) -> torch.Tensor:
+    """[N, K] row-major -> [N/16, K/32, 64, 8]: lane l = 16*g + c of tile (t, s)
+    holds w[16t + c, 32s + 8g : 32s + 8g + 8] (the MFMA 16x16x32 B fragment)."""
+    N, K = w.shape
+    if N % 16 or K % 32:
+        raise ValueError(f"cannot pack a [{N}, {K}] weight (needs N % 16 == 0, K % 32 == 0)")
+    return w.reshape(N // 16, 16, K // 32, 4, 8).permute(0, 2, 3, 1, 4).contiguous().view(N // 16, K // 32, 64, 8)
+
+
+def pack_decode_gate_up(w13: torch.Tensor) -> torch.Tensor:
+    """[2F, K] = [gate; up] -> packed tiles interleaved (gate t, up t, gate t+1, ...),
+    so one workgroup holds both halves of the same 16 outputs (EPI silu)."""
+    F2, K = w13.shape
+    F = F2 // 2
+    g = pack_decode_weight(w13[:F])
+    u = pack_decode_weight(w13[F:])
+    return torch.stack([g, u], 1).reshape(F2 // 16, K // 32, 64, 8)
+
+
+def unpack_decode_weight(wp: torch.Tensor) -> torch.Tensor:
+    T, S = wp.shape[0], wp.shape[1]
+    return wp.view(T, S, 4, 16, 8).permute(0, 3, 1, 2, 4).reshape(T * 16, S * 32)
+
+
+def unpack_decode_gate_up(wp: torch.Tensor) -> torch.Tensor:
+    T, S = wp.shape[0], wp.shape[1]
+    pairs = wp.view(T // 2, 2, S, 64, 8)
+    return torch.cat([unpack_decode_weight(pairs[:, 0]), unpack_decode_weight(pairs[:, 1])], 0)
+
+
+def decode_gemm(x: torch.Tensor, wp: torch.Tensor, epi: str = "plain", norm: bool = False,
+                eps: float = 1e-5, resid: Optional[torch.Tensor] = None,
+                out: Optional[torch.Tensor] = None, nt: int = 0, waves: int = 0) -> torch.Tensor:
+    """y = epi(rownorm(x) @ W.T) for M <= 64 rows with W packed by pack_decode_weight
+    (gate_up: pack_decode_gate_up). `norm` scales each row by rsqrt(mean(x^2)+eps)
+    (the RMSNorm weight must already be folded into W); epi "silu" returns
+    silu(gate)*up [M, F]; epi "resid" returns resid + acc (out may alias resid)."""
+    M, K = x.shape
+    N = wp.shape[0] * 16
+    code = DECODE_EPI[epi]
+    NO = N // 2 if code == 1 else N
+    if out is None:
+        out = torch.empty(M, NO, dtype=x.dtype, device=x.device)
+    if _on_gpu(x):
+        if not require_native().decode_gemm(out, x, wp, resid, code, bool(norm), float(eps), int(nt), int(waves)):
+            raise ValueError(f"decode_gemm does not handle M={M} N={N} K={K} epi={epi} nt={nt} waves={waves}")
+        return out
+    xf = x.float()
+    W = unpack_decode_gate_up(wp) if code == 1 else unpack_decode_weight(wp)
+    acc = xf @ W.float().T
+    if norm:
+        acc = acc * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps)
+    if code == 1:
+        g, u = acc[:, :NO], acc[:, NO:]
+        acc = g * torch.sigmoid(g) * u
+    elif code == 2:
+        acc = acc + resid.float()
+    out.copy_(acc.to(out.dtype))
+    return out

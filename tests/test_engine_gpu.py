@@ -66,13 +66,15 @@ def test_sampling_batch_invariance(engine):
 
 
 def test_top_k_top_p_graph_variant(engine):
-    """top-k = 1 reproduces greedy through the truncating graph variant; mixed
-    batches (truncating + plain rows) keep the plain rows' tokens unchanged."""
+    """top-k = 1 decodes an argmax token at every step through the truncating graph
+    variant (checked against the fp32 reference: bf16 logits of a random-init
+    model tie often enough that "the same token as greedy" is not well defined);
+    mixed batches (truncating + plain rows) keep the plain rows' tokens unchanged."""
     tok = engine.tok
     p = tok.encode("nucleus sampling probe for the engine")
-    greedy = engine.generate([p], temperature=0.0, max_tokens=8, ignore_eos=True)[0]
     k1 = engine.generate([p], temperature=1.2, max_tokens=8, ignore_eos=True, top_k=1, seed=9)[0]
-    assert k1.token_ids == greedy.token_ids
+    assert len(k1.token_ids) == 8
+    _check_greedy(engine, p, k1.token_ids)
     plain = engine.generate([p], temperature=0.8, max_tokens=8, ignore_eos=True, seed=77)[0]
     both = engine.generate([p, p], temperature=0.8, max_tokens=8, ignore_eos=True, seed=77, top_p=0.5)
     # top_p applies to both rows here; a plain-only rerun must match the first plain run

@@ -270,3 +270,40 @@ def test_topkp_threshold_matches_reference(gpu, V):
                 assert allowed[tok[i]]
         if trial == 0:
             assert tok[1].item() == int(lg[1].argmax())  # k = 1 is greedy
+
+
+@pytest.mark.parametrize("M,N,K,epi,norm", [
+    (1, 6144, 4096, "plain", True), (8, 4096, 4096, "resid", False), (13, 28672, 4096, "silu", True),
+    (16, 4096, 14336, "resid", False), (5, 128256, 4096, "plain", False), (29, 6144, 4096, "plain", False),
+    (64, 1024, 512, "silu", True), (40, 768, 512, "resid", False)])
+def test_decode_gemm(gpu, M, N, K, epi, norm):
+    """Packed-weight decode projection (csrc/ops/gemm_decode.hip) vs fp32: the
+    folded RMSNorm, SwiGLU and residual epilogues, every default tile config."""
+    torch.manual_seed(11)
+    x = _bf(M, K, dev=gpu)
+    w = _bf(N, K, dev=gpu, scale=0.05)
+    resid = _bf(M, N, dev=gpu) if epi == "resid" else None
+    wp = ops.pack_decode_gate_up(w) if epi == "silu" else ops.pack_decode_weight(w)
+    y = ops.decode_gemm(x, wp, epi, norm=norm, resid=resid)
+    acc = x.float() @ w.float().T
+    if norm:
+        acc = acc * torch.rsqrt(x.float().pow(2).mean(-1, keepdim=True) + 1e-5)
+    if epi == "silu":
+        acc = torch.nn.functional.silu(acc[:, :N // 2]) * acc[:, N // 2:]
+    elif epi == "resid":
+        acc = acc + resid.float()
+    torch.testing.assert_close(y.float(), acc, atol=3e-2, rtol=2e-2)
+    if epi == "resid":  # in place on the residual stream
+        r2 = resid.clone()
+        ops.decode_gemm(x, wp, "resid", resid=r2, out=r2)
+        torch.testing.assert_close(r2, y, atol=0, rtol=0)
+
+
+@pytest.mark.parametrize("nt,waves", [(1, 8), (1, 16), (2, 8), (2, 16), (4, 8), (4, 16)])
+def test_decode_gemm_configs(gpu, nt, waves):
+    torch.manual_seed(12)
+    M, N, K = 16, 4096, 4096
+    x = _bf(M, K, dev=gpu)
+    w = _bf(N, K, dev=gpu, scale=0.05)
+    y = ops.decode_gemm(x, ops.pack_decode_weight(w), "plain", nt=nt, waves=waves)
+    torch.testing.assert_close(y.float(), x.float() @ w.float().T, atol=3e-2, rtol=2e-2)
