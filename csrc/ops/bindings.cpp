@@ -33,6 +33,9 @@ int pa_skinny_gemm(void* y, const void* x, const void* w, int M, int N, int K, i
 int pa_decode_gemm(void* y, const void* x, const void* wp, const void* resid, int M, int N, int K,
                    int ldx, int ldy, int ldr, int epi, int norm, float eps, int nt, int waves,
                    hipStream_t st);
+int pa_decode_qkv_rope(const void* x, const void* wp, int M, int N, int K, int ldx, float eps, void* q_out,
+                       void* k_cache, void* v_cache, const int* positions, const int* slots,
+                       const float* cos_sin, int H, int KV, int nt, int waves, hipStream_t st);
 long long pa_cosine_topk_workspace_bytes(int Q, int N, int K);
 int pa_cosine_topk(float* out_scores, int* out_rows, void* workspace, const void* queries,
                    const void* index, int Q, int N, int D, int K, const int* row_priority,
@@ -199,6 +202,35 @@ bool decode_gemm(at::Tensor y, at::Tensor x, at::Tensor wp, c10::optional<at::Te
   return rc == 0;
 }
 
+// Decode QKV projection + RoPE + paged KV write (csrc/ops/gemm_decode.hip, EPI_ROPE).
+void decode_qkv_rope(at::Tensor x, at::Tensor wp, double eps, at::Tensor q_out, at::Tensor k_cache,
+                     at::Tensor v_cache, at::Tensor positions, at::Tensor slots, at::Tensor cos_sin, int64_t H,
+                     int64_t KV) {
+  check_gpu(wp, "wp"); check_gpu(q_out, "q_out"); check_gpu(k_cache, "k_cache"); check_gpu(v_cache, "v_cache");
+  check_gpu(positions, "positions"); check_gpu(slots, "slots"); check_gpu(cos_sin, "cos_sin");
+  TORCH_CHECK(x.is_cuda() && x.dim() == 2 && x.stride(1) == 1, "x must be a 2-D GPU tensor, unit inner stride");
+  check_dtype(x, at::kBFloat16, "x"); check_dtype(wp, at::kBFloat16, "wp"); check_dtype(q_out, at::kBFloat16, "q_out");
+  check_dtype(k_cache, at::kBFloat16, "k_cache"); check_dtype(v_cache, at::kBFloat16, "v_cache");
+  check_dtype(positions, at::kInt, "positions"); check_dtype(slots, at::kInt, "slots");
+  check_dtype(cos_sin, at::kFloat, "cos_sin");
+  TORCH_CHECK(wp.dim() == 4 && wp.size(2) == 64 && wp.size(3) == 8, "wp must be packed [N/16, K/32, 64, 8]");
+  const int M = x.size(0), K = x.size(1), N = wp.size(0) * 16;
+  TORCH_CHECK(wp.size(1) * 32 == K, "packed weight K mismatch");
+  TORCH_CHECK(N == (H + 2 * KV) * 128, "packed QKV has ", N, " columns, expected (H + 2 KV) * 128");
+  TORCH_CHECK(q_out.numel() >= (int64_t)M * H * 128, "q_out too small");
+  TORCH_CHECK(positions.numel() >= M && slots.numel() >= M, "positions/slots shorter than x");
+  TORCH_CHECK(cos_sin.dim() == 2 && cos_sin.size(1) == 128, "cos_sin must be [max_pos, 128]");
+  TORCH_CHECK(k_cache.dim() == 5 && k_cache.size(1) == KV && k_cache.size(2) == 16 && k_cache.size(3) == 16 &&
+                  k_cache.size(4) == 8, "k_cache must be [NB, KV, 16, 16, 8]");
+  TORCH_CHECK(v_cache.dim() == 4 && v_cache.size(1) == KV && v_cache.size(2) == 128 && v_cache.size(3) == 16,
+              "v_cache must be [NB, KV, 128, 16]");
+  const int rc = pa_decode_qkv_rope(x.data_ptr(), wp.data_ptr(), M, N, K, x.stride(0), (float)eps, q_out.data_ptr(),
+                                    k_cache.data_ptr(), v_cache.data_ptr(), positions.data_ptr<int>(),
+                                    slots.data_ptr<int>(), cos_sin.data_ptr<float>(), (int)H, (int)KV, 0, 0,
+                                    cur_stream());
+  check_rc(rc < 0 ? rc : (rc > 0 ? -1 : 0), "decode_qkv_rope");
+}
+
 int64_t sample_workspace_floats(int64_t rows, int64_t V) {
   return pa_sample_workspace_floats(rows, V);
 }
@@ -330,6 +362,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("decode_gemm", &decode_gemm, py::arg("y"), py::arg("x"), py::arg("wp"), py::arg("resid") = py::none(),
         py::arg("epi") = 0, py::arg("norm") = false, py::arg("eps") = 1e-5, py::arg("nt") = 0,
         py::arg("waves") = 0);
+  m.def("decode_qkv_rope", &decode_qkv_rope);
   m.def("paged_attention", &paged_attention, py::arg("out"), py::arg("part_o"), py::arg("part_ml"), py::arg("q"),
         py::arg("k_cache"), py::arg("v_cache"), py::arg("items"), py::arg("n_items"), py::arg("counters"),
         py::arg("q_start"), py::arg("q_len"), py::arg("ctx_len"), py::arg("block_table"), py::arg("scale"),

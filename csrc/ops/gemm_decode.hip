@@ -35,18 +35,48 @@
 
 namespace pa {
 
-enum { EPI_PLAIN = 0, EPI_SILU = 1, EPI_RESID = 2 };
+enum { EPI_PLAIN = 0, EPI_SILU = 1, EPI_RESID = 2, EPI_ROPE = 3 };
+
+// EPI_ROPE: the QKV projection with RoPE + paged KV write in its epilogue
+// (replaces rope_cache.hip on decode steps). The packed QKV columns are permuted
+// per 128-wide head to tile order [0,4,1,5,2,6,3,7], so a workgroup of NT = 2
+// tiles holds rotary dims i and i + 64 of one head for 16 consecutive i.
+struct RopeArgs {
+  bf16* q_out;           // [M, H, 128]
+  bf16* k_cache;         // [NB, KV, 16, 16, 8]  fragment-major pages (rope_cache.hip)
+  bf16* v_cache;         // [NB, KV, 128, 16]
+  const int* positions;  // [M]
+  const int* slots;      // [M], < 0 = no cache write
+  const float* cos_sin;  // [max_pos, 128] (cos | sin)
+  int H, KV;
+};
+
+struct DgArgs {
+  bf16* y;
+  const bf16* x;
+  const bf16* wp;
+  const bf16* resid;
+  int M, N, K, ldx, ldy, ldr;
+  float eps;
+  RopeArgs rope;
+};
 
 template <int MT, int NT, int WAVES, int U, int EPI, bool NORM>
-__global__ __launch_bounds__(WAVES * 64) void decode_gemm_kernel(
-    bf16* __restrict__ y, const bf16* __restrict__ x, const bf16* __restrict__ wp,
-    const bf16* resid, int M, int N, int K, int ldx, int ldy, int ldr, float eps) {
+__global__ __launch_bounds__(WAVES * 64) void decode_gemm_kernel(const DgArgs A) {
+  bf16* __restrict__ y = A.y;
+  const bf16* __restrict__ x = A.x;
+  const bf16* __restrict__ wp = A.wp;
+  const bf16* resid = A.resid;
+  const int M = A.M, K = A.K, ldx = A.ldx, ldy = A.ldy, ldr = A.ldr;
+  const float eps = A.eps;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int TM = MT * 16, TN = NT * 16;
   float* red = reinterpret_cast<float*>(smem);  // [WAVES][TM][TN]
   float* ssq = red + WAVES * TM * TN;            // [WAVES][TM]
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int g = lane >> 4, c = lane & 15;
+  const int N = A.N;
+  (void)N;
   const int nwg = gridDim.x, bid = blockIdx.x;
   const int q = nwg / 8, rr = nwg % 8, xcd = bid % 8;
   const int grp = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + bid / 8;
@@ -129,6 +159,58 @@ __global__ __launch_bounds__(WAVES * 64) void decode_gemm_kernel(
     }
   }
   __syncthreads();
+  if constexpr (EPI == EPI_ROPE) {
+    static_assert(NT == 2, "EPI_ROPE pairs the two tiles of a workgroup");
+    const RopeArgs& R = A.rope;
+    const int hh = tile0 >> 3, i0 = 16 * ((tile0 & 7) >> 1);
+    for (int e = threadIdx.x; e < TM * 16; e += WAVES * 64) {
+      const int m = e >> 4, cc = e & 15;
+      if (m >= M) continue;
+      float rs = 1.f;
+      if constexpr (NORM) {
+        float t = 0.f;
+#pragma unroll
+        for (int wv = 0; wv < WAVES; ++wv) t += ssq[wv * TM + m];
+        rs = rsqrtf(t / (float)K + eps);
+      }
+      float a = 0.f, b = 0.f;
+#pragma unroll
+      for (int wv = 0; wv < WAVES; ++wv) {
+        a += red[(wv * TM + m) * TN + cc];
+        b += red[(wv * TM + m) * TN + 16 + cc];
+      }
+      a *= rs;
+      b *= rs;
+      const int i = i0 + cc;
+      float o1 = a, o2 = b;
+      if (hh < R.H + R.KV) {
+        const float* cs = R.cos_sin + (size_t)R.positions[m] * 128;
+        const float c = cs[i], sn = cs[64 + i];
+        o1 = a * c - b * sn;
+        o2 = b * c + a * sn;
+      }
+      if (hh < R.H) {
+        bf16* dst = R.q_out + ((size_t)m * R.H + hh) * 128;
+        dst[i] = (bf16)o1;
+        dst[i + 64] = (bf16)o2;
+      } else {
+        const int slot = R.slots[m];
+        if (slot >= 0) {
+          const int blk = slot >> 4, off = slot & 15;
+          if (hh < R.H + R.KV) {
+            bf16* page = R.k_cache + ((size_t)blk * R.KV + (hh - R.H)) * 128 * 16;
+            page[((size_t)(i >> 3) * 16 + off) * 8 + (i & 7)] = (bf16)o1;
+            page[((size_t)((i + 64) >> 3) * 16 + off) * 8 + (i & 7)] = (bf16)o2;
+          } else {
+            bf16* page = R.v_cache + ((size_t)blk * R.KV + (hh - R.H - R.KV)) * 128 * 16 + off;
+            page[(size_t)i * 16] = (bf16)o1;
+            page[(size_t)(i + 64) * 16] = (bf16)o2;
+          }
+        }
+      }
+    }
+    return;
+  }
   constexpr int TNO = EPI == EPI_SILU ? TN / 2 : TN;
   const int n0 = (EPI == EPI_SILU ? tile0 / 2 : tile0) * 16;
   const float inv_k = 1.f / (float)K;
@@ -165,8 +247,7 @@ __global__ __launch_bounds__(WAVES * 64) void decode_gemm_kernel(
 }
 
 template <int MT, int NT, int WAVES, int EPI, bool NORM>
-static int launch_dg(bf16* y, const bf16* x, const bf16* wp, const bf16* resid, int M, int N, int K,
-                     int ldx, int ldy, int ldr, float eps, hipStream_t st) {
+static int launch_dg(const DgArgs& a, hipStream_t st) {
   constexpr int U = MT == 1 ? 8 : (MT == 2 ? 4 : 2);
   const size_t lds = (size_t)WAVES * MT * 16 * (NT * 16 + 1) * sizeof(float);
   auto kern = decode_gemm_kernel<MT, NT, WAVES, U, EPI, NORM>;
@@ -175,41 +256,73 @@ static int launch_dg(bf16* y, const bf16* x, const bf16* wp, const bf16* resid, 
     hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr = true;
   }
-  hipLaunchKernelGGL(kern, dim3(N / (16 * NT)), dim3(WAVES * 64), lds, st, y, x, wp, resid, M, N, K, ldx,
-                     ldy, ldr, eps);
+  hipLaunchKernelGGL(kern, dim3(a.N / (16 * NT)), dim3(WAVES * 64), lds, st, a);
   return 0;
 }
 
 template <int MT, int EPI, bool NORM>
-static int pick_nw(int nt, int waves, bf16* y, const bf16* x, const bf16* wp, const bf16* resid, int M,
-                   int N, int K, int ldx, int ldy, int ldr, float eps, hipStream_t st) {
-#define PA_DG(NT_, W_)                                                                                 \
-  if (nt == NT_ && waves == W_)                                                                        \
-    return launch_dg<MT, NT_, W_, EPI, NORM>(y, x, wp, resid, M, N, K, ldx, ldy, ldr, eps, st);
-  if constexpr (EPI != EPI_SILU) {
-    PA_DG(1, 8) PA_DG(1, 16)
-  }
-  PA_DG(2, 8) PA_DG(2, 16)
-  if constexpr (MT <= 2) {
-    PA_DG(4, 8) PA_DG(4, 16)
+static int pick_nw(int nt, int waves, const DgArgs& a, hipStream_t st) {
+#define PA_DG(NT_, W_) \
+  if (nt == NT_ && waves == W_) return launch_dg<MT, NT_, W_, EPI, NORM>(a, st);
+  if constexpr (EPI == EPI_ROPE) {
+    PA_DG(2, 8) PA_DG(2, 16)
+    return 1;
   } else {
-    PA_DG(4, 8)
+    if constexpr (EPI != EPI_SILU) {
+      PA_DG(1, 8) PA_DG(1, 16)
+    }
+    PA_DG(2, 8) PA_DG(2, 16)
+    if constexpr (MT <= 2) {
+      PA_DG(4, 8) PA_DG(4, 16)
+    } else {
+      PA_DG(4, 8)
+    }
   }
 #undef PA_DG
   return 1;
 }
 
-// Default (tile width, waves) per shape — chosen from tools/gemm_bench.py --decode
-// (profiles/r1_decode_gemm.md): enough workgroups to cover 256 CUs, K split over
-// 16 waves when there is only ~one workgroup per CU.
-static void default_cfg(int MT, int N, int K, int epi, int& nt, int& waves) {
+// Default (tile width, waves) per shape, from tools/decode_gemm_bench.py on MI355X
+// (profiles/r1_decode_gemm.md): 2 column tiles per workgroup once there are >= 384
+// tiles (x fragments re-used across both), 4 for wide matrices at M > 8 (the x
+// stream grows with M); K split over 16 waves when a workgroup is alone on its CU.
+static void default_cfg(int MT, int M, int N, int epi, int& nt, int& waves) {
   const int tiles = N / 16;
-  nt = (epi == EPI_SILU) ? 2 : (tiles >= 2048 ? 2 : 1);
-  if (MT >= 4 && nt == 1 && epi != EPI_SILU) nt = 1;
-  const int wgs = tiles / nt;
-  waves = wgs <= 512 ? 16 : 8;
-  if (MT >= 4) waves = 8;
-  (void)K;
+  if (epi == EPI_ROPE) nt = 2;
+  else if (epi == EPI_SILU) nt = (M > 8 && tiles % 4 == 0) ? 4 : 2;
+  else if (MT >= 2 && tiles >= 1792 && tiles % 4 == 0) nt = 4;
+  else nt = (tiles >= 384 && tiles % 2 == 0) ? 2 : 1;
+  waves = (tiles / nt <= 256 && M <= 8) ? 16 : 8;
+}
+
+
+static int dispatch(const DgArgs& a, int epi, int norm, int nt, int waves, hipStream_t st) {
+  const int M = a.M, N = a.N;
+  if (M <= 0) return 0;
+  if (M > 64 || a.K % 32 != 0 || N % 16 != 0 || epi < 0 || epi > 3) return 1;
+  if ((epi == EPI_SILU || epi == EPI_ROPE) && (N / 16) % 2) return 1;
+  if (epi == EPI_RESID && !a.resid) return 1;
+  const int MT = M <= 16 ? 1 : (M <= 32 ? 2 : 4);
+  if (nt <= 0 || waves <= 0) default_cfg(MT, M, N, epi, nt, waves);
+  if ((N / 16) % nt) return 1;
+  int rc = 1;
+#define PA_DGE(MT_)                                                                 \
+  switch (epi * 2 + (norm ? 1 : 0)) {                                               \
+    case 0: rc = pick_nw<MT_, EPI_PLAIN, false>(nt, waves, a, st); break;           \
+    case 1: rc = pick_nw<MT_, EPI_PLAIN, true>(nt, waves, a, st); break;            \
+    case 3: rc = pick_nw<MT_, EPI_SILU, true>(nt, waves, a, st); break;             \
+    case 4: rc = pick_nw<MT_, EPI_RESID, false>(nt, waves, a, st); break;           \
+    case 7: rc = pick_nw<MT_, EPI_ROPE, true>(nt, waves, a, st); break;             \
+    default: rc = 1;                                                                \
+  }
+  switch (MT) {
+    case 1: PA_DGE(1) break;
+    case 2: PA_DGE(2) break;
+    default: PA_DGE(4) break;
+  }
+#undef PA_DGE
+  if (rc != 0) return rc;
+  return (int)hipGetLastError() == 0 ? 0 : -2;
 }
 
 }  // namespace pa
@@ -220,32 +333,20 @@ extern "C" int pa_decode_gemm(void* y, const void* x, const void* wp, const void
                               int ldx, int ldy, int ldr, int epi, int norm, float eps, int nt, int waves,
                               hipStream_t st) {
   using namespace pa;
-  if (M <= 0) return 0;
-  if (M > 64 || K % 32 != 0 || N % 16 != 0 || epi < 0 || epi > 2) return 1;
-  if (epi == EPI_SILU && (N / 16) % 2) return 1;
-  if (epi == EPI_RESID && !resid) return 1;
-  const int MT = M <= 16 ? 1 : (M <= 32 ? 2 : 4);
-  if (nt <= 0 || waves <= 0) default_cfg(MT, N, K, epi, nt, waves);
-  if ((N / 16) % nt) return 1;
-  bf16* Y = (bf16*)y;
-  const bf16* X = (const bf16*)x;
-  const bf16* W = (const bf16*)wp;
-  const bf16* R = (const bf16*)resid;
-  int rc = 1;
-#define PA_DGE(MT_)                                                                                         \
-  switch (epi * 2 + (norm ? 1 : 0)) {                                                                       \
-    case 0: rc = pick_nw<MT_, EPI_PLAIN, false>(nt, waves, Y, X, W, R, M, N, K, ldx, ldy, ldr, eps, st); break; \
-    case 1: rc = pick_nw<MT_, EPI_PLAIN, true>(nt, waves, Y, X, W, R, M, N, K, ldx, ldy, ldr, eps, st); break;  \
-    case 3: rc = pick_nw<MT_, EPI_SILU, true>(nt, waves, Y, X, W, R, M, N, K, ldx, ldy, ldr, eps, st); break;   \
-    case 4: rc = pick_nw<MT_, EPI_RESID, false>(nt, waves, Y, X, W, R, M, N, K, ldx, ldy, ldr, eps, st); break; \
-    default: rc = 1;                                                                                        \
-  }
-  switch (MT) {
-    case 1: PA_DGE(1) break;
-    case 2: PA_DGE(2) break;
-    default: PA_DGE(4) break;
-  }
-#undef PA_DGE
-  if (rc != 0) return rc;
-  return (int)hipGetLastError() == 0 ? 0 : -2;
+  if (epi == EPI_ROPE) return 1;
+  DgArgs a{(bf16*)y, (const bf16*)x, (const bf16*)wp, (const bf16*)resid, M, N, K, ldx, ldy, ldr, eps, RopeArgs{}};
+  return dispatch(a, epi, norm, nt, waves, st);
+}
+
+// QKV projection (RMSNorm folded, rope-permuted packed weights) + RoPE + paged KV
+// write: q -> q_out [M, H, 128], k/v -> the layer's cache pages at slots[m].
+extern "C" int pa_decode_qkv_rope(const void* x, const void* wp, int M, int N, int K, int ldx, float eps,
+                                  void* q_out, void* k_cache, void* v_cache, const int* positions,
+                                  const int* slots, const float* cos_sin, int H, int KV, int nt, int waves,
+                                  hipStream_t st) {
+  using namespace pa;
+  if (N != (H + 2 * KV) * 128) return 1;
+  DgArgs a{nullptr, (const bf16*)x, (const bf16*)wp, nullptr, M, N, K, ldx, 0, 0, eps,
+           RopeArgs{(bf16*)q_out, (bf16*)k_cache, (bf16*)v_cache, positions, slots, cos_sin, H, KV}};
+  return dispatch(a, EPI_ROPE, 1, nt, waves, st);
 }

@@ -165,7 +165,7 @@ class LlamaModel:
         folded into the columns of the matrices they feed (QKV <- ln1, gate_up <-
         ln2), so the decode path needs no separate norm kernel."""
         for L in self.layers:
-            L["wqkv_p"] = ops.pack_decode_weight(L["wqkv"] * L["ln1"][None, :])
+            L["wqkv_p"] = ops.pack_decode_qkv_rope(L["wqkv"] * L["ln1"][None, :])
             L["wo_p"] = ops.pack_decode_weight(L["wo"])
             L["w13_p"] = ops.pack_decode_gate_up(L["w13"] * L["ln2"][None, :])
             L["w2_p"] = ops.pack_decode_weight(L["w2"])
@@ -326,8 +326,8 @@ class LlamaModel:
 
     def _forward_decode(self, meta: StepMeta, kv: KVCache, T: int, num_logit_rows: int,
                         part_o: torch.Tensor, part_ml: torch.Tensor) -> torch.Tensor:
-        """Decode-sized step on the packed weights: 6 launches per layer
-        (QKV+norm, RoPE/KV write, attention, O+residual, gate_up+norm+SwiGLU,
+        """Decode-sized step on the packed weights: 5 launches per layer
+        (norm+QKV+RoPE+KV write, attention, O+residual, norm+gate_up+SwiGLU,
         down+residual) instead of 9; the residual stream h is updated in place."""
         cfg = self.cfg
         H, KVh, hd = self.h_local, self.kv_local, cfg.head_dim
@@ -338,9 +338,9 @@ class LlamaModel:
         if not h.is_contiguous():
             h = h.contiguous()
         for li, L in enumerate(self.layers):
-            qkv = ops.decode_gemm(h, L["wqkv_p"], "plain", norm=True, eps=eps)
             q = torch.empty(T, H, hd, dtype=self.dtype, device=self.device)
-            ops.rope_cache(q, kv.k[li], kv.v[li], qkv, meta.positions, meta.slots, self.cos_sin, H, KVh)
+            ops.decode_qkv_rope(h, L["wqkv_p"], eps, q, kv.k[li], kv.v[li], meta.positions, meta.slots,
+                                self.cos_sin, H, KVh)
             attn = torch.empty(T, H, hd, dtype=self.dtype, device=self.device)
             ops.paged_attention(attn, part_o, part_ml, q, kv.k[li], kv.v[li], meta.items, meta.n_items,
                                 meta.att_counters, meta.q_start, meta.q_len, meta.ctx_len,

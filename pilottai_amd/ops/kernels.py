@@ -290,3 +290,42 @@ def decode_gemm(x: torch.Tensor, wp: torch.Tensor, epi: str = "plain", norm: boo
         acc = acc + resid.float()
     out.copy_(acc.to(out.dtype))
     return out
+
+
+# per-head tile order of the rope-fused QKV weights: tiles (i, i + 4) adjacent
+_ROPE_TILE_ORDER = (0, 4, 1, 5, 2, 6, 3, 7)
+
+
+def pack_decode_qkv_rope(wqkv: torch.Tensor) -> torch.Tensor:
+    """Packed QKV weights for decode_qkv_rope: within every 128-row head the
+    16-row tiles are reordered to (0, 4, 1, 5, 2, 6, 3, 7), so one workgroup of
+    two tiles holds rotary dims i and i + 64 (csrc/ops/gemm_decode.hip EPI_ROPE)."""
+    N, K = wqkv.shape
+    if N % 128:
+        raise ValueError("QKV rows must be a multiple of the 128-wide head")
+    idx = torch.tensor(_ROPE_TILE_ORDER, device=wqkv.device)
+    w = wqkv.reshape(N // 128, 8, 16, K).index_select(1, idx).reshape(N, K)
+    return pack_decode_weight(w)
+
+
+def unpack_decode_qkv_rope(wp: torch.Tensor) -> torch.Tensor:
+    w = unpack_decode_weight(wp)
+    N, K = w.shape
+    inv = torch.argsort(torch.tensor(_ROPE_TILE_ORDER)).to(w.device)
+    return w.reshape(N // 128, 8, 16, K).index_select(1, inv).reshape(N, K)
+
+
+def decode_qkv_rope(x: torch.Tensor, wp: torch.Tensor, eps: float, q_out: torch.Tensor, k_cache, v_cache,
+                    positions, slots, cos_sin, H: int, KV: int) -> torch.Tensor:
+    """Decode QKV projection with the RMSNorm folded in (norm weight pre-multiplied
+    into the packed weights), RoPE and the paged KV write fused in the epilogue:
+    replaces rmsnorm + QKV GEMM + rope_cache on decode-sized steps."""
+    if _on_gpu(x):
+        require_native().decode_qkv_rope(x, wp, float(eps), q_out, k_cache, v_cache, positions, slots,
+                                         cos_sin, int(H), int(KV))
+        return q_out
+    xf = x.float()
+    w = unpack_decode_qkv_rope(wp).float()
+    qkv = (xf @ w.T) * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps)
+    ref.rope_cache(q_out, k_cache, v_cache, qkv.to(x.dtype), positions, slots, cos_sin, H, KV)
+    return q_out

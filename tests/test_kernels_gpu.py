@@ -307,3 +307,34 @@ def test_decode_gemm_configs(gpu, nt, waves):
     w = _bf(N, K, dev=gpu, scale=0.05)
     y = ops.decode_gemm(x, ops.pack_decode_weight(w), "plain", nt=nt, waves=waves)
     torch.testing.assert_close(y.float(), x.float() @ w.float().T, atol=3e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("M,H,KV,K", [(7, 32, 8, 4096), (16, 4, 1, 512), (1, 8, 2, 1024)])
+def test_decode_qkv_rope(gpu, M, H, KV, K):
+    """Norm-folded QKV projection with RoPE + paged KV write in the epilogue vs the
+    fp32 projection followed by the reference rope_cache."""
+    torch.manual_seed(13)
+    N = (H + 2 * KV) * 128
+    x = _bf(M, K, dev=gpu)
+    w = _bf(N, K, dev=gpu, scale=0.05)
+    g = (torch.rand(K, device=gpu) + 0.5).to(torch.bfloat16)
+    wp = ops.pack_decode_qkv_rope(w * g[None, :])
+    NB = 8
+    cos_sin = ref.rope_cos_sin(4096).to(gpu)
+    pos = torch.randint(0, 4000, (M,), dtype=torch.int32, device=gpu)
+    slots = torch.randperm(NB * 16, device=gpu)[:M].to(torch.int32)
+    if M > 2:
+        slots[1] = -1
+    kc = torch.zeros(NB, KV, 16, 16, 8, dtype=torch.bfloat16, device=gpu)
+    vc = torch.zeros(NB, KV, 128, 16, dtype=torch.bfloat16, device=gpu)
+    q = torch.empty(M, H, 128, dtype=torch.bfloat16, device=gpu)
+    ops.decode_qkv_rope(x, wp, 1e-5, q, kc, vc, pos, slots, cos_sin, H, KV)
+    xn = x.float() * torch.rsqrt(x.float().pow(2).mean(-1, keepdim=True) + 1e-5) * g.float()
+    qkv = (xn @ w.float().T).cpu()
+    rq = torch.empty(M, H, 128, dtype=torch.float32)
+    rk = torch.zeros(NB, KV, 16, 16, 8)
+    rv = torch.zeros(NB, KV, 128, 16)
+    ref.rope_cache(rq, rk, rv, qkv, pos.cpu(), slots.cpu(), cos_sin.cpu(), H, KV)
+    torch.testing.assert_close(q.float().cpu(), rq, atol=3e-2, rtol=2e-2)
+    torch.testing.assert_close(kc.float().cpu(), rk, atol=3e-2, rtol=2e-2)
+    torch.testing.assert_close(vc.float().cpu(), rv, atol=3e-2, rtol=2e-2)

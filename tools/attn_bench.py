@@ -23,7 +23,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from pilottai_amd import ops  # noqa: E402
 
 
-def setup(q_lens, ctx_lens, H=32, KV=8, pad_items=0, dev="cuda"):
+def setup(q_lens, ctx_lens, H=32, KV=8, pad_items=0, dev="cuda", part=512):
     G = H // KV
     blk = 16
     ns = len(q_lens)
@@ -41,7 +41,7 @@ def setup(q_lens, ctx_lens, H=32, KV=8, pad_items=0, dev="cuda"):
     q_start = np.concatenate([[0], np.cumsum(q_lens)[:-1]]).astype(np.int32)
     T = int(sum(q_lens))
     q = (torch.randn(T, H, 128, device=dev) * 0.5).to(torch.bfloat16)
-    items, _ = ops.build_attention_items(q_lens, ctx_lens, G)
+    items, _ = ops.build_attention_items(q_lens, ctx_lens, G, part=part)
     n_items = len(items)
     items = items + [(0, 0, 0, 0)] * max(1, pad_items - len(items))
     it = torch.tensor(items, dtype=torch.int32, device=dev)
@@ -52,7 +52,7 @@ def setup(q_lens, ctx_lens, H=32, KV=8, pad_items=0, dev="cuda"):
     part_ml = torch.empty(it.shape[0] * KV * 16 * 2, dtype=torch.float32, device=dev)
     out = torch.zeros(T, H, 128, dtype=torch.bfloat16, device=dev)
     args = (out, part_o, part_ml, q, kc, vc, it, n_it, cnt, di(q_start), di(q_lens), di(ctx_lens),
-            bt.to(dev), 1.0 / math.sqrt(128))
+            bt.to(dev), 1.0 / math.sqrt(128), None, di([part]))
     kv_bytes = sum(ctx_lens) * KV * 128 * 2 * 2
     flops = sum(4 * ql * (c - ql + (ql + 1) / 2) * H * 128 for ql, c in zip(q_lens, ctx_lens))
     return args, kv_bytes, flops, n_items
@@ -76,6 +76,7 @@ def main():
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--pad", type=int, default=2228, help="items reserved by the 768-token bucket")
     ap.add_argument("--scan", action="store_true", help="prefill length scan instead of the step cases")
+    ap.add_argument("--small", action="store_true", help="small-batch decode (8/16 rows) over partition sizes")
     a = ap.parse_args()
     torch.manual_seed(0)
     cases = {
@@ -88,6 +89,15 @@ def main():
     if a.scan:
         cases = {f"pf{n}": ([n], [n]) for n in (8, 32, 128, 256, 512, 1024, 2048, 4096)}
         cases.update({f"pf8x{n}": ([n] * 8, [n] * 8) for n in (128, 512)})
+    if a.small:
+        for ns in (8, 16):
+            for ctx in (600, 1000):
+                for part in (128, 256, 512):
+                    args, kvb, fl, n = setup([1] * ns, [ctx] * ns, part=part)
+                    us = timeit(args, a.iters)
+                    print(json.dumps({"case": f"decode{ns}_ctx{ctx}", "part": part, "items": n, "us": round(us, 1),
+                                      "kv_TBps": round(kvb / us / 1e6, 2)}), flush=True)
+        return
     for name, (ql, cl) in cases.items():
         for pad in ((0,) if a.scan else (0, a.pad)):
             args, kvb, fl, n = setup(ql, cl, pad_items=pad)
