@@ -57,6 +57,8 @@ def parse():
     ap.add_argument("--max-batched-tokens", type=int, default=2048)
     ap.add_argument("--temperature", type=float, default=0.7)
     ap.add_argument("--steps-per-task", type=int, default=1)
+    ap.add_argument("--fused-max-t", type=int, default=None,
+                    help="largest step on the fused packed-weight decode path (default: the model's)")
     ap.add_argument("--token-align", type=int, default=256, help="GEMM-friendly step sizes (0 = off)")
     ap.add_argument("--align-slack", type=int, default=96)
     ap.add_argument("--cpu", action="store_true", help="tiny model on CPU (plumbing smoke only)")
@@ -85,7 +87,8 @@ async def run_rank(a, rank: int, world: int, device):
     eng = LLMEngine(EngineConfig(model=a.model if not a.cpu else "tiny", max_num_seqs=max(64, 2 * n_local),
                                  max_num_batched_tokens=a.max_batched_tokens, kv_cache_gb=a.kv_gb if not a.cpu else None,
                                  num_kv_blocks=4096 if a.cpu else None, seed=1234 + rank,
-                                 token_align=a.token_align, align_slack=a.align_slack), device=device)
+                                 token_align=a.token_align, align_slack=a.align_slack,
+                                 decode_fused_max_t=a.fused_max_t), device=device)
     register_engine(eng.model_cfg.name, eng)
     eng.start()
     llm = LocalLLM(LLMConfig(model_name=eng.model_cfg.name, temperature=a.temperature, max_tokens=1024,
@@ -127,6 +130,7 @@ async def run_rank(a, rank: int, world: int, device):
     if a.warmup > 0:
         await round_(a.warmup, False)
     st0 = dict(eng.stats)
+    bh0 = {b: list(v) for b, v in eng.bucket_hist.items()}
     u0 = dict(llm.usage)
     n_timed0 = len(eng.timings)
     comm.barrier()
@@ -153,6 +157,8 @@ async def run_rank(a, rank: int, world: int, device):
         "bucket_tokens": st1["bucket_tokens"] - st0["bucket_tokens"],
         "prompt_total": em["prompt_tokens"], "hbm_used_gb": em.get("hbm_used_gb", 0.0),
         "req_lat": eng.latency_summary(n_timed0),
+        "buckets": {b: [v[0] - bh0.get(b, [0, 0.0])[0], v[1] - bh0.get(b, [0, 0.0])[1]]
+                    for b, v in eng.bucket_hist.items()},
     }
     return local
 
@@ -228,6 +234,9 @@ def main():
             "tpot_p50_ms": round(lat0.get("tpot_p50_ms") or 0.0, 2),
             "init_s": round(max(g["init_s"] for g in gathered), 1),
             "hbm_used_gb_per_gpu": round(max(g["hbm_used_gb"] for g in gathered), 1),
+            # rank 0's engine steps per graph bucket: [steps, ms per step]
+            "step_buckets": {str(b): [v[0], round(1000 * v[1] / max(1, v[0]), 2)]
+                             for b, v in sorted(gathered[0]["buckets"].items()) if v[0] > 0},
             "notes": "BASELINE.md publishes no number for this config (vs_baseline null); the reference's "
                      "structural bound with a remote LLM is ~0.8 tasks/s per LLMHandler (BASELINE.md §2).",
         }

@@ -77,6 +77,7 @@ class EngineConfig:
     token_align: int = 256   # GEMM-friendly step sizes (runtime/scheduler.h); 0 = off
     align_slack: int = 96
     decode_fused: Optional[bool] = None  # packed-weight fused decode path; None = when it fits in HBM
+    decode_fused_max_t: Optional[int] = None  # largest step (tokens) on that path; None = model default
 
 
 # TP step header: [op, T, ns, nsamp, bucket, masks_changed, n_copy, truncate]
@@ -157,6 +158,8 @@ class LLMEngine:
         t0 = time.time()
         self.model = LlamaModel(mc, self.device, tp=self.tp, seed=cfg.seed, weights_path=cfg.weights_path,
                                 decode_pack=cfg.decode_fused)
+        if cfg.decode_fused_max_t is not None:
+            self.model.DECODE_FUSED_MAX_T = int(cfg.decode_fused_max_t)
         self.load_time = time.time() - t0
         self.max_model_len = min(cfg.max_model_len, mc.max_position)
         # ---- KV cache sizing (288 GB HBM: the default leaves room for graphs/activations)
@@ -240,6 +243,7 @@ class LLMEngine:
         self.stats = {"steps": 0, "tokens": 0, "sampled": 0, "requests": 0, "finished": 0,
                       "busy_s": 0.0, "prefill_tokens": 0, "decode_steps": 0, "graph_replays": 0,
                       "bucket_tokens": 0}
+        self.bucket_hist: Dict[int, list] = {}  # bucket -> [steps, seconds]
         # graphs contain the TP collectives, so every rank captures every bucket up front
         if self.use_graphs and (cfg.capture_on_start or self.tp.size > 1):
             self.capture_graphs()
@@ -577,7 +581,11 @@ class LLMEngine:
         st["tokens"] += T
         st["bucket_tokens"] += bucket
         st["sampled"] += nsamp
-        st["busy_s"] += time.perf_counter() - t0
+        dt = time.perf_counter() - t0
+        st["busy_s"] += dt
+        bh = self.bucket_hist.setdefault(bucket, [0, 0.0])
+        bh[0] += 1
+        bh[1] += dt
         for o in outs:
             self._deliver(o)
         return True
