@@ -59,6 +59,8 @@ def parse():
     ap.add_argument("--steps-per-task", type=int, default=1)
     ap.add_argument("--fused-max-t", type=int, default=None,
                     help="largest step on the fused packed-weight decode path (default: the model's)")
+    ap.add_argument("--wide-max-t", type=int, default=None,
+                    help="largest step on the packed small-batch path (default: the model's)")
     ap.add_argument("--token-align", type=int, default=256, help="GEMM-friendly step sizes (0 = off)")
     ap.add_argument("--align-slack", type=int, default=96)
     ap.add_argument("--cpu", action="store_true", help="tiny model on CPU (plumbing smoke only)")
@@ -88,7 +90,7 @@ async def run_rank(a, rank: int, world: int, device):
                                  max_num_batched_tokens=a.max_batched_tokens, kv_cache_gb=a.kv_gb if not a.cpu else None,
                                  num_kv_blocks=4096 if a.cpu else None, seed=1234 + rank,
                                  token_align=a.token_align, align_slack=a.align_slack,
-                                 decode_fused_max_t=a.fused_max_t), device=device)
+                                 decode_fused_max_t=a.fused_max_t, wide_max_t=a.wide_max_t), device=device)
     register_engine(eng.model_cfg.name, eng)
     eng.start()
     llm = LocalLLM(LLMConfig(model_name=eng.model_cfg.name, temperature=a.temperature, max_tokens=1024,

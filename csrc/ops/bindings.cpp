@@ -36,6 +36,9 @@ int pa_decode_gemm(void* y, const void* x, const void* wp, const void* resid, in
 int pa_decode_qkv_rope(const void* x, const void* wp, int M, int N, int K, int ldx, float eps, void* q_out,
                        void* k_cache, void* v_cache, const int* positions, const int* slots,
                        const float* cos_sin, int H, int KV, int nt, int waves, hipStream_t st);
+int pa_wide_gemm(void* y, const void* x, const void* wp, const void* resid, float* ws, long long ws_floats,
+                 int* counters, int n_counters, int M, int N, int K, int ldx, int ldy, int ldr, int epi, int norm,
+                 float eps, int ntw, int waves, int splits, hipStream_t st);
 long long pa_cosine_topk_workspace_bytes(int Q, int N, int K);
 int pa_cosine_topk(float* out_scores, int* out_rows, void* workspace, const void* queries,
                    const void* index, int Q, int N, int D, int K, const int* row_priority,
@@ -231,6 +234,41 @@ void decode_qkv_rope(at::Tensor x, at::Tensor wp, double eps, at::Tensor q_out, 
   check_rc(rc < 0 ? rc : (rc > 0 ? -1 : 0), "decode_qkv_rope");
 }
 
+// y = epi(rownorm(x) . W^T) for 16 < M <= 128 on packed weights (csrc/ops/gemm_wide.hip).
+// epi 0 plain, 1 silu(gate)*up (y has N/2 columns), 2 resid + acc, 3 plain with the
+// RoPE tile permutation of the packed QKV undone. ws/counters: split-K slabs and
+// zeroed tickets. Returns false if the shape/config is not handled.
+bool wide_gemm(at::Tensor y, at::Tensor x, at::Tensor wp, c10::optional<at::Tensor> resid, at::Tensor ws,
+               at::Tensor counters, int64_t epi, bool norm, double eps, int64_t ntw, int64_t waves, int64_t splits) {
+  check_gpu(wp, "wp"); check_gpu(ws, "ws"); check_gpu(counters, "counters");
+  TORCH_CHECK(x.is_cuda() && x.dim() == 2 && x.stride(1) == 1, "x must be a 2-D GPU tensor, unit inner stride");
+  TORCH_CHECK(y.is_cuda() && y.dim() == 2 && y.stride(1) == 1, "y must be a 2-D GPU tensor, unit inner stride");
+  check_dtype(x, at::kBFloat16, "x"); check_dtype(wp, at::kBFloat16, "wp"); check_dtype(y, at::kBFloat16, "y");
+  check_dtype(ws, at::kFloat, "ws"); check_dtype(counters, at::kInt, "counters");
+  TORCH_CHECK(wp.dim() == 4 && wp.size(2) == 64 && wp.size(3) == 8, "wp must be packed [N/16, K/32, 64, 8]");
+  const int M = x.size(0), K = x.size(1), N = wp.size(0) * 16;
+  TORCH_CHECK(wp.size(1) * 32 == K, "packed weight K mismatch");
+  TORCH_CHECK(x.stride(0) % 8 == 0, "x rows must be 16-byte aligned");
+  const int NO = epi == 1 ? N / 2 : N;
+  TORCH_CHECK(y.size(0) == M && y.size(1) == NO, "y shape mismatch");
+  const void* rp = nullptr;
+  int ldr = 0;
+  if (epi == 2) {
+    TORCH_CHECK(resid.has_value(), "epi=2 needs resid");
+    const auto& r = *resid;
+    TORCH_CHECK(r.is_cuda() && r.dim() == 2 && r.stride(1) == 1 && r.size(0) == M && r.size(1) == N,
+                "resid must be [M, N] with unit inner stride");
+    check_dtype(r, at::kBFloat16, "resid");
+    rp = r.data_ptr();
+    ldr = r.stride(0);
+  }
+  const int rc = pa_wide_gemm(y.data_ptr(), x.data_ptr(), wp.data_ptr(), rp, ws.data_ptr<float>(), ws.numel(),
+                              counters.data_ptr<int>(), counters.numel(), M, N, K, x.stride(0), y.stride(0), ldr,
+                              (int)epi, norm ? 1 : 0, (float)eps, (int)ntw, (int)waves, (int)splits, cur_stream());
+  TORCH_CHECK(rc >= 0, "wide_gemm launch failed");
+  return rc == 0;
+}
+
 int64_t sample_workspace_floats(int64_t rows, int64_t V) {
   return pa_sample_workspace_floats(rows, V);
 }
@@ -363,6 +401,9 @@ PYBIND11_MODULE(_C, m) {
         py::arg("epi") = 0, py::arg("norm") = false, py::arg("eps") = 1e-5, py::arg("nt") = 0,
         py::arg("waves") = 0);
   m.def("decode_qkv_rope", &decode_qkv_rope);
+  m.def("wide_gemm", &wide_gemm, py::arg("y"), py::arg("x"), py::arg("wp"), py::arg("resid"), py::arg("ws"),
+        py::arg("counters"), py::arg("epi") = 0, py::arg("norm") = false, py::arg("eps") = 1e-5, py::arg("ntw") = 0,
+        py::arg("waves") = 0, py::arg("splits") = 0);
   m.def("paged_attention", &paged_attention, py::arg("out"), py::arg("part_o"), py::arg("part_ml"), py::arg("q"),
         py::arg("k_cache"), py::arg("v_cache"), py::arg("items"), py::arg("n_items"), py::arg("counters"),
         py::arg("q_start"), py::arg("q_len"), py::arg("ctx_len"), py::arg("block_table"), py::arg("scale"),

@@ -121,6 +121,9 @@ class LlamaModel:
     # decode steps of at most this many tokens run the fused packed-weight path
     # (csrc/ops/gemm_decode.hip; tools/decode_gemm_bench.py, profiles/r1_decode_gemm.md)
     DECODE_FUSED_MAX_T = 16
+    # steps of up to this many tokens (above DECODE_FUSED_MAX_T) run the packed-weight
+    # small-batch kernels (csrc/ops/gemm_wide.hip; tools/wide_gemm_bench.py)
+    WIDE_MAX_T = 32
 
     def __init__(self, cfg: LlamaConfig, device, dtype=torch.bfloat16, tp: Optional[TPGroup] = None,
                  seed: int = 0, weights_path: Optional[str] = None, decode_pack: Optional[bool] = None):
@@ -170,6 +173,8 @@ class LlamaModel:
             L["w13_p"] = ops.pack_decode_gate_up(L["w13"] * L["ln2"][None, :])
             L["w2_p"] = ops.pack_decode_weight(L["w2"])
         self.lm_head_p = ops.pack_decode_weight(self.lm_head)
+        if self.device.type == "cuda":
+            ops.wide_workspace(self.device)  # split-K slabs + tickets, before any graph capture
         self.decode_packed = True
 
     # -- weights -----------------------------------------------------------------
@@ -295,6 +300,8 @@ class LlamaModel:
         T = num_tokens
         if self.decode_packed and T <= self.DECODE_FUSED_MAX_T:
             return self._forward_decode(meta, kv, T, num_logit_rows, part_o, part_ml)
+        if self.decode_packed and T <= self.WIDE_MAX_T:
+            return self._forward_wide(meta, kv, T, num_logit_rows, part_o, part_ml)
         H, KVh, hd = self.h_local, self.kv_local, cfg.head_dim
         ids = meta.input_ids[:T].long() if self.device.type == "cpu" else meta.input_ids[:T]
         h = self._embed(ids)
@@ -363,6 +370,50 @@ class LlamaModel:
         rows = rows.long() if self.device.type == "cpu" else rows
         xs = ops.rmsnorm(h.index_select(0, rows), self.norm, eps)
         return ops.decode_gemm(xs, self.lm_head_p, "plain")
+
+    def _forward_wide(self, meta: StepMeta, kv: KVCache, T: int, num_logit_rows: int,
+                      part_o: torch.Tensor, part_ml: torch.Tensor) -> torch.Tensor:
+        """Small-batch step (DECODE_FUSED_MAX_T < T <= WIDE_MAX_T: decode rows plus
+        grammar jump-forward runs or a short prefill chunk) on the packed weights:
+        x staged once per workgroup through LDS, split-K for the narrow projections,
+        RMSNorm folded into QKV / gate_up, SwiGLU and residual adds in the epilogues
+        (csrc/ops/gemm_wide.hip); RoPE + paged KV write stay a separate kernel."""
+        cfg = self.cfg
+        H, KVh, hd = self.h_local, self.kv_local, cfg.head_dim
+        eps = cfg.rms_eps
+        tp = self.tp.size > 1
+        ids = meta.input_ids[:T].long() if self.device.type == "cpu" else meta.input_ids[:T]
+        h = self._embed(ids)
+        if not h.is_contiguous():
+            h = h.contiguous()
+        for li, L in enumerate(self.layers):
+            qkv = ops.wide_gemm(h, L["wqkv_p"], "rope_perm", norm=True, eps=eps)
+            q = torch.empty(T, H, hd, dtype=self.dtype, device=self.device)
+            ops.rope_cache(q, kv.k[li], kv.v[li], qkv, meta.positions, meta.slots, self.cos_sin, H, KVh)
+            attn = torch.empty(T, H, hd, dtype=self.dtype, device=self.device)
+            ops.paged_attention(attn, part_o, part_ml, q, kv.k[li], kv.v[li], meta.items, meta.n_items,
+                                meta.att_counters, meta.q_start, meta.q_len, meta.ctx_len,
+                                meta.block_table, self.scale, num_seqs=meta.num_seqs, part_size=meta.part_size)
+            a2 = attn.view(T, H * hd)
+            if tp:
+                o = ops.wide_gemm(a2, L["wo_p"], "plain")
+                self.tp.all_reduce(o)
+                h.add_(o)
+            else:
+                ops.wide_gemm(a2, L["wo_p"], "resid", resid=h, out=h)
+            a = ops.wide_gemm(h, L["w13_p"], "silu", norm=True, eps=eps)
+            if tp:
+                d = ops.wide_gemm(a, L["w2_p"], "plain")
+                self.tp.all_reduce(d)
+                h.add_(d)
+            else:
+                ops.wide_gemm(a, L["w2_p"], "resid", resid=h, out=h)
+        rows = meta.logit_rows[:num_logit_rows]
+        rows = rows.long() if self.device.type == "cpu" else rows
+        xs = ops.rmsnorm(h.index_select(0, rows), self.norm, eps)
+        if num_logit_rows <= 16:  # decode_gemm beats hipBLASLt on the LM head only up to 16 rows
+            return ops.decode_gemm(xs, self.lm_head_p, "plain")
+        return ops.linear(xs, self.lm_head, "lm_head")
 
     # -- reference (dense, no cache) forward used by numerics tests ----------------
     @torch.no_grad()

@@ -3,6 +3,8 @@ from .kernels import (  # noqa: F401
     cosine_topk,
     decode_gemm,
     decode_qkv_rope,
+    wide_gemm,
+    wide_workspace,
     pack_decode_qkv_rope,
     pack_decode_gate_up,
     pack_decode_weight,

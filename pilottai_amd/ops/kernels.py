@@ -329,3 +329,58 @@ def decode_qkv_rope(x: torch.Tensor, wp: torch.Tensor, eps: float, q_out: torch.
     qkv = (xf @ w.T) * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps)
     ref.rope_cache(q_out, k_cache, v_cache, qkv.to(x.dtype), positions, slots, cos_sin, H, KV)
     return q_out
+
+
+# ---------------------------------------------------------------------------
+# Small-batch projections (16 < M <= 256) on the packed weights (csrc/ops/gemm_wide.hip)
+
+WIDE_EPI = {"plain": 0, "silu": 1, "resid": 2, "rope_perm": 3}
+WIDE_WS_FLOATS = 8 << 20  # 32 MB of split-K slabs per device
+_wide_ws = {}
+
+
+def wide_workspace(device):
+    """(slabs, tickets) for wide_gemm on `device`; allocate before hipGraph capture
+    (the tickets must start zeroed; every launch leaves them zeroed)."""
+    key = str(device)
+    if key not in _wide_ws:
+        _wide_ws[key] = (torch.empty(WIDE_WS_FLOATS, dtype=torch.float32, device=device),
+                         torch.zeros(16384, dtype=torch.int32, device=device))
+    return _wide_ws[key]
+
+
+def wide_gemm(x: torch.Tensor, wp: torch.Tensor, epi: str = "plain", resid: Optional[torch.Tensor] = None,
+              out: Optional[torch.Tensor] = None, norm: bool = False, eps: float = 1e-5, ntw: int = 0,
+              waves: int = 0, splits: int = 0) -> torch.Tensor:
+    """y = epi(rownorm(x) @ W.T) for 16 < M <= 128 with W packed by pack_decode_weight
+    (gate_up: pack_decode_gate_up + epi "silu"; QKV: pack_decode_qkv_rope + epi
+    "rope_perm", which returns the natural column order); "resid": resid + acc.
+    `norm` scales rows by rsqrt(mean(x^2) + eps) (RMSNorm weight folded into W)."""
+    M, K = x.shape
+    N = wp.shape[0] * 16
+    code = WIDE_EPI[epi]
+    NO = N // 2 if code == 1 else N
+    if out is None:
+        out = torch.empty(M, NO, dtype=x.dtype, device=x.device)
+    if _on_gpu(x):
+        ws, cnt = wide_workspace(x.device)
+        if not require_native().wide_gemm(out, x, wp, resid, ws, cnt, code, bool(norm), float(eps), int(ntw),
+                                          int(waves), int(splits)):
+            raise ValueError(f"wide_gemm does not handle M={M} N={N} K={K} epi={epi} ntw={ntw} waves={waves}")
+        return out
+    if code == 3:
+        W = unpack_decode_qkv_rope(wp)
+    elif code == 1:
+        W = unpack_decode_gate_up(wp)
+    else:
+        W = unpack_decode_weight(wp)
+    xf = x.float()
+    acc = xf @ W.float().T
+    if norm:
+        acc = acc * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps)
+    if code == 1:
+        acc = torch.nn.functional.silu(acc[:, :NO]) * acc[:, NO:]
+    elif code == 2:
+        acc = acc + resid.float()
+    out.copy_(acc.to(out.dtype))
+    return out

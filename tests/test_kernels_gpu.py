@@ -338,3 +338,31 @@ def test_decode_qkv_rope(gpu, M, H, KV, K):
     torch.testing.assert_close(q.float().cpu(), rq, atol=3e-2, rtol=2e-2)
     torch.testing.assert_close(kc.float().cpu(), rk, atol=3e-2, rtol=2e-2)
     torch.testing.assert_close(vc.float().cpu(), rv, atol=3e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("M,N,K,epi,norm,ntw,waves,splits", [
+    (17, 4096, 4096, "plain", False, 0, 0, 0), (48, 6144, 4096, "rope_perm", True, 0, 0, 0),
+    (128, 28672, 4096, "silu", True, 0, 0, 0), (64, 4096, 14336, "resid", False, 0, 0, 0),
+    (33, 1024, 512, "silu", True, 2, 4, 2), (100, 768, 512, "rope_perm", False, 1, 4, 1),
+    (120, 4096, 4096, "resid", False, 1, 8, 3), (90, 6144, 4096, "plain", True, 2, 4, 5),
+    (64, 2048, 1024, "plain", False, 2, 8, 1), (29, 4096, 4096, "plain", True, 1, 4, 4)])
+def test_wide_gemm(gpu, M, N, K, epi, norm, ntw, waves, splits):
+    """Small-batch packed-weight GEMM (csrc/ops/gemm_wide.hip) vs fp32, every epilogue
+    and the folded row norm, with and without split-K; run twice so the
+    self-resetting split-K tickets are exercised."""
+    torch.manual_seed(15)
+    x = _bf(M, K, dev=gpu)
+    w = _bf(N, K, dev=gpu, scale=0.05)
+    resid = _bf(M, N, dev=gpu) if epi == "resid" else None
+    pack = {"silu": ops.pack_decode_gate_up, "rope_perm": ops.pack_decode_qkv_rope}.get(epi, ops.pack_decode_weight)
+    wp = pack(w)
+    acc = x.float() @ w.float().T
+    if norm:
+        acc = acc * torch.rsqrt(x.float().pow(2).mean(-1, keepdim=True) + 1e-5)
+    if epi == "silu":
+        acc = torch.nn.functional.silu(acc[:, :N // 2]) * acc[:, N // 2:]
+    elif epi == "resid":
+        acc = acc + resid.float()
+    for _ in range(2):
+        y = ops.wide_gemm(x, wp, epi, resid=resid, norm=norm, ntw=ntw, waves=waves, splits=splits)
+        torch.testing.assert_close(y.float(), acc, atol=3e-2, rtol=2e-2)

@@ -266,6 +266,7 @@ def test_fused_decode_path_matches_unfused_logits():
         assert eng.model.decode_packed
         if not fused:
             eng.model.DECODE_FUSED_MAX_T = 0
+            eng.model.WIDE_MAX_T = 0
         seen = []
         fwd = eng.model.forward
 
@@ -281,3 +282,33 @@ def test_fused_decode_path_matches_unfused_logits():
     assert a.shape == b.shape
     torch.testing.assert_close(a, b, atol=0.05 * float(b.abs().max()), rtol=0.05)
     assert int(a.argmax(-1)[0]) == int(b.argmax(-1)[0]) or float((a - b).abs().max()) < 1e-2
+
+
+def test_wide_path_matches_library_path_logits():
+    """The packed small-batch forward (16 < T <= 32: folded norms, split-K kernels,
+    SwiGLU / residual epilogues) and the library-GEMM forward give the same logits
+    for a 24-token prefill step on a tiny model (CPU references of both paths)."""
+    import torch
+
+    from pilottai_amd.engine.engine import EngineConfig, LLMEngine
+
+    logits = {}
+    for wide in (True, False):
+        eng = LLMEngine(EngineConfig(model="tiny", max_num_seqs=8, use_graphs=False, decode_fused=True,
+                                     num_kv_blocks=256, max_model_len=512))
+        if not wide:
+            eng.model.WIDE_MAX_T = 0
+        seen = []
+        fwd = eng.model.forward
+
+        def rec(*a, _f=fwd, _s=seen, **k):
+            out = _f(*a, **k)
+            _s.append((a[2], out.float().clone()))
+            return out
+
+        eng.model.forward = rec
+        eng.generate([list(range(1, 25))], max_tokens=2, temperature=0.0, ignore_eos=True)
+        assert 16 < seen[0][0] <= 32
+        logits[wide] = seen[0][1]
+    a, b = logits[True], logits[False]
+    torch.testing.assert_close(a, b, atol=0.05 * float(b.abs().max()), rtol=0.05)

@@ -1,10 +1,10 @@
-# 8-worker bench (per-rank load of the N=8 run) over the fused-decode step threshold.
+# N=1 bench (64 workers) over step-size knobs.
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-mkdir -p gpurun_out/sweep
-for t in 16 32 64; do
-  timeout -k 10 300 python -u bench.py --steps 3 --warmup 1 --workers 8 --fused-max-t $t > gpurun_out/sweep/w8_t$t.log 2>&1 || exit $?
-done
-timeout -k 10 300 python -u bench.py --steps 3 --warmup 1 --workers 16 > gpurun_out/sweep/w16.log 2>&1 && \
-timeout -k 10 300 python -u bench.py --steps 3 --warmup 1 --workers 32 > gpurun_out/sweep/w32.log 2>&1
+mkdir -p gpurun_out/sweep64
+timeout -k 10 300 python -u bench.py --steps 3 --warmup 1 > gpurun_out/sweep64/base.log 2>&1 || exit $?
+timeout -k 10 300 python -u bench.py --steps 3 --warmup 1 --max-batched-tokens 3072 > gpurun_out/sweep64/mbt3072.log 2>&1 || exit $?
+timeout -k 10 300 python -u bench.py --steps 3 --warmup 1 --max-batched-tokens 4096 > gpurun_out/sweep64/mbt4096.log 2>&1 || exit $?
+timeout -k 10 300 python -u bench.py --steps 3 --warmup 1 --token-align 512 --align-slack 192 > gpurun_out/sweep64/align512.log 2>&1 || exit $?
+timeout -k 10 300 python -u bench.py --steps 3 --warmup 1 --token-align 0 > gpurun_out/sweep64/noalign.log 2>&1
 echo EXIT $?
