@@ -31,11 +31,12 @@ int pa_topkp_threshold(float* tau, const void* logits, int rows, int V, int ld, 
 void pa_skinny_set_variant(int v);
 int pa_skinny_gemm(void* y, const void* x, const void* w, int M, int N, int K, int ldy, hipStream_t st);
 int pa_decode_gemm(void* y, const void* x, const void* wp, const void* resid, int M, int N, int K,
-                   int ldx, int ldy, int ldr, int epi, int norm, float eps, int nt, int waves,
-                   hipStream_t st);
+                   int ldx, int ldy, int ldr, int epi, int norm, float eps, int nt, int waves, int splits,
+                   float* ws, long long ws_floats, int* counters, int n_counters, hipStream_t st);
 int pa_decode_qkv_rope(const void* x, const void* wp, int M, int N, int K, int ldx, float eps, void* q_out,
                        void* k_cache, void* v_cache, const int* positions, const int* slots,
-                       const float* cos_sin, int H, int KV, int nt, int waves, hipStream_t st);
+                       const float* cos_sin, int H, int KV, int nt, int waves, int splits, float* ws,
+                       long long ws_floats, int* counters, int n_counters, hipStream_t st);
 int pa_wide_gemm(void* y, const void* x, const void* wp, const void* resid, float* ws, long long ws_floats,
                  int* counters, int n_counters, int M, int N, int K, int ldx, int ldy, int ldr, int epi, int norm,
                  float eps, int ntw, int waves, int splits, hipStream_t st);
@@ -177,7 +178,8 @@ bool skinny_gemm(at::Tensor y, at::Tensor x, at::Tensor w) {
 // (csrc/ops/gemm_decode.hip). epi 0 plain, 1 silu(gate)*up (y has N/2 columns),
 // 2 y = resid + acc. Returns false if the shape is not handled.
 bool decode_gemm(at::Tensor y, at::Tensor x, at::Tensor wp, c10::optional<at::Tensor> resid, int64_t epi,
-                 bool norm, double eps, int64_t nt, int64_t waves) {
+                 bool norm, double eps, int64_t nt, int64_t waves, int64_t splits, c10::optional<at::Tensor> ws,
+                 c10::optional<at::Tensor> counters) {
   check_gpu(wp, "wp");
   TORCH_CHECK(x.is_cuda() && x.dim() == 2 && x.stride(1) == 1, "x must be a 2-D GPU tensor, unit inner stride");
   TORCH_CHECK(y.is_cuda() && y.dim() == 2 && y.stride(1) == 1, "y must be a 2-D GPU tensor, unit inner stride");
@@ -199,8 +201,18 @@ bool decode_gemm(at::Tensor y, at::Tensor x, at::Tensor wp, c10::optional<at::Te
     rp = r.data_ptr();
     ldr = r.stride(0);
   }
+  float* wsp = nullptr;
+  long long wsn = 0;
+  int* cp = nullptr;
+  int cn = 0;
+  if (ws.has_value() && counters.has_value()) {
+    check_gpu(*ws, "ws"); check_gpu(*counters, "counters");
+    check_dtype(*ws, at::kFloat, "ws"); check_dtype(*counters, at::kInt, "counters");
+    wsp = ws->data_ptr<float>(); wsn = ws->numel(); cp = counters->data_ptr<int>(); cn = counters->numel();
+  }
   const int rc = pa_decode_gemm(y.data_ptr(), x.data_ptr(), wp.data_ptr(), rp, M, N, K, x.stride(0), y.stride(0),
-                                ldr, (int)epi, norm ? 1 : 0, (float)eps, (int)nt, (int)waves, cur_stream());
+                                ldr, (int)epi, norm ? 1 : 0, (float)eps, (int)nt, (int)waves, (int)splits, wsp, wsn,
+                                cp, cn, cur_stream());
   TORCH_CHECK(rc >= 0, "decode_gemm launch failed");
   return rc == 0;
 }
@@ -208,7 +220,7 @@ bool decode_gemm(at::Tensor y, at::Tensor x, at::Tensor wp, c10::optional<at::Te
 // Decode QKV projection + RoPE + paged KV write (csrc/ops/gemm_decode.hip, EPI_ROPE).
 void decode_qkv_rope(at::Tensor x, at::Tensor wp, double eps, at::Tensor q_out, at::Tensor k_cache,
                      at::Tensor v_cache, at::Tensor positions, at::Tensor slots, at::Tensor cos_sin, int64_t H,
-                     int64_t KV) {
+                     int64_t KV, int64_t splits, c10::optional<at::Tensor> ws, c10::optional<at::Tensor> counters) {
   check_gpu(wp, "wp"); check_gpu(q_out, "q_out"); check_gpu(k_cache, "k_cache"); check_gpu(v_cache, "v_cache");
   check_gpu(positions, "positions"); check_gpu(slots, "slots"); check_gpu(cos_sin, "cos_sin");
   TORCH_CHECK(x.is_cuda() && x.dim() == 2 && x.stride(1) == 1, "x must be a 2-D GPU tensor, unit inner stride");
@@ -227,10 +239,19 @@ void decode_qkv_rope(at::Tensor x, at::Tensor wp, double eps, at::Tensor q_out, 
                   k_cache.size(4) == 8, "k_cache must be [NB, KV, 16, 16, 8]");
   TORCH_CHECK(v_cache.dim() == 4 && v_cache.size(1) == KV && v_cache.size(2) == 128 && v_cache.size(3) == 16,
               "v_cache must be [NB, KV, 128, 16]");
+  float* wsp = nullptr;
+  long long wsn = 0;
+  int* cp = nullptr;
+  int cn = 0;
+  if (ws.has_value() && counters.has_value()) {
+    check_gpu(*ws, "ws"); check_gpu(*counters, "counters");
+    check_dtype(*ws, at::kFloat, "ws"); check_dtype(*counters, at::kInt, "counters");
+    wsp = ws->data_ptr<float>(); wsn = ws->numel(); cp = counters->data_ptr<int>(); cn = counters->numel();
+  }
   const int rc = pa_decode_qkv_rope(x.data_ptr(), wp.data_ptr(), M, N, K, x.stride(0), (float)eps, q_out.data_ptr(),
                                     k_cache.data_ptr(), v_cache.data_ptr(), positions.data_ptr<int>(),
                                     slots.data_ptr<int>(), cos_sin.data_ptr<float>(), (int)H, (int)KV, 0, 0,
-                                    cur_stream());
+                                    (int)splits, wsp, wsn, cp, cn, cur_stream());
   check_rc(rc < 0 ? rc : (rc > 0 ? -1 : 0), "decode_qkv_rope");
 }
 
@@ -399,8 +420,11 @@ PYBIND11_MODULE(_C, m) {
   m.def("skinny_set_variant", [](int v) { pa_skinny_set_variant(v); });
   m.def("decode_gemm", &decode_gemm, py::arg("y"), py::arg("x"), py::arg("wp"), py::arg("resid") = py::none(),
         py::arg("epi") = 0, py::arg("norm") = false, py::arg("eps") = 1e-5, py::arg("nt") = 0,
-        py::arg("waves") = 0);
-  m.def("decode_qkv_rope", &decode_qkv_rope);
+        py::arg("waves") = 0, py::arg("splits") = 0, py::arg("ws") = py::none(), py::arg("counters") = py::none());
+  m.def("decode_qkv_rope", &decode_qkv_rope, py::arg("x"), py::arg("wp"), py::arg("eps"), py::arg("q_out"),
+        py::arg("k_cache"), py::arg("v_cache"), py::arg("positions"), py::arg("slots"), py::arg("cos_sin"),
+        py::arg("H"), py::arg("KV"), py::arg("splits") = 0, py::arg("ws") = py::none(),
+        py::arg("counters") = py::none());
   m.def("wide_gemm", &wide_gemm, py::arg("y"), py::arg("x"), py::arg("wp"), py::arg("resid"), py::arg("ws"),
         py::arg("counters"), py::arg("epi") = 0, py::arg("norm") = false, py::arg("eps") = 1e-5, py::arg("ntw") = 0,
         py::arg("waves") = 0, py::arg("splits") = 0);

@@ -33,6 +33,8 @@
 // model path (models/llama.py forward) for decode-sized steps.
 #include "common.h"
 
+#include <algorithm>
+
 namespace pa {
 
 enum { EPI_PLAIN = 0, EPI_SILU = 1, EPI_RESID = 2, EPI_ROPE = 3 };
@@ -59,7 +61,12 @@ struct DgArgs {
   int M, N, K, ldx, ldy, ldr;
   float eps;
   RopeArgs rope;
+  int S;          // K slices (split-K across workgroups; 1 = none)
+  float* ws;      // split-K slabs [groups][S][TM*TN + TM] fp32
+  int* counters;  // [groups] arrival tickets, zero between launches
 };
+
+typedef __attribute__((address_space(1))) int dg_gi32;
 
 template <int MT, int NT, int WAVES, int U, int EPI, bool NORM>
 __global__ __launch_bounds__(WAVES * 64) void decode_gemm_kernel(const DgArgs A) {
@@ -79,13 +86,17 @@ __global__ __launch_bounds__(WAVES * 64) void decode_gemm_kernel(const DgArgs A)
   (void)N;
   const int nwg = gridDim.x, bid = blockIdx.x;
   const int q = nwg / 8, rr = nwg % 8, xcd = bid % 8;
-  const int grp = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + bid / 8;
+  const int work = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + bid / 8;
+  const int S = A.S, G = nwg / S;
+  const int sl = work / G, grp = work % G;  // slice-major: workgroups sharing a K slice of x share an XCD
   const int tile0 = grp * NT;
 
   const int KS = K / 32;
-  const int per = (KS + WAVES - 1) / WAVES;
-  const int ks0 = min(KS, wid * per);
-  const int ks1 = min(KS, ks0 + per);
+  const int perS = (KS + S - 1) / S;
+  const int kb0 = min(KS, sl * perS), kb1 = min(KS, kb0 + perS);
+  const int per = (kb1 - kb0 + WAVES - 1) / WAVES;
+  const int ks0 = min(kb1, kb0 + wid * per);
+  const int ks1 = min(kb1, ks0 + per);
 
   f32x4 acc[MT][NT];
 #pragma unroll
@@ -159,6 +170,54 @@ __global__ __launch_bounds__(WAVES * 64) void decode_gemm_kernel(const DgArgs A)
     }
   }
   __syncthreads();
+  // workgroup sum over waves -> fin [TM][TN], fss [TM] (row sums of squares)
+  float* fin = ssq + WAVES * TM;
+  float* fss = fin + TM * TN;
+  int* lflag = reinterpret_cast<int*>(fss + TM);
+  for (int e = threadIdx.x; e < TM * TN; e += WAVES * 64) {
+    float t = 0.f;
+#pragma unroll
+    for (int wv = 0; wv < WAVES; ++wv) t += red[wv * TM * TN + e];
+    fin[e] = t;
+  }
+  if constexpr (NORM) {
+    for (int m = threadIdx.x; m < TM; m += WAVES * 64) {
+      float t = 0.f;
+#pragma unroll
+      for (int wv = 0; wv < WAVES; ++wv) t += ssq[wv * TM + m];
+      fss[m] = t;
+    }
+  }
+  __syncthreads();
+  if (S > 1) {
+    // split-K hand-off (cdna_hip_programming.md §5 item 2, sc1 form): publish the
+    // slice's partial tile write-through, take a ticket; the last slice reduces.
+    constexpr int SLAB = TM * TN + TM;
+    float* gslab = A.ws + (size_t)grp * S * SLAB;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(gslab + (size_t)sl * SLAB, 0, SLAB * 4, 0x00020000);
+    for (int e = threadIdx.x; e < SLAB; e += WAVES * 64)
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(e < TM * TN ? fin[e] : fss[e - TM * TN]), rs, e * 4, 0, 16);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      dg_gi32* cp = (dg_gi32*)(A.counters + grp);
+      const int tk = __hip_atomic_fetch_add(cp, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int last = tk == S - 1;
+      if (last) __hip_atomic_store(cp, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      *lflag = last;
+    }
+    __syncthreads();
+    if (!*lflag) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(gslab, 0, S * SLAB * 4, 0x00020000);
+    for (int e = threadIdx.x; e < SLAB; e += WAVES * 64) {
+      float t = 0.f;
+      for (int p = 0; p < S; ++p) t += __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(ra, (p * SLAB + e) * 4, 0, 16));
+      if (e < TM * TN) fin[e] = t;
+      else fss[e - TM * TN] = t;
+    }
+    __syncthreads();
+  }
   if constexpr (EPI == EPI_ROPE) {
     static_assert(NT == 2, "EPI_ROPE pairs the two tiles of a workgroup");
     const RopeArgs& R = A.rope;
@@ -167,20 +226,8 @@ __global__ __launch_bounds__(WAVES * 64) void decode_gemm_kernel(const DgArgs A)
       const int m = e >> 4, cc = e & 15;
       if (m >= M) continue;
       float rs = 1.f;
-      if constexpr (NORM) {
-        float t = 0.f;
-#pragma unroll
-        for (int wv = 0; wv < WAVES; ++wv) t += ssq[wv * TM + m];
-        rs = rsqrtf(t / (float)K + eps);
-      }
-      float a = 0.f, b = 0.f;
-#pragma unroll
-      for (int wv = 0; wv < WAVES; ++wv) {
-        a += red[(wv * TM + m) * TN + cc];
-        b += red[(wv * TM + m) * TN + 16 + cc];
-      }
-      a *= rs;
-      b *= rs;
+      if constexpr (NORM) rs = rsqrtf(fss[m] / (float)K + eps);
+      const float a = fin[m * TN + cc] * rs, b = fin[m * TN + 16 + cc] * rs;
       const int i = i0 + cc;
       float o1 = a, o2 = b;
       if (hh < R.H + R.KV) {
@@ -218,28 +265,13 @@ __global__ __launch_bounds__(WAVES * 64) void decode_gemm_kernel(const DgArgs A)
     const int m = e / TNO, n = e % TNO;
     if (m >= M) continue;
     float rs = 1.f;
-    if constexpr (NORM) {
-      float t = 0.f;
-#pragma unroll
-      for (int wv = 0; wv < WAVES; ++wv) t += ssq[wv * TM + m];
-      rs = rsqrtf(t * inv_k + eps);
-    }
+    if constexpr (NORM) rs = rsqrtf(fss[m] * inv_k + eps);
     if constexpr (EPI == EPI_SILU) {
       const int p = n >> 4, cc = n & 15;
-      float gs = 0.f, us = 0.f;
-#pragma unroll
-      for (int wv = 0; wv < WAVES; ++wv) {
-        gs += red[(wv * TM + m) * TN + 32 * p + cc];
-        us += red[(wv * TM + m) * TN + 32 * p + 16 + cc];
-      }
-      gs *= rs;
-      us *= rs;
+      const float gs = fin[m * TN + 32 * p + cc] * rs, us = fin[m * TN + 32 * p + 16 + cc] * rs;
       y[(size_t)m * ldy + n0 + n] = (bf16)(gs / (1.f + __expf(-gs)) * us);
     } else {
-      float s = 0.f;
-#pragma unroll
-      for (int wv = 0; wv < WAVES; ++wv) s += red[(wv * TM + m) * TN + n];
-      s *= rs;
+      float s = fin[m * TN + n] * rs;
       if constexpr (EPI == EPI_RESID) s += (float)resid[(size_t)m * ldr + n0 + n];
       y[(size_t)m * ldy + n0 + n] = (bf16)s;
     }
@@ -249,14 +281,14 @@ __global__ __launch_bounds__(WAVES * 64) void decode_gemm_kernel(const DgArgs A)
 template <int MT, int NT, int WAVES, int EPI, bool NORM>
 static int launch_dg(const DgArgs& a, hipStream_t st) {
   constexpr int U = MT == 1 ? 8 : (MT == 2 ? 4 : 2);
-  const size_t lds = (size_t)WAVES * MT * 16 * (NT * 16 + 1) * sizeof(float);
+  const size_t lds = ((size_t)(WAVES + 1) * MT * 16 * (NT * 16 + 1) + 16) * sizeof(float);
   auto kern = decode_gemm_kernel<MT, NT, WAVES, U, EPI, NORM>;
   static bool attr = false;
   if (!attr) {
     hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr = true;
   }
-  hipLaunchKernelGGL(kern, dim3(a.N / (16 * NT)), dim3(WAVES * 64), lds, st, a);
+  hipLaunchKernelGGL(kern, dim3(a.N / (16 * NT) * a.S), dim3(WAVES * 64), lds, st, a);
   return 0;
 }
 
@@ -265,15 +297,15 @@ static int pick_nw(int nt, int waves, const DgArgs& a, hipStream_t st) {
 #define PA_DG(NT_, W_) \
   if (nt == NT_ && waves == W_) return launch_dg<MT, NT_, W_, EPI, NORM>(a, st);
   if constexpr (EPI == EPI_ROPE) {
-    PA_DG(2, 8) PA_DG(2, 16)
+    PA_DG(2, 4) PA_DG(2, 8) PA_DG(2, 16)
     return 1;
   } else {
     if constexpr (EPI != EPI_SILU) {
       PA_DG(1, 8) PA_DG(1, 16)
     }
-    PA_DG(2, 8) PA_DG(2, 16)
+    PA_DG(2, 4) PA_DG(2, 8) PA_DG(2, 16)
     if constexpr (MT <= 2) {
-      PA_DG(4, 8) PA_DG(4, 16)
+      PA_DG(4, 4) PA_DG(4, 8) PA_DG(4, 16)
     } else {
       PA_DG(4, 8)
     }
@@ -282,29 +314,47 @@ static int pick_nw(int nt, int waves, const DgArgs& a, hipStream_t st) {
   return 1;
 }
 
-// Default (tile width, waves) per shape, from tools/decode_gemm_bench.py on MI355X
-// (profiles/r1_decode_gemm.md): 2 column tiles per workgroup once there are >= 384
-// tiles (x fragments re-used across both), 4 for wide matrices at M > 8 (the x
-// stream grows with M); K split over 16 waves when a workgroup is alone on its CU.
-static void default_cfg(int MT, int M, int N, int epi, int& nt, int& waves) {
+// Default (tile width, waves, K slices) per shape, from tools/decode_gemm_bench.py on
+// MI355X (profiles/r1_decode_gemm.md, r1_decode_gemm_splitk.jsonl): 2 column tiles per
+// workgroup once there are >= 384 tiles (x fragments re-used across both), 4 for wide
+// matrices at M > 8 (the x stream grows with M); K split over 16 waves when a
+// workgroup is alone on its CU. Split-K across workgroups is available (splits > 0)
+// but off by default: it won only on down in isolation and lost inside the engine.
+static void default_cfg(int MT, int M, int N, int K, int epi, int& nt, int& waves, int& S) {
   const int tiles = N / 16;
   if (epi == EPI_ROPE) nt = 2;
   else if (epi == EPI_SILU) nt = (M > 8 && tiles % 4 == 0) ? 4 : 2;
   else if (MT >= 2 && tiles >= 1792 && tiles % 4 == 0) nt = 4;
   else nt = (tiles >= 384 && tiles % 2 == 0) ? 2 : 1;
   waves = (tiles / nt <= 256 && M <= 8) ? 16 : 8;
+  S = 1;
+  (void)K;  // split-K (S > 1) measured no faster inside the engine: r1_decode_gemm.md
 }
 
-
-static int dispatch(const DgArgs& a, int epi, int norm, int nt, int waves, hipStream_t st) {
+static int dispatch(DgArgs a, int epi, int norm, int nt, int waves, int splits, long long ws_floats,
+                    int n_counters, hipStream_t st) {
   const int M = a.M, N = a.N;
   if (M <= 0) return 0;
   if (M > 64 || a.K % 32 != 0 || N % 16 != 0 || epi < 0 || epi > 3) return 1;
   if ((epi == EPI_SILU || epi == EPI_ROPE) && (N / 16) % 2) return 1;
   if (epi == EPI_RESID && !a.resid) return 1;
   const int MT = M <= 16 ? 1 : (M <= 32 ? 2 : 4);
-  if (nt <= 0 || waves <= 0) default_cfg(MT, M, N, epi, nt, waves);
+  int dn, dw, dS;
+  default_cfg(MT, M, N, a.K, epi, dn, dw, dS);
+  if (nt <= 0) nt = dn;
+  if (waves <= 0) waves = dw;
+  int S = splits > 0 ? splits : dS;
   if ((N / 16) % nt) return 1;
+  S = std::max(1, std::min(S, a.K / 32));
+  const int G = N / 16 / nt;
+  if (S > 1) {
+    const long long slab = (long long)MT * 16 * (nt * 16 + 1);
+    if (!a.ws || !a.counters || n_counters < G || (long long)G * S * slab > ws_floats) {
+      if (splits > 0) return 1;
+      S = 1;  // default split without a workspace: run unsplit
+    }
+  }
+  a.S = S;
   int rc = 1;
 #define PA_DGE(MT_)                                                                 \
   switch (epi * 2 + (norm ? 1 : 0)) {                                               \
@@ -329,13 +379,16 @@ static int dispatch(const DgArgs& a, int epi, int norm, int nt, int waves, hipSt
 
 // Returns 1 if the shape/config is not handled, 0 on success, -2 on a launch error.
 // epi: 0 plain, 1 silu(gate)*up over interleaved tile pairs, 2 residual add.
+// nt/waves/splits <= 0 pick the defaults; ws/counters: split-K slabs and zeroed tickets.
 extern "C" int pa_decode_gemm(void* y, const void* x, const void* wp, const void* resid, int M, int N, int K,
                               int ldx, int ldy, int ldr, int epi, int norm, float eps, int nt, int waves,
+                              int splits, float* ws, long long ws_floats, int* counters, int n_counters,
                               hipStream_t st) {
   using namespace pa;
   if (epi == EPI_ROPE) return 1;
-  DgArgs a{(bf16*)y, (const bf16*)x, (const bf16*)wp, (const bf16*)resid, M, N, K, ldx, ldy, ldr, eps, RopeArgs{}};
-  return dispatch(a, epi, norm, nt, waves, st);
+  DgArgs a{(bf16*)y, (const bf16*)x, (const bf16*)wp, (const bf16*)resid, M, N, K, ldx, ldy, ldr, eps, RopeArgs{},
+           1, ws, counters};
+  return dispatch(a, epi, norm, nt, waves, splits, ws_floats, n_counters, st);
 }
 
 // QKV projection (RMSNorm folded, rope-permuted packed weights) + RoPE + paged KV
@@ -343,10 +396,12 @@ extern "C" int pa_decode_gemm(void* y, const void* x, const void* wp, const void
 extern "C" int pa_decode_qkv_rope(const void* x, const void* wp, int M, int N, int K, int ldx, float eps,
                                   void* q_out, void* k_cache, void* v_cache, const int* positions,
                                   const int* slots, const float* cos_sin, int H, int KV, int nt, int waves,
+                                  int splits, float* ws, long long ws_floats, int* counters, int n_counters,
                                   hipStream_t st) {
   using namespace pa;
   if (N != (H + 2 * KV) * 128) return 1;
   DgArgs a{nullptr, (const bf16*)x, (const bf16*)wp, nullptr, M, N, K, ldx, 0, 0, eps,
-           RopeArgs{(bf16*)q_out, (bf16*)k_cache, (bf16*)v_cache, positions, slots, cos_sin, H, KV}};
-  return dispatch(a, EPI_ROPE, 1, nt, waves, st);
+           RopeArgs{(bf16*)q_out, (bf16*)k_cache, (bf16*)v_cache, positions, slots, cos_sin, H, KV},
+           1, ws, counters};
+  return dispatch(a, EPI_ROPE, 1, nt, waves, splits, ws_floats, n_counters, st);
 }

@@ -12,6 +12,12 @@ forward per step instead of queueing behind a 5-slot HTTP semaphore. Replies
 can be constrained to a schema via `response_format` (source/rules.yaml
 `schemas:`); agents and the orchestrator always pass one, so every reply parses.
 
+Task queue on the GPU stream: an agent step's call is
+`engine.submit()` -> the engine thread batches it into the next captured step on
+the GPU's stream; the completion callback resolves the caller's asyncio future
+with `loop.call_soon_threadsafe`, so the orchestrator's event loop never blocks
+on the device.
+
 `SchemaLLM` is a model-free implementation of the same protocol that emits
 schema-valid JSON directly (used by CPU tests and the plumbing benchmark,
 BASELINE config 1).

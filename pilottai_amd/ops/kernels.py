@@ -263,7 +263,7 @@ def unpack_decode_gate_up(wp: torch.Tensor) -> torch.Tensor:
 
 def decode_gemm(x: torch.Tensor, wp: torch.Tensor, epi: str = "plain", norm: bool = False,
                 eps: float = 1e-5, resid: Optional[torch.Tensor] = None,
-                out: Optional[torch.Tensor] = None, nt: int = 0, waves: int = 0) -> torch.Tensor:
+                out: Optional[torch.Tensor] = None, nt: int = 0, waves: int = 0, splits: int = 0) -> torch.Tensor:
     """y = epi(rownorm(x) @ W.T) for M <= 64 rows with W packed by pack_decode_weight
     (gate_up: pack_decode_gate_up). `norm` scales each row by rsqrt(mean(x^2)+eps)
     (the RMSNorm weight must already be folded into W); epi "silu" returns
@@ -275,7 +275,9 @@ def decode_gemm(x: torch.Tensor, wp: torch.Tensor, epi: str = "plain", norm: boo
     if out is None:
         out = torch.empty(M, NO, dtype=x.dtype, device=x.device)
     if _on_gpu(x):
-        if not require_native().decode_gemm(out, x, wp, resid, code, bool(norm), float(eps), int(nt), int(waves)):
+        ws, cnt = wide_workspace(x.device)
+        if not require_native().decode_gemm(out, x, wp, resid, code, bool(norm), float(eps), int(nt), int(waves),
+                                            int(splits), ws, cnt):
             raise ValueError(f"decode_gemm does not handle M={M} N={N} K={K} epi={epi} nt={nt} waves={waves}")
         return out
     xf = x.float()
@@ -316,13 +318,14 @@ def unpack_decode_qkv_rope(wp: torch.Tensor) -> torch.Tensor:
 
 
 def decode_qkv_rope(x: torch.Tensor, wp: torch.Tensor, eps: float, q_out: torch.Tensor, k_cache, v_cache,
-                    positions, slots, cos_sin, H: int, KV: int) -> torch.Tensor:
+                    positions, slots, cos_sin, H: int, KV: int, splits: int = 0) -> torch.Tensor:
     """Decode QKV projection with the RMSNorm folded in (norm weight pre-multiplied
     into the packed weights), RoPE and the paged KV write fused in the epilogue:
     replaces rmsnorm + QKV GEMM + rope_cache on decode-sized steps."""
     if _on_gpu(x):
+        ws, cnt = wide_workspace(x.device)
         require_native().decode_qkv_rope(x, wp, float(eps), q_out, k_cache, v_cache, positions, slots,
-                                         cos_sin, int(H), int(KV))
+                                         cos_sin, int(H), int(KV), int(splits), ws, cnt)
         return q_out
     xf = x.float()
     w = unpack_decode_qkv_rope(wp).float()

@@ -299,18 +299,32 @@ def test_decode_gemm(gpu, M, N, K, epi, norm):
         torch.testing.assert_close(r2, y, atol=0, rtol=0)
 
 
-@pytest.mark.parametrize("nt,waves", [(1, 8), (1, 16), (2, 8), (2, 16), (4, 8), (4, 16)])
-def test_decode_gemm_configs(gpu, nt, waves):
+@pytest.mark.parametrize("nt,waves,splits", [(1, 8, 1), (1, 16, 1), (2, 8, 1), (2, 16, 1), (4, 8, 1), (4, 16, 1),
+                                             (2, 8, 4), (4, 8, 2), (1, 16, 3), (2, 4, 8)])
+def test_decode_gemm_configs(gpu, nt, waves, splits):
+    """Every tile config, with split-K (sc1 slabs + last-arriver reduce) for the
+    norm-folded, SwiGLU and residual epilogues; twice, for the self-resetting tickets."""
     torch.manual_seed(12)
-    M, N, K = 16, 4096, 4096
+    M, N, K = 13, 4096, 4096
     x = _bf(M, K, dev=gpu)
     w = _bf(N, K, dev=gpu, scale=0.05)
-    y = ops.decode_gemm(x, ops.pack_decode_weight(w), "plain", nt=nt, waves=waves)
+    y = ops.decode_gemm(x, ops.pack_decode_weight(w), "plain", nt=nt, waves=waves, splits=splits)
     torch.testing.assert_close(y.float(), x.float() @ w.float().T, atol=3e-2, rtol=2e-2)
+    rs = torch.rsqrt(x.float().pow(2).mean(-1, keepdim=True) + 1e-5)
+    gu = (x.float() @ w.float().T) * rs
+    want = torch.nn.functional.silu(gu[:, :N // 2]) * gu[:, N // 2:]
+    resid = _bf(M, N, dev=gpu)
+    for _ in range(2):
+        if nt % 2 == 0:
+            got = ops.decode_gemm(x, ops.pack_decode_gate_up(w), "silu", norm=True, nt=nt, waves=waves, splits=splits)
+            torch.testing.assert_close(got.float(), want, atol=3e-2, rtol=2e-2)
+        got = ops.decode_gemm(x, ops.pack_decode_weight(w), "resid", resid=resid, nt=nt, waves=waves, splits=splits)
+        torch.testing.assert_close(got.float(), x.float() @ w.float().T + resid.float(), atol=3e-2, rtol=2e-2)
 
 
-@pytest.mark.parametrize("M,H,KV,K", [(7, 32, 8, 4096), (16, 4, 1, 512), (1, 8, 2, 1024)])
-def test_decode_qkv_rope(gpu, M, H, KV, K):
+@pytest.mark.parametrize("M,H,KV,K,splits", [(7, 32, 8, 4096, 0), (16, 4, 1, 512, 0), (1, 8, 2, 1024, 0),
+                                              (9, 32, 8, 4096, 3), (16, 4, 1, 512, 2)])
+def test_decode_qkv_rope(gpu, M, H, KV, K, splits):
     """Norm-folded QKV projection with RoPE + paged KV write in the epilogue vs the
     fp32 projection followed by the reference rope_cache."""
     torch.manual_seed(13)
@@ -328,7 +342,7 @@ def test_decode_qkv_rope(gpu, M, H, KV, K):
     kc = torch.zeros(NB, KV, 16, 16, 8, dtype=torch.bfloat16, device=gpu)
     vc = torch.zeros(NB, KV, 128, 16, dtype=torch.bfloat16, device=gpu)
     q = torch.empty(M, H, 128, dtype=torch.bfloat16, device=gpu)
-    ops.decode_qkv_rope(x, wp, 1e-5, q, kc, vc, pos, slots, cos_sin, H, KV)
+    ops.decode_qkv_rope(x, wp, 1e-5, q, kc, vc, pos, slots, cos_sin, H, KV, splits=splits)
     xn = x.float() * torch.rsqrt(x.float().pow(2).mean(-1, keepdim=True) + 1e-5) * g.float()
     qkv = (xn @ w.float().T).cpu()
     rq = torch.empty(M, H, 128, dtype=torch.float32)

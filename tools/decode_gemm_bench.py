@@ -23,7 +23,8 @@ C = kernels.require_native()
 shapes = [(6144, 4096, "qkv", "plain", True), (4096, 4096, "o", "resid", False),
           (28672, 4096, "gate_up", "silu", True), (4096, 14336, "down", "resid", False),
           (128256, 4096, "lm_head", "plain", False)]
-CFGS = [(1, 8), (1, 16), (2, 8), (2, 16), (4, 8), (4, 16)]
+CFGS = [(1, 8, 1), (1, 16, 1), (2, 8, 1), (2, 16, 1), (4, 8, 1), (2, 8, 2), (2, 8, 4), (2, 16, 2), (4, 8, 2),
+        (4, 8, 4), (1, 8, 2), (1, 8, 4), (2, 4, 4), (4, 4, 4)]
 
 
 def timeit(fn, ncopies, iters=30):
@@ -57,15 +58,19 @@ for N, K, name, epi, norm in shapes:
             row["skinny"] = round(timeit(lambda i: C.skinny_gemm(y, x, ws[i]), ncopies), 1)
         # plain packed kernel over configs
         best = None
-        for nt, wv in CFGS:
+        bestk = None
+        for nt, wv, sp in CFGS:
             if (N // 16) % nt:
                 continue
             try:
-                t = timeit(lambda i: kernels.decode_gemm(x, wps[i], "plain", out=y, nt=nt, waves=wv), ncopies)
+                t = timeit(lambda i: kernels.decode_gemm(x, wps[i], "plain", out=y, nt=nt, waves=wv, splits=sp),
+                           ncopies)
             except (ValueError, RuntimeError):
                 continue
-            row[f"p{nt}x{wv}"] = round(t, 1)
-            best = t if best is None else min(best, t)
+            row[f"p{nt}x{wv}s{sp}"] = round(t, 1)
+            if best is None or t < best:
+                best, bestk = t, f"p{nt}x{wv}s{sp}"
+        row["best_cfg"] = bestk
         row["auto"] = round(timeit(lambda i: kernels.decode_gemm(x, wps[i], "plain", out=y), ncopies), 1)
         ref = x.float() @ ws[0].float().T
         got = kernels.decode_gemm(x, wps[0], "plain").float()
