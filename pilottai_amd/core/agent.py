@@ -389,10 +389,21 @@ class BaseAgent:
         iterations = 0
         try:
             self._validate_task(task)
-            analysis = await self._analyze_task(task)
+            # Task analysis and tool selection are independent LLM calls (the
+            # reference's _select_tools, pilott/core/agent.py:259-268, does not read
+            # the analysis; it runs them back to back, :176-179): issue both into the
+            # continuous batch at once and keep the reference's outcome rules — a
+            # "cannot execute" analysis fails the task and the selection is dropped.
+            sel_fut = asyncio.ensure_future(self._select_tools(task))
+            try:
+                analysis = await self._analyze_task(task)
+            except BaseException:
+                sel_fut.cancel()
+                raise
             if analysis.get("can_execute", True) is False:
+                sel_fut.cancel()
                 raise ValueError(f"Cannot execute task: {analysis.get('reason')}")
-            selection = await self._select_tools(task)
+            selection = await sel_fut
             chosen = [t for t in selection.get("selected_tools", []) if t in self.tools]
             for name in sorted(set(chosen)):  # fixed order -> no deadlock
                 lock = self._tool_locks.setdefault(name, asyncio.Lock())

@@ -328,3 +328,45 @@ def test_complex_workflow_steps_go_to_specialised_children():
     assert r.success and r.output == {"extract": "extract-out", "analyze": "analyze-out", "summarize": "summarize-out"}
     assert seen == [("extract", "extract", None), ("analyze", "analyze", "extract-out"),
                     ("summarize", "summarize", "analyze-out")]
+
+
+async def test_agent_analysis_and_tool_selection_overlap():
+    """The two independent opening calls of an agent task are in flight together
+    (one continuous-batch step for both), and a "cannot execute" analysis still
+    fails the task (reference pilott/core/agent.py:176-182)."""
+    class SlowLLM(SchemaLLM):
+        def __init__(self, *a, **k):
+            super().__init__(*a, **k)
+            self.inflight, self.peak = 0, 0
+
+        async def generate_response(self, messages, tools=None, **kw):
+            self.inflight += 1
+            self.peak = max(self.peak, self.inflight)
+            await asyncio.sleep(0.02)
+            try:
+                return await super().generate_response(messages, tools, **kw)
+            finally:
+                self.inflight -= 1
+
+    llm = SlowLLM(seed=3)
+    a = make_agent(llm=llm)
+    await a.start()
+    r = await a.execute_task(Task(description="summarize y"))
+    assert r.success, r.error
+    assert llm.peak == 2
+
+    class NoLLM(SlowLLM):
+        async def generate_response(self, messages, tools=None, **kw):
+            out = await super().generate_response(messages, tools, **kw)
+            text = json.dumps(messages)
+            if "can_execute" in text:
+                obj = json.loads(out["content"])
+                obj["can_execute"] = False
+                obj["reason"] = "no"
+                out["content"] = json.dumps(obj)
+            return out
+
+    b = make_agent(llm=NoLLM(seed=4), policy=ControlPolicy("model"))
+    await b.start()
+    r = await b.execute_task(Task(description="summarize z"))
+    assert not r.success and "Cannot execute" in (r.error or "")
