@@ -61,7 +61,7 @@ def main():
     planted = {i: int(r) for i, r in zip(range(0, Q, 8), torch.randint(0, a.rows, (Q,), generator=g, device=dev)
                                                      .tolist()[: (Q + 7) // 8])}
     for i, r in planted.items():
-        qv[i] = idx.vectors[r].float()
+        qv[i] = idx.row(r).float()
     qv = qv.cpu().numpy()
     minp = [0 if i in planted else (i % 3) for i in range(Q)]
     tags = [[] if i in planted else ([f"topic{i % 8}"] if i % 2 else []) for i in range(Q)]

@@ -355,13 +355,15 @@ void cosine_topk(at::Tensor out_scores, at::Tensor out_rows, at::Tensor workspac
   check_dtype(row_priority, at::kInt, "row_priority"); check_dtype(row_tags, at::kLong, "row_tags");
   check_dtype(row_expiry, at::kFloat, "row_expiry");
   check_dtype(q_min_priority, at::kInt, "q_min_priority"); check_dtype(q_tags, at::kLong, "q_tags");
-  TORCH_CHECK(queries.dim() == 2 && index.dim() == 2 && queries.size(1) == index.size(1),
-              "queries [Q, D] and index [N, D] must agree on D");
-  const int Q = queries.size(0), N = index.size(0), D = index.size(1);
+  TORCH_CHECK(index.dim() == 4 && index.size(2) == 64 && index.size(3) == 8,
+              "index must be packed in 16-row tiles [N/16, D/32, 64, 8] (memory/semantic_index.py)");
+  const int Q = queries.size(0), N = index.size(0) * 16, D = index.size(1) * 32;
+  TORCH_CHECK(queries.dim() == 2 && queries.size(1) == D, "queries [Q, D] and the index must agree on D");
   TORCH_CHECK(Q <= 64, "cosine_topk takes at most 64 queries per call (ops.cosine_topk chunks larger batches)");
   TORCH_CHECK(n_valid <= N, "n_valid exceeds index rows");
-  TORCH_CHECK(queries.is_contiguous() && index.stride(1) == 1 && index.stride(0) == D,
-              "queries and index must be contiguous row-major");
+  TORCH_CHECK(row_priority.numel() >= n_valid && row_tags.numel() >= n_valid && row_expiry.numel() >= n_valid,
+              "row metadata shorter than n_valid");
+  TORCH_CHECK(queries.is_contiguous(), "queries must be contiguous");
   TORCH_CHECK(out_scores.numel() >= (int64_t)Q * K && out_rows.numel() >= (int64_t)Q * K,
               "output too small");
   TORCH_CHECK(workspace.numel() * workspace.element_size() >=

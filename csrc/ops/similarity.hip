@@ -11,9 +11,11 @@
 // (priority index range, tag-set intersection, is_expired) evaluated in-kernel.
 //
 // Stage 1 (one pass over the index for up to 64 queries): each workgroup owns a
-// slice of rows; its 8 waves take 16-row groups and multiply them by EVERY query
+// slice of rows; its 16 waves take 16-row groups and multiply them by EVERY query
 // tile with v_mfma_f32_16x16x32_bf16 — index rows stream from HBM straight into
-// the A operand once, the (<= 64) queries sit in LDS as B operands, so a 205 GB
+// the A operand once (the index is stored in 16-row tiles, fragment-major:
+// [N/16][D/32][64 lanes][8], so each wave load is 1 KiB contiguous instead of
+// 16 rows x 64 B — half the load-path work per streamed byte), the (<= 64) queries sit in LDS as B operands, so a 205 GB
 // 100M x 1024 index is read exactly once per batch of agent queries. Scores
 // above a query's running threshold (and passing the filters) are appended to
 // that query's candidate buffer (global workspace, per workgroup); a full buffer
@@ -30,7 +32,7 @@ constexpr int SIM_MAXQ = 64;      // queries per pass (4 tiles resident in LDS)
 constexpr int SIM_MAXD = 1024;    // LDS query capacity per query (bf16)
 constexpr int SIM_THREADS = 1024; // 16 waves: 128 KB of row loads in flight per CU
 constexpr int SIM_MIN_ROWS_PER_WG = 2048;
-constexpr int SIM_KB = 4;         // k-steps of row loads issued ahead per batch
+constexpr int SIM_KB = 8;         // k-steps per row-load batch (two batches in flight)
 constexpr int SIM_MAX_WG = 256;    // one resident workgroup per CU: the threshold warm-up is paid once per CU
 
 __host__ __device__ inline int sim_num_wg(int N) {
@@ -136,31 +138,43 @@ __global__ __launch_bounds__(SIM_THREADS) void cosine_stage1_kernel(
 
   float* my_s = cand_s + (size_t)wg * SIM_MAXQ * SIM_CAND;
   int* my_r = cand_r + (size_t)wg * SIM_MAXQ * SIM_CAND;
-  const int per = (N + nwg - 1) / nwg;
+  const int per = ((N + nwg - 1) / nwg + 15) / 16 * 16;  // slices start on 16-row tiles
   const int r0 = wg * per, r1 = min(N, r0 + per);
   const int ngroups = (max(0, r1 - r0) + 15) / 16;
   constexpr int NW = SIM_THREADS / 64;
   const int nrounds = (ngroups + NW - 1) / NW;
   const int ksteps = D / 32;
 
+  // Row loads are double-buffered in batches of SIM_KB k-steps (bufA / bufB) and
+  // the first batch of a wave's NEXT 16-row group is issued before the round's
+  // candidate work and barrier, so ~2 x SIM_KB KiB per wave stay in flight across
+  // group and round boundaries (a round-synchronous loop drains the stream at
+  // every barrier: 3.5-3.8 TB/s before).
+  auto tile_ptr = [&](int grp_) {
+    return index + ((size_t)((r0 + grp_ * 16) >> 4) * ksteps) * 512 + lane * 8;
+  };
+  auto load_batch = [&](const bf16* ap, int m, bf16x8 (&dst)[SIM_KB]) {
+#pragma unroll
+    for (int u = 0; u < SIM_KB; ++u)
+      dst[u] = (m + u < ksteps) ? __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(ap + 512 * (m + u)))
+                                : bf16x8{};
+  };
+  bf16x8 bufA[SIM_KB], bufB[SIM_KB];
+  if (wid < ngroups) load_batch(tile_ptr(wid), 0, bufA);
+
   for (int round = 0; round < nrounds; ++round) {
     const int grp = round * NW + wid;
     if (grp < ngroups) {
       const int gbase = r0 + grp * 16;
-      const int arow = min(gbase + col, N - 1);
-      const bf16* ap = index + (size_t)arow * D + 8 * g;
+      // packed tile gbase/16: k-step m is 64 lanes x 16 B contiguous (1 KiB per wave load)
+      const bf16* ap = tile_ptr(grp);
       f32x4 acc[SIM_MAXQ / SIM_QT];
 #pragma unroll
       for (int t = 0; t < SIM_MAXQ / SIM_QT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-      // batches of SIM_KB k-steps: independent 16-B row loads in flight per lane
-      // (16 waves x SIM_KB KB per CU) before their MFMAs consume them
-      int m = 0;
-      for (; m + SIM_KB <= ksteps; m += SIM_KB) {
-        bf16x8 av[SIM_KB];
-#pragma unroll
-        for (int u = 0; u < SIM_KB; ++u) av[u] = __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(ap + 32 * (m + u)));
+      auto compute = [&](const bf16x8 (&av)[SIM_KB], int m) {
 #pragma unroll
         for (int u = 0; u < SIM_KB; ++u) {
+          if (m + u >= ksteps) break;
 #pragma unroll
           for (int t = 0; t < SIM_MAXQ / SIM_QT; ++t) {
             if (t < NQT) {
@@ -168,19 +182,14 @@ __global__ __launch_bounds__(SIM_THREADS) void cosine_stage1_kernel(
               acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[u], b, acc[t], 0, 0, 0);
             }
           }
-          // one k-step's B reads live at a time (the row loads stay in flight)
-          asm volatile("" ::: "memory");
         }
-      }
-      for (; m < ksteps; ++m) {
-        const bf16x8 a = *reinterpret_cast<const bf16x8*>(ap + 32 * m);
-#pragma unroll
-        for (int t = 0; t < SIM_MAXQ / SIM_QT; ++t) {
-          if (t < NQT) {
-            const bf16x8 b = *reinterpret_cast<const bf16x8*>(qt + (size_t)(t * SIM_QT + col) * QLD + 32 * m + 8 * g);
-            acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc[t], 0, 0, 0);
-          }
-        }
+      };
+      for (int m = 0; m < ksteps; m += 2 * SIM_KB) {
+        if (m + SIM_KB < ksteps) load_batch(ap, m + SIM_KB, bufB);
+        compute(bufA, m);
+        if (m + 2 * SIM_KB < ksteps) load_batch(ap, m + 2 * SIM_KB, bufA);
+        else if (grp + NW < ngroups) load_batch(tile_ptr(grp + NW), 0, bufA);  // next group's first batch
+        if (m + SIM_KB < ksteps) compute(bufB, m + SIM_KB);
       }
       // lane holds rows gbase + 4g + r for queries t*16 + col
 #pragma unroll

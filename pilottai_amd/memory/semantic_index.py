@@ -81,7 +81,14 @@ class SemanticIndex:
     def _alloc(self, cap: int):
         d = self.device
         self.capacity = cap
-        self.vectors = torch.zeros(cap, self.dim, dtype=torch.bfloat16, device=d)
+        # Rows are stored fragment-major in tiles of 16 (csrc/ops/similarity.hip):
+        # packed[t, s, 16*g + c, :] = row (16t + c), dims 32s + 8g .. +8 — the A
+        # operand of one v_mfma_f32_16x16x32_bf16, so every wave load of the scan is
+        # 1 KiB contiguous. Row-major access goes through read_rows()/write_rows().
+        if self.dim % 32:
+            raise ValueError(f"index dim {self.dim} must be a multiple of 32")
+        tiles = (cap + 15) // 16
+        self.packed = torch.zeros(tiles, self.dim // 32, 64, 8, dtype=torch.bfloat16, device=d)
         self.priority = torch.full((cap,), -(1 << 30), dtype=torch.int32, device=d)
         self.tagbits = torch.zeros(cap, dtype=torch.int64, device=d)
         self.expiry = torch.zeros(cap, dtype=torch.float32, device=d)
@@ -93,10 +100,10 @@ class SemanticIndex:
         new = min(new, self.max_capacity)
         if new <= self.capacity:
             return
-        old = (self.vectors, self.priority, self.tagbits, self.expiry, self.capacity)
+        old = (self.packed, self.priority, self.tagbits, self.expiry, self.capacity)
         self._alloc(new)
         n = old[4]
-        self.vectors[:n] = old[0]
+        self.packed[:old[0].shape[0]] = old[0]
         self.priority[:n] = old[1]
         self.tagbits[:n] = old[2]
         self.expiry[:n] = old[3]
@@ -104,6 +111,37 @@ class SemanticIndex:
     @property
     def count(self) -> int:
         return min(self.size, self.capacity)
+
+    # -- row-major views of the packed storage ------------------------------------
+    def _p5(self) -> torch.Tensor:
+        return self.packed.view(self.packed.shape[0], self.dim // 32, 4, 16, 8)
+
+    def write_rows(self, rows: torch.Tensor, vals: torch.Tensor):
+        """Scatter row-major `vals` [n, dim] into rows `rows` (long tensor)."""
+        rows = rows.to(self.device)
+        v = vals.to(self.device, torch.bfloat16).reshape(-1, self.dim // 32, 4, 8)
+        self._p5()[rows // 16, :, :, rows % 16, :] = v
+
+    def write_range(self, r0: int, vals: torch.Tensor):
+        """Rows r0 .. r0 + len(vals): whole tiles move as one permuted copy."""
+        m = int(vals.shape[0])
+        if m == 0:
+            return
+        if r0 % 16 == 0 and m % 16 == 0:
+            v = vals.to(self.device, torch.bfloat16).reshape(m // 16, 16, self.dim // 32, 4, 8)
+            self.packed[r0 // 16:(r0 + m) // 16].view(m // 16, self.dim // 32, 4, 16, 8).copy_(
+                v.permute(0, 2, 3, 1, 4))
+        else:
+            self.write_rows(torch.arange(r0, r0 + m, device=self.device), vals)
+
+    def read_rows(self, r0: int, r1: int) -> torch.Tensor:
+        """Row-major copy of rows [r0, r1) as [r1 - r0, dim] bf16."""
+        t0, t1 = r0 // 16, (r1 + 15) // 16
+        blk = self._p5()[t0:t1].permute(0, 3, 1, 2, 4).reshape((t1 - t0) * 16, self.dim)
+        return blk[r0 - 16 * t0:r1 - 16 * t0]
+
+    def row(self, r: int) -> torch.Tensor:
+        return self.read_rows(r, r + 1)[0]
 
     def now(self) -> float:
         return time.time() - self.epoch
@@ -120,7 +158,7 @@ class SemanticIndex:
             self.size += n
             idx = torch.tensor(rows, dtype=torch.long, device=self.device)
             v = torch.nn.functional.normalize(v, dim=1)
-            self.vectors.index_copy_(0, idx, v.to(self.device, torch.bfloat16))
+            self.write_rows(idx, v.to(self.device, torch.bfloat16))
             self.priority.index_copy_(0, idx, torch.tensor(list(priorities), dtype=torch.int32, device=self.device))
             masks = []
             for r, ts in zip(rows, tags):
@@ -158,7 +196,7 @@ class SemanticIndex:
                 r0 = (start + done) % self.capacity
                 m = min(n - done, self.capacity - r0)
                 sl = slice(r0, r0 + m)
-                self.vectors[sl].copy_(v[done:done + m])
+                self.write_range(r0, v[done:done + m])
                 self.priority[sl].copy_(priorities[done:done + m])
                 self.tagbits[sl].copy_(tag_masks[done:done + m])
                 if expiry is None:
@@ -207,7 +245,7 @@ class SemanticIndex:
             qd = torch.nn.functional.normalize(q, dim=1).to(self.device, torch.bfloat16)
             minp = torch.tensor(list(min_priority), dtype=torch.int32, device=self.device)
             qt = torch.tensor(qmasks, dtype=torch.int64, device=self.device)
-            s, r = ops.cosine_topk(qd, self.vectors, n, kk, self.priority, self.tagbits, self.expiry, minp, qt,
+            s, r = ops.cosine_topk(qd, self.packed, n, kk, self.priority, self.tagbits, self.expiry, minp, qt,
                                    self.now() if now is None else now - self.epoch, workspace=self._ws)
             s, r = s.cpu().numpy(), r.cpu().numpy()
         out = []
@@ -225,7 +263,7 @@ class SemanticIndex:
         return out
 
     def memory_bytes(self) -> int:
-        return self.vectors.numel() * 2 + self.capacity * (4 + 8 + 4)
+        return self.packed.numel() * 2 + self.capacity * (4 + 8 + 4)
 
 
 class ShardedSemanticIndex:

@@ -192,6 +192,8 @@ def cosine_topk(queries, index, n_valid: int, K: int, row_priority, row_tags, ro
                           int(n_valid), int(K), row_priority, row_tags, row_expiry,
                           q_min_priority[q0:q1].contiguous(), q_tags[q0:q1].contiguous(), float(now))
         return out_s, out_r
+    if index.dim() == 4:  # packed tiles (memory/semantic_index.py) -> row-major for the reference
+        index = unpack_decode_weight(index)
     return ref.cosine_topk(queries, index, n_valid, K, row_priority, row_tags, row_expiry,
                            q_min_priority, q_tags, now)
 

@@ -118,7 +118,7 @@ def save_index(index, path) -> str:
     path = Path(path)
     path.mkdir(parents=True, exist_ok=True)
     n = index.count
-    vec = index.vectors[:n].view(dtype=__import__("torch").int16).cpu().numpy().view(np.uint16)
+    vec = index.read_rows(0, n).contiguous().view(dtype=__import__("torch").int16).cpu().numpy().view(np.uint16)
     np.save(path / "index.npy", vec, allow_pickle=False)
     meta = {"dim": index.dim, "count": n, "size": index.size, "epoch": index.epoch,
             "priority": index.priority[:n].cpu().tolist(), "tagbits": index.tagbits[:n].cpu().tolist(),
@@ -138,7 +138,7 @@ def load_index(path, device=None):
     arr = np.load(path / "index.npy", mmap_mode="r", allow_pickle=False)
     n = meta["count"]
     idx = SemanticIndex(dim=meta["dim"], capacity=max(1, n), device=device)
-    idx.vectors[:n].copy_(torch.from_numpy(np.ascontiguousarray(arr).view(np.int16)).view(torch.bfloat16))
+    idx.write_range(0, torch.from_numpy(np.ascontiguousarray(arr).view(np.int16)).view(torch.bfloat16))
     idx.priority[:n] = torch.tensor(meta["priority"], dtype=torch.int32)
     idx.tagbits[:n] = torch.tensor(meta["tagbits"], dtype=torch.int64)
     idx.expiry[:n] = torch.tensor(meta["expiry"], dtype=torch.float32)

@@ -213,7 +213,9 @@ def test_cosine_topk(gpu, N, D, Q, K):
     exp[::7] = 50.0  # expired at now=100
     qmin = torch.tensor([0, 0, 2, 4, 0] * ((Q + 4) // 5), dtype=torch.int32)[:Q]
     qt = torch.tensor([0, 0, 1, 2, 3] * ((Q + 4) // 5), dtype=torch.int64)[:Q]
-    s, r = ops.cosine_topk(qs.to(gpu), idx.to(gpu), N, K, prio.to(gpu), tags.to(gpu), exp.to(gpu),
+    Np = (N + 15) // 16 * 16  # the index is stored in packed 16-row tiles
+    packed = ops.pack_decode_weight(torch.cat([idx, torch.zeros(Np - N, D, dtype=idx.dtype)]).to(gpu))
+    s, r = ops.cosine_topk(qs.to(gpu), packed, N, K, prio.to(gpu), tags.to(gpu), exp.to(gpu),
                            qmin.to(gpu), qt.to(gpu), 100.0)
     rs, rr = ref.cosine_topk(qs, idx, N, K, prio, tags, exp, qmin, qt, 100.0)
     torch.testing.assert_close(s.cpu(), rs, atol=2e-3, rtol=2e-3)
@@ -380,3 +382,30 @@ def test_wide_gemm(gpu, M, N, K, epi, norm, ntw, waves, splits):
     for _ in range(2):
         y = ops.wide_gemm(x, wp, epi, resid=resid, norm=norm, ntw=ntw, waves=waves, splits=splits)
         torch.testing.assert_close(y.float(), acc, atol=3e-2, rtol=2e-2)
+
+
+def test_semantic_index_packed_storage(gpu):
+    """SemanticIndex keeps rows in packed 16-row tiles: scattered and bulk writes
+    (aligned and unaligned ranges, ring wrap) read back exactly, and the HIP
+    search finds planted rows."""
+    from pilottai_amd.memory.semantic_index import SemanticIndex
+
+    torch.manual_seed(16)
+    D = 256
+    idx = SemanticIndex(dim=D, capacity=4096, device=gpu, growable=False)
+    a = torch.nn.functional.normalize(torch.randn(37, D), dim=1)
+    rows = idx.add(a.numpy(), [1] * 37, [[]] * 37, [None] * 37)
+    b = torch.nn.functional.normalize(torch.randn(1003, D, device=gpu), dim=1).to(torch.bfloat16)
+    idx.add_device(b, torch.ones(1003, dtype=torch.int32, device=gpu), torch.zeros(1003, dtype=torch.int64, device=gpu),
+                   normalized=True)
+    c = torch.nn.functional.normalize(torch.randn(1024, D, device=gpu), dim=1).to(torch.bfloat16)
+    idx.size = 1024  # aligned bulk write at row 1024
+    idx.add_device(c, torch.ones(1024, dtype=torch.int32, device=gpu), torch.zeros(1024, dtype=torch.int64, device=gpu),
+                   normalized=True)
+    assert rows == list(range(37))
+    torch.testing.assert_close(idx.read_rows(0, 37).float().cpu(), a.to(torch.bfloat16).float(), atol=0, rtol=0)
+    torch.testing.assert_close(idx.read_rows(37, 1024), b[:987], atol=0, rtol=0)
+    torch.testing.assert_close(idx.read_rows(1024, 2048), c, atol=0, rtol=0)
+    q = torch.stack([idx.row(5), idx.row(1500), idx.row(700)]).float().cpu().numpy()
+    res = idx.search(q, 3, [0, 0, 0], [[], [], []])
+    assert [r[0][0] for r in res] == [5, 1500, 700]
