@@ -64,6 +64,8 @@ def parse():
     ap.add_argument("--token-align", type=int, default=256, help="GEMM-friendly step sizes (0 = off)")
     ap.add_argument("--align-slack", type=int, default=96)
     ap.add_argument("--cpu", action="store_true", help="tiny model on CPU (plumbing smoke only)")
+    ap.add_argument("--share-gpu", action="store_true",
+                    help="rehearsal: every rank on GPU 0 (use with PILOTTAI_DIST_BACKEND=gloo)")
     return ap.parse_args()
 
 
@@ -178,8 +180,9 @@ def main():
         device = torch.device("cpu")
         a.cpu = True
     else:
-        torch.cuda.set_device(local_rank)
-        device = torch.device("cuda", local_rank)
+        dev_idx = 0 if a.share_gpu else local_rank
+        torch.cuda.set_device(dev_idx)
+        device = torch.device("cuda", dev_idx)
     res = asyncio.run(run_rank(a, rank, world, device))
     gathered = [res]
     if world > 1:

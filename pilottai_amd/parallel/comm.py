@@ -77,7 +77,9 @@ def init_distributed(backend: Optional[str] = None, timeout_s: int = 600) -> tup
         return 0, 1, 0
     if not dist.is_initialized():
         if backend is None:
-            backend = "nccl" if torch.cuda.is_available() else "gloo"
+            # PILOTTAI_DIST_BACKEND=gloo lets several ranks share one GPU (a 1-GPU
+            # rehearsal of the multi-rank bench); RCCL refuses duplicate devices
+            backend = os.environ.get("PILOTTAI_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29511")
         kw = {}
