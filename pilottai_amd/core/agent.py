@@ -137,6 +137,7 @@ class BaseAgent:
         self.iteration_count = 0
         self.conversation_history: Deque[Dict[str, str]] = deque(maxlen=self.MAX_HISTORY_SIZE)
         self.execution_locks: Dict[str, asyncio.Lock] = {}
+        self._openings: Dict[str, "asyncio.Future"] = {}  # prefetched opening calls by task id
         self._tool_locks: Dict[str, asyncio.Lock] = {}
         self.tasks: Dict[str, Task] = {}
         self.active_tasks: set = set()
@@ -388,22 +389,18 @@ class BaseAgent:
         held: List[str] = []
         iterations = 0
         try:
-            self._validate_task(task)
-            # Task analysis and tool selection are independent LLM calls (the
-            # reference's _select_tools, pilott/core/agent.py:259-268, does not read
-            # the analysis; it runs them back to back, :176-179): issue both into the
-            # continuous batch at once and keep the reference's outcome rules — a
-            # "cannot execute" analysis fails the task and the selection is dropped.
-            sel_fut = asyncio.ensure_future(self._select_tools(task))
+            opening = self._openings.pop(task.id, None)
             try:
-                analysis = await self._analyze_task(task)
+                self._validate_task(task)
             except BaseException:
-                sel_fut.cancel()
+                if opening is not None:
+                    opening.cancel()
                 raise
+            if opening is None:
+                opening = self.prefetch_opening(task, _store=False)
+            analysis, selection = await opening
             if analysis.get("can_execute", True) is False:
-                sel_fut.cancel()
                 raise ValueError(f"Cannot execute task: {analysis.get('reason')}")
-            selection = await sel_fut
             chosen = [t for t in selection.get("selected_tools", []) if t in self.tools]
             for name in sorted(set(chosen)):  # fixed order -> no deadlock
                 lock = self._tool_locks.setdefault(name, asyncio.Lock())
@@ -424,6 +421,36 @@ class BaseAgent:
                 lock = self._tool_locks.get(name)
                 if lock is not None and lock.locked():
                     lock.release()
+
+    def prefetch_opening(self, task: Task, _store: bool = True) -> "asyncio.Future":
+        """Start a task's two opening LLM calls — task analysis and tool selection.
+
+        They are independent (the reference's _select_tools, pilott/core/agent.py:
+        259-268, does not read the analysis; it runs them back to back, :176-179),
+        so both go into the continuous batch at once. Neither has side effects: the
+        orchestrator may start them speculatively while it analyses the task itself
+        (Serve._submit) and drop them (drop_opening) if it decomposes the task."""
+        async def both():
+            sel = asyncio.ensure_future(self._select_tools(task))
+            try:
+                ana = await self._analyze_task(task)
+            except BaseException:
+                sel.cancel()
+                raise
+            if ana.get("can_execute", True) is False:
+                sel.cancel()
+                return ana, {}
+            return ana, await sel
+
+        fut = asyncio.ensure_future(both())
+        if _store:
+            self._openings[task.id] = fut
+        return fut
+
+    def drop_opening(self, task_id: str):
+        fut = self._openings.pop(task_id, None)
+        if fut is not None and not fut.done():
+            fut.cancel()
 
     def _validate_task(self, task: Task):
         if not task.description:

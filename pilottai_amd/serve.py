@@ -30,7 +30,7 @@ from typing import Any, Callable, Deque, Dict, List, Optional, Sequence, Union
 
 from pydantic import BaseModel, Field
 
-from .core.agent import BaseAgent, _content, _resolve_default_llm
+from .core.agent import BaseAgent, _content, _is_workflow as _is_workflow_task, _resolve_default_llm
 from .core.config import AgentConfig, LLMConfig
 from .core.factory import AgentFactory
 from .core.memory import Memory
@@ -57,6 +57,9 @@ class ServeConfig(BaseModel):
     steps_per_task: int = Field(default=1, ge=0)
     routing: str = "first_idle"      # "first_idle" | "scored" (TaskRouter)
     analyze_tasks: bool = True       # orchestrator LLM analysis per task
+    # start a simple task's agent opening calls (analysis + tool selection: LLM calls
+    # without side effects) while the orchestrator analyses the task; dropped if it decomposes
+    speculative_start: bool = True
     evaluate_results: bool = True    # orchestrator LLM evaluation per task
     agent_wait_timeout: float = Field(default=60.0, gt=0)
     enable_load_balancer: bool = False
@@ -297,8 +300,15 @@ class Serve:
         self.tasks[task.id] = task
         self._futures.setdefault(task.id, asyncio.get_running_loop().create_future())
         task.metadata.setdefault("_t_submit", time.perf_counter())
-        analysis = await self._analyze_task(task) if self.config.analyze_tasks else {}
+        spec = await self._speculative_agent(task) if inline else None
+        try:
+            analysis = await self._analyze_task(task) if self.config.analyze_tasks else {}
+        except BaseException:
+            await self._drop_speculation(task, spec)
+            raise
         if analysis.get("requires_decomposition", False):
+            await self._drop_speculation(task, spec)
+            spec = None
             subtasks = await self._decompose_task(task)
             if len(subtasks) > 1 or (subtasks and subtasks[0].id != task.id):
                 task.update_status(TaskStatus.DELEGATED)
@@ -318,14 +328,48 @@ class Serve:
             # slot accounting, timeout, evaluation and callbacks are the worker's
             self._active += 1
             try:
-                await self._run(task)
+                await self._run(task, agent=spec)
             except Exception as e:  # noqa: BLE001 — as the worker loop
                 self._finish(task, TaskResult(success=False, error=str(e)))
             finally:
                 self._active -= 1
             return task.id
+        await self._drop_speculation(task, spec)
         await self._enqueue(task)
         return task.id
+
+    async def _speculative_agent(self, task: Task) -> Optional[BaseAgent]:
+        """Reserve an idle agent and start the task's opening agent calls now, so they
+        overlap the orchestrator's own analysis call (which only decides whether to
+        decompose: the reference, pilott/pilott.py:184-231, runs the two back to
+        back). Only where the caller-runs path will take the task and the plain
+        first-idle pick applies (no manager agent, no scored router)."""
+        if not (self.config.speculative_start and self.config.analyze_tasks) or self.manager_agent is not None \
+                or self.router is not None or _is_workflow_task(task):
+            return None
+        if not self._queue.empty() or self._active >= self.config.max_concurrent_tasks or \
+                any(d in self.tasks and d not in self.completed_tasks for d in task.dependencies):
+            return None
+        async with self._agent_cv:
+            agent = self._pick_idle(task, None)
+            if agent is None:
+                return None
+            n = self._inflight.get(agent.id, 0) + 1
+            self._inflight[agent.id] = n
+            if n >= self._capacity(agent):
+                agent.status = AgentStatus.BUSY
+        prefetch = getattr(agent, "prefetch_opening", None)
+        if prefetch is not None:
+            prefetch(task)
+        return agent
+
+    async def _drop_speculation(self, task: Task, agent: Optional[BaseAgent]):
+        if agent is None:
+            return
+        drop = getattr(agent, "drop_opening", None)
+        if drop is not None:
+            drop(task.id)
+        await self._release_agent(agent)
 
     async def execute_task(self, task: Union[Task, Dict[str, Any], str], timeout: Optional[float] = None) -> TaskResult:
         """Documented API: submit and wait for the TaskResult."""
@@ -388,10 +432,10 @@ class Serve:
                 self._active -= 1
                 self._queue.task_done()
 
-    async def _run(self, task: Task):
+    async def _run(self, task: Task, agent: Optional[BaseAgent] = None):
         t_start = time.perf_counter()
         try:
-            result = await with_timeout(self._execute_task(task), self.config.task_timeout)
+            result = await with_timeout(self._execute_task(task, agent), self.config.task_timeout)
         except asyncio.TimeoutError:
             self.metrics["timeout_tasks"] += 1
             result = TaskResult(success=False, error="Task execution timed out",
@@ -441,8 +485,10 @@ class Serve:
                          metadata={"subtasks": list(parent.subtasks)})
         self._finish(parent, agg)
 
-    async def _execute_task(self, task: Task) -> TaskResult:
-        agent = await self._acquire_agent(task)
+    async def _execute_task(self, task: Task, agent: Optional[BaseAgent] = None) -> TaskResult:
+        """`agent`: already reserved (speculative start in _submit)."""
+        if agent is None:
+            agent = await self._acquire_agent(task)
         try:
             task.mark_started() if task.status in (TaskStatus.PENDING, TaskStatus.RETRY) else None
             self.running_tasks[task.id] = agent.id

@@ -370,3 +370,54 @@ async def test_agent_analysis_and_tool_selection_overlap():
     await b.start()
     r = await b.execute_task(Task(description="summarize z"))
     assert not r.success and "Cannot execute" in (r.error or "")
+
+
+class _CountingLLM(SchemaLLM):
+    """SchemaLLM with a small per-call latency that records peak concurrency."""
+
+    def __init__(self, *a, **k):
+        super().__init__(*a, **k)
+        self.inflight, self.peak, self.total = 0, 0, 0
+
+    async def _complete(self, messages, response_format, tools):
+        self.inflight += 1
+        self.total += 1
+        self.peak = max(self.peak, self.inflight)
+        await asyncio.sleep(0.02)
+        try:
+            return await super()._complete(messages, response_format, tools)
+        finally:
+            self.inflight -= 1
+
+
+async def test_serve_speculative_agent_start_overlaps_orchestrator_analysis():
+    """The orchestrator's analysis and the agent's two opening calls (analysis, tool
+    selection) run together; the task still makes exactly the same LLM calls."""
+    llm = _CountingLLM(seed=8)
+    s = Serve(agents=[make_agent("w", llm=llm)], manager_llm=llm, config={"policy": "fixed"})
+    await s.start()
+    r = await s.execute_task(Task(description="summarize q"))
+    assert r.success, r.error
+    assert llm.peak == 3
+    # orchestrator analysis + evaluation; agent analysis, tools, 3 step plans (FIXED: 2 steps + done), evaluation
+    assert llm.total == 2 + 2 + 3 + 1
+    assert all(str(a.status) == "idle" for a in s.agents.values())
+    assert not any(a._openings for a in s.agents.values())
+    await s.stop()
+
+
+async def test_serve_speculation_dropped_on_decomposition():
+    """A speculatively started agent is released and its opening calls dropped when
+    the orchestrator decomposes the task; the subtasks then run normally."""
+    llm = _CountingLLM(seed=9)
+    s = Serve(agents=[make_agent(f"w{i}", llm=llm) for i in range(2)], manager_llm=llm,
+              config={"max_concurrent_tasks": 2, "policy": "fixed"})
+    await s.start()
+    r = await s.execute_task(Task(description="big job", metadata={"decompose": True}))
+    assert r.success
+    parent = [t for t in s.tasks.values() if t.subtasks][0]
+    assert len(parent.subtasks) == 2 and s.metrics["decomposed_tasks"] == 1
+    await asyncio.sleep(0.1)
+    assert all(str(a.status) == "idle" for a in s.agents.values())
+    assert not any(a._openings for a in s.agents.values())
+    await s.stop()
