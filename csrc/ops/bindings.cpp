@@ -45,6 +45,15 @@ int pa_cosine_topk(float* out_scores, int* out_rows, void* workspace, const void
                    const void* index, int Q, int N, int D, int K, const int* row_priority,
                    const uint64_t* row_tags, const float* row_expiry, const int* q_min_priority,
                    const uint64_t* q_tags, float now, int n_valid, hipStream_t st);
+int pa_car_group();
+long long pa_car_flag_bytes();
+void* pa_car_alloc(long long bytes, void* handle_out);
+void* pa_car_open(const void* handle);
+int pa_car_close(void* p);
+int pa_car_free(void* p);
+int pa_car_all_reduce(void* const* bases, int W, int rank0, int nranks_local, const void* const* ins,
+                      void* const* outs, long long nelem, long long cap_bytes, uint32_t* epochs, int* err,
+                      int two_shot, hipStream_t st);
 }
 
 namespace {
@@ -412,6 +421,50 @@ void topkp_threshold(at::Tensor tau, at::Tensor logits, int64_t V, at::Tensor te
            "topkp_threshold");
 }
 
+// ---- custom P2P all-reduce (csrc/ops/custom_ar.hip) ----
+py::tuple car_alloc(int64_t bytes) {
+  char h[64];
+  void* p = pa_car_alloc(bytes, h);
+  TORCH_CHECK(p != nullptr, "car_alloc: uncached IPC allocation of ", bytes, " bytes failed");
+  return py::make_tuple((int64_t)(uintptr_t)p, py::bytes(h, 64));
+}
+
+int64_t car_open(py::bytes handle) {
+  std::string h = handle;
+  TORCH_CHECK(h.size() == 64, "car_open: IPC handle must be 64 bytes");
+  void* p = pa_car_open(h.data());
+  TORCH_CHECK(p != nullptr, "car_open: hipIpcOpenMemHandle failed");
+  return (int64_t)(uintptr_t)p;
+}
+
+void car_all_reduce(std::vector<int64_t> bases, int64_t rank0, std::vector<at::Tensor> ins,
+                    std::vector<at::Tensor> outs, int64_t cap_bytes, at::Tensor epochs, at::Tensor err,
+                    bool two_shot) {
+  const int W = (int)bases.size();
+  const int nl = (int)ins.size();
+  TORCH_CHECK(W >= 2 && W <= 8, "custom all-reduce supports 2..8 ranks");
+  TORCH_CHECK(nl >= 1 && (int)outs.size() == nl && rank0 >= 0 && rank0 + nl <= W, "bad rank range");
+  const int64_t n = ins[0].numel();
+  std::vector<void*> b(W), ip(nl), op(nl);
+  for (int i = 0; i < W; ++i) b[i] = (void*)(uintptr_t)bases[i];
+  for (int i = 0; i < nl; ++i) {
+    check_gpu(ins[i], "in"); check_gpu(outs[i], "out");
+    check_dtype(ins[i], at::kBFloat16, "in"); check_dtype(outs[i], at::kBFloat16, "out");
+    TORCH_CHECK(ins[i].numel() == n && outs[i].numel() == n, "all-reduce tensors differ in size");
+    TORCH_CHECK(((uintptr_t)ins[i].data_ptr() & 15) == 0 && ((uintptr_t)outs[i].data_ptr() & 15) == 0,
+                "all-reduce tensors must be 16-byte aligned");
+    ip[i] = ins[i].data_ptr(); op[i] = outs[i].data_ptr();
+  }
+  TORCH_CHECK(n % 8 == 0 && n * 2 <= cap_bytes, "message of ", n, " bf16 does not fit the custom all-reduce");
+  check_gpu(epochs, "epochs"); check_dtype(epochs, at::kInt, "epochs");
+  TORCH_CHECK(epochs.numel() >= (int64_t)nl * pa_car_group(), "epochs too short");
+  check_gpu(err, "err"); check_dtype(err, at::kInt, "err");
+  check_rc(pa_car_all_reduce(b.data(), W, (int)rank0, nl, ip.data(), op.data(), n, cap_bytes,
+                             reinterpret_cast<uint32_t*>(epochs.data_ptr<int>()), err.data_ptr<int>(),
+                             two_shot ? 1 : 0, cur_stream()),
+           "custom all-reduce");
+}
+
 PYBIND11_MODULE(_C, m) {
   m.doc() = "pilottai_amd CDNA4 (gfx950) HIP kernels";
   m.def("rmsnorm", &rmsnorm);
@@ -442,6 +495,13 @@ PYBIND11_MODULE(_C, m) {
   m.def("topkp_threshold", &topkp_threshold);
   m.def("cosine_topk_workspace_bytes", &cosine_topk_workspace_bytes);
   m.def("cosine_topk", &cosine_topk);
+  m.def("car_alloc", &car_alloc);
+  m.def("car_open", &car_open);
+  m.def("car_close", [](int64_t p) { return pa_car_close((void*)(uintptr_t)p); });
+  m.def("car_free", [](int64_t p) { return pa_car_free((void*)(uintptr_t)p); });
+  m.def("car_all_reduce", &car_all_reduce);
+  m.def("car_group", &pa_car_group);
+  m.def("car_flag_bytes", &pa_car_flag_bytes);
   m.attr("ATT_PART") = 512;
   m.attr("SAMPLE_CHUNK") = 4096;
 }

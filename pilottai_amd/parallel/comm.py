@@ -9,8 +9,9 @@ Groups used by the framework:
             row-parallel outputs are all-reduced, sampling winners all-gathered.
 
 xGMI is point-to-point (7 links per GPU): decode-size TP all-reduces are latency
-bound, so the engine keeps them inside the captured hipGraph (RCCL supports
-graph capture) and never splits them into extra small collectives.
+bound, so bf16 messages up to 8 MiB go through the custom one-shot/two-shot P2P
+kernel (parallel/custom_ar.py, csrc/ops/custom_ar.hip) and larger ones through
+RCCL. Both are captured inside the engine's hipGraphs.
 """
 from __future__ import annotations
 
@@ -30,6 +31,7 @@ class TPGroup:
     size: int = 1
     root: int = 0                                   # global rank of TP rank 0 (the step driver)
     cpu_group: Optional["dist.ProcessGroup"] = None  # gloo group for host-side step headers
+    custom: Optional[object] = None                 # CustomAllReduce over P2P IPC buffers (GPU TP)
 
     @staticmethod
     def single() -> "TPGroup":
@@ -37,6 +39,8 @@ class TPGroup:
 
     def all_reduce(self, t: torch.Tensor) -> torch.Tensor:
         if self.size > 1:
+            if self.custom is not None and self.custom.eligible(t):
+                return self.custom.all_reduce(t)
             dist.all_reduce(t, group=self.group)
         return t
 
@@ -106,6 +110,11 @@ def new_tp_groups(tp_size: int) -> TPGroup:
         cg = dist.new_group(ranks, backend="gloo") if gloo_needed else g
         if rank in ranks:
             mine = TPGroup(g, rank - start, tp_size, root=start, cpu_group=cg)
+    if dist.get_backend() == "nccl" and torch.cuda.is_available():
+        from pilottai_amd.parallel.custom_ar import CustomAllReduce
+
+        dev = torch.device("cuda", torch.cuda.current_device())
+        mine.custom = CustomAllReduce.create(mine.cpu_group, mine.rank, mine.size, dev)
     return mine
 
 

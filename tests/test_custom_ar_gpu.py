@@ -1,0 +1,154 @@
+"""Custom P2P all-reduce (csrc/ops/custom_ar.hip, parallel/custom_ar.py) on one MI355X.
+
+Two forms, both compared bit-exactly against a plain PyTorch fp32 sum in rank order:
+* several "ranks" in one launch on one GPU (blockIdx.y = rank): the kernel's
+  barrier/parity/epoch logic for W = 2..8, one-shot and two-shot, repeated calls,
+  sizes that do not fill the chunk grid, and hipGraph replay;
+* two processes sharing GPU 0 that exchange real IPC handles over a gloo group —
+  the same setup path (`CustomAllReduce.create`) the TP engine uses over xGMI.
+"""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _C():
+    from pilottai_amd.ops.kernels import require_native
+
+    return require_native()
+
+
+def _ref(ts):
+    acc = torch.zeros_like(ts[0], dtype=torch.float32)
+    for t in ts:
+        acc += t.float()
+    return acc.bfloat16()
+
+
+@pytest.mark.parametrize("W", [2, 4, 8])
+@pytest.mark.parametrize("two_shot", [False, True])
+def test_custom_ar_local_ranks(W, two_shot):
+    from pilottai_amd.parallel.custom_ar import local_group_all_reduce
+
+    C = _C()
+    state = {}
+    cap = 1 << 20
+    g = torch.Generator(device="cuda").manual_seed(W)
+    # sizes: one vector, partial chunk, several chunks per workgroup, the full cap
+    for n in [8, 4096 * 3 + 8, 8192 * 40, cap // 2]:
+        for rep in range(3):  # alternate data parities
+            ins = [torch.randn(n, device="cuda", generator=g).bfloat16() for _ in range(W)]
+            want = _ref(ins)
+            local_group_all_reduce(C, ins, cap, two_shot, state)
+            torch.cuda.synchronize()
+            for r in range(W):
+                assert torch.equal(ins[r], want), (n, rep, r)
+    err = state[(W, cap)][2]
+    assert int(err.item()) == 0
+
+
+def test_custom_ar_local_graph_replay():
+    from pilottai_amd.parallel.custom_ar import local_group_all_reduce
+
+    C = _C()
+    W, n, cap = 4, 8192 * 16, 1 << 20
+    state = {}
+    bufs = [torch.empty(n, dtype=torch.bfloat16, device="cuda") for _ in range(W)]
+    local_group_all_reduce(C, bufs, cap, False, state)  # allocate before capture
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(graph, stream=s):
+            local_group_all_reduce(C, bufs, cap, False, state)
+            local_group_all_reduce(C, bufs, cap, True, state)
+    torch.cuda.current_stream().wait_stream(s)
+    for it in range(4):
+        ins = [torch.randn(n, device="cuda").bfloat16() for _ in range(W)]
+        want = _ref(ins)
+        want = _ref([want] * W)  # two reductions back to back
+        for b, x in zip(bufs, ins):
+            b.copy_(x)
+        graph.replay()
+        torch.cuda.synchronize()
+        for r in range(W):
+            assert torch.equal(bufs[r], want), (it, r)
+    assert int(state[(W, cap)][2].item()) == 0
+
+
+_WORKER = r"""
+import json, os, sys, datetime
+import torch, torch.distributed as dist
+sys.path.insert(0, os.environ["ROOT"])
+rank = int(sys.argv[1])
+dist.init_process_group("gloo", rank=rank, world_size=2, timeout=datetime.timedelta(seconds=60))
+torch.cuda.set_device(0)
+from pilottai_amd.parallel.custom_ar import CustomAllReduce
+car = CustomAllReduce.create(dist.group.WORLD, rank, 2, torch.device("cuda", 0), cap_bytes=1 << 20)
+out = {"rank": rank, "created": car is not None, "ok": []}
+if car is not None:
+    g = torch.Generator(device="cuda").manual_seed(1234)
+    for n in [8, 8192 + 8, 8192 * 40]:
+        for rep in range(3):
+            both = [torch.randn(n, device="cuda", generator=g).bfloat16() for _ in range(2)]
+            want = (both[0].float() + both[1].float()).bfloat16()
+            t = both[rank].clone()
+            car.all_reduce(t, two_shot=bool(rep % 2))
+            torch.cuda.synchronize()
+            out["ok"].append(bool(torch.equal(t, want)))
+    # hipGraph replay of the same call
+    t = torch.empty(8192 * 4, dtype=torch.bfloat16, device="cuda")
+    car.all_reduce(t)
+    s = torch.cuda.Stream(); s.wait_stream(torch.cuda.current_stream())
+    gr = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(gr, stream=s):
+            car.all_reduce(t)
+    torch.cuda.current_stream().wait_stream(s)
+    for it in range(3):
+        base = torch.randn(t.numel(), device="cuda", generator=g).bfloat16()
+        t.copy_(base * (rank + 1))
+        both = [base * 1, base * 2]
+        want = (both[0].float() + both[1].float()).bfloat16()
+        gr.replay(); torch.cuda.synchronize()
+        out["ok"].append(bool(torch.equal(t, want)))
+    out["healthy"] = car.healthy()
+    dist.barrier()
+    car.close()
+print("RESULT " + json.dumps(out), flush=True)
+dist.destroy_process_group()
+"""
+
+
+def test_custom_ar_two_processes_ipc(tmp_path):
+    """Two ranks on GPU 0 exchange real IPC handles (the TP setup path, minus xGMI)."""
+    script = tmp_path / "car_worker.py"
+    script.write_text(_WORKER)
+    env = dict(os.environ, ROOT=ROOT, MASTER_ADDR="127.0.0.1", MASTER_PORT="29581")
+    procs = [subprocess.Popen([sys.executable, "-u", str(script), str(r)], env=env, stdout=subprocess.PIPE,
+                              stderr=subprocess.STDOUT, text=True) for r in range(2)]
+    outs = []
+    for p in procs:
+        try:
+            o, _ = p.communicate(timeout=100)
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise
+        outs.append((p.returncode, o))
+    res = []
+    for rc, o in outs:
+        assert rc == 0, o[-3000:]
+        line = [ln for ln in o.splitlines() if ln.startswith("RESULT ")][-1]
+        res.append(json.loads(line[7:]))
+    for r in res:
+        assert r["created"], res
+        assert all(r["ok"]) and r["healthy"], r
