@@ -48,7 +48,7 @@ class TPGroup:
         """Concatenate `t` from every rank along a new leading dim: [size, *t.shape]."""
         if self.size == 1:
             return t.unsqueeze(0)
-        if t.device.type == "cpu":  # gloo: list form
+        if t.device.type == "cpu" or dist.get_backend(self.group) == "gloo":  # gloo: list form
             parts = [torch.empty_like(t) for _ in range(self.size)]
             dist.all_gather(parts, t.contiguous(), group=self.group)
             return torch.stack(parts)
@@ -95,8 +95,12 @@ def init_distributed(backend: Optional[str] = None, timeout_s: int = 600) -> tup
     return rank, world, local
 
 
-def new_tp_groups(tp_size: int) -> TPGroup:
-    """Split the world into contiguous TP groups of `tp_size`; return this rank's group."""
+def new_tp_groups(tp_size: int, custom_ar: Optional[bool] = None) -> TPGroup:
+    """Split the world into contiguous TP groups of `tp_size`; return this rank's group.
+
+    custom_ar: None = use the P2P all-reduce whenever the backend is RCCL; True = also
+    under gloo when a GPU is visible (the 1-GPU test that shares GPU 0 between ranks).
+    """
     if not dist.is_initialized() or tp_size <= 1:
         return TPGroup.single()
     world = dist.get_world_size()
@@ -110,7 +114,8 @@ def new_tp_groups(tp_size: int) -> TPGroup:
         cg = dist.new_group(ranks, backend="gloo") if gloo_needed else g
         if rank in ranks:
             mine = TPGroup(g, rank - start, tp_size, root=start, cpu_group=cg)
-    if dist.get_backend() == "nccl" and torch.cuda.is_available():
+    want = custom_ar if custom_ar is not None else dist.get_backend() == "nccl"
+    if want and torch.cuda.is_available():
         from pilottai_amd.parallel.custom_ar import CustomAllReduce
 
         dev = torch.device("cuda", torch.cuda.current_device())
