@@ -98,14 +98,16 @@ __device__ __forceinline__ void decode_item(
   for (int n = 0; n < 8; ++n) o[n] = f32x4{0.f, 0.f, 0.f, 0.f};
   float m_run = NEG_BIG, l_run = 0.f;
 
-  for (int t = t_first + wid; t < t_last; t += 4) {
+  // K/V fragments of one 32-key tile; the loop keeps the next tile's loads in flight
+  // while computing this one (small decode batches have too few workgroups to hide
+  // HBM latency by occupancy alone: 8 sequences x 8 KV heads x 2 partitions).
+  auto load_tile = [&](int t, bf16x8 (&kf)[2][4], bf16x8 (&vf)[8]) {
     const int b0 = min(2 * t, nblk - 1), b1 = min(2 * t + 1, nblk - 1);
     const int pb0 = bt[b0], pb1 = bt[b1];
     const int pk = (kin >= 16) ? pb1 : pb0;
     // dims 32m + 8g = chunk 4m + g; key (kin & 15) + 4c
     const bf16* kbase = k_cache + (size_t)pk * kv_stride_blk +
                         (((size_t)kvh * 16 + g) * ATT_BLK + (kin & 15)) * 8;
-    bf16x8 kf[2][4];
 #pragma unroll
     for (int c = 0; c < 2; ++c)
 #pragma unroll
@@ -114,10 +116,15 @@ __device__ __forceinline__ void decode_item(
     const int pv = (g >> 1) ? pb1 : pb0;
     const bf16* vbase =
         v_cache + (size_t)pv * kv_stride_blk + ((size_t)kvh * ATT_HD + col) * ATT_BLK + 8 * (g & 1);
-    bf16x8 vf[8];
 #pragma unroll
     for (int n = 0; n < 8; ++n)
       vf[n] = *reinterpret_cast<const bf16x8*>(vbase + (size_t)16 * n * ATT_BLK);
+  };
+  bf16x8 kf[2][4], vf[8];
+  if (t_first + wid < t_last) load_tile(t_first + wid, kf, vf);
+  for (int t = t_first + wid; t < t_last; t += 4) {
+    bf16x8 kn[2][4], vn[8];
+    if (t + 4 < t_last) load_tile(t + 4, kn, vn);
 
     f32x4 sc[2];
 #pragma unroll
@@ -161,6 +168,12 @@ __device__ __forceinline__ void decode_item(
       o[n] *= alpha;
       o[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf[n], pf, o[n], 0, 0, 0);
     }
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int m = 0; m < 4; ++m) kf[c][m] = kn[c][m];
+#pragma unroll
+    for (int n = 0; n < 8; ++n) vf[n] = vn[n];
   }
   l_run += __shfl_xor(l_run, 16, 64);
   l_run += __shfl_xor(l_run, 32, 64);

@@ -243,29 +243,25 @@ int32_t Scheduler::schedule(int32_t* buf) {
   const int32_t tpw = 16 / std::max(1, cfg_.gqa_group);
 
   int32_t T = 0, ns = 0, nsamp = 0, nit = 0, nparted = 0, pslot = 0;
-  // decode partition size: with few decode rows, smaller flash-decoding
-  // partitions give the attention launch enough workgroups to fill the chip
-  // (>= ~512 across the KV heads); the item list must still fit max_items
+  // decode partition size: with few decode rows, 256-key flash-decoding partitions
+  // give the attention launch more workgroups. 128-key partitions lose more to the
+  // extra partial merges than they gain (profiles/r1_attention_small_batch.jsonl:
+  // 8 rows x ctx 1000: 13.8 us at 128, 10.9 at 256, 11.2 at 512; 16 rows: 24.2 /
+  // 17.7 / 18.5). The item list must still fit max_items.
   int32_t psz = 512;
   if (cfg_.split_decode) {
-    int64_t parts[3] = {0, 0, 0};  // partition sizes 512, 256, 128
-    int64_t nprefill = 0;
+    int64_t parts512 = 0, parts256 = 0, nprefill = 0;
     for (const Planned& p : last_plan_) {
       const int32_t c = p.s->num_computed + p.n;
       if (p.n <= tpw) {
-        parts[0] += std::max(1, (c + 511) / 512);
-        parts[1] += std::max(1, (c + 255) / 256);
-        parts[2] += std::max(1, (c + 127) / 128);
+        parts512 += std::max(1, (c + 511) / 512);
+        parts256 += std::max(1, (c + 255) / 256);
       } else {
         nprefill += (p.n + 31) / 32 + 1;
       }
     }
     const int64_t kv = std::max(1, cfg_.kv_heads), target = 512;
-    if (parts[0] * kv < target) {
-      psz = parts[1] * kv < target ? 128 : 256;
-      const int64_t need = nprefill + (psz == 128 ? parts[2] : parts[1]);
-      if (need > L.max_items) psz = 512;
-    }
+    if (parts512 * kv < target && nprefill + parts256 <= L.max_items) psz = 256;
   }
   buf[L.part_size] = psz;
 
