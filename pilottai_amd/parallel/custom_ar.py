@@ -20,6 +20,7 @@ so it is captured into the engine's hipGraphs like any other kernel.
 """
 from __future__ import annotations
 
+import contextlib
 import logging
 import os
 from typing import List, Optional
@@ -70,8 +71,12 @@ class CustomAllReduce:
             return None
         C = _native()
         own, handle, err = 0, b"", ""
+
+        def on_device():
+            return torch.cuda.device(device) if device.type == "cuda" else contextlib.nullcontext()
+
         try:
-            with torch.cuda.device(device):
+            with on_device():
                 own, handle = C.car_alloc(cls.buffer_bytes(cap_bytes))
         except Exception as e:  # noqa: BLE001 - reported collectively below
             err = str(e)
@@ -82,7 +87,7 @@ class CustomAllReduce:
         ok = 1 if own else 0
         if ok:
             try:
-                with torch.cuda.device(device):
+                with on_device():
                     for i, h in enumerate(handles):
                         if i == rank:
                             bases.append(own)
