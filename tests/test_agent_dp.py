@@ -1,8 +1,9 @@
-"""Agent-DP global load view over 2 gloo ranks."""
+"""Agent-DP global load view over 2 and 4 gloo ranks (§4.4 world-size parametrisation)."""
 import json
 import os
 import socket
 
+import pytest
 import torch.multiprocessing as mp
 
 from pilottai_amd.parallel.agent_dp import shard_workers
@@ -39,9 +40,12 @@ def _worker(rank, world, port, out):
     torch.distributed.destroy_process_group()
 
 
-def test_global_load_view_two_ranks(tmp_path):
+@pytest.mark.parametrize("world", [2, 4])
+def test_global_load_view_ranks(tmp_path, world):
     out = str(tmp_path / "load")
-    mp.start_processes(_worker, args=(2, _port(), out), nprocs=2, join=True, start_method="spawn")
-    r0, r1 = (json.load(open(f"{out}.{r}")) for r in range(2))
-    assert r0 == r1
-    assert r0["least"] == 1 and r0["totals"]["queue_size"] == 6.0 and len(r0["table"]) == 2
+    mp.start_processes(_worker, args=(world, _port(), out), nprocs=world, join=True, start_method="spawn")
+    res = [json.load(open(f"{out}.{r}")) for r in range(world)]
+    assert all(r == res[0] for r in res)  # every rank holds the same global view
+    # queue sizes 5 - 4r: the last rank has the smallest (most negative) load
+    assert res[0]["least"] == world - 1 and len(res[0]["table"]) == world
+    assert res[0]["totals"]["queue_size"] == sum(5.0 - 4 * r for r in range(world))
