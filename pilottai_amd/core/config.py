@@ -95,6 +95,7 @@ class LLMConfig(BaseModel):
     timeout: float = Field(default=30.0, gt=0)
     max_rpm: Optional[int] = Field(default=None, gt=0)
     max_concurrent: Optional[int] = Field(default=None, gt=0)
+    base_url: Optional[str] = None  # provider "openai": an OpenAI-compatible endpoint (serving/http_server.py)
 
     @field_validator("api_key", mode="before")
     @classmethod

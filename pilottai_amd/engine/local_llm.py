@@ -208,7 +208,8 @@ class LocalLLM(BaseLLM):
 
         rf = response_format or {}
         temp = float(rf.get("temperature", self.temperature))
-        rid = self.engine.submit(ids, done, temperature=temp, max_tokens=self.max_tokens, grammar=grammar,
+        rid = self.engine.submit(ids, done, temperature=temp, max_tokens=int(rf.get("max_tokens", self.max_tokens)),
+                                 grammar=grammar,
                                  seed=rf.get("seed"), top_k=int(rf.get("top_k", self.top_k)),
                                  top_p=float(rf.get("top_p", self.top_p)))
         try:
@@ -319,11 +320,16 @@ class SchemaLLM(BaseLLM):
 
 
 def make_llm(config: Union[Dict[str, Any], Any, None] = None, engine=None) -> BaseLLM:
-    """LLM factory keyed by provider: "local" (MI355X engine, default) or "schema"."""
+    """LLM factory keyed by provider: "local" (MI355X engine, default), "schema" (model-free),
+    or "openai" (any OpenAI-compatible endpoint, e.g. a remote pilottai_amd server)."""
     provider = str(_cfg_get(config, "provider", "local")).lower()
     if provider in ("schema", "fake", "mock"):
         return SchemaLLM(config)
     if provider in ("local", "pilottai", "amd", "rocm", "mi355x"):
         return LocalLLM(config, engine=engine)
-    raise ValueError(f"unsupported LLM provider {provider!r}: this framework serves models on-node "
-                     "(provider='local'); remote providers are not available")
+    if provider in ("openai", "http", "openai_compat", "remote"):
+        from .http_llm import OpenAICompatLLM
+
+        return OpenAICompatLLM(config)
+    raise ValueError(f"unsupported LLM provider {provider!r}: use 'local' (on-node engine), 'schema' "
+                     "or 'openai' (an OpenAI-compatible endpoint with base_url)")

@@ -282,6 +282,7 @@ def test_a39_no_asyncio_timeout():
 # #40 every third-party top-level import of the package is a declared dependency (or optional/gated)
 def test_a40_imports_are_declared():
     declared = {"torch", "pydantic", "yaml", "numpy", "psutil", "safetensors",  # [project] deps + extras
+                "fastapi", "uvicorn", "httpx",                                # extra "serve"
                 "pybind11"}                                                   # [build-system] requires
     stdlib = set(sys.stdlib_module_names)
     seen = set()
