@@ -40,7 +40,7 @@ struct WgArgs {
   const bf16* resid;
   float* ws;      // split-K slabs [groups][S][16*MT][cols per group] fp32
   int* counters;  // [groups], zero between launches
-  int M, N, K, ldx, ldy, ldr, S, per;  // per = k-steps per slice (multiple of 2)
+  int M, N, K, ldx, ldy, ldr, S, per;  // per = k-steps per slice (multiple of the chunk's k-steps)
   float eps;                           // NORM: rows scaled by rsqrt(mean(x^2) + eps)
 };
 
@@ -53,10 +53,14 @@ template <int MT, int NTW, int WAVES, int EPI, bool NORM>
 __global__ __launch_bounds__(WAVES * 64) void wide_gemm_kernel(const WgArgs A) {
   constexpr int NTH = WAVES * 64;
   constexpr int ROWS = MT * 16;
-  constexpr int XU = ROWS * 8;                   // 16-B units of one x chunk (64 k per row)
+  // k-steps (32 k) per chunk = per barrier: 4 from M = 64 up, where the per-chunk barrier and
+  // x staging, not the weight stream, set the pace; the register ring holds the same bytes
+  constexpr int KC = MT >= 4 ? 4 : 2;
+  constexpr int UPR = 4 * KC;                    // 16-B units per row of one x chunk
+  constexpr int XU = ROWS * UPR;                 // 16-B units of one x chunk
   constexpr int XPT = (XU + NTH - 1) / NTH;      // units per thread
   constexpr int TPG = WAVES * NTW;               // tiles per column group
-  __shared__ __attribute__((aligned(16))) bf16x8 xs[2][ROWS][8];  // the only LDS object (guide §5 trap 4a)
+  __shared__ __attribute__((aligned(16))) bf16x8 xs[2][ROWS][UPR];  // the only LDS object (guide §5 trap 4a)
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int g = lane >> 4, c = lane & 15;
   const int M = A.M, K = A.K, S = A.S;
@@ -67,7 +71,7 @@ __global__ __launch_bounds__(WAVES * 64) void wide_gemm_kernel(const WgArgs A) {
   const int s = work / G, grp = work % G;
   const int KS = K / 32;
   const int ks0 = min(KS, s * A.per), ks1 = min(KS, ks0 + A.per);
-  const int nch = (ks1 - ks0) / 2;  // chunks of 2 k-steps (K % 64 == 0, per even)
+  const int nch = (ks1 - ks0) / KC;  // chunks of KC k-steps (host: K and per multiples of 32 * KC)
 
   f32x4 acc[MT][NTW];
 #pragma unroll
@@ -86,16 +90,16 @@ __global__ __launch_bounds__(WAVES * 64) void wide_gemm_kernel(const WgArgs A) {
   // x staging: unit u -> (row u>>3, 16-B unit u&7) of a 64-k chunk. Chunk k of x and
   // of W lives in ring slot k % D (registers), D chunks in flight; the LDS image is
   // double-buffered and written one chunk ahead of its use.
-  constexpr int D = 4;
+  constexpr int D = 8 / KC;
   bf16x8 xring[D][XPT];
-  bf16x8 wring[D][2][NTW];
+  bf16x8 wring[D][KC][NTW];
   auto load_x = [&](int ch, bf16x8 (&dst)[XPT]) {
-    const int k0 = (ks0 + 2 * ch) * 32;
+    const int k0 = (ks0 + KC * ch) * 32;
 #pragma unroll
     for (int i = 0; i < XPT; ++i) {
       const int u = threadIdx.x + i * NTH;
       if (XU % NTH == 0 || u < XU) {
-        const int row = u >> 3, unit = u & 7;
+        const int row = u / UPR, unit = u % UPR;
         const int rsrc = row < M ? row : 0;
         dst[i] = *reinterpret_cast<const bf16x8*>(A.x + (size_t)rsrc * A.ldx + k0 + unit * 8);
       }
@@ -106,16 +110,16 @@ __global__ __launch_bounds__(WAVES * 64) void wide_gemm_kernel(const WgArgs A) {
     for (int i = 0; i < XPT; ++i) {
       const int u = threadIdx.x + i * NTH;
       if (XU % NTH == 0 || u < XU) {
-        const int row = u >> 3, unit = u & 7;
+        const int row = u / UPR, unit = u % UPR;
         xs[buf][row][unit ^ (row & 7)] = src[i];
       }
     }
   };
-  auto load_w = [&](int ch, bf16x8 (&dst)[2][NTW]) {
+  auto load_w = [&](int ch, bf16x8 (&dst)[KC][NTW]) {
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
+    for (int kk = 0; kk < KC; ++kk)
 #pragma unroll
-      for (int j = 0; j < NTW; ++j) dst[kk][j] = wsrc[j][(size_t)(ks0 + 2 * ch + kk) * 64];
+      for (int j = 0; j < NTW; ++j) dst[kk][j] = wsrc[j][(size_t)(ks0 + KC * ch + kk) * 64];
   };
 
 #pragma unroll
@@ -136,14 +140,14 @@ __global__ __launch_bounds__(WAVES * 64) void wide_gemm_kernel(const WgArgs A) {
       const int ch = cb + sub;
       if (ch >= nch) break;
       const int buf = ch & 1;
-      bf16x8 wcur[2][NTW];
+      bf16x8 wcur[KC][NTW];
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk)
+      for (int kk = 0; kk < KC; ++kk)
 #pragma unroll
         for (int j = 0; j < NTW; ++j) wcur[kk][j] = wring[sub][kk][j];
       if (ch + D < nch) load_w(ch + D, wring[sub]);
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
+      for (int kk = 0; kk < KC; ++kk) {
 #pragma unroll
         for (int i = 0; i < MT; ++i) {
           const int row = 16 * i + c;
@@ -383,16 +387,18 @@ extern "C" int pa_wide_gemm(void* y, const void* x, const void* wp, const void* 
   const int G = N / 16 / TPG;
   const int MT = (M + 15) / 16;
   const int MTp = MT <= 2 ? 2 : (MT <= 4 ? 4 : 8);
+  const int KC = MTp >= 4 ? 4 : 2;  // k-steps per chunk (kernel constexpr)
+  if ((K / 32) % KC) return 1;
   auto ws_need = [&](int s_) { return (long long)G * s_ * MTp * 16 * (TPG * 16 + 1); };
   const int KS = K / 32;
-  S = std::max(1, std::min(S, KS / 2));
+  S = std::max(1, std::min(S, KS / KC));
   int per = (KS + S - 1) / S;
-  per = (per + 1) / 2 * 2;
+  per = (per + KC - 1) / KC * KC;
   S = (KS + per - 1) / per;  // no empty slices
   if (S > 1 && splits <= 0) {  // default split: shrink to the workspace
     while (S > 1 && ws_need(S) > ws_floats) {
       --S;
-      per = ((KS + S - 1) / S + 1) / 2 * 2;
+      per = ((KS + S - 1) / S + KC - 1) / KC * KC;
       S = (KS + per - 1) / per;
     }
   }

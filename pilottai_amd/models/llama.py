@@ -123,7 +123,7 @@ class LlamaModel:
     DECODE_FUSED_MAX_T = 16
     # steps of up to this many tokens (above DECODE_FUSED_MAX_T) run the packed-weight
     # small-batch kernels (csrc/ops/gemm_wide.hip; tools/wide_gemm_bench.py)
-    WIDE_MAX_T = 32
+    WIDE_MAX_T = 48  # measured: the packed path wins the 48-token bucket, loses at 64 (BENCHMARKS.md)
 
     def __init__(self, cfg: LlamaConfig, device, dtype=torch.bfloat16, tp: Optional[TPGroup] = None,
                  seed: int = 0, weights_path: Optional[str] = None, decode_pack: Optional[bool] = None):
