@@ -13,7 +13,7 @@
 //     narrow projections are split over K so the grid fills 256 CUs; the split-K
 //     partials go to fp32 slabs (write-through sc1 stores) and the last slice to
 //     arrive (agent-scope ticket, self-resetting) reduces them — one launch;
-//   * x is staged once per workgroup through LDS in FULL 128-B lines (64 k per row
+//   * x is staged once per workgroup through LDS in FULL 128-B lines (128 k per row
 //     per chunk, two chunks in flight, 16-B units XOR-swizzled by row so the
 //     16-row A-fragment reads are conflict-free), and shared by all waves — the
 //     fragment-shaped direct loads cost twice the load-path work (guide §5) and
@@ -53,9 +53,11 @@ template <int MT, int NTW, int WAVES, int EPI, bool NORM>
 __global__ __launch_bounds__(WAVES * 64) void wide_gemm_kernel(const WgArgs A) {
   constexpr int NTH = WAVES * 64;
   constexpr int ROWS = MT * 16;
-  // k-steps (32 k) per chunk = per barrier: 4 from M = 64 up, where the per-chunk barrier and
-  // x staging, not the weight stream, set the pace; the register ring holds the same bytes
-  constexpr int KC = MT >= 4 ? 4 : 2;
+  // k-steps (32 k) per chunk = per barrier. The per-chunk barrier and x staging set the
+  // pace (not LDS bandwidth: profiles/r1_wide_gemm_wavegrid_rejected.jsonl); 4 k-steps (128 k)
+  // beat 2 at every M and 8 (profiles/r1_wide_gemm_chunks.jsonl). The register ring holds
+  // D * KC = 8 k-steps of weights in flight either way.
+  constexpr int KC = 4;
   constexpr int UPR = 4 * KC;                    // 16-B units per row of one x chunk
   constexpr int XU = ROWS * UPR;                 // 16-B units of one x chunk
   constexpr int XPT = (XU + NTH - 1) / NTH;      // units per thread
@@ -387,7 +389,7 @@ extern "C" int pa_wide_gemm(void* y, const void* x, const void* wp, const void* 
   const int G = N / 16 / TPG;
   const int MT = (M + 15) / 16;
   const int MTp = MT <= 2 ? 2 : (MT <= 4 ? 4 : 8);
-  const int KC = MTp >= 4 ? 4 : 2;  // k-steps per chunk (kernel constexpr)
+  const int KC = 4;  // k-steps per chunk (kernel constexpr)
   if ((K / 32) % KC) return 1;
   auto ws_need = [&](int s_) { return (long long)G * s_ * MTp * 16 * (TPG * 16 + 1); };
   const int KS = K / 32;
