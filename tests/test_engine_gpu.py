@@ -69,3 +69,53 @@ def test_sampling_batch_invariance(engine):
     alone = engine.generate([p], temperature=0.8, max_tokens=10, ignore_eos=True, seed=1234)[0]
     crowd = engine.generate([p] + others, temperature=0.8, max_tokens=10, ignore_eos=True, seed=1234)[0]
     assert alone.token_ids == crowd.token_ids
+
+
+def test_http_server_on_gpu_engine(engine):
+    """The OpenAI-compatible server in front of the GPU engine (hipGraph steps): concurrent
+    clients get grammar-constrained replies, and /health reports the engine's counters."""
+    import asyncio
+    import socket
+    import threading
+    import time
+
+    import uvicorn
+
+    from pilottai_amd.core.config import LLMConfig
+    from pilottai_amd.engine.local_llm import LocalLLM, make_llm
+    from pilottai_amd.serving.http_server import create_app
+
+    engine.start()
+    backend = LocalLLM(LLMConfig(model_name="tiny-gqa4", max_tokens=64), engine=engine)
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    server = uvicorn.Server(uvicorn.Config(create_app(backend, "tiny-gqa4", engine=engine), host="127.0.0.1",
+                                           port=port, log_level="error"))
+    th = threading.Thread(target=server.run, daemon=True)
+    th.start()
+    t0 = time.time()
+    while not server.started:
+        assert time.time() - t0 < 30
+        time.sleep(0.05)
+    url = f"http://127.0.0.1:{port}/v1"
+
+    async def go():
+        llm = make_llm(LLMConfig(provider="openai", base_url=url, model_name="tiny-gqa4", retry_attempts=1,
+                                 timeout=60))
+        rs = await asyncio.gather(*(llm.generate_response(
+            [{"role": "user", "content": f"evaluate result {i}"}],
+            response_format={"schema": "orchestrator.result_evaluation"}) for i in range(6)))
+        h = (await llm._http().get(url.replace("/v1", "/health"))).json()
+        await llm.aclose()
+        return rs, h
+
+    try:
+        rs, h = asyncio.run(go())
+    finally:
+        server.should_exit = True
+        th.join(timeout=10)
+    for r in rs:
+        assert set(json.loads(r["content"])) == {"success", "quality", "requires_retry"}
+    assert h["status"] == "ok" and h["engine"]
