@@ -365,11 +365,19 @@ class LlamaModel:
                 self.tp.all_reduce(d)
                 h.add_(d)
             else:
-                ops.decode_gemm(a, L["w2_p"], "resid", resid=h, out=h)
+                ops.decode_gemm(a, L["w2_p"], "resid", resid=h, out=h, **self._down_cfg(T))
         rows = meta.logit_rows[:num_logit_rows]
         rows = rows.long() if self.device.type == "cpu" else rows
         xs = ops.rmsnorm(h.index_select(0, rows), self.norm, eps)
         return ops.decode_gemm(xs, self.lm_head_p, "plain")
+
+    @staticmethod
+    def _down_cfg(T: int) -> dict:
+        """down_proj config for 9-16-row decode steps: 2 column tiles x 16 waves x 2 K-slices
+        (sc1 slabs + last-arriver reduce). Measured end to end: 16-token decode steps
+        4.16 -> 4.04 ms (16 workers) and 4.09 -> 3.97 ms (8 workers); the 8-row steps keep
+        the unsplit default (BENCHMARKS.md)."""
+        return {"nt": 2, "waves": 16, "splits": 2} if T > 8 else {}
 
     def _forward_wide(self, meta: StepMeta, kv: KVCache, T: int, num_logit_rows: int,
                       part_o: torch.Tensor, part_ml: torch.Tensor) -> torch.Tensor:
