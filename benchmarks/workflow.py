@@ -40,6 +40,11 @@ def parse():
     ap.add_argument("--kv-gb", type=float, default=40.0)
     ap.add_argument("--no-fault", action="store_true")
     ap.add_argument("--cpu", action="store_true")
+    ap.add_argument("--max-batched-tokens", type=int, default=2048)
+    ap.add_argument("--no-graphs", action="store_true", help="eager steps (required with --share-gpu)")
+    ap.add_argument("--share-gpu", action="store_true",
+                    help="1-GPU rehearsal of TP=N: every rank on GPU 0, gloo control plane "
+                         "(PILOTTAI_DIST_BACKEND=gloo), TP all-reduces through the custom P2P kernel")
     return ap.parse_args()
 
 
@@ -87,12 +92,19 @@ async def drive(a, engine):
         per = [total // a.clients + (1 if i < total % a.clients else 0) for i in range(a.clients)]
         await asyncio.gather(*(client(i, per[i], rec) for i in range(a.clients)))
 
+    async def progress():  # long rehearsals must show life (one line per 30 s)
+        while True:
+            await asyncio.sleep(30)
+            print(f"[workflow] done={done['n']} engine_steps={engine.stats['steps']}", file=sys.stderr, flush=True)
+
+    prog = asyncio.ensure_future(progress())
     await round_(a.warmup, False)
     st0, u0 = dict(engine.stats), dict(llm.usage)
     t0 = time.perf_counter()
     await round_(a.workflows, True)
     dt = time.perf_counter() - t0
     st1, u1 = dict(engine.stats), dict(llm.usage)
+    prog.cancel()
     await asyncio.sleep(1.5)  # let FaultTolerance finish a replacement started at the very end
     ftm = ft.get_health_metrics()
     await ft.stop()
@@ -130,19 +142,27 @@ def main():
     from pilottai_amd.parallel import comm
 
     rank, world, local = comm.init_distributed()
-    tp = comm.new_tp_groups(world)
+    if a.share_gpu:
+        # gloo cannot carry >8 MiB GPU all-reduces quickly nor be graph-captured: keep every
+        # row-parallel message on the custom kernel (tokens x hidden x 2 B <= 8 MiB) and run eagerly
+        a.no_graphs = True
+        a.max_batched_tokens = min(a.max_batched_tokens, 256)
+    tp = comm.new_tp_groups(world, custom_ar=True if a.share_gpu else None)
     if a.cpu or not torch.cuda.is_available():
         a.cpu = True
         device = torch.device("cpu")
-        model = "tiny"
+        model = "tiny" if world == 1 else "tiny-gqa4"  # TP needs heads divisible by the TP size
     else:
-        torch.cuda.set_device(local)
-        device = torch.device("cuda", local)
+        dev_idx = 0 if a.share_gpu else local
+        torch.cuda.set_device(dev_idx)
+        device = torch.device("cuda", dev_idx)
         model = a.model
     t0 = time.time()
-    eng = LLMEngine(EngineConfig(model=model, max_num_seqs=max(64, 4 * a.clients), max_num_batched_tokens=2048,
+    mbt = a.max_batched_tokens
+    buckets = [b for b in (8, 16, 32, 64, 128, 256, 512, 768, 1024, 1536, 2048) if b < mbt] + [mbt]
+    eng = LLMEngine(EngineConfig(model=model, max_num_seqs=max(64, 4 * a.clients), max_num_batched_tokens=mbt,
                                  kv_cache_gb=None if a.cpu else a.kv_gb, num_kv_blocks=4096 if a.cpu else None,
-                                 token_buckets=[8, 16, 32, 64, 128, 256, 512, 768, 1024, 1536, 2048]),
+                                 token_buckets=buckets, use_graphs=not a.no_graphs),
                     device=device, tp=tp)
     init_s = time.time() - t0
     if tp.rank != 0:
