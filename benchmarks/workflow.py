@@ -162,7 +162,9 @@ def main():
     buckets = [b for b in (8, 16, 32, 64, 128, 256, 512, 768, 1024, 1536, 2048) if b < mbt] + [mbt]
     eng = LLMEngine(EngineConfig(model=model, max_num_seqs=max(64, 4 * a.clients), max_num_batched_tokens=mbt,
                                  kv_cache_gb=None if a.cpu else a.kv_gb, num_kv_blocks=4096 if a.cpu else None,
-                                 token_buckets=buckets, use_graphs=not a.no_graphs),
+                                 token_buckets=buckets, use_graphs=not a.no_graphs,
+                                 # 8 ranks x 2 copies of 17.6 GB do not fit one card: no packed copy
+                                 decode_fused=False if a.share_gpu else None),
                     device=device, tp=tp)
     init_s = time.time() - t0
     if tp.rank != 0:
