@@ -465,11 +465,17 @@ __global__ __launch_bounds__(256, 2) void paged_attn_kernel(
     const int* __restrict__ block_table, int max_blocks, int H, int KV, float scale_log2) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int TPW = 16 / G;
+  // The first item is loaded together with the item count, not after it: one dependent
+  // memory round trip less before the K/V stream starts (decode steps with few rows are
+  // latency-bound). In bounds: the host sizes the grid to gridDim.x <= max_items, the
+  // length of `items`.
+  int4 it_next = items[blockIdx.x];
   const int n = n_items[0];
   const int psz = part_size ? part_size[0] : ATT_PART;  // decode partition (keys), per step
   const int kvh = blockIdx.y;
   for (int item = blockIdx.x; item < n; item += gridDim.x) {
-    const int4 it = items[item];
+    const int4 it = it_next;
+    if (item + (int)gridDim.x < n) it_next = items[item + gridDim.x];
     if ((it.z & 0xff) <= TPW)
       decode_item<G>(it, smem, out, part_o, part_ml, counters, q, k_cache, v_cache, q_start, q_len, ctx_len,
                      block_table, max_blocks, H, KV, kvh, scale_log2, psz);
