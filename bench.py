@@ -61,6 +61,8 @@ def parse():
                     help="largest step on the fused packed-weight decode path (default: the model's)")
     ap.add_argument("--wide-max-t", type=int, default=None,
                     help="largest step on the packed small-batch path (default: the model's)")
+    ap.add_argument("--mid-max-t", type=int, default=None,
+                    help="largest step on the LDS-DMA tiled mid-size path (default: the model's; 0 = off)")
     ap.add_argument("--token-align", type=int, default=256, help="GEMM-friendly step sizes (0 = off)")
     ap.add_argument("--align-slack", type=int, default=96)
     ap.add_argument("--cpu", action="store_true", help="tiny model on CPU (plumbing smoke only)")
@@ -92,7 +94,8 @@ async def run_rank(a, rank: int, world: int, device):
                                  max_num_batched_tokens=a.max_batched_tokens, kv_cache_gb=a.kv_gb if not a.cpu else None,
                                  num_kv_blocks=4096 if a.cpu else None, seed=1234 + rank,
                                  token_align=a.token_align, align_slack=a.align_slack,
-                                 decode_fused_max_t=a.fused_max_t, wide_max_t=a.wide_max_t), device=device)
+                                 decode_fused_max_t=a.fused_max_t, wide_max_t=a.wide_max_t,
+                                 mid_max_t=a.mid_max_t), device=device)
     register_engine(eng.model_cfg.name, eng)
     eng.start()
     llm = LocalLLM(LLMConfig(model_name=eng.model_cfg.name, temperature=a.temperature, max_tokens=1024,
@@ -167,15 +170,33 @@ async def run_rank(a, rank: int, world: int, device):
     return local
 
 
+def _launch_ranks(n: int) -> int:
+    """`bench.py --gpus N` (N > 1) started without a launcher: run N rank processes under
+    torch.distributed.run as a CHILD process (nothing here has touched the GPU; never exec)
+    and return its exit code, so the run can never silently measure one rank."""
+    import socket
+    import subprocess
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__), *sys.argv[1:]]
+    print(f"[bench] --gpus {n} without a launcher: starting {n} ranks: {' '.join(cmd)}", file=sys.stderr, flush=True)
+    return subprocess.call(cmd)
+
+
 def main():
     a = parse()
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(_launch_ranks(a.gpus))
     import torch
 
     from pilottai_amd.parallel import comm
 
     rank, world, local_rank = comm.init_distributed()
-    if world != a.gpus and world > 1:
-        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
+    if world != a.gpus:
+        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}: launch one rank per GPU")
     if a.cpu or not torch.cuda.is_available():
         device = torch.device("cpu")
         a.cpu = True

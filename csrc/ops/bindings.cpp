@@ -40,6 +40,14 @@ int pa_decode_qkv_rope(const void* x, const void* wp, int M, int N, int K, int l
 int pa_wide_gemm(void* y, const void* x, const void* wp, const void* resid, float* ws, long long ws_floats,
                  int* counters, int n_counters, int M, int N, int K, int ldx, int ldy, int ldr, int epi, int norm,
                  float eps, int ntw, int waves, int splits, hipStream_t st);
+int pa_mid_gemm_plan(int M, int N, int K, int epi, int* fm, int* fn, int* S);
+long long pa_mid_gemm_ws_floats(int M, int N, int K, int fm, int fn, int S);
+int pa_mid_gemm(void* y, const void* x, const void* wp, const void* resid, float* ws, long long ws_floats,
+                int* counters, int n_counters, int M, int N, int K, int ldx, int ldy, int ldr, int epi,
+                const float* ss_in, float* ss_out, float* ss_zero, float eps, int fm, int fn, int splits,
+                void* q_out, void* k_cache, void* v_cache, const int* positions, const int* slots,
+                const float* cos_sin, int H, int KV, hipStream_t st);
+int pa_row_sumsq(float* out, const void* x, int M, int K, int ldx, hipStream_t st);
 long long pa_cosine_topk_workspace_bytes(int Q, int N, int K);
 int pa_cosine_topk(float* out_scores, int* out_rows, void* workspace, const void* queries,
                    const void* index, int Q, int N, int D, int K, const int* row_priority,
@@ -299,6 +307,107 @@ bool wide_gemm(at::Tensor y, at::Tensor x, at::Tensor wp, c10::optional<at::Tens
   return rc == 0;
 }
 
+const float* opt_rows(const c10::optional<at::Tensor>& t, int M, const char* name) {
+  if (!t.has_value()) return nullptr;
+  check_gpu(*t, name);
+  check_dtype(*t, at::kFloat, name);
+  TORCH_CHECK(t->numel() >= M, name, " must hold >= M floats");
+  return t->data_ptr<float>();
+}
+
+// y = epi(rowscale(x) . W^T) for mid-size token counts on packed weights (csrc/ops/gemm_mid.hip).
+// epi 0 plain, 1 silu(gate)*up (y has N/2 columns), 2 resid + acc, 3 plain with the RoPE tile
+// permutation undone. ss_in: [M] fp32 row sums of x^2 -> rows scaled by rsqrt(ss/K + eps) (the
+// RMSNorm weight folded into W). ss_out (epi 2): [M] += row sums of y^2. ss_zero: [M] zeroed.
+// Returns false if the shape/config is not handled.
+bool mid_gemm(at::Tensor y, at::Tensor x, at::Tensor wp, c10::optional<at::Tensor> resid, at::Tensor ws,
+              at::Tensor counters, int64_t epi, c10::optional<at::Tensor> ss_in, c10::optional<at::Tensor> ss_out,
+              c10::optional<at::Tensor> ss_zero, double eps, int64_t fm, int64_t fn, int64_t splits) {
+  check_gpu(wp, "wp"); check_gpu(ws, "ws"); check_gpu(counters, "counters");
+  TORCH_CHECK(x.is_cuda() && x.dim() == 2 && x.stride(1) == 1, "x must be a 2-D GPU tensor, unit inner stride");
+  TORCH_CHECK(y.is_cuda() && y.dim() == 2 && y.stride(1) == 1, "y must be a 2-D GPU tensor, unit inner stride");
+  check_dtype(x, at::kBFloat16, "x"); check_dtype(wp, at::kBFloat16, "wp"); check_dtype(y, at::kBFloat16, "y");
+  check_dtype(ws, at::kFloat, "ws"); check_dtype(counters, at::kInt, "counters");
+  TORCH_CHECK(epi >= 0 && epi <= 3, "mid_gemm epi must be 0..3 (RoPE + KV write: mid_qkv_rope)");
+  TORCH_CHECK(wp.dim() == 4 && wp.size(2) == 64 && wp.size(3) == 8, "wp must be packed [N/16, K/32, 64, 8]");
+  const int M = x.size(0), K = x.size(1), N = wp.size(0) * 16;
+  TORCH_CHECK(wp.size(1) * 32 == K, "packed weight K mismatch");
+  TORCH_CHECK(x.stride(0) % 8 == 0 && y.stride(0) % 4 == 0, "x rows must be 16-byte, y rows 8-byte aligned");
+  const int NO = epi == 1 ? N / 2 : N;
+  TORCH_CHECK(y.size(0) == M && y.size(1) == NO, "y shape mismatch");
+  const void* rp = nullptr;
+  int ldr = 0;
+  if (epi == 2) {
+    TORCH_CHECK(resid.has_value(), "epi=2 needs resid");
+    const auto& r = *resid;
+    TORCH_CHECK(r.is_cuda() && r.dim() == 2 && r.stride(1) == 1 && r.size(0) == M && r.size(1) == N &&
+                    r.stride(0) % 4 == 0,
+                "resid must be [M, N] with unit inner stride");
+    check_dtype(r, at::kBFloat16, "resid");
+    rp = r.data_ptr();
+    ldr = r.stride(0);
+  }
+  const int rc = pa_mid_gemm(y.data_ptr(), x.data_ptr(), wp.data_ptr(), rp, ws.data_ptr<float>(), ws.numel(),
+                             counters.data_ptr<int>(), counters.numel(), M, N, K, x.stride(0), y.stride(0), ldr,
+                             (int)epi, opt_rows(ss_in, M, "ss_in"), const_cast<float*>(opt_rows(ss_out, M, "ss_out")),
+                             const_cast<float*>(opt_rows(ss_zero, M, "ss_zero")), (float)eps, (int)fm, (int)fn,
+                             (int)splits, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0, cur_stream());
+  TORCH_CHECK(rc >= 0, "mid_gemm launch failed");
+  return rc == 0;
+}
+
+// Mid-size QKV projection (RMSNorm folded into the rope-packed weights, row statistics
+// ss_in) with RoPE and the paged KV write in the epilogue (csrc/ops/gemm_mid.hip, EP_ROPEKV).
+bool mid_qkv_rope(at::Tensor x, at::Tensor wp, at::Tensor ss_in, double eps, at::Tensor q_out, at::Tensor k_cache,
+                  at::Tensor v_cache, at::Tensor positions, at::Tensor slots, at::Tensor cos_sin, int64_t H,
+                  int64_t KV, at::Tensor ws, at::Tensor counters, int64_t fm, int64_t fn, int64_t splits) {
+  check_gpu(wp, "wp"); check_gpu(q_out, "q_out"); check_gpu(k_cache, "k_cache"); check_gpu(v_cache, "v_cache");
+  check_gpu(positions, "positions"); check_gpu(slots, "slots"); check_gpu(cos_sin, "cos_sin");
+  check_gpu(ws, "ws"); check_gpu(counters, "counters");
+  TORCH_CHECK(x.is_cuda() && x.dim() == 2 && x.stride(1) == 1, "x must be a 2-D GPU tensor, unit inner stride");
+  check_dtype(x, at::kBFloat16, "x"); check_dtype(wp, at::kBFloat16, "wp"); check_dtype(q_out, at::kBFloat16, "q_out");
+  check_dtype(k_cache, at::kBFloat16, "k_cache"); check_dtype(v_cache, at::kBFloat16, "v_cache");
+  check_dtype(positions, at::kInt, "positions"); check_dtype(slots, at::kInt, "slots");
+  check_dtype(cos_sin, at::kFloat, "cos_sin");
+  check_dtype(ws, at::kFloat, "ws"); check_dtype(counters, at::kInt, "counters");
+  TORCH_CHECK(wp.dim() == 4 && wp.size(2) == 64 && wp.size(3) == 8, "wp must be packed [N/16, K/32, 64, 8]");
+  const int M = x.size(0), K = x.size(1), N = wp.size(0) * 16;
+  TORCH_CHECK(wp.size(1) * 32 == K, "packed weight K mismatch");
+  TORCH_CHECK(x.stride(0) % 8 == 0, "x rows must be 16-byte aligned");
+  TORCH_CHECK(N == (H + 2 * KV) * 128, "packed QKV has ", N, " columns, expected (H + 2 KV) * 128");
+  TORCH_CHECK(q_out.numel() >= (int64_t)M * H * 128, "q_out too small");
+  TORCH_CHECK(positions.numel() >= M && slots.numel() >= M, "positions/slots shorter than x");
+  TORCH_CHECK(cos_sin.dim() == 2 && cos_sin.size(1) == 128, "cos_sin must be [max_pos, 128]");
+  TORCH_CHECK(k_cache.dim() == 5 && k_cache.size(1) == KV && k_cache.size(2) == 16 && k_cache.size(3) == 16 &&
+                  k_cache.size(4) == 8, "k_cache must be [NB, KV, 16, 16, 8]");
+  TORCH_CHECK(v_cache.dim() == 4 && v_cache.size(1) == KV && v_cache.size(2) == 128 && v_cache.size(3) == 16,
+              "v_cache must be [NB, KV, 128, 16]");
+  const float* ssp = opt_rows(c10::optional<at::Tensor>(ss_in), M, "ss_in");
+  const int rc = pa_mid_gemm(nullptr, x.data_ptr(), wp.data_ptr(), nullptr, ws.data_ptr<float>(), ws.numel(),
+                             counters.data_ptr<int>(), counters.numel(), M, N, K, x.stride(0), 0, 0, 4, ssp, nullptr,
+                             nullptr, (float)eps, (int)fm, (int)fn, (int)splits, q_out.data_ptr(), k_cache.data_ptr(),
+                             v_cache.data_ptr(), positions.data_ptr<int>(), slots.data_ptr<int>(),
+                             cos_sin.data_ptr<float>(), (int)H, (int)KV, cur_stream());
+  TORCH_CHECK(rc >= 0, "mid_qkv_rope launch failed");
+  return rc == 0;
+}
+
+// out[m] = sum_k x[m, k]^2 (fp32)
+void row_sumsq(at::Tensor out, at::Tensor x) {
+  check_gpu(out, "out");
+  TORCH_CHECK(x.is_cuda() && x.dim() == 2 && x.stride(1) == 1, "x must be a 2-D GPU tensor, unit inner stride");
+  check_dtype(x, at::kBFloat16, "x"); check_dtype(out, at::kFloat, "out");
+  TORCH_CHECK(out.numel() >= x.size(0), "out shorter than x");
+  check_rc(pa_row_sumsq(out.data_ptr<float>(), x.data_ptr(), x.size(0), x.size(1), x.stride(0), cur_stream()),
+           "row_sumsq");
+}
+
+std::vector<int64_t> mid_gemm_plan(int64_t M, int64_t N, int64_t K, int64_t epi) {
+  int fm, fn, S;
+  pa_mid_gemm_plan((int)M, (int)N, (int)K, (int)epi, &fm, &fn, &S);
+  return {fm, fn, S, pa_mid_gemm_ws_floats((int)M, (int)N, (int)K, fm, fn, S)};
+}
+
 int64_t sample_workspace_floats(int64_t rows, int64_t V) {
   return pa_sample_workspace_floats(rows, V);
 }
@@ -483,6 +592,16 @@ PYBIND11_MODULE(_C, m) {
   m.def("wide_gemm", &wide_gemm, py::arg("y"), py::arg("x"), py::arg("wp"), py::arg("resid"), py::arg("ws"),
         py::arg("counters"), py::arg("epi") = 0, py::arg("norm") = false, py::arg("eps") = 1e-5, py::arg("ntw") = 0,
         py::arg("waves") = 0, py::arg("splits") = 0);
+  m.def("mid_gemm", &mid_gemm, py::arg("y"), py::arg("x"), py::arg("wp"), py::arg("resid"), py::arg("ws"),
+        py::arg("counters"), py::arg("epi") = 0, py::arg("ss_in") = py::none(), py::arg("ss_out") = py::none(),
+        py::arg("ss_zero") = py::none(), py::arg("eps") = 1e-5, py::arg("fm") = 0, py::arg("fn") = 0,
+        py::arg("splits") = 0);
+  m.def("mid_qkv_rope", &mid_qkv_rope, py::arg("x"), py::arg("wp"), py::arg("ss_in"), py::arg("eps"),
+        py::arg("q_out"), py::arg("k_cache"), py::arg("v_cache"), py::arg("positions"), py::arg("slots"),
+        py::arg("cos_sin"), py::arg("H"), py::arg("KV"), py::arg("ws"), py::arg("counters"), py::arg("fm") = 0,
+        py::arg("fn") = 0, py::arg("splits") = 0);
+  m.def("row_sumsq", &row_sumsq, py::arg("out"), py::arg("x"));
+  m.def("mid_gemm_plan", &mid_gemm_plan, "default (fm, fn, splits, workspace floats) of mid_gemm");
   m.def("paged_attention", &paged_attention, py::arg("out"), py::arg("part_o"), py::arg("part_ml"), py::arg("q"),
         py::arg("k_cache"), py::arg("v_cache"), py::arg("items"), py::arg("n_items"), py::arg("counters"),
         py::arg("q_start"), py::arg("q_len"), py::arg("ctx_len"), py::arg("block_table"), py::arg("scale"),

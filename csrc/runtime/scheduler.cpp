@@ -3,6 +3,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cstring>
+#include <stdexcept>
 
 namespace rt {
 
@@ -248,6 +249,7 @@ int32_t Scheduler::schedule(int32_t* buf) {
   // extra partial merges than they gain (profiles/r1_attention_small_batch.jsonl:
   // 8 rows x ctx 1000: 13.8 us at 128, 10.9 at 256, 11.2 at 512; 16 rows: 24.2 /
   // 17.7 / 18.5). The item list must still fit max_items.
+  const int32_t qtile = 32 / std::max(1, cfg_.gqa_group);
   int32_t psz = 512;
   if (cfg_.split_decode) {
     int64_t parts512 = 0, parts256 = 0, nprefill = 0;
@@ -257,7 +259,7 @@ int32_t Scheduler::schedule(int32_t* buf) {
         parts512 += std::max(1, (c + 511) / 512);
         parts256 += std::max(1, (c + 255) / 256);
       } else {
-        nprefill += (p.n + 31) / 32 + 1;
+        nprefill += (p.n + qtile - 1) / qtile;  // exactly the q-tiles emitted below
       }
     }
     const int64_t kv = std::max(1, cfg_.kv_heads), target = 512;
@@ -267,7 +269,6 @@ int32_t Scheduler::schedule(int32_t* buf) {
 
   // prefill (q-split) tiles go first in the item list, heaviest (last) tile of a
   // chunk first, so the long-running workgroups start before the decode items
-  const int32_t qtile = 32 / std::max(1, cfg_.gqa_group);
   for (size_t si = 0; si < last_plan_.size(); ++si) {
     const int32_t n = last_plan_[si].n;
     if (n <= tpw) continue;
@@ -351,6 +352,8 @@ int32_t Scheduler::schedule(int32_t* buf) {
   counts[4] = nparted;
   counts[5] = pslot;
   counts[6] = ntrunc;  // rows that need the top-k / top-p threshold pass
+  if (nit > L.max_items)  // by construction (psz guard above, max_items sizing) this cannot happen
+    throw std::logic_error("scheduler: attention item list overflows max_items");
   buf[L.n_items] = nit;
   if (T > 0) ++stat_steps_;
   return T;

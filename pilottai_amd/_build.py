@@ -30,6 +30,9 @@ CSRC = ROOT / "csrc"
 BUILD = ROOT / "build"
 ARCH = os.environ.get("PILOTTAI_GPU_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+# Per-file code-generation flags. gemm_mid.hip: MFMA accumulators in the VGPR form; with
+# the AGPR form hipcc shuffles them through v_accvgpr moves in the software-pipelined loop.
+FILE_FLAGS = {"gemm_mid.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"]}
 
 
 def _torch_paths():
@@ -82,7 +85,8 @@ def build_ops(verbose: bool = False, workers: int | None = None) -> Path:
     for src in sorted(glob.glob(str(CSRC / "ops" / "*.hip"))):
         obj = str(BUILD / (Path(src).stem + ".hip.o"))
         cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-c", src,
-               "-o", obj, "-ffast-math", "-fno-gpu-rdc", "-Wno-unused-result"]
+               "-o", obj, "-ffast-math", "-fno-gpu-rdc", "-Wno-unused-result",
+               *FILE_FLAGS.get(Path(src).name, [])]
         jobs.append((src, obj, cmd, headers))
         objs.append(obj)
     bsrc = str(CSRC / "ops" / "bindings.cpp")

@@ -79,6 +79,7 @@ class EngineConfig:
     decode_fused: Optional[bool] = None  # packed-weight fused decode path; None = when it fits in HBM
     decode_fused_max_t: Optional[int] = None  # largest step (tokens) on that path; None = model default
     wide_max_t: Optional[int] = None  # largest step on the packed small-batch path; None = model default
+    mid_max_t: Optional[int] = None  # largest step on the LDS-DMA tiled mid-size path; None = model default
 
 
 # TP step header: [op, T, ns, nsamp, bucket, masks_changed, n_copy, truncate]
@@ -163,6 +164,8 @@ class LLMEngine:
             self.model.DECODE_FUSED_MAX_T = int(cfg.decode_fused_max_t)
         if cfg.wide_max_t is not None:
             self.model.WIDE_MAX_T = int(cfg.wide_max_t)
+        if cfg.mid_max_t is not None:
+            self.model.MID_MAX_T = int(cfg.mid_max_t)
         self.load_time = time.time() - t0
         self.max_model_len = min(cfg.max_model_len, mc.max_position)
         # ---- KV cache sizing (288 GB HBM: the default leaves room for graphs/activations)

@@ -71,6 +71,9 @@ PRESETS: Dict[str, LlamaConfig] = {
                         num_heads=4, num_kv_heads=1, max_position=4096),
     "tiny-gqa4": LlamaConfig(name="tiny-gqa4", hidden_size=1024, intermediate_size=2048,
                              num_layers=2, num_heads=8, num_kv_heads=2, max_position=4096),
+    # the exact Llama-3-8B layer (4096 / 14336 / 32:8 heads / full vocabulary), 2 layers deep:
+    # production shapes through every forward path at test cost
+    "llama-3-8b-2l": LlamaConfig(name="llama-3-8b-2l", num_layers=2, max_position=4096),
 }
 
 
@@ -124,6 +127,17 @@ class LlamaModel:
     # steps of up to this many tokens (above DECODE_FUSED_MAX_T) run the packed-weight
     # small-batch kernels (csrc/ops/gemm_wide.hip; tools/wide_gemm_bench.py)
     WIDE_MAX_T = 48  # measured: the packed path wins the 48-token bucket, loses at 64 (BENCHMARKS.md)
+    # steps of up to this many tokens (above WIDE_MAX_T) run the LDS-DMA tiled projections
+    # (csrc/ops/gemm_mid.hip) with every norm / SwiGLU / residual / RoPE + KV write fused
+    MID_MAX_T = 256
+    # (largest M, fm, fn, K-slices) per projection, best of tools/mid_gemm_bench.py on MI355X
+    # (profiles/r2_mid_gemm_sweep.jsonl); the first row whose M covers the step is used
+    MID_CFG = {
+        "qkv": [(64, 2, 2, 2), (128, 2, 2, 1), (256, 4, 2, 1), (1 << 30, 4, 4, 1)],
+        "o": [(64, 2, 2, 4), (128, 2, 2, 2), (256, 2, 2, 1), (1 << 30, 4, 2, 1)],
+        "gate_up": [(64, 2, 4, 1), (128, 4, 4, 1), (256, 8, 4, 1), (1 << 30, 8, 4, 1)],
+        "down": [(64, 2, 2, 4), (96, 4, 2, 4), (128, 2, 2, 2), (256, 4, 2, 2), (1 << 30, 4, 4, 2)],
+    }
 
     def __init__(self, cfg: LlamaConfig, device, dtype=torch.bfloat16, tp: Optional[TPGroup] = None,
                  seed: int = 0, weights_path: Optional[str] = None, decode_pack: Optional[bool] = None):
@@ -175,6 +189,9 @@ class LlamaModel:
         self.lm_head_p = ops.pack_decode_weight(self.lm_head)
         if self.device.type == "cuda":
             ops.wide_workspace(self.device)  # split-K slabs + tickets, before any graph capture
+            ops.mid_workspace(self.device)
+        # RMSNorm row statistics handed from each residual epilogue to the next projection
+        self._ss = torch.zeros(2, 1 << 14, dtype=torch.float32, device=self.device)
         self.decode_packed = True
 
     # -- weights -----------------------------------------------------------------
@@ -302,6 +319,8 @@ class LlamaModel:
             return self._forward_decode(meta, kv, T, num_logit_rows, part_o, part_ml)
         if self.decode_packed and T <= self.WIDE_MAX_T:
             return self._forward_wide(meta, kv, T, num_logit_rows, part_o, part_ml)
+        if self.decode_packed and T <= self.MID_MAX_T:
+            return self._forward_mid(meta, kv, T, num_logit_rows, part_o, part_ml)
         H, KVh, hd = self.h_local, self.kv_local, cfg.head_dim
         ids = meta.input_ids[:T].long() if self.device.type == "cpu" else meta.input_ids[:T]
         h = self._embed(ids)
@@ -420,6 +439,70 @@ class LlamaModel:
         rows = rows.long() if self.device.type == "cpu" else rows
         xs = ops.rmsnorm(h.index_select(0, rows), self.norm, eps)
         if num_logit_rows <= 16:  # decode_gemm beats hipBLASLt on the LM head only up to 16 rows
+            return ops.decode_gemm(xs, self.lm_head_p, "plain")
+        return ops.linear(xs, self.lm_head, "lm_head")
+
+    def _mid_cfg(self, kind: str, T: int) -> dict:
+        for mmax, fm, fn, S in self.MID_CFG[kind]:
+            if T <= mmax:
+                return {"fm": fm, "fn": fn, "splits": S}
+        return {}
+
+    def _forward_mid(self, meta: StepMeta, kv: KVCache, T: int, num_logit_rows: int,
+                     part_o: torch.Tensor, part_ml: torch.Tensor) -> torch.Tensor:
+        """Mid-size step (WIDE_MAX_T < T <= MID_MAX_T: decode rows plus prefill chunks) on
+        the packed weights, 4 projection launches + attention per layer
+        (csrc/ops/gemm_mid.hip):
+
+          QKV (RMSNorm folded, RoPE + paged KV write in the epilogue) -> attention ->
+          O (+ residual, accumulating the next norm's row statistics) ->
+          gate_up (RMSNorm folded, SwiGLU epilogue) -> down (+ residual, statistics)
+
+        The RMSNorm statistics sum(h^2) of each row are produced by the residual epilogue
+        that writes h (buffers ss_a / ss_b alternate; each residual launch zeroes the
+        buffer the next one fills), so no norm kernel runs. Under TP the row-parallel
+        outputs are all-reduced first and the statistics recomputed (row_sumsq)."""
+        cfg = self.cfg
+        H, KVh, hd = self.h_local, self.kv_local, cfg.head_dim
+        eps = cfg.rms_eps
+        tp = self.tp.size > 1
+        ids = meta.input_ids[:T].long() if self.device.type == "cpu" else meta.input_ids[:T]
+        h = self._embed(ids)
+        if not h.is_contiguous():
+            h = h.contiguous()
+        ss_a, ss_b = self._ss[0, :T], self._ss[1, :T]
+        ops.row_sumsq(h, out=ss_a)
+        ss_b.zero_()
+        c_qkv, c_o = self._mid_cfg("qkv", T), self._mid_cfg("o", T)
+        c_gu, c_dn = self._mid_cfg("gate_up", T), self._mid_cfg("down", T)
+        for li, L in enumerate(self.layers):
+            q = torch.empty(T, H, hd, dtype=self.dtype, device=self.device)
+            ops.mid_qkv_rope(h, L["wqkv_p"], eps, q, kv.k[li], kv.v[li], meta.positions, meta.slots,
+                             self.cos_sin, H, KVh, ss_in=ss_a, **c_qkv)
+            attn = torch.empty(T, H, hd, dtype=self.dtype, device=self.device)
+            ops.paged_attention(attn, part_o, part_ml, q, kv.k[li], kv.v[li], meta.items, meta.n_items,
+                                meta.att_counters, meta.q_start, meta.q_len, meta.ctx_len,
+                                meta.block_table, self.scale, num_seqs=meta.num_seqs, part_size=meta.part_size)
+            a2 = attn.view(T, H * hd)
+            if tp:
+                o = ops.mid_gemm(a2, L["wo_p"], "plain", **c_o)
+                self.tp.all_reduce(o)
+                h.add_(o)
+                ops.row_sumsq(h, out=ss_b)
+            else:  # ss_b was zeroed by the previous down launch (or above)
+                ops.mid_gemm(a2, L["wo_p"], "resid", resid=h, out=h, ss_out=ss_b, ss_zero=ss_a, **c_o)
+            a = ops.mid_gemm(h, L["w13_p"], "silu", norm=True, eps=eps, ss_in=ss_b, **c_gu)
+            if tp:
+                d = ops.mid_gemm(a, L["w2_p"], "plain", **c_dn)
+                self.tp.all_reduce(d)
+                h.add_(d)
+                ops.row_sumsq(h, out=ss_a)
+            else:
+                ops.mid_gemm(a, L["w2_p"], "resid", resid=h, out=h, ss_out=ss_a, ss_zero=ss_b, **c_dn)
+        rows = meta.logit_rows[:num_logit_rows]
+        rows = rows.long() if self.device.type == "cpu" else rows
+        xs = ops.rmsnorm(h.index_select(0, rows), self.norm, eps)
+        if num_logit_rows <= 16:
             return ops.decode_gemm(xs, self.lm_head_p, "plain")
         return ops.linear(xs, self.lm_head, "lm_head")
 

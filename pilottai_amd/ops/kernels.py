@@ -389,3 +389,104 @@ def wide_gemm(x: torch.Tensor, wp: torch.Tensor, epi: str = "plain", resid: Opti
         acc = acc + resid.float()
     out.copy_(acc.to(out.dtype))
     return out
+
+
+# ---------------------------------------------------------------------------
+# Mid-size projections (48 < M <= 512) on the packed weights (csrc/ops/gemm_mid.hip)
+
+MID_EPI = {"plain": 0, "silu": 1, "resid": 2, "rope_perm": 3}
+MID_WS_FLOATS = 16 << 20  # 64 MB of split-K slabs per device
+_mid_ws = {}
+
+
+def mid_workspace(device):
+    """(slabs, tickets) for mid_gemm / mid_qkv_rope on `device`; allocate before hipGraph
+    capture (the tickets start zeroed and every launch leaves them zeroed)."""
+    key = str(device)
+    if key not in _mid_ws:
+        _mid_ws[key] = (torch.empty(MID_WS_FLOATS, dtype=torch.float32, device=device),
+                        torch.zeros(16384, dtype=torch.int32, device=device))
+    return _mid_ws[key]
+
+
+def _unpack_for(code: int, wp: torch.Tensor) -> torch.Tensor:
+    if code == 3:
+        return unpack_decode_qkv_rope(wp)
+    if code == 1:
+        return unpack_decode_gate_up(wp)
+    return unpack_decode_weight(wp)
+
+
+def row_sumsq(x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """out[m] = sum_k x[m, k]^2 in fp32 (RMSNorm row statistics)."""
+    out = torch.empty(x.shape[0], dtype=torch.float32, device=x.device) if out is None else out
+    if _on_gpu(x):
+        require_native().row_sumsq(out, x)
+        return out
+    out[:x.shape[0]].copy_(x.float().pow(2).sum(-1))
+    return out
+
+
+def mid_gemm(x: torch.Tensor, wp: torch.Tensor, epi: str = "plain", resid: Optional[torch.Tensor] = None,
+             out: Optional[torch.Tensor] = None, norm: bool = False, eps: float = 1e-5, fm: int = 0, fn: int = 0,
+             splits: int = 0, ss_in: Optional[torch.Tensor] = None, ss_out: Optional[torch.Tensor] = None,
+             ss_zero: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """y = epi(rownorm(x) @ W.T) for mid-size M with W packed by pack_decode_weight (gate_up:
+    pack_decode_gate_up + epi "silu"; QKV: pack_decode_qkv_rope + epi "rope_perm", which
+    returns the natural column order); "resid": resid + acc (out may alias resid).
+
+    `norm` scales rows by rsqrt(mean(x^2) + eps) (RMSNorm weight folded into W); the row
+    statistics are `ss_in` ([M] fp32 sum of x^2, e.g. the `ss_out` of the residual epilogue
+    that produced x) or computed here by row_sumsq. `ss_out` (resid only): [M] += row sums
+    of the written output squared. `ss_zero`: an [M] buffer zeroed by the launch."""
+    M, K = x.shape
+    N = wp.shape[0] * 16
+    code = MID_EPI[epi]
+    NO = N // 2 if code == 1 else N
+    if out is None:
+        out = torch.empty(M, NO, dtype=x.dtype, device=x.device)
+    if norm and ss_in is None:
+        ss_in = row_sumsq(x)
+    if _on_gpu(x):
+        ws, cnt = mid_workspace(x.device)
+        if not require_native().mid_gemm(out, x, wp, resid, ws, cnt, code, ss_in if norm else None, ss_out, ss_zero,
+                                          float(eps), int(fm), int(fn), int(splits)):
+            raise ValueError(f"mid_gemm does not handle M={M} N={N} K={K} epi={epi} fm={fm} fn={fn} S={splits}")
+        return out
+    W = _unpack_for(code, wp)
+    acc = x.float() @ W.float().T
+    if norm:
+        acc = acc * torch.rsqrt(ss_in[:M].float().unsqueeze(-1) / K + eps)
+    if code == 1:
+        acc = torch.nn.functional.silu(acc[:, :NO]) * acc[:, NO:]
+    elif code == 2:
+        acc = acc + resid.float()
+    y = acc.to(out.dtype)
+    if ss_zero is not None:
+        ss_zero[:M].zero_()
+    if ss_out is not None:
+        ss_out[:M] += y.float().pow(2).sum(-1)
+    out.copy_(y)
+    return out
+
+
+def mid_qkv_rope(x: torch.Tensor, wp: torch.Tensor, eps: float, q_out: torch.Tensor, k_cache, v_cache, positions,
+                 slots, cos_sin, H: int, KV: int, fm: int = 0, fn: int = 0, splits: int = 0,
+                 ss_in: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Mid-size QKV projection with the RMSNorm folded in (norm weight pre-multiplied into
+    the rope-packed weights; row statistics `ss_in`, computed here if absent), RoPE and the
+    paged KV write in the epilogue: replaces rmsnorm + QKV GEMM + rope_cache on 49-512-token
+    steps."""
+    if ss_in is None:
+        ss_in = row_sumsq(x)
+    if _on_gpu(x):
+        ws, cnt = mid_workspace(x.device)
+        if not require_native().mid_qkv_rope(x, wp, ss_in, float(eps), q_out, k_cache, v_cache, positions, slots,
+                                              cos_sin, int(H), int(KV), ws, cnt, int(fm), int(fn), int(splits)):
+            raise ValueError(f"mid_qkv_rope does not handle M={x.shape[0]} K={x.shape[1]} fm={fm} fn={fn}")
+        return q_out
+    M, K = x.shape
+    w = unpack_decode_qkv_rope(wp).float()
+    qkv = (x.float() @ w.T) * torch.rsqrt(ss_in[:M].float().unsqueeze(-1) / K + eps)
+    ref.rope_cache(q_out, k_cache, v_cache, qkv.to(x.dtype), positions, slots, cos_sin, H, KV)
+    return q_out

@@ -384,6 +384,102 @@ def test_wide_gemm(gpu, M, N, K, epi, norm, ntw, waves, splits):
         torch.testing.assert_close(y.float(), acc, atol=3e-2, rtol=2e-2)
 
 
+@pytest.mark.parametrize("M,N,K,epi,norm,fm,fn,splits", [
+    (64, 4096, 4096, "plain", False, 0, 0, 0), (128, 6144, 4096, "rope_perm", True, 0, 0, 0),
+    (256, 28672, 4096, "silu", True, 0, 0, 0), (192, 4096, 14336, "resid", False, 0, 0, 0),
+    (100, 1024, 512, "silu", True, 4, 2, 2), (77, 768, 512, "rope_perm", False, 2, 2, 1),
+    (300, 4096, 4096, "resid", False, 8, 4, 3), (512, 6144, 4096, "plain", True, 8, 2, 1),
+    (49, 2048, 1024, "plain", False, 2, 4, 8), (250, 4096, 4096, "plain", True, 4, 4, 4),
+    (130, 1024, 1024, "silu", False, 8, 4, 2), (33, 512, 2048, "resid", False, 4, 2, 6)])
+def test_mid_gemm(gpu, M, N, K, epi, norm, fm, fn, splits):
+    _check_mid(gpu, M, N, K, epi, norm, fm, fn, splits)
+
+
+def _check_mid(gpu, M, N, K, epi, norm, fm, fn, splits):
+    """Mid-size packed-weight GEMM (csrc/ops/gemm_mid.hip: LDS-DMA staged, C^T = W x^T)
+    vs fp32, every epilogue and the folded row norm, partial row tiles, with and
+    without split-K; run twice so the self-resetting split-K tickets are exercised."""
+    torch.manual_seed(17)
+    x = _bf(M, K, dev=gpu)
+    w = _bf(N, K, dev=gpu, scale=0.05)
+    resid = _bf(M, N, dev=gpu) if epi == "resid" else None
+    pack = {"silu": ops.pack_decode_gate_up, "rope_perm": ops.pack_decode_qkv_rope}.get(epi, ops.pack_decode_weight)
+    wp = pack(w)
+    acc = x.float() @ w.float().T
+    if norm:
+        acc = acc * torch.rsqrt(x.float().pow(2).mean(-1, keepdim=True) + 1e-5)
+    if epi == "silu":
+        acc = torch.nn.functional.silu(acc[:, :N // 2]) * acc[:, N // 2:]
+    elif epi == "resid":
+        acc = acc + resid.float()
+    for _ in range(2):
+        y = ops.mid_gemm(x, wp, epi, resid=resid, norm=norm, fm=fm, fn=fn, splits=splits)
+        torch.testing.assert_close(y.float(), acc, atol=3e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("M,fm,fn,S", [(160, 0, 0, 1), (160, 0, 0, 4), (100, 2, 4, 3), (300, 8, 2, 2)])
+def test_mid_gemm_resid_in_place_with_row_stats(gpu, M, fm, fn, S):
+    """The residual epilogue may write over its residual input (h += x W^T) and accumulates
+    the next norm's row statistics sum(h^2) of the written bf16 rows (ss_out), while zeroing
+    another buffer (ss_zero); a following norm-folded projection consuming those statistics
+    matches rmsnorm + GEMM."""
+    torch.manual_seed(18)
+    N, K = 4096, 4096
+    x = _bf(M, K, dev=gpu)
+    w = _bf(N, K, dev=gpu, scale=0.05)
+    h = _bf(M, N, dev=gpu)
+    want = h.float() + x.float() @ w.float().T
+    hh = h.clone()
+    ss = torch.zeros(M, dtype=torch.float32, device=gpu)
+    junk = torch.full((M,), 7.0, device=gpu)
+    ops.mid_gemm(x, ops.pack_decode_weight(w), "resid", resid=hh, out=hh, fm=fm, fn=fn, splits=S, ss_out=ss,
+                 ss_zero=junk)
+    torch.testing.assert_close(hh.float(), want, atol=3e-2, rtol=2e-2)
+    torch.testing.assert_close(ss, hh.float().pow(2).sum(-1), rtol=1e-4, atol=1e-2)
+    assert float(junk.abs().max()) == 0.0
+    w2 = _bf(2048, N, dev=gpu, scale=0.05)
+    g = (torch.rand(N, device=gpu) + 0.5).to(torch.bfloat16)
+    wg = w2 * g[None, :]
+    y = ops.mid_gemm(hh, ops.pack_decode_weight(wg), norm=True, ss_in=ss)
+    xn = hh.float() * torch.rsqrt(hh.float().pow(2).mean(-1, keepdim=True) + 1e-5)
+    ref_y = xn @ wg.float().T
+    torch.testing.assert_close(y.float(), ref_y, atol=3e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("M,H,KV,K,fm,fn,splits", [
+    (64, 32, 8, 4096, 0, 0, 0), (200, 32, 8, 4096, 0, 0, 0), (96, 8, 2, 1024, 4, 2, 3),
+    (300, 4, 1, 512, 8, 4, 1), (128, 32, 8, 4096, 4, 4, 5), (160, 32, 8, 4096, 8, 2, 2),
+    (96, 8, 2, 1024, 2, 2, 1), (300, 4, 1, 512, 4, 4, 3), (200, 4, 1, 512, 8, 2, 2)])
+def test_mid_qkv_rope(gpu, M, H, KV, K, fm, fn, splits):
+    """Mid-size norm-folded QKV projection with RoPE + paged KV write in the epilogue vs
+    the fp32 projection followed by the reference rope_cache (padding slots skipped)."""
+    torch.manual_seed(19)
+    N = (H + 2 * KV) * 128
+    x = _bf(M, K, dev=gpu)
+    w = _bf(N, K, dev=gpu, scale=0.05)
+    g = (torch.rand(K, device=gpu) + 0.5).to(torch.bfloat16)
+    wp = ops.pack_decode_qkv_rope(w * g[None, :])
+    NB = (M + 15) // 16 + 4
+    cos_sin = ref.rope_cos_sin(4096).to(gpu)
+    pos = torch.randint(0, 4000, (M,), dtype=torch.int32, device=gpu)
+    slots = torch.randperm(NB * 16, device=gpu)[:M].to(torch.int32)
+    slots[1] = -1
+    kc = torch.zeros(NB, KV, 16, 16, 8, dtype=torch.bfloat16, device=gpu)
+    vc = torch.zeros(NB, KV, 128, 16, dtype=torch.bfloat16, device=gpu)
+    q = torch.empty(M, H, 128, dtype=torch.bfloat16, device=gpu)
+    for _ in range(2):
+        ops.mid_qkv_rope(x, wp, 1e-5, q, kc, vc, pos, slots, cos_sin, H, KV, fm=fm, fn=fn, splits=splits)
+    xn = x.float() * torch.rsqrt(x.float().pow(2).mean(-1, keepdim=True) + 1e-5) * g.float()
+    qkv = (xn @ w.float().T).cpu()
+    rq = torch.empty(M, H, 128, dtype=torch.float32)
+    rk = torch.zeros(NB, KV, 16, 16, 8)
+    rv = torch.zeros(NB, KV, 128, 16)
+    ref.rope_cache(rq, rk, rv, qkv, pos.cpu(), slots.cpu(), cos_sin.cpu(), H, KV)
+    torch.testing.assert_close(q.float().cpu(), rq, atol=3e-2, rtol=2e-2)
+    torch.testing.assert_close(kc.float().cpu(), rk, atol=3e-2, rtol=2e-2)
+    torch.testing.assert_close(vc.float().cpu(), rv, atol=3e-2, rtol=2e-2)
+
+
 def test_semantic_index_packed_storage(gpu):
     """SemanticIndex keeps rows in packed 16-row tiles: scattered and bulk writes
     (aligned and unaligned ranges, ring wrap) read back exactly, and the HIP
