@@ -5,10 +5,13 @@
     "Manager + 64 workers, Llama-3-8B continuous-batched across N x MI355X (agent-DP)"
 
 One process per GPU (torchrun); the 64 worker agents are sharded over the ranks
-(strong scaling: the node always runs 64 concurrent workers). Every rank runs a
-`Serve` orchestrator (the manager) and an on-node Llama-3-8B engine (random-init
-bf16 weights, full 32-layer architecture). Each worker is a closed-loop client:
-it submits a synthetic document task, awaits the TaskResult, submits the next.
+(strong scaling: the node always runs 64 concurrent workers), each rank with an
+on-node Llama-3-8B engine (random-init bf16 weights, full 32-layer architecture).
+ONE manager `Serve` on rank 0 orchestrates the node-wide pool: the agents of the other
+ranks are reached through the node control plane (parallel/node_plane.py), the
+manager's own LLM calls go to the least-loaded rank. 64 closed-loop clients on rank 0
+each submit a synthetic document task, await the TaskResult, submit the next.
+(`--dp-mode independent`: one Serve per rank over its own shard, round 1's layout.)
 
 Per-task LLM work is fixed by the `fixed` control policy (core/policy.py) and the
 reply schemas (source/rules.yaml): 7 LLM calls per task — orchestrator analysis,
@@ -66,6 +69,8 @@ def parse():
     ap.add_argument("--token-align", type=int, default=256, help="GEMM-friendly step sizes (0 = off)")
     ap.add_argument("--align-slack", type=int, default=96)
     ap.add_argument("--cpu", action="store_true", help="tiny model on CPU (plumbing smoke only)")
+    ap.add_argument("--dp-mode", choices=["node", "independent"], default="node",
+                    help="node: one manager over the node-wide pool; independent: one Serve per rank")
     ap.add_argument("--share-gpu", action="store_true",
                     help="rehearsal: every rank on GPU 0 (use with PILOTTAI_DIST_BACKEND=gloo)")
     return ap.parse_args()
@@ -108,14 +113,50 @@ async def run_rank(a, rank: int, world: int, device):
                           max_iterations=a.steps_per_task + 1, task_timeout=900)
         agents.append(BaseAgent(cfg, llm=llm, tools=[Tool(name="echo", description="identity tool",
                                                           function=echo_tool, max_retries=1)], policy=policy))
-    serve = Serve(agents=agents, manager_llm=llm,
-                  config={"name": f"bench-r{rank}", "max_concurrent_tasks": n_local, "policy": "fixed",
-                          "steps_per_task": a.steps_per_task, "max_queue_size": 100000, "task_timeout": 900,
-                          "agent_wait_timeout": 900})
-    await serve.start()
+    node = a.dp_mode == "node" and world > 1
+    serve_cfg = {"name": f"bench-r{rank}", "policy": "fixed", "steps_per_task": a.steps_per_task,
+                 "max_queue_size": 100000, "task_timeout": 900, "agent_wait_timeout": 900}
+    serve = plane = worker = None
+    if node and rank > 0:
+        # worker rank: host this shard's agents (and this GPU's engine) for the manager
+        from pilottai_amd.parallel.node_plane import PlaneWorker
+
+        for ag in agents:
+            await ag.start()
+
+        def kv_load():
+            m = eng.metrics()
+            return {"kv_cache_utilization": 1.0 - m.get("free_kv_blocks", 1) / max(1, m.get("total_kv_blocks", 1))}
+        worker = PlaneWorker(rank, agents, llm=llm, load_fn=kv_load)
+        await worker.connect()
+        serving = asyncio.ensure_future(worker.serve_forever())
+    elif node:
+        from pilottai_amd.parallel.node_plane import DistributedLLM, NodeManager, PlaneServer
+
+        plane = PlaneServer(world)
+        await plane.start()
+        serve = Serve(agents=agents, config={**serve_cfg, "max_concurrent_tasks": a.workers})
+        mgr = NodeManager(plane, serve)
+        mgr.register_local(agents)
+        mgr.attach_remote_agents()
+        serve._manager_llm = DistributedLLM(plane, llm)
+        await serve.start()
+    else:
+        serve = Serve(agents=agents, manager_llm=llm, config={**serve_cfg, "max_concurrent_tasks": n_local})
+        await serve.start()
+    async def coll(fn, *args):
+        """A blocking collective off the event loop (worker ranks keep serving the control
+        plane meanwhile); the thread binds this rank's GPU first (RCCL uses the current device)."""
+        def run():
+            if device.type == "cuda":
+                torch.cuda.set_device(device)
+            return fn(*args)
+        return await asyncio.to_thread(run)
+
     # shared-context broadcast (SURVEY N14): rank 0 fixes the workload seed for every rank
-    seed = comm.broadcast_object(int(time.time()) & 0xFFFF if rank == 0 else None)
+    seed = await coll(comm.broadcast_object, int(time.time()) & 0xFFFF if rank == 0 else None)
     init_s = time.time() - t_init
+    n_clients = a.workers if node else n_local  # node mode: all 64 clients talk to the one manager
 
     latencies = []
 
@@ -132,30 +173,42 @@ async def run_rank(a, rank: int, world: int, device):
                 latencies.append(dt)
 
     async def round_(n, rec):
-        await asyncio.gather(*(client(i, n, rec) for i in range(n_local)))
+        if serve is not None and not (node and rank > 0):
+            await asyncio.gather(*(client(i, n, rec) for i in range(n_clients)))
 
     if a.warmup > 0:
         await round_(a.warmup, False)
-    st0 = dict(eng.stats)
+    await coll(comm.barrier)  # worker ranks keep serving the plane meanwhile
+    st0 = dict(eng.stats)  # after the barrier: every rank's warmup work is behind it
     bh0 = {b: list(v) for b, v in eng.bucket_hist.items()}
     u0 = dict(llm.usage)
     n_timed0 = len(eng.timings)
-    comm.barrier()
     if device.type == "cuda":
         torch.cuda.synchronize()
     t0 = time.perf_counter()
     await round_(a.steps, True)
     if device.type == "cuda":
         torch.cuda.synchronize()
-    comm.barrier()
+    await coll(comm.barrier)
     dt = time.perf_counter() - t0
     st1 = dict(eng.stats)
     u1 = dict(llm.usage)
     em = eng.metrics()
-    await serve.stop()
+    requeued = 0
+    if plane is not None:
+        requeued = int(serve.metrics.get("requeued_tasks", 0))
+        await serve.stop()
+        await plane.stop()
+    elif worker is not None:
+        await serving
+        for ag in agents:
+            await ag.stop()
+    else:
+        await serve.stop()
     eng.stop()
     local = {
-        "dt": dt, "tasks": len(latencies), "lat": latencies, "init_s": init_s,
+        "dt": dt, "tasks": len(latencies), "lat": latencies, "init_s": init_s, "requeued": requeued,
+        "managers": 1 if serve is not None else 0, "dp_mode": a.dp_mode if world > 1 else "single",
         "tokens": st1["tokens"] - st0["tokens"], "steps": st1["steps"] - st0["steps"],
         "sampled": st1["sampled"] - st0["sampled"], "calls": u1["calls"] - u0["calls"],
         "prompt_tokens": u1["prompt_tokens"] - u0["prompt_tokens"],
@@ -239,6 +292,7 @@ def main():
                 "global_batch": a.workers,
                 "seq_len": round(tot("prompt_tokens") / calls, 1),
                 "parallelism": f"agent-dp{world}",
+                "managers": tot("managers"),
                 "workers": a.workers,
                 "llm_calls_per_task": round(calls / max(1, tasks), 2),
                 "policy": "fixed",
@@ -253,6 +307,8 @@ def main():
             "sampled_tokens_per_call": round(tot("sampled") / calls, 1),
             "engine_tokens_per_s": round(tot("tokens") / dt, 1),
             "engine_steps": tot("steps"),
+            "requeued_tasks": tot("requeued"),
+            "llm_calls_per_rank": [g["calls"] for g in gathered],
             "engine_busy_frac": round(tot("busy_s") / (dt * len(gathered)), 3),
             "prefix_cache_hit_frac": round(tot("prefix_hit") / max(1, tot("prompt_total")), 3),
             "graph_pad_frac": round(1 - tot("tokens") / max(1, tot("bucket_tokens")), 3),

@@ -32,6 +32,7 @@ from pydantic import BaseModel, Field
 
 from .core.agent import BaseAgent, _content, _is_workflow as _is_workflow_task, _resolve_default_llm
 from .core.config import AgentConfig, LLMConfig
+from .core.errors import AgentLostError
 from .core.factory import AgentFactory
 from .core.memory import Memory
 from .core.policy import DEFAULT_POLICY, ControlPolicy
@@ -112,6 +113,8 @@ class Serve:
         self._started = False
         self._idle: Deque[str] = deque()
         self._inflight: Dict[str, int] = {}  # tasks running per agent (capacity accounting)
+        self.agent_rank: Optional[Callable[[Any], int]] = None  # node-wide pool: agent -> rank
+        self.node = None  # parallel.node_plane.NodeManager when the pool spans ranks
         for a in agents or []:
             self._register_agent(a)
         self.tasks: Dict[str, Task] = {}
@@ -188,7 +191,12 @@ class Serve:
 
     # orchestrator protocol used by DynamicScaling / FaultTolerance
     async def create_agent(self, **kw) -> BaseAgent:
-        template = next(iter(self.agents.values()), None)
+        node = getattr(self, "node", None)
+        if node is not None:  # node-wide pool: the new worker goes to the least-loaded rank
+            remote = await node.create_agent(**kw)
+            if remote is not None:
+                return remote
+        template = next((a for a in self.agents.values() if isinstance(a, BaseAgent)), None)
         role = kw.get("role") or (template.config.role if template else "worker")
         agent_type = kw.get("agent_type")
         if agent_type and agent_type in AgentFactory._agent_types:
@@ -485,17 +493,28 @@ class Serve:
                          metadata={"subtasks": list(parent.subtasks)})
         self._finish(parent, agg)
 
+    async def _run_on_agent(self, task: Task, agent: Optional[BaseAgent], prefer: Optional[str] = None) -> TaskResult:
+        """Execute on `agent` (or a newly acquired one). If the agent is lost mid-task (its
+        rank died: AgentLostError), the task did not complete there: re-queue it on another
+        agent — not a retry, and each task still completes exactly once."""
+        while True:
+            if agent is None:
+                agent = await self._acquire_agent(task, prefer=prefer)
+            try:
+                self.running_tasks[task.id] = agent.id
+                return await agent.execute_task(task)
+            except AgentLostError as e:
+                self.metrics["requeued_tasks"] += 1
+                self.logger.warning("task %s re-queued: %s", task.id, e)
+            finally:
+                self.running_tasks.pop(task.id, None)
+                await self._release_agent(agent)
+            agent, prefer = None, None
+
     async def _execute_task(self, task: Task, agent: Optional[BaseAgent] = None) -> TaskResult:
         """`agent`: already reserved (speculative start in _submit)."""
-        if agent is None:
-            agent = await self._acquire_agent(task)
-        try:
-            task.mark_started() if task.status in (TaskStatus.PENDING, TaskStatus.RETRY) else None
-            self.running_tasks[task.id] = agent.id
-            result = await agent.execute_task(task)
-        finally:
-            self.running_tasks.pop(task.id, None)
-            await self._release_agent(agent)
+        task.mark_started() if task.status in (TaskStatus.PENDING, TaskStatus.RETRY) else None
+        result = await self._run_on_agent(task, agent)
         evaluation = await self._evaluate_result(task, result) if self.config.evaluate_results else \
             {"success": result.success, "requires_retry": not result.success}
         if not evaluation.get("success", result.success):
@@ -518,14 +537,7 @@ class Serve:
             for k, v in mods.items():
                 if k in ("description", "priority", "tools", "config", "metadata"):
                     setattr(task, k, v)
-        preferred = evaluation.get("agent")
-        agent = await self._acquire_agent(task, prefer=preferred)
-        try:
-            self.running_tasks[task.id] = agent.id
-            return await agent.execute_task(task)
-        finally:
-            self.running_tasks.pop(task.id, None)
-            await self._release_agent(agent)
+        return await self._run_on_agent(task, None, prefer=evaluation.get("agent"))
 
     # ------------------------------------------------------------------ agents
     def _is_available(self, a: BaseAgent) -> bool:
@@ -576,6 +588,8 @@ class Serve:
                 if a is not None and (aid == prefer or a.config.role == prefer):
                     self._idle.remove(aid)
                     return a
+        if self.agent_rank is not None:
+            return self._pick_idle_balanced()
         n = len(self._idle)
         for _ in range(n):
             aid = self._idle.popleft()
@@ -589,6 +603,31 @@ class Serve:
             if str(a.status) not in ("stopped", "error"):
                 self._idle.append(aid)  # paused (LoadBalancer): keep it, skip it
         return None
+
+    def _pick_idle_balanced(self) -> Optional[BaseAgent]:
+        """Node-wide pool (parallel/node_plane.py): the available agent on the rank with
+        the fewest tasks in flight, so work spreads evenly over the GPUs whatever the
+        submission pattern."""
+        per_rank: Dict[int, int] = defaultdict(int)
+        for aid in self.running_tasks.values():
+            a = self.agents.get(aid)
+            if a is not None:
+                per_rank[self.agent_rank(a)] += 1
+        for aid, n in self._inflight.items():  # reserved but not yet running
+            a = self.agents.get(aid)
+            if a is not None and aid not in self.running_tasks.values():
+                per_rank[self.agent_rank(a)] += n
+        best, best_key = None, None
+        for aid in list(self._idle):
+            a = self.agents.get(aid)
+            if a is None or not self._is_available(a) or self._inflight.get(aid, 0) >= self._capacity(a):
+                continue
+            key = (per_rank[self.agent_rank(a)], self.agent_rank(a))
+            if best_key is None or key < best_key:
+                best, best_key = a, key
+        if best is not None and self._inflight.get(best.id, 0) + 1 >= self._capacity(best):
+            self._idle.remove(best.id)
+        return best
 
     async def _release_agent(self, agent: BaseAgent):
         n = self._inflight.get(agent.id, 1) - 1

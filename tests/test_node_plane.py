@@ -1,0 +1,53 @@
+"""Node-global control plane for agent-DP (parallel/node_plane.py), multi-process on the CPU.
+
+One process per rank (as on an 8-GPU node, minus the engines): rank 0 runs the single
+manager Serve over the node-wide agent pool, the other ranks host worker agents behind
+the TCP control plane. Model-free schema LLMs keep it fast; the scenarios are
+parallel/node_rehearsal.py's.
+"""
+import pytest
+
+from pilottai_amd.parallel.node_rehearsal import run
+
+
+@pytest.mark.parametrize("world", [4, 8])
+def test_skewed_submission_is_balanced_over_ranks(world):
+    """Half the tasks submitted at rank 0, half at the last rank (forwarded to the manager):
+    one wave of exactly one task per agent lands one task per agent, i.e. the per-rank
+    counts differ by at most one; the manager's own LLM calls are spread over the ranks."""
+    r = run(world, "balance", per_rank=2)
+    assert r["exitcodes"] == [0] * world, r
+    assert r["succeeded"] == r["submitted"] == 2 * world
+    assert r["unique_completed"] == r["submitted"]
+    per_rank = [r["local_executed"]] + [x["executed"] for x in r["ranks"]]
+    assert len(per_rank) == world
+    assert max(per_rank) - min(per_rank) <= 1, per_rank
+    assert r["ranks"][-1]["forwarded_ok"] == world  # the forwarded half all came back
+    assert len(r["llm_calls_by_rank"]) >= world // 2, r["llm_calls_by_rank"]
+
+
+def test_load_balancer_moves_queued_task_across_ranks():
+    r = run(4, "lb_move")
+    assert r["moved"] == 2
+    moved = [t for t in r["queued_ids"] if t in r["dst_queue"]]
+    assert len(moved) == 2 and len(r["src_queue"]) == 1
+    assert not set(moved) & set(r["src_queue"])
+
+
+def test_dynamic_scaling_creates_agent_on_least_loaded_rank():
+    r = run(4, "scale")
+    assert r["registered"] and r["scaled_ok"]
+    assert r["new_rank"] in (1, 2, 3)  # rank 0 was made to look busy
+
+
+def test_rank_loss_requeues_and_completes_every_task_exactly_once():
+    """Rank 2 dies mid-run (os._exit in the middle of its third task): the plane detects
+    it, its in-flight tasks are re-queued on the survivors, its agents leave the pool, and
+    every submitted task completes exactly once."""
+    r = run(4, "kill", per_rank=2)
+    assert r["exitcodes"][2] == 17 and r["exitcodes"][0] == 0, r["exitcodes"]
+    assert r["lost_ranks"] == [2]
+    assert r["succeeded"] == r["submitted"] == 40
+    assert r["completed_ids"] == r["unique_completed"] == 40
+    assert r["requeued"] >= 1
+    assert r["agents_after"] == 6

@@ -1,0 +1,59 @@
+"""The RCCL ("nccl" backend) branch of parallel/comm.py, executed for real on the GPU box.
+
+The driver's multi-GPU bench runs this path over xGMI; here it runs at world 1 (and 2
+ranks on ONE GPU is refused by RCCL), so the collectives, the device binding and the
+load view at least execute once on a real MI355X: init_process_group(nccl, device_id),
+the device barrier, all_gather_into_tensor, broadcast_object, GlobalLoadView.update and
+a TP all-reduce.
+"""
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+SCRIPT = r"""
+import os, sys, json
+sys.path.insert(0, os.environ["ROOT"])
+import torch, torch.distributed as dist
+from pilottai_amd.parallel import comm
+from pilottai_amd.parallel.agent_dp import GlobalLoadView
+os.environ["WORLD_SIZE"] = "1"
+rank, world, local = comm.env_rank_world()
+dist.init_process_group(backend="nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+assert dist.get_backend() == "nccl"
+comm.barrier()
+x = torch.arange(8, dtype=torch.float32, device="cuda")
+out = torch.empty(1, 8, device="cuda")
+dist.all_gather_into_tensor(out, x)
+assert torch.equal(out[0], x)
+y = torch.ones(4, device="cuda")
+dist.all_reduce(y)
+assert float(y.sum()) == 4.0
+assert comm.broadcast_object({"k": 3}) == {"k": 3}
+view = GlobalLoadView()
+t = view.update([1.0, 2.0, 3.0, 0.5, 100.0])
+assert t[0]["running_tasks"] == 2.0 and view.least_loaded_rank() == 0
+dist.destroy_process_group()
+print(json.dumps({"rccl": "ok"}))
+"""
+
+
+def _port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_rccl_branch_executes_on_gpu(tmp_path):
+    f = tmp_path / "rccl_probe.py"
+    f.write_text(SCRIPT)
+    env = dict(os.environ, ROOT=ROOT, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_port()), RANK="0",
+               LOCAL_RANK="0", WORLD_SIZE="1")
+    p = subprocess.run([sys.executable, str(f)], env=env, capture_output=True, text=True, timeout=170)
+    assert p.returncode == 0, p.stderr[-3000:]
+    assert '"rccl": "ok"' in p.stdout
