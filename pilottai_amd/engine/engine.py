@@ -250,6 +250,13 @@ class LLMEngine:
                       "busy_s": 0.0, "prefill_tokens": 0, "decode_steps": 0, "graph_replays": 0,
                       "bucket_tokens": 0}
         self.bucket_hist: Dict[int, list] = {}  # bucket -> [steps, seconds]
+        # custom all-reduce health: its spin-waits give up after ~5 s and set an error word
+        # instead of hanging; the word is copied back with every step and checked after the
+        # step's synchronize, failing the engine rather than continuing on partial sums
+        self._car = getattr(self.tp, "custom", None) if self.tp.size > 1 else None
+        self._car_err_host = torch.zeros(1, dtype=torch.int32, pin_memory=pin) if self._car is not None else None
+        if self.tp.size > 1:  # ranks reach graph capture together (their init times differ)
+            torch.distributed.barrier(group=self.tp.cpu_group)
         # graphs contain the TP collectives, so every rank captures every bucket up front
         if self.use_graphs and (cfg.capture_on_start or self.tp.size > 1):
             self.capture_graphs()
@@ -501,11 +508,22 @@ class LLMEngine:
                     self.tp.broadcast(self._class_masks)
                 self.tp.broadcast(self._dev_meta[:n_copy])
                 self._run(bucket, ns, bool(trunc), n_copy)
+                self._car_fetch()
                 if self.on_gpu:
                     torch.cuda.current_stream().synchronize()
+                self._car_check()
                 n += 1
         self.stats["steps"] += n
         return n
+
+    def _car_fetch(self):
+        if self._car is not None:
+            self._car_err_host.copy_(self._car.err, non_blocking=True)
+
+    def _car_check(self):
+        if self._car is not None and int(self._car_err_host[0]) != 0:
+            raise RuntimeError("custom all-reduce barrier timed out (a TP peer stalled > 5 s): "
+                               "the step's activations are partial; engine stopped")
 
     @property
     def failed(self) -> Optional[BaseException]:
@@ -578,8 +596,10 @@ class LLMEngine:
             self._run(bucket, ns, trunc, n_copy)
         if nsamp:
             self._sampled_host[:nsamp].copy_(self._sampled_dev[:nsamp], non_blocking=self.on_gpu)
+        self._car_fetch()
         if self.on_gpu:
             torch.cuda.current_stream().synchronize()
+        self._car_check()
         with trace_range("engine.commit"):
             outs = self.sched.commit(self._sampled_host.data_ptr(), nsamp)
         st = self.stats

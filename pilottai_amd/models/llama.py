@@ -71,6 +71,9 @@ PRESETS: Dict[str, LlamaConfig] = {
                         num_heads=4, num_kv_heads=1, max_position=4096),
     "tiny-gqa4": LlamaConfig(name="tiny-gqa4", hidden_size=1024, intermediate_size=2048,
                              num_layers=2, num_heads=8, num_kv_heads=2, max_position=4096),
+    # 8 KV heads like Llama-3-8B/70B: shardable at TP = 2, 4 and 8 (TP tests)
+    "tiny-kv8": LlamaConfig(name="tiny-kv8", hidden_size=1024, intermediate_size=2048, num_layers=2,
+                            num_heads=16, num_kv_heads=8, max_position=4096),
     # the exact Llama-3-8B layer (4096 / 14336 / 32:8 heads / full vocabulary), 2 layers deep:
     # production shapes through every forward path at test cost
     "llama-3-8b-2l": LlamaConfig(name="llama-3-8b-2l", num_layers=2, max_position=4096),

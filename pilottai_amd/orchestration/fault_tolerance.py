@@ -234,7 +234,8 @@ class FaultTolerance:
     def _check_stuck_tasks(self, agent) -> int:
         n = 0
         now = datetime.now()
-        for t in list(getattr(agent, "tasks", {}).values()):
+        tasks = getattr(agent, "tasks", None)
+        for t in list(tasks.values()) if isinstance(tasks, dict) else []:
             if self._is_task_stuck(t, now):
                 n += 1
         return n
@@ -316,7 +317,10 @@ class FaultTolerance:
             return None
 
     async def _transfer_tasks(self, old, new):
-        for tid, t in list(getattr(old, "tasks", {}).items()):
+        tasks = getattr(old, "tasks", None)
+        if not isinstance(tasks, dict):  # the agent protocol's task map; mocks / proxies without one: nothing to move
+            return
+        for tid, t in list(tasks.items()):
             if not self._is_task_recoverable(t):
                 continue
             try:

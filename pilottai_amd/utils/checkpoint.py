@@ -60,14 +60,28 @@ def save_serve_checkpoint(serve, path) -> str:
         "agents": agents,
     }
     (tmp / "state.json").write_text(json.dumps(state, indent=1, default=str))
+    # crash-safe swap: the previous checkpoint is renamed aside (not deleted) until the new
+    # one is in place; a crash between the two renames leaves it at <path>.bak, which
+    # load_checkpoint falls back to
+    bak = path.with_name(path.name + ".bak")
+    if bak.exists():
+        shutil.rmtree(bak)
     if path.exists():
-        shutil.rmtree(path)
+        os.replace(path, bak)
     os.replace(tmp, path)
+    if bak.exists():
+        shutil.rmtree(bak)
     return str(path)
 
 
 def load_checkpoint(path) -> Dict[str, Any]:
-    st = json.loads((Path(path) / "state.json").read_text())
+    path = Path(path)
+    f = path / "state.json"
+    if not f.exists():
+        bak = path.with_name(path.name + ".bak") / "state.json"
+        if bak.exists():  # interrupted swap (save_serve_checkpoint): the previous checkpoint
+            f = bak
+    st = json.loads(f.read_text())
     if st.get("format_version") != FORMAT_VERSION:
         raise ValueError(f"unsupported checkpoint format {st.get('format_version')}")
     return st

@@ -267,6 +267,7 @@ def test_fused_decode_path_matches_unfused_logits():
         if not fused:
             eng.model.DECODE_FUSED_MAX_T = 0
             eng.model.WIDE_MAX_T = 0
+            eng.model.MID_MAX_T = 0
         seen = []
         fwd = eng.model.forward
 
@@ -298,6 +299,7 @@ def test_wide_path_matches_library_path_logits():
                                      num_kv_blocks=256, max_model_len=512))
         if not wide:
             eng.model.WIDE_MAX_T = 0
+            eng.model.MID_MAX_T = 0
         seen = []
         fwd = eng.model.forward
 
@@ -312,3 +314,53 @@ def test_wide_path_matches_library_path_logits():
         logits[wide] = seen[0][1]
     a, b = logits[True], logits[False]
     torch.testing.assert_close(a, b, atol=0.05 * float(b.abs().max()), rtol=0.05)
+
+
+def test_mid_path_matches_library_path_logits():
+    """The mid-size forward (48 < T <= 256: norm folded into QKV / gate_up with the row
+    statistics handed over by the residual epilogues, RoPE + KV write in the QKV
+    epilogue, SwiGLU / residual epilogues) and the library-GEMM forward give the same
+    logits for a 100-token prefill step (CPU references of both paths)."""
+    import torch
+
+    from pilottai_amd.engine.engine import EngineConfig, LLMEngine
+
+    logits = {}
+    for mid in (True, False):
+        eng = LLMEngine(EngineConfig(model="tiny", max_num_seqs=8, use_graphs=False, decode_fused=True,
+                                     num_kv_blocks=256, max_model_len=512, token_align=0))
+        if not mid:
+            eng.model.MID_MAX_T = 0
+        seen = []
+        fwd = eng.model.forward
+
+        def rec(*a, _f=fwd, _s=seen, **k):
+            out = _f(*a, **k)
+            _s.append((a[2], out.float().clone()))
+            return out
+
+        eng.model.forward = rec
+        eng.generate([list(range(1, 101))], max_tokens=2, temperature=0.0, ignore_eos=True)
+        assert 48 < seen[0][0] <= 256
+        logits[mid] = seen[0][1]
+    a, b = logits[True], logits[False]
+    torch.testing.assert_close(a, b, atol=0.05 * float(b.abs().max()), rtol=0.05)
+
+
+def test_engine_fails_on_custom_allreduce_timeout():
+    """A TP peer that stalls past the custom all-reduce's spin budget sets its error word;
+    the engine must stop with an error instead of stepping on with partial sums."""
+    import types
+
+    import torch
+
+    from pilottai_amd.engine.engine import EngineConfig, LLMEngine
+
+    eng = LLMEngine(EngineConfig(model="tiny", max_num_seqs=4, use_graphs=False, num_kv_blocks=64,
+                                 max_model_len=256))
+    eng._car = types.SimpleNamespace(err=torch.ones(1, dtype=torch.int32))
+    eng._car_err_host = torch.zeros(1, dtype=torch.int32)
+    eng.submit([1, 2, 3], lambda o: None, max_tokens=2)
+    with pytest.raises(RuntimeError, match="custom all-reduce"):
+        for _ in range(4):
+            eng.step()

@@ -18,10 +18,10 @@ def _free_port() -> int:
     return p
 
 
-def _cfg():
+def _cfg(model="tiny-gqa4"):
     from pilottai_amd.engine.engine import EngineConfig
 
-    return EngineConfig(model="tiny-gqa4", max_num_seqs=8, max_num_batched_tokens=128, max_model_len=512,
+    return EngineConfig(model=model, max_num_seqs=8, max_num_batched_tokens=128, max_model_len=512,
                         num_kv_blocks=96, use_graphs=False)
 
 
@@ -29,16 +29,16 @@ def _prompts(tok):
     return [tok.encode("Task: summarize the quarterly report."), tok.encode("Task: plan a trip")]
 
 
-def _worker(rank, world, port, out_path):
+def _worker(rank, world, port, out_path, model="tiny-gqa4"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
-    torch.set_num_threads(2)
+    torch.set_num_threads(1 if world > 2 else 2)
     from pilottai_amd.engine.engine import LLMEngine
     from pilottai_amd.parallel.comm import init_distributed, new_tp_groups
 
     init_distributed("gloo")
     tp = new_tp_groups(world)
-    e = LLMEngine(_cfg(), device="cpu", tp=tp)
+    e = LLMEngine(_cfg(model), device="cpu", tp=tp)
     if rank != 0:
         e.follow()
         torch.distributed.destroy_process_group()
@@ -54,10 +54,13 @@ def _worker(rank, world, port, out_path):
                    "steps": e.stats["steps"]}, f)
 
 
-def test_tp2_engine_matches_tp1(tmp_path):
+@pytest.mark.parametrize("world,model", [(2, "tiny-gqa4"), (4, "tiny-kv8"), (8, "tiny-kv8")])
+def test_tp_engine_matches_tp1(tmp_path, world, model):
+    """TP = 2 / 4 / 8 (config 5 runs Llama-3-70B at TP = 8): canonical shards, vocab-parallel
+    embedding and sampling, row-parallel all-reduces; greedy tokens equal TP = 1's."""
     out = str(tmp_path / "tp.json")
     port = _free_port()
-    mp.start_processes(_worker, args=(2, port, out), nprocs=2, join=True, start_method="spawn")
+    mp.start_processes(_worker, args=(world, port, out, model), nprocs=world, join=True, start_method="spawn")
     res = json.load(open(out))
     # structured output is valid JSON of the schema under TP sampling
     obj = json.loads(res["json"])
@@ -65,7 +68,7 @@ def test_tp2_engine_matches_tp1(tmp_path):
 
     from pilottai_amd.engine.engine import LLMEngine
 
-    e1 = LLMEngine(_cfg(), device="cpu")
+    e1 = LLMEngine(_cfg(model), device="cpu")
     ref = e1.generate(_prompts(e1.tok), temperature=0.0, max_tokens=6, ignore_eos=True)
     # identical weights (canonical shards) -> identical greedy tokens, up to bf16
     # rounding of the split all-reduce: require the first token and most others.
