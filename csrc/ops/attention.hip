@@ -299,6 +299,61 @@ __device__ __forceinline__ void decode_item(
 __device__ __forceinline__ int swap23(int x) { return (x & ~12) | ((x & 4) << 1) | ((x & 8) >> 1); }
 constexpr int PF_LD = ATT_HD + 4;  // padded LDS row (floats) of the merge image
 
+// One 32-key tile of the online softmax + its PV product, shared by both prefill
+// paths. The tile is VALU-bound if written naively (the r2 counters showed ~25 VALU
+// instructions per MFMA): the scale is folded into one FMA feeding v_exp, the causal
+// mask runs only on tiles that cross some column's end (`mask`, wave-uniform), and the
+// O rescale (64 multiplies) only when some column's running max actually grew.
+// s: raw scores of S^T (lane column, registers g -> keys key0 + 16(g>>3) + (g&7),
+// key0 = 32t + 8h); m_run is kept in scaled log2 units.
+__device__ __forceinline__ void softmax_pv_tile(f32x16 s, bool mask, int key0, int key_limit, float scale_log2,
+                                                float& m_run, float& l_run, f32x16 (&o)[4],
+                                                const bf16x8 (&vf)[2][4]) {
+  if (mask) {  // wave-uniform
+    const int lim = key_limit - key0;
+#pragma unroll
+    for (int g = 0; g < 16; ++g) s[g] = (16 * (g >> 3) + (g & 7)) < lim ? s[g] : NEG_BIG;
+  }
+  float tmax = s[0];
+#pragma unroll
+  for (int g = 1; g < 16; ++g) tmax = fmaxf(tmax, s[g]);
+  tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+  const float m_new = fmaxf(m_run, tmax * scale_log2);
+  if (__any(m_new > m_run)) {  // wave-uniform: lanes whose max did not grow get alpha = 1
+    const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
+    l_run *= alpha;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) o[m] *= alpha;
+    m_run = m_new;
+  }
+  const float nm = -m_run;
+  float psum = 0.f;
+  bf16x8 pf[2];
+#pragma unroll
+  for (int g = 0; g < 16; ++g) {
+    const float p = __builtin_amdgcn_exp2f(fmaf(s[g], scale_log2, nm));
+    psum += p;
+    pf[g >> 3][g & 7] = (bf16)p;
+  }
+  l_run += psum;
+#pragma unroll
+  for (int st = 0; st < 2; ++st)
+#pragma unroll
+    for (int m = 0; m < 4; ++m) o[m] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[st][m], pf[st], o[m], 0, 0, 0);
+}
+
+// S^T tile = K · Q^T over the 128-dim head: one accumulation chain (the 32x32x16
+// MFMA's dependent-issue rate equals its independent one, so a second chain only
+// adds 16 zeroing moves and 16 adds per tile).
+__device__ __forceinline__ f32x16 qk_tile(const bf16x8 (&kf)[8], const bf16x8 (&qf)[8]) {
+  f32x16 s;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) s[j] = 0.f;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[i], qf[i], s, 0, 0, 0);
+  return s;
+}
+
 template <int G>
 __device__ __forceinline__ void prefill_item(
     const int4 it, char* smem, bf16* __restrict__ out, const bf16* __restrict__ q,
@@ -315,6 +370,7 @@ __device__ __forceinline__ void prefill_item(
   const int key_limit = colvalid ? (ctx - ql + tok + 1) : 0;
   const int head = kvh * G + hg;
   const int ntiles = (ctx - ql + qb + nq + 31) >> 5;
+  const int kmin = ctx - ql + qb + 1;  // smallest causal end of the item's columns
 
   bf16x8 qf[8];
   {
@@ -357,44 +413,8 @@ __device__ __forceinline__ void prefill_item(
 #pragma unroll
       for (int m = 0; m < 4; ++m) vf[st][m] = *reinterpret_cast<const bf16x8*>(vbase + (size_t)32 * m * ATT_BLK);
     }
-    // two independent accumulation chains over the head dimension
-    f32x16 sa, sb;
-#pragma unroll
-    for (int j = 0; j < 16; ++j) { sa[j] = 0.f; sb[j] = 0.f; }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      sa = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[i], qf[i], sa, 0, 0, 0);
-      sb = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[4 + i], qf[4 + i], sb, 0, 0, 0);
-    }
-    float tmax = NEG_BIG;
-    float sc[16];
-#pragma unroll
-    for (int g = 0; g < 16; ++g) {
-      const int key = 32 * t + 16 * (g >> 3) + 8 * h + (g & 7);
-      float v = (sa[g] + sb[g]) * scale_log2;
-      v = key < key_limit ? v : NEG_BIG;
-      sc[g] = v;
-      tmax = fmaxf(tmax, v);
-    }
-    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
-    const float m_new = fmaxf(m_run, tmax);
-    const float alpha = exp2f(m_run - m_new);
-    m_run = m_new;
-    float psum = 0.f;
-    bf16x8 pf[2];
-#pragma unroll
-    for (int g = 0; g < 16; ++g) {
-      const float p = exp2f(sc[g] - m_new);
-      psum += p;
-      pf[g >> 3][g & 7] = (bf16)p;
-    }
-    l_run = l_run * alpha + psum;
-#pragma unroll
-    for (int m = 0; m < 4; ++m) o[m] *= alpha;
-#pragma unroll
-    for (int st = 0; st < 2; ++st)
-#pragma unroll
-      for (int m = 0; m < 4; ++m) o[m] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[st][m], pf[st], o[m], 0, 0, 0);
+    const f32x16 sc = qk_tile(kf, qf);
+    softmax_pv_tile(sc, 32 * t + 32 > kmin, 32 * t + 8 * h, key_limit, scale_log2, m_run, l_run, o, vf);
   }
   l_run += __shfl_xor(l_run, 32, 64);
 
@@ -448,9 +468,150 @@ __device__ __forceinline__ void prefill_item(
   }
 }
 
+// ---------------------------------------------------------------------------
+// wide prefill path (nq > 32/G): an item is 4 waves x 32 columns = 128/G tokens. The
+// 32-key K/V tiles (two 16-key pages; a page of one KV head is 4 KiB contiguous in both
+// caches) are staged ONCE per workgroup into LDS by LDS-DMA and read by all 4 waves,
+// double-buffered (tile t+1 lands while tile t is computed): 4x less K/V traffic per
+// query column than the one-wave-per-tile path above, whose 32-column items made every
+// CU pull ~4x the L2 bandwidth it has (the prefill microbenchmark ran at 160-170
+// TFLOP/s, profiles/r1_attention_microbench_final.jsonl). Each wave owns its columns
+// outright: no cross-wave merge; the O^T tile is transposed through LDS for 16-B stores.
+// 64 KiB of LDS per workgroup (4 staged tiles): two workgroups per CU.
+constexpr int PW_TILE = 16384;  // bytes per staged tile: K pb0 | K pb1 | V pb0 | V pb1
+
+typedef __attribute__((address_space(3))) void att_lds_t;
+typedef __attribute__((address_space(1))) void att_gbl_t;
+
+constexpr int PW_NBUF = 4;     // staged tiles (3 in flight while one is computed)
+template <int N>
+__device__ __forceinline__ void att_wait_vm() { __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8)); }
+
+template <int G>
+__device__ __forceinline__ void prefill_item_wg(
+    const int4 it, char* smem, bf16* __restrict__ out, const bf16* __restrict__ q,
+    const bf16* __restrict__ k_cache, const bf16* __restrict__ v_cache,
+    const int* __restrict__ q_start, const int* __restrict__ q_len, const int* __restrict__ ctx_len,
+    const int* __restrict__ block_table, int max_blocks, int H, int KV, int kvh, float scale_log2) {
+  constexpr int TPWV = 32 / G;  // tokens per wave
+  const int s = it.x, qb = it.y, nq = it.z & 0xff;
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int r = lane & 31, h = lane >> 5;
+  const int hg = r % G, tq = wid * TPWV + r / G;
+  const int ctx = ctx_len[s], ql = q_len[s], q0 = q_start[s];
+  const bool colvalid = tq < nq;
+  const int tok = qb + tq;
+  const int key_limit = colvalid ? (ctx - ql + tok + 1) : 0;
+  const int head = kvh * G + hg;
+  const int wave_keys = wid * TPWV < nq ? ctx - ql + qb + min(nq, (wid + 1) * TPWV) : 0;  // wave's causal end
+  const int ntiles = (ctx - ql + qb + nq + 31) >> 5;
+  const int kmin = ctx - ql + qb + wid * TPWV + 1;  // smallest causal end of the wave's columns
+
+  bf16x8 qf[8];
+  {
+    const bf16* qrow = q + ((size_t)(q0 + (colvalid ? tok : 0)) * H + head) * ATT_HD + 8 * h;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      bf16x8 v = *reinterpret_cast<const bf16x8*>(qrow + 16 * i);
+      if (!colvalid) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = (bf16)0.f;
+      }
+      qf[i] = v;
+    }
+  }
+  const int* bt = block_table + (size_t)s * max_blocks;
+  const int nblk = (ctx + ATT_BLK - 1) / ATT_BLK;
+  const size_t kv_stride_blk = (size_t)KV * ATT_BLK * ATT_HD;
+  const int krow = swap23(r);
+  // wave w stages the 1-KiB pieces 4w..4w+3 of a tile: K pb0, K pb1, V pb0, V pb1 in order
+  auto stage = [&](int t, int buf) {
+    const int pb0 = bt[min(2 * t, nblk - 1)], pb1 = bt[min(2 * t + 1, nblk - 1)];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int p = wid * 4 + i;
+      // V^T pieces land with 16-B chunks c and c ^ 1 swapped where bit 4 of c is set:
+      // the PV fragment reads of dims r and r + 8 then fall in different banks
+      const int chunk = p < 8 ? lane : lane ^ ((lane >> 4) & 1);
+      const bf16* src = (p < 8 ? k_cache : v_cache) + (size_t)(((p >> 2) & 1) ? pb1 : pb0) * kv_stride_blk +
+                        (size_t)kvh * ATT_BLK * ATT_HD + (p & 3) * 512 + chunk * 8;
+      __builtin_amdgcn_global_load_lds((att_gbl_t*)src, (att_lds_t*)(smem + buf * PW_TILE + p * 1024), 16, 0, 0);
+    }
+  };
+
+  f32x16 o[4];
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int j = 0; j < 16; ++j) o[m][j] = 0.f;
+  float m_run = NEG_BIG, l_run = 0.f;
+
+  // PW_NBUF buffers, PW_NBUF - 1 tiles in flight: a tile's DMA is issued three compute
+  // phases before its use (one phase in flight left each tile ~1.5 us of L2/HBM latency
+  // to wait out: the 2048-token case ran at 0.3 PFLOP/s).
+#pragma unroll
+  for (int p = 0; p < PW_NBUF - 1; ++p)
+    if (p < ntiles) stage(p, p);
+  for (int t = 0; t < ntiles; ++t) {
+    const int buf = t % PW_NBUF;
+    const int after = min(PW_NBUF - 2, ntiles - 1 - t);  // tiles issued after t, still in flight
+    if (after >= 2) att_wait_vm<8>();  // this wave's pieces of tile t have landed ...
+    else if (after == 1) att_wait_vm<4>();
+    else att_wait_vm<0>();
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // ... and everyone's; every wave is also done with tile t-1
+    asm volatile("" ::: "memory");
+    if (t + PW_NBUF - 1 < ntiles) stage(t + PW_NBUF - 1, (t + PW_NBUF - 1) % PW_NBUF);  // tile t-1's buffer
+    if (32 * t >= wave_keys) continue;  // wave-uniform: beyond this wave's causal end
+    const char* tb = smem + buf * PW_TILE;
+    // K rows: dims 16i + 8h = chunk 2i + h; key krow & 15 of page krow >> 4
+    const char* kb = tb + (krow >= 16 ? 4096 : 0) + ((h * ATT_BLK + (krow & 15)) << 4);
+    bf16x8 kf[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) kf[i] = *reinterpret_cast<const bf16x8*>(kb + i * 2 * ATT_BLK * 16);
+    bf16x8 vf[2][4];
+#pragma unroll
+    for (int st = 0; st < 2; ++st)
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+        vf[st][m] = *reinterpret_cast<const bf16x8*>(tb + 8192 + st * 4096 + (32 * m + r) * 32 +
+                                                     16 * (h ^ ((r >> 3) & 1)));
+    const f32x16 sc = qk_tile(kf, qf);
+    softmax_pv_tile(sc, 32 * t + 32 > kmin, 32 * t + 8 * h, key_limit, scale_log2, m_run, l_run, o, vf);
+  }
+  l_run += __shfl_xor(l_run, 32, 64);
+  const float inv = l_run > 0.f ? 1.f / l_run : 0.f;
+
+  // transpose O^T through LDS (the tile buffers are free once every wave passed here):
+  // wave image [32 columns][128 dims] bf16, 8 KiB per wave
+  __syncthreads();
+  char* img = smem + wid * 8192;
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int gq = 0; gq < 4; ++gq) {
+      bf16x4 v;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = (bf16)(o[m][4 * gq + j] * inv);
+      *reinterpret_cast<bf16x4*>(img + (r * ATT_HD + 32 * m + 8 * gq + 4 * h) * 2) = v;
+    }
+  __syncthreads();
+  const int ccol = lane >> 1, dhalf = (lane & 1) * 64;
+  const int ctq = wid * TPWV + ccol / G, chg = ccol % G;
+  if (ctq < nq) {
+    bf16* orow = out + ((size_t)(q0 + qb + ctq) * H + kvh * G + chg) * ATT_HD + dhalf;
+#pragma unroll
+    for (int c8 = 0; c8 < 8; ++c8)
+      *reinterpret_cast<bf16x8*>(orow + 8 * c8) =
+          *reinterpret_cast<const bf16x8*>(img + (ccol * ATT_HD + dhalf + 8 * c8) * 2);
+  }
+}
+
 constexpr int ATT_LDS_DECODE = ATT_LDS_DECODE_BYTES + 16;  // + last-arriver flag
 constexpr int ATT_LDS_PREFILL = (4 * 32 * PF_LD + 2 * 4 * 32) * 4;
-constexpr int ATT_LDS_BYTES = ATT_LDS_PREFILL > ATT_LDS_DECODE ? ATT_LDS_PREFILL : ATT_LDS_DECODE;
+constexpr int ATT_LDS_BYTES0 = ATT_LDS_PREFILL > ATT_LDS_DECODE ? ATT_LDS_PREFILL : ATT_LDS_DECODE;
+constexpr int ATT_LDS_BYTES = ATT_LDS_BYTES0 > PW_NBUF * PW_TILE ? ATT_LDS_BYTES0 : PW_NBUF * PW_TILE;
 
 // One launch serves a whole ragged step: items (seq, q_begin, nq | part<<8 |
 // nparts<<20, partial slot) are strided over the grid, so the shape-stable
@@ -476,12 +637,16 @@ __global__ __launch_bounds__(256, 2) void paged_attn_kernel(
   for (int item = blockIdx.x; item < n; item += gridDim.x) {
     const int4 it = it_next;
     if (item + (int)gridDim.x < n) it_next = items[item + gridDim.x];
-    if ((it.z & 0xff) <= TPW)
+    const int nq = it.z & 0xff;
+    if (nq <= TPW)
       decode_item<G>(it, smem, out, part_o, part_ml, counters, q, k_cache, v_cache, q_start, q_len, ctx_len,
                      block_table, max_blocks, H, KV, kvh, scale_log2, psz);
-    else
+    else if (nq <= 32 / G)
       prefill_item<G>(it, smem, out, q, k_cache, v_cache, q_start, q_len, ctx_len, block_table,
                       max_blocks, H, KV, kvh, scale_log2);
+    else
+      prefill_item_wg<G>(it, smem, out, q, k_cache, v_cache, q_start, q_len, ctx_len, block_table,
+                         max_blocks, H, KV, kvh, scale_log2);
     __syncthreads();  // LDS reuse by the next item
   }
 }

@@ -94,6 +94,8 @@ PYBIND11_MODULE(_runtime, m) {
           c.max_prefill_tokens = d["max_prefill_tokens"].cast<int32_t>();
         if (d.contains("max_model_len")) c.max_model_len = d["max_model_len"].cast<int32_t>();
         if (d.contains("gqa_group")) c.gqa_group = d["gqa_group"].cast<int32_t>();
+        if (d.contains("att_qcols")) c.att_qcols = d["att_qcols"].cast<int32_t>();
+        if (d.contains("att_wide_min_tokens")) c.att_wide_min_tokens = d["att_wide_min_tokens"].cast<int32_t>();
         if (d.contains("prefix_caching")) c.prefix_caching = d["prefix_caching"].cast<bool>();
         if (d.contains("split_decode")) c.split_decode = d["split_decode"].cast<bool>();
         if (d.contains("token_align")) c.token_align = d["token_align"].cast<int32_t>();

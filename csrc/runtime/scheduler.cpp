@@ -249,7 +249,15 @@ int32_t Scheduler::schedule(int32_t* buf) {
   // extra partial merges than they gain (profiles/r1_attention_small_batch.jsonl:
   // 8 rows x ctx 1000: 13.8 us at 128, 10.9 at 256, 11.2 at 512; 16 rows: 24.2 /
   // 17.7 / 18.5). The item list must still fit max_items.
-  const int32_t qtile = 32 / std::max(1, cfg_.gqa_group);
+  // prefill item width: the 4-wave LDS-staged items (att_qcols columns) only pay when
+  // the step has enough prefill work to fill the chip with 4x fewer items (tools/
+  // attn_bench.py --scan: 8 x 512 tokens 50.8 us wide vs 68.8 narrow, 8 x 128 14.8 vs
+  // 13.8, a single 512-token chunk 19.5 vs 12.7)
+  int64_t prefill_tokens = 0;
+  for (const Planned& p : last_plan_)
+    if (p.n > tpw) prefill_tokens += p.n;
+  const int32_t qcols = prefill_tokens >= cfg_.att_wide_min_tokens ? std::max(32, cfg_.att_qcols) : 32;
+  const int32_t qtile = std::max(1, qcols / std::max(1, cfg_.gqa_group));
   int32_t psz = 512;
   if (cfg_.split_decode) {
     int64_t parts512 = 0, parts256 = 0, nprefill = 0;

@@ -32,6 +32,10 @@ struct SchedulerConfig {
   int32_t max_prefill_tokens = 2048;  // per-step budget for new prompt tokens
   int32_t max_model_len = 8192;
   int32_t gqa_group = 4;               // query heads per KV head (attention work items)
+  int32_t att_qcols = 128;             // MFMA columns (heads x tokens) per prefill attention item:
+                                       // 128 = the LDS-staged 4-wave path, 32 = one wave per item
+  int32_t att_wide_min_tokens = 2048;  // ... used only when the step's prefill tokens reach this
+                                       // (fewer, 4x wider items underfill the chip below it)
   bool prefix_caching = true;
   bool split_decode = true;            // flash-decoding partitions for long contexts
   // GEMM-friendly step sizes: when a step has T > token_align tokens and

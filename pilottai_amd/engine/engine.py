@@ -80,6 +80,8 @@ class EngineConfig:
     decode_fused_max_t: Optional[int] = None  # largest step (tokens) on that path; None = model default
     wide_max_t: Optional[int] = None  # largest step on the packed small-batch path; None = model default
     mid_max_t: Optional[int] = None  # largest step on the LDS-DMA tiled mid-size path; None = model default
+    att_qcols: int = 128  # prefill attention item width in MFMA columns (128: LDS-staged 4-wave items)
+    att_wide_min_tokens: int = 2048  # ... used only for steps with at least this many prefill tokens
 
 
 # TP step header: [op, T, ns, nsamp, bucket, masks_changed, n_copy, truncate]
@@ -194,6 +196,8 @@ class LLMEngine:
             "max_num_batched_tokens": cfg.max_num_batched_tokens,
             "max_prefill_tokens": cfg.max_prefill_tokens, "max_model_len": self.max_model_len,
             "gqa_group": self.model.h_local // self.model.kv_local,
+            "att_qcols": cfg.att_qcols,
+            "att_wide_min_tokens": cfg.att_wide_min_tokens,
             "prefix_caching": cfg.prefix_caching, "split_decode": cfg.split_decode,
             "token_align": cfg.token_align, "align_slack": cfg.align_slack,
             "kv_heads": self.model.kv_local,

@@ -12,14 +12,20 @@ ATT_PART = 512  # keys per decode partition (must match csrc/ops/attention.hip)
 
 
 def build_attention_items(q_lens: Sequence[int], ctx_lens: Sequence[int], group: int,
-                          split: bool = True, part: int = ATT_PART) -> Tuple[List[Tuple[int, int, int, int]], int]:
+                          split: bool = True, part: int = ATT_PART,
+                          qcols: int = 128, wide_min_tokens: int = 2048) -> Tuple[List[Tuple[int, int, int, int]], int]:
     """Return (items, n_partial_slots).
 
     item = (seq, q_begin, nq | part << 8 | nparts << 20, partial_slot); the
     partitions of a split decode row are merged in-kernel by the last to finish.
     """
     tpw = 16 // group  # query tokens per wave (kv-split path)
-    qtile = 32 // group  # tokens per prefill item (32 MFMA columns)
+    # tokens per prefill item: qcols MFMA columns (128: the LDS-staged 4-wave path of
+    # csrc/ops/attention.hip; 32: one wave per item)
+    # (wide items only when the step's prefill tokens reach wide_min_tokens, as the scheduler)
+    if sum(ql for ql in q_lens if ql > tpw) < wide_min_tokens:
+        qcols = 32
+    qtile = max(1, max(32, qcols) // group)
     items: List[Tuple[int, int, int, int]] = []
     # prefill tiles first, heaviest tile of each chunk first (as the scheduler)
     for s, (ql, ctx) in enumerate(zip(q_lens, ctx_lens)):

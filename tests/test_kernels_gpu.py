@@ -69,7 +69,7 @@ def test_rope_cache(gpu):
     torch.testing.assert_close(vc.cpu().float(), vc_r.float(), atol=0, rtol=0)
 
 
-def _run_attention(gpu, H, KV, q_lens, ctx_lens, seed=0, split=True, part=512):
+def _run_attention(gpu, H, KV, q_lens, ctx_lens, seed=0, split=True, part=512, qcols=128):
     torch.manual_seed(seed)
     G = H // KV
     blk = 16
@@ -87,7 +87,8 @@ def _run_attention(gpu, H, KV, q_lens, ctx_lens, seed=0, split=True, part=512):
     q_start = np.concatenate([[0], np.cumsum(q_lens)[:-1]]).astype(np.int32)
     T = int(sum(q_lens))
     q = _bf(T, H, 128, dev=gpu)
-    items, nslots = ops.build_attention_items(q_lens, ctx_lens, G, split=split, part=part)
+    items, nslots = ops.build_attention_items(q_lens, ctx_lens, G, split=split, part=part,
+                                               qcols=qcols, wide_min_tokens=0)
     it = torch.tensor(items + [(0, 0, 0, 0)], dtype=torch.int32, device=gpu)
     cnt = torch.zeros(ns * KV, dtype=torch.int32, device=gpu)
     n_it = torch.tensor([len(items)], dtype=torch.int32, device=gpu)
@@ -112,11 +113,14 @@ def test_attention_decode(gpu, H, KV):
     torch.testing.assert_close(o, r, atol=2e-2, rtol=2e-2)
 
 
+@pytest.mark.parametrize("qcols", [32, 128])
 @pytest.mark.parametrize("H,KV", [(32, 8), (8, 1)])
-def test_attention_prefill_and_mixed(gpu, H, KV):
-    q_lens = [37, 1, 100, 3, 16, 5, 250]
-    ctx = [37, 700, 164, 40, 16, 1029, 260]
-    o, r = _run_attention(gpu, H, KV, q_lens, ctx, seed=5)
+def test_attention_prefill_and_mixed(gpu, H, KV, qcols):
+    """Prefill chunks of every length class next to decode rows; qcols 128 = the LDS-staged
+    4-wave items (plus their 32-column / decode-path tails), 32 = one wave per item."""
+    q_lens = [37, 1, 100, 3, 16, 5, 250, 129, 33]
+    ctx = [37, 700, 164, 40, 16, 1029, 260, 1000, 2100]
+    o, r = _run_attention(gpu, H, KV, q_lens, ctx, seed=5, qcols=qcols)
     torch.testing.assert_close(o, r, atol=2e-2, rtol=2e-2)
 
 

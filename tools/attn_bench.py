@@ -23,7 +23,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from pilottai_amd import ops  # noqa: E402
 
 
-def setup(q_lens, ctx_lens, H=32, KV=8, pad_items=0, dev="cuda", part=512):
+def setup(q_lens, ctx_lens, H=32, KV=8, pad_items=0, dev="cuda", part=512, qcols=128):
     G = H // KV
     blk = 16
     ns = len(q_lens)
@@ -41,7 +41,7 @@ def setup(q_lens, ctx_lens, H=32, KV=8, pad_items=0, dev="cuda", part=512):
     q_start = np.concatenate([[0], np.cumsum(q_lens)[:-1]]).astype(np.int32)
     T = int(sum(q_lens))
     q = (torch.randn(T, H, 128, device=dev) * 0.5).to(torch.bfloat16)
-    items, _ = ops.build_attention_items(q_lens, ctx_lens, G, part=part)
+    items, _ = ops.build_attention_items(q_lens, ctx_lens, G, part=part, qcols=qcols, wide_min_tokens=0)
     n_items = len(items)
     items = items + [(0, 0, 0, 0)] * max(1, pad_items - len(items))
     it = torch.tensor(items, dtype=torch.int32, device=dev)
@@ -85,6 +85,8 @@ def main():
         "prefill": ([320, 320], [480, 480]),
         "prefill_cold": ([480], [480]),
         "mix": ([1] * 64 + [320, 320], [512] * 64 + [480, 480]),
+        "prefill8x256": ([256] * 8, [768] * 8),
+        "prefill2048": ([2048], [2048]),
     }
     if a.scan:
         cases = {f"pf{n}": ([n], [n]) for n in (8, 32, 128, 256, 512, 1024, 2048, 4096)}
@@ -99,12 +101,13 @@ def main():
                                       "kv_TBps": round(kvb / us / 1e6, 2)}), flush=True)
         return
     for name, (ql, cl) in cases.items():
-        for pad in ((0,) if a.scan else (0, a.pad)):
-            args, kvb, fl, n = setup(ql, cl, pad_items=pad)
-            us = timeit(args, a.iters)
-            print(json.dumps({"case": name, "items": n, "grid_items": args[6].shape[0], "us": round(us, 1),
-                              "kv_TBps": round(kvb / us / 1e6, 2), "TFLOPs": round(fl / us / 1e6, 1)}),
-                  flush=True)
+        for qcols in (32, 128):
+            for pad in ((0,) if a.scan else (0, a.pad)):
+                args, kvb, fl, n = setup(ql, cl, pad_items=pad, qcols=qcols)
+                us = timeit(args, a.iters)
+                print(json.dumps({"case": name, "qcols": qcols, "items": n, "grid_items": args[6].shape[0],
+                                  "us": round(us, 1), "kv_TBps": round(kvb / us / 1e6, 2),
+                                  "TFLOPs": round(fl / us / 1e6, 1)}), flush=True)
 
 
 if __name__ == "__main__":
