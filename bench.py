@@ -71,6 +71,11 @@ def parse():
     ap.add_argument("--cpu", action="store_true", help="tiny model on CPU (plumbing smoke only)")
     ap.add_argument("--dp-mode", choices=["node", "independent"], default="node",
                     help="node: one manager over the node-wide pool; independent: one Serve per rank")
+    ap.add_argument("--reply-tokens", type=int, default=None,
+                    help="fixed length of every reply's free-text slot (workload sensitivity; default: schema sizes)")
+    ap.add_argument("--memory-rows", type=int, default=0,
+                    help="semantic memory on the engine's GPU with this many rows; every agent step looks it up")
+    ap.add_argument("--memory-top-k", type=int, default=3)
     ap.add_argument("--share-gpu", action="store_true",
                     help="rehearsal: every rank on GPU 0 (use with PILOTTAI_DIST_BACKEND=gloo)")
     return ap.parse_args()
@@ -95,12 +100,16 @@ async def run_rank(a, rank: int, world: int, device):
 
     n_local = len(shard_workers(a.workers, world, rank))
     t_init = time.time()
+    memory = lookup = None
+    if a.memory_rows > 0:
+        # before the engine sizes its KV pool: the index is resident beside the model
+        memory, lookup = build_memory(a, device)
     eng = LLMEngine(EngineConfig(model=a.model if not a.cpu else "tiny", max_num_seqs=max(64, 2 * n_local),
                                  max_num_batched_tokens=a.max_batched_tokens, kv_cache_gb=a.kv_gb if not a.cpu else None,
                                  num_kv_blocks=4096 if a.cpu else None, seed=1234 + rank,
                                  token_align=a.token_align, align_slack=a.align_slack,
                                  decode_fused_max_t=a.fused_max_t, wide_max_t=a.wide_max_t,
-                                 mid_max_t=a.mid_max_t), device=device)
+                                 mid_max_t=a.mid_max_t, reply_tokens=a.reply_tokens), device=device)
     register_engine(eng.model_cfg.name, eng)
     eng.start()
     llm = LocalLLM(LLMConfig(model_name=eng.model_cfg.name, temperature=a.temperature, max_tokens=1024,
@@ -112,7 +121,8 @@ async def run_rank(a, rank: int, world: int, device):
                           backstory="A careful analyst agent in a document-processing workflow.",
                           max_iterations=a.steps_per_task + 1, task_timeout=900)
         agents.append(BaseAgent(cfg, llm=llm, tools=[Tool(name="echo", description="identity tool",
-                                                          function=echo_tool, max_retries=1)], policy=policy))
+                                                          function=echo_tool, max_retries=1)], policy=policy,
+                                memory_lookup=lookup, memory_top_k=a.memory_top_k))
     node = a.dp_mode == "node" and world > 1
     serve_cfg = {"name": f"bench-r{rank}", "policy": "fixed", "steps_per_task": a.steps_per_task,
                  "max_queue_size": 100000, "task_timeout": 900, "agent_wait_timeout": 900}
@@ -180,6 +190,7 @@ async def run_rank(a, rank: int, world: int, device):
         await round_(a.warmup, False)
     await coll(comm.barrier)  # worker ranks keep serving the plane meanwhile
     st0 = dict(eng.stats)  # after the barrier: every rank's warmup work is behind it
+    mem0 = dict(lookup.stats, device_s=lookup.lookup_device_seconds()) if lookup is not None else None
     bh0 = {b: list(v) for b, v in eng.bucket_hist.items()}
     u0 = dict(llm.usage)
     n_timed0 = len(eng.timings)
@@ -194,6 +205,24 @@ async def run_rank(a, rank: int, world: int, device):
     st1 = dict(eng.stats)
     u1 = dict(llm.usage)
     em = eng.metrics()
+    mem = None
+    if lookup is not None:
+        dev_s = lookup.lookup_device_seconds()
+        mem = {"rows": memory.index.count, "index_gb": round(memory.index.memory_bytes() / 2**30, 2),
+               "lookups": lookup.stats["lookups"] - mem0["lookups"],
+               "passes": lookup.stats["passes"] - mem0["passes"],
+               "stores": lookup.stats["stores"] - mem0["stores"],
+               # HIP events around each pass on the lookup stream (includes any wait for
+               # CUs the engine holds: an upper bound on the passes' kernel time)
+               "lookup_device_s": round(dev_s - mem0["device_s"], 3),
+               "lookup_ms_per_pass": round(1000 * (dev_s - mem0["device_s"]) /
+                                                  max(1, lookup.stats["passes"] - mem0["passes"]), 2)}
+    node_load = None
+    if world > 1 and a.dp_mode == "independent":
+        # node-wide load picture (parallel/agent_dp.py GlobalLoadView) after the run
+        from pilottai_amd.parallel.agent_dp import GlobalLoadView, local_load
+
+        node_load = (await coll(GlobalLoadView().update, local_load(serve)))
     requeued = 0
     if plane is not None:
         requeued = int(serve.metrics.get("requeued_tasks", 0))
@@ -214,13 +243,46 @@ async def run_rank(a, rank: int, world: int, device):
         "prompt_tokens": u1["prompt_tokens"] - u0["prompt_tokens"],
         "completion_tokens": u1["completion_tokens"] - u0["completion_tokens"],
         "busy_s": st1["busy_s"] - st0["busy_s"], "prefix_hit": em["prefix_cache_hit_tokens"],
+        "host_phases": {k: st1[k] - st0[k] for k in ("host_sched_s", "host_launch_s", "device_wait_s",
+                                                     "host_commit_s", "host_deliver_s")},
         "bucket_tokens": st1["bucket_tokens"] - st0["bucket_tokens"],
         "prompt_total": em["prompt_tokens"], "hbm_used_gb": em.get("hbm_used_gb", 0.0),
-        "req_lat": eng.latency_summary(n_timed0),
+        "req_lat": eng.latency_summary(n_timed0), "memory": mem, "node_load": node_load,
         "buckets": {b: [v[0] - bh0.get(b, [0, 0.0])[0], v[1] - bh0.get(b, [0, 0.0])[1]]
                     for b, v in eng.bucket_hist.items()},
     }
     return local
+
+
+def build_memory(a, device):
+    """Semantic memory co-resident with the engine: an EnhancedMemory
+    whose HBM index holds `a.memory_rows` rows (random unit vectors standing in for an
+    archive of past findings, filled on the device in 1M-row chunks) plus whatever the
+    agents write back; one MemoryLookupBatcher shared by the rank's agents."""
+    import torch
+
+    from pilottai_amd.memory.batcher import MemoryLookupBatcher
+    from pilottai_amd.memory.enhanced_memory import EnhancedMemory
+
+    dim = 1024
+    cap = a.memory_rows + 65536  # room for the run's write-backs
+    mem = EnhancedMemory(max_size=cap, device=device, dim=dim,
+                         fallback_text=lambda r: f"archived finding {r}: prior document review notes")
+    idx = mem.index
+    idx._grow(cap)
+    g = torch.Generator(device=device).manual_seed(7)
+    tags = [idx.tags.bit(t) for t in ("archive", "finance", "ops", "legal")]
+    done = 0
+    while done < a.memory_rows:
+        m = min(1 << 20, a.memory_rows - done)
+        v = torch.randn(m, dim, device=device, generator=g, dtype=torch.float32)
+        pr = torch.randint(0, 3, (m,), device=device, dtype=torch.int32, generator=g)
+        tb = (1 << tags[0]) | (1 << torch.randint(1, 4, (m,), device=device, generator=g)).to(torch.int64)
+        idx.add_device(v, pr, tb)
+        done += m
+    if device.type == "cuda":
+        torch.cuda.synchronize(device)
+    return mem, MemoryLookupBatcher(mem)
 
 
 def _launch_ranks(n: int) -> int:
@@ -312,6 +374,10 @@ def main():
             "engine_busy_frac": round(tot("busy_s") / (dt * len(gathered)), 3),
             "prefix_cache_hit_frac": round(tot("prefix_hit") / max(1, tot("prompt_total")), 3),
             "graph_pad_frac": round(1 - tot("tokens") / max(1, tot("bucket_tokens")), 3),
+            # rank 0's engine thread, ms per step: schedule / copy+launch / wait for the device /
+            # commit / deliver (the host phases are the device's idle time between steps)
+            "step_phase_ms": {k.replace("_s", ""): round(1000 * v / max(1, gathered[0]["steps"]), 3)
+                              for k, v in gathered[0]["host_phases"].items()},
             "ttft_p50_ms": round(lat0.get("ttft_p50_ms") or 0.0, 1),
             "tpot_p50_ms": round(lat0.get("tpot_p50_ms") or 0.0, 2),
             "init_s": round(max(g["init_s"] for g in gathered), 1),
@@ -319,6 +385,9 @@ def main():
             # rank 0's engine steps per graph bucket: [steps, ms per step]
             "step_buckets": {str(b): [v[0], round(1000 * v[1] / max(1, v[0]), 2)]
                              for b, v in sorted(gathered[0]["buckets"].items()) if v[0] > 0},
+            "reply_tokens": a.reply_tokens,
+            "memory": gathered[0]["memory"],
+            "node_load": gathered[0]["node_load"],
             "notes": "BASELINE.md publishes no number for this config (vs_baseline null); the reference's "
                      "structural bound with a remote LLM is ~0.8 tasks/s per LLMHandler (BASELINE.md §2).",
         }

@@ -22,6 +22,7 @@ void Grammar::next(int32_t* cls, int32_t* forced) const {
       return;
     case Segment::STR:
       if (pos_ >= s.max_tokens) *forced = s.end_tok;
+      else if (s.cls_last >= 0 && pos_ < s.min_items) *cls = s.cls_last;  // body shorter than its minimum
       else *cls = s.cls;
       return;
     case Segment::LIST:

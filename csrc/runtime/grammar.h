@@ -8,6 +8,8 @@
 //   CHOICE exactly one token from a mask class   (true/false, low/medium/high, 1..10)
 //   STR    free string body from a class that also contains the closing-quote
 //          token; the body ends when that token is sampled or max_tokens is hit
+//          (with cls_last >= 0: the first min_items body tokens come from cls_last,
+//          a class without the quote — a reply of a fixed minimum length)
 //   LIST   list of strings; class contains the body, the separator '", "' and the
 //          close '"]'; min/max item counts bound the work
 //

@@ -96,7 +96,7 @@ class BaseAgent:
                  allow_delegation: Optional[bool] = None, tools: Optional[Sequence[Any]] = None,
                  step_callback: Optional[Callable] = None, *, agent_config: Optional[AgentConfig] = None,
                  llm_config: Optional[Union[LLMConfig, dict]] = None, policy: Optional[ControlPolicy] = None,
-                 memory: Any = None):
+                 memory: Any = None, memory_lookup: Any = None, memory_top_k: int = 3):
         # --- accept BaseAgent(agent_config, llm_config) and factory-style cls(config)
         if isinstance(role, AgentConfig):
             agent_config, role = role, None
@@ -147,6 +147,11 @@ class BaseAgent:
         self.child_agents: Dict[str, "BaseAgent"] = {}
         self.parent: Optional["BaseAgent"] = None
         self._memory = memory
+        # per-step semantic memory (memory/batcher.py MemoryLookupBatcher, shared by the
+        # agents of a Serve): every step-planning call carries the top-k hits for the
+        # task + last result, and each finished task is written back
+        self.memory_lookup = memory_lookup
+        self.memory_top_k = int(memory_top_k)
         self.last_error: Optional[str] = None
         self.last_heartbeat = datetime.now()
         self._accepting = True
@@ -409,6 +414,7 @@ class BaseAgent:
             steps, iterations = await self._execute_steps(task, chosen)
             evaluation = await self._evaluate_result(task, steps)
             ok = bool(evaluation.get("success", False))
+            await self._remember(task, ok, evaluation)
             return TaskResult(success=ok, output=steps, error=None if ok else evaluation.get("reasoning", "evaluation failed"),
                               execution_time=time.perf_counter() - t0,
                               metadata={"analysis": analysis, "tools_used": selection, "evaluation": evaluation,
@@ -480,12 +486,13 @@ class BaseAgent:
                 return [{"role": "user", "content": f"{head}\n\n{system.rstrip()}\n\n{tail}"}]
         return [{"role": "system", "content": system}, {"role": "user", "content": prompt}]
 
-    async def _llm_json(self, kind: str, fixed: Optional[Dict[str, Any]] = None, **kw) -> Dict[str, Any]:
+    async def _llm_json(self, kind: str, fixed: Optional[Dict[str, Any]] = None, schema: Optional[str] = None,
+                        **kw) -> Dict[str, Any]:
         prompt = self.prompts.format_prompt(kind, **kw)
         system = self.prompts.format_prompt("system_base", role=self.config.role, goal=self.config.goal,
                                             backstory=self.config.backstory or "No specific backstory.")
         messages = self._compose_messages(system, prompt)
-        rf = {"schema": f"agent.{kind}", "fixed": fixed or {}}
+        rf = {"schema": f"agent.{schema or kind}", "fixed": fixed or {}}
         try:
             resp = await self.llm.generate_response(messages, response_format=rf)
         except TypeError:  # a third-party LLM without structured-output support
@@ -519,10 +526,15 @@ class BaseAgent:
             fixed = self.policy.step_planning(iterations, tool)
             if self.policy.fixed_mode:
                 fixed["next_step.inputs"] = step_inputs
-            plan = await self._llm_json("step_planning", fixed, task_description=task.description,
-                                        completed_steps=json.dumps(_short(completed, 800)),
-                                        available_tools=json.dumps(tools),
-                                        last_result=json.dumps(_short(completed[-1] if completed else None)))
+            last = json.dumps(_short(completed[-1] if completed else None))
+            common = dict(task_description=task.description, completed_steps=json.dumps(_short(completed, 800)),
+                          available_tools=json.dumps(tools), last_result=last)
+            if self.memory_lookup is not None and self.memory_top_k > 0:
+                ctx = await self._memory_context(task, last)
+                plan = await self._llm_json("step_planning_memory", fixed, schema="step_planning",
+                                            memory_context=ctx, **common)
+            else:
+                plan = await self._llm_json("step_planning", fixed, **common)
             if plan.get("task_complete", False):
                 break
             step = plan.get("next_step") or {k: plan[k] for k in ("tool", "inputs") if k in plan}
@@ -534,6 +546,28 @@ class BaseAgent:
                 await self._execute_callback(self.step_callback, step=step, result=result,
                                              context={"task": task.id, "completed_steps": completed})
         return completed, iterations
+
+    async def _memory_context(self, task: Task, last_result: str) -> str:
+        """Top-k memory hits for this step (one batched index pass per event-loop tick
+        across all agents), as a short text block for the step-planning prompt."""
+        query = f"{task.description[:400]} {last_result[:200]}"
+        try:
+            hits = await self.memory_lookup.search(query, limit=self.memory_top_k)
+        except Exception as e:  # noqa: BLE001 — memory is advisory (reference: warn and go on)
+            self.logger.warning("memory search failed: %s", e)
+            return "none"
+        return "; ".join(h.text[:160] for h in hits) or "none"
+
+    async def _remember(self, task: Task, ok: bool, evaluation: Dict[str, Any]):
+        if self.memory_lookup is None or self.memory_top_k <= 0:
+            return
+        try:
+            await self.memory_lookup.store(
+                f"{task.description[:300]} => {'done' if ok else 'failed'}: {str(evaluation.get('reasoning', ''))[:200]}",
+                metadata={"task_id": task.id, "agent": self.id, "success": ok}, tags={self.config.role},
+                priority=1 if ok else 0)
+        except Exception as e:  # noqa: BLE001
+            self.logger.warning("memory store failed: %s", e)
 
     async def _execute_step(self, step: Dict[str, Any]) -> Any:
         name = step.get("tool")

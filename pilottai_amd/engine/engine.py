@@ -82,6 +82,7 @@ class EngineConfig:
     mid_max_t: Optional[int] = None  # largest step on the LDS-DMA tiled mid-size path; None = model default
     att_qcols: int = 128  # prefill attention item width in MFMA columns (128: LDS-staged 4-wave items)
     att_wide_min_tokens: int = 2048  # ... used only for steps with at least this many prefill tokens
+    reply_tokens: Optional[int] = None  # fixed length of every reply schema's free-text slot (grammar.py)
 
 
 # TP step header: [op, T, ns, nsamp, bucket, masks_changed, n_copy, truncate]
@@ -152,7 +153,7 @@ class LLMEngine:
             torch.cuda.set_device(self.device)
         self.tp = tp or TPGroup.single()
         self.tok = tokenizer or get_tokenizer()
-        self.grammar = GrammarCompiler(self.tok)
+        self.grammar = GrammarCompiler(self.tok, reply_tokens=cfg.reply_tokens)
         self.model_cfg = get_config(cfg.model)
         mc = self.model_cfg
         if self.on_gpu:
@@ -252,7 +253,8 @@ class LLMEngine:
         self.timings: "deque" = deque(maxlen=1 << 20)  # (ttft_s, tpot_s, output_tokens) per request
         self.stats = {"steps": 0, "tokens": 0, "sampled": 0, "requests": 0, "finished": 0,
                       "busy_s": 0.0, "prefill_tokens": 0, "decode_steps": 0, "graph_replays": 0,
-                      "bucket_tokens": 0}
+                      "bucket_tokens": 0, "host_sched_s": 0.0, "host_launch_s": 0.0, "device_wait_s": 0.0,
+                      "host_commit_s": 0.0, "host_deliver_s": 0.0}
         self.bucket_hist: Dict[int, list] = {}  # bucket -> [steps, seconds]
         # custom all-reduce health: its spin-waits give up after ~5 s and set an error word
         # instead of hanging; the word is copied back with every step and checked after the
@@ -579,6 +581,7 @@ class LLMEngine:
         t0 = time.perf_counter()
         with trace_range("engine.schedule"):
             T = self.sched.schedule(self._host_ptr)
+        t_sched = time.perf_counter()
         if T == 0:
             if self.sched.num_running == 0 and self.sched.num_waiting > 0:
                 raise RuntimeError("KV cache too small for the head request")
@@ -601,12 +604,18 @@ class LLMEngine:
         if nsamp:
             self._sampled_host[:nsamp].copy_(self._sampled_dev[:nsamp], non_blocking=self.on_gpu)
         self._car_fetch()
+        t_launch = time.perf_counter()
         if self.on_gpu:
             torch.cuda.current_stream().synchronize()
         self._car_check()
+        t_sync = time.perf_counter()
         with trace_range("engine.commit"):
             outs = self.sched.commit(self._sampled_host.data_ptr(), nsamp)
         st = self.stats
+        # host-side phases: schedule, metadata copy + launch, device wait, commit
+        st["host_sched_s"] += t_sched - t0
+        st["host_launch_s"] += t_launch - t_sched
+        st["device_wait_s"] += t_sync - t_launch
         st["steps"] += 1
         st["tokens"] += T
         st["bucket_tokens"] += bucket
@@ -616,8 +625,11 @@ class LLMEngine:
         bh = self.bucket_hist.setdefault(bucket, [0, 0.0])
         bh[0] += 1
         bh[1] += dt
+        t_deliver = time.perf_counter()
         for o in outs:
             self._deliver(o)
+        st["host_commit_s"] += t_deliver - t_sync
+        st["host_deliver_s"] += time.perf_counter() - t_deliver
         return True
 
     def _loop(self):

@@ -52,6 +52,7 @@ class MaskRegistry:
         for t in (self.quote, self.list_sep, self.list_close):
             assert t >= 0
         self.cls_str = self._add("str", self._safe | self._onehot([self.quote]))
+        self.cls_str_body = self._add("str_body", self._safe.copy())  # no closing quote: forced length
         self.cls_list = self._add("list", self._safe | self._onehot([self.list_sep, self.list_close]))
         self.cls_list_last = self._add("list_last", self._safe | self._onehot([self.list_close]))
         self.cls_bool = self.enum(["true", "false"])
@@ -95,11 +96,25 @@ class MaskRegistry:
 
 _TYPE_RE = re.compile(r"^(\w+)\((.*)\)$")
 
+# The free-text slot of each reply schema that `reply_tokens` resizes (the workload
+# sensitivity knob of bench.py --reply-tokens); schemas without one get a trailing
+# "notes" string. The reference's replies are unconstrained prose up to
+# max_tokens=2000 (pilott/core/config.py:52); the default schemas keep them short.
+REPLY_SLOTS = {
+    "agent.task_analysis": "alignment",
+    "agent.step_planning": "next_step.expected_outcome",
+    "agent.result_evaluation": "reasoning",
+    "workflow.summarize": "summary",
+}
+
 
 class GrammarCompiler:
-    def __init__(self, tok: Tokenizer, reg: Optional[MaskRegistry] = None):
+    def __init__(self, tok: Tokenizer, reg: Optional[MaskRegistry] = None, reply_tokens: Optional[int] = None):
         self.tok = tok
         self.reg = reg or MaskRegistry(tok)
+        # reply_tokens = N: every named schema's free-text slot (REPLY_SLOTS, else an added
+        # "notes" field) is exactly N tokens long — N sampled tokens per call at least
+        self.reply_tokens = int(reply_tokens) if reply_tokens else None
         self._cache: Dict[Tuple[str, str], List[Segment]] = {}
         self._lock = threading.Lock()
         # pre-register every class used by the shipped schemas so the GPU mask
@@ -119,8 +134,14 @@ class GrammarCompiler:
             spec = load_schemas()[schema]
         else:
             spec = schema
+        reply = None
+        if self.reply_tokens and isinstance(schema, str) and isinstance(spec, dict):
+            reply = REPLY_SLOTS.get(schema)
+            if reply is None:
+                spec = {**spec, "notes": f"str({self.reply_tokens})"}
+                reply = "notes"
         parts: List[Any] = []
-        self._value(spec, "", fixed, parts)
+        self._value(spec, "", fixed, parts, reply)
         segs = self._finalize(parts)
         if key is not None:
             with self._lock:
@@ -134,7 +155,7 @@ class GrammarCompiler:
         else:
             parts.append(text)
 
-    def _value(self, spec: Any, path: str, fixed: Dict[str, Any], parts: List[Any]):
+    def _value(self, spec: Any, path: str, fixed: Dict[str, Any], parts: List[Any], reply: Optional[str] = None):
         if path in fixed:
             self._lit(parts, json.dumps(fixed[path]))
             return
@@ -145,13 +166,13 @@ class GrammarCompiler:
                 for i in range(n):
                     if i:
                         self._lit(parts, ", ")
-                    self._value(spec["item"], f"{path}[{i}]", fixed, parts)
+                    self._value(spec["item"], f"{path}[{i}]", fixed, parts, reply)
                 self._lit(parts, "]")
                 return
             self._lit(parts, "{")
             for i, (k, v) in enumerate(spec.items()):
                 self._lit(parts, (", " if i else "") + json.dumps(str(k)) + ": ")
-                self._value(v, f"{path}.{k}" if path else str(k), fixed, parts)
+                self._value(v, f"{path}.{k}" if path else str(k), fixed, parts, reply)
             self._lit(parts, "}")
             return
         s = str(spec).strip()
@@ -168,7 +189,11 @@ class GrammarCompiler:
             parts.append((CHOICE, [], reg.int_range(lo, hi), -1, -1, -1, 0, 1, 1))
         elif kind == "str":
             self._lit(parts, '"')
-            parts.append((STR, [], reg.cls_str, -1, reg.quote, -1, int(arg), 1, 1))
+            if reply is not None and path == reply:
+                n = self.reply_tokens
+                parts.append((STR, [], reg.cls_str, reg.cls_str_body, reg.quote, -1, n, n, 1))
+            else:
+                parts.append((STR, [], reg.cls_str, -1, reg.quote, -1, int(arg), 1, 1))
         elif kind == "enum":
             self._lit(parts, '"')
             parts.append((CHOICE, [], reg.enum(arg.split("|")), -1, -1, -1, 0, 1, 1))

@@ -1,0 +1,105 @@
+"""Per-step semantic-memory lookups from many agents, coalesced into one index pass.
+
+The reference's agents consult memory inside their work, one query at a time
+(pilott/memory/enhanced_memory.py:93-116 `semantic_search`, called from
+docs/examples/pdf_processing/example_agents.py:328-331). With 64 workers on one
+GPU that is 64 separate scans of the index per agent step. Here every agent step
+`await`s `MemoryLookupBatcher.search(...)`; the requests that arrive within one
+event-loop tick are answered by ONE `EnhancedMemory.search_batch` call, i.e. one
+streaming pass of the HIP cosine top-k kernel over the HBM-resident rows
+(csrc/ops/similarity.hip, up to 64 queries per pass), on the same GPU as the
+engine. Writes (`store`) are coalesced the same way.
+
+`stats` reports lookups, passes and the device time of the passes (HIP events around
+the kernel on the index's own stream; beside a busy engine that span also contains any
+wait for CUs the engine holds, so it bounds the kernel time from above).
+"""
+from __future__ import annotations
+
+import asyncio
+import time
+from typing import Any, Dict, List, Optional, Set, Tuple
+
+from .enhanced_memory import EnhancedMemory, MemoryItem
+
+
+class MemoryLookupBatcher:
+    def __init__(self, memory: EnhancedMemory, max_batch: int = 256, time_device: bool = True):
+        self.memory = memory
+        self.max_batch = max_batch
+        self.time_device = time_device
+        self._pending: List[Tuple[str, Optional[Set[str]], int, int, "asyncio.Future"]] = []
+        self._writes: List[Tuple[str, Dict[str, Any], Set[str], int, "asyncio.Future"]] = []
+        self._flush_scheduled = False
+        if time_device and getattr(getattr(memory.index, "device", None), "type", "cpu") == "cuda":
+            memory.index.pass_events = []  # the index records (start, end) around each pass
+        self.stats = {"lookups": 0, "passes": 0, "stores": 0, "store_batches": 0, "host_s": 0.0,
+                      "device_s": 0.0, "max_batch_seen": 0}
+
+    # ----------------------------------------------------------------- API
+    async def search(self, query: str, limit: int = 5, tags: Optional[Set[str]] = None,
+                     min_priority: int = 0) -> List[MemoryItem]:
+        fut = asyncio.get_running_loop().create_future()
+        self._pending.append((query, tags, int(min_priority), int(limit), fut))
+        self._schedule()
+        return await fut
+
+    async def store(self, text: str, metadata: Optional[Dict[str, Any]] = None, tags: Optional[Set[str]] = None,
+                    priority: int = 0) -> int:
+        fut = asyncio.get_running_loop().create_future()
+        self._writes.append((text, dict(metadata or {}), set(tags or ()), int(priority), fut))
+        self._schedule()
+        return await fut
+
+    def lookup_device_seconds(self) -> float:
+        """Device time of every finished lookup pass so far (synchronises the events)."""
+        evs = getattr(self.memory.index, "pass_events", None) or []
+        while evs:
+            a, b = evs.pop(0)
+            b.synchronize()
+            self.stats["device_s"] += a.elapsed_time(b) / 1e3
+        return self.stats["device_s"]
+
+    # ----------------------------------------------------------------- batching
+    def _schedule(self):
+        if not self._flush_scheduled:
+            self._flush_scheduled = True
+            asyncio.get_running_loop().call_soon(self._start_flush)
+
+    def _start_flush(self):
+        self._flush_scheduled = False
+        asyncio.ensure_future(self._flush())
+
+    async def _flush(self):
+        writes, self._writes = self._writes, []
+        if writes:
+            try:
+                rows = await self.memory.store_semantic_batch([w[0] for w in writes], [w[1] for w in writes],
+                                                              [w[2] for w in writes], [w[3] for w in writes])
+                for w, r in zip(writes, rows):
+                    if not w[4].done():
+                        w[4].set_result(r)
+            except Exception as e:  # noqa: BLE001
+                for w in writes:
+                    if not w[4].done():
+                        w[4].set_exception(e)
+            self.stats["stores"] += len(writes)
+            self.stats["store_batches"] += 1
+        while self._pending:
+            batch, self._pending = self._pending[: self.max_batch], self._pending[self.max_batch:]
+            limit = max(b[3] for b in batch)
+            t0 = time.perf_counter()
+            try:
+                hits = await self.memory.search_batch([b[0] for b in batch], tags=[b[1] for b in batch],
+                                                      min_priority=[b[2] for b in batch], limit=limit)
+                for b, h in zip(batch, hits):
+                    if not b[4].done():
+                        b[4].set_result(h[: b[3]])
+            except Exception as e:  # noqa: BLE001
+                for b in batch:
+                    if not b[4].done():
+                        b[4].set_exception(e)
+            self.stats["host_s"] += time.perf_counter() - t0
+            self.stats["lookups"] += len(batch)
+            self.stats["passes"] += 1
+            self.stats["max_batch_seen"] = max(self.stats["max_batch_seen"], len(batch))

@@ -17,7 +17,7 @@ from __future__ import annotations
 import asyncio
 from collections import deque
 from datetime import datetime, timedelta
-from typing import Any, Deque, Dict, List, Optional, Sequence, Set
+from typing import Any, Callable, Deque, Dict, List, Optional, Sequence, Set
 
 from pydantic import BaseModel, ConfigDict, Field
 
@@ -41,7 +41,8 @@ class MemoryItem(BaseModel):
 
 class EnhancedMemory:
     def __init__(self, max_size: int = 10000, cleanup_interval: float = 3600, embedder=None,
-                 index: Optional[SemanticIndex] = None, dim: int = 1024, device=None):
+                 index: Optional[SemanticIndex] = None, dim: int = 1024, device=None,
+                 fallback_text: Optional[Callable[[int], str]] = None):
         self.max_size = max_size
         self.cleanup_interval = cleanup_interval
         self.embedder = embedder or HashingEmbedder(dim)
@@ -59,6 +60,9 @@ class EnhancedMemory:
         self._interaction_lock = asyncio.Lock()
         self._pattern_lock = asyncio.Lock()
         self._cleanup_task: Optional[asyncio.Task] = None
+        # rows bulk-loaded on the device (SemanticIndex.add_device) have no host-side
+        # MemoryItem; with fallback_text their hits are returned as MemoryItem(text=...)
+        self.fallback_text = fallback_text
 
     async def start(self):
         if self._cleanup_task is None:
@@ -119,11 +123,22 @@ class EnhancedMemory:
         async with self._semantic_lock:
             if mode == "substring":
                 return [self._substring(q, t, p, limit) for q, t, p in zip(queries, tags, minp)]
-            vecs = self.embedder(list(queries))
-            hits = self.index.search(vecs, limit, minp, [t or () for t in tags])
+
+            def run():
+                vecs = self.embedder(list(queries))
+                return self.index.search(vecs, limit, minp, [t or () for t in tags])
+
+            if getattr(self.index.device, "type", "cpu") == "cuda":
+                # embed + one kernel pass + wait in a worker thread: the event loop (all
+                # the agents) keeps running while the pass is on the GPU
+                hits = await asyncio.get_running_loop().run_in_executor(None, run)
+            else:
+                hits = run()
         out = []
         for lst in hits:
             items = [self._items[r] for r, _ in lst if r in self._items and not self._items[r].is_expired()]
+            if self.fallback_text is not None:
+                items += [MemoryItem(text=self.fallback_text(r)) for r, _ in lst if r not in self._items]
             out.append(sorted(items, key=lambda x: (-x.priority, x.timestamp)))
         return out
 

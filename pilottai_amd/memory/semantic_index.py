@@ -77,6 +77,8 @@ class SemanticIndex:
         self.epoch = time.time()
         self._lock = threading.Lock()
         self._ws: Optional[torch.Tensor] = None
+        self._stream = None
+        self.pass_events: Optional[list] = None  # set to [] to time every search pass (HIP events)
 
     def _alloc(self, cap: int):
         d = self.device
@@ -241,12 +243,19 @@ class SemanticIndex:
         if n == 0:
             return [[] for _ in range(Q)]
         kk = k if all(exact) else min(64, 4 * k)
-        with self._lock:
+        with self._lock, self._stream_ctx():
             qd = torch.nn.functional.normalize(q, dim=1).to(self.device, torch.bfloat16)
             minp = torch.tensor(list(min_priority), dtype=torch.int32, device=self.device)
             qt = torch.tensor(qmasks, dtype=torch.int64, device=self.device)
+            ev = None
+            if self.pass_events is not None and self.device.type == "cuda":
+                ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                ev[0].record()
             s, r = ops.cosine_topk(qd, self.packed, n, kk, self.priority, self.tagbits, self.expiry, minp, qt,
                                    self.now() if now is None else now - self.epoch, workspace=self._ws)
+            if ev is not None:
+                ev[1].record()
+                self.pass_events.append(ev)
             s, r = s.cpu().numpy(), r.cpu().numpy()
         out = []
         for i in range(Q):
@@ -261,6 +270,25 @@ class SemanticIndex:
                     break
             out.append(res)
         return out
+
+    def _stream_ctx(self):
+        """Searches run on the index's own HIP stream (non-blocking w.r.t. the engine's):
+        co-resident with a serving engine, a lookup pass overlaps the engine's step
+        instead of queueing behind its graph, and waiting for the result syncs only
+        this stream. Also pins the calling thread to the index's device."""
+        import contextlib
+
+        if self.device.type != "cuda":
+            return contextlib.nullcontext()
+        if self._stream is None:
+            # high priority: a lookup pass is on an agent step's critical path, and at
+            # normal priority its workgroups wait behind the engine's (10M rows: 36 ms
+            # per pass beside a 64-worker engine vs ~4 ms alone)
+            self._stream = torch.cuda.Stream(device=self.device, priority=-1)
+        st = contextlib.ExitStack()
+        st.enter_context(torch.cuda.device(self.device))
+        st.enter_context(torch.cuda.stream(self._stream))
+        return st
 
     def memory_bytes(self) -> int:
         return self.packed.numel() * 2 + self.capacity * (4 + 8 + 4)
@@ -299,9 +327,10 @@ class ShardedSemanticIndex:
                 t[i, j, 1] = sc
         dev = self.local.device if dist.get_backend(self.group) == "nccl" else torch.device("cpu")
         t = t.to(dev)
-        allt = torch.empty((self.world,) + tuple(t.shape), dtype=t.dtype, device=dev)
-        dist.all_gather_into_tensor(allt, t, group=self.group)
-        allt = allt.cpu()
+        # output concatenated along dim 0 (the form both gloo and RCCL accept)
+        flat = torch.empty((self.world * Q,) + tuple(t.shape[1:]), dtype=t.dtype, device=dev)
+        dist.all_gather_into_tensor(flat, t, group=self.group)
+        allt = flat.view((self.world,) + tuple(t.shape)).cpu()
         out = []
         for i in range(Q):
             cand = allt[:, i].reshape(-1, 2)

@@ -1,0 +1,140 @@
+"""Semantic memory inside the agent loop (memory/batcher.py + core/agent.py) and the
+row-sharded index (memory/semantic_index.py ShardedSemanticIndex) on gloo ranks.
+
+Reference behaviour being reproduced: agents consult memory while they work
+(pilott/memory/enhanced_memory.py:93-116, docs/examples/pdf_processing/
+example_agents.py:328-331); here the lookups of concurrent agents are coalesced into
+one index pass per event-loop tick.
+"""
+import asyncio
+import multiprocessing as mp
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+
+from pilottai_amd.core.agent import BaseAgent
+from pilottai_amd.core.config import AgentConfig
+from pilottai_amd.core.policy import ControlPolicy
+from pilottai_amd.core.task import Task
+from pilottai_amd.engine.local_llm import SchemaLLM
+from pilottai_amd.memory.batcher import MemoryLookupBatcher
+from pilottai_amd.memory.enhanced_memory import EnhancedMemory
+from pilottai_amd.memory.semantic_index import SemanticIndex, ShardedSemanticIndex
+from pilottai_amd.tools.tool import Tool, echo_tool
+
+
+class _RecordingLLM(SchemaLLM):
+    def __init__(self):
+        super().__init__(seed=0)
+        self.prompts = []
+
+    async def generate_response(self, messages, tools=None, response_format=None):
+        self.prompts.append(messages[-1]["content"])
+        return await super().generate_response(messages, tools=tools, response_format=response_format)
+
+
+def test_agents_consult_memory_every_step_in_batched_passes():
+    async def go():
+        mem = EnhancedMemory(max_size=4096, device="cpu")
+        await mem.store_semantic_batch([f"prior finding {i}: quarterly revenue of unit {i} grew" for i in range(40)],
+                                       tags=[{"worker"}] * 40, priorities=[1] * 40)
+        lookup = MemoryLookupBatcher(mem)
+        llm = _RecordingLLM()
+        pol = ControlPolicy("fixed", 2)
+        agents = [BaseAgent(AgentConfig(role="worker", goal="Summarize documents", max_iterations=2), llm=llm,
+                            tools=[Tool(name="echo", description="identity", function=echo_tool, max_retries=1)],
+                            policy=pol, memory_lookup=lookup, memory_top_k=2) for _ in range(8)]
+        for a in agents:
+            await a.start()
+        tasks = [Task(description=f"Summarize the revenue report of unit {i}") for i in range(8)]
+        res = await asyncio.gather(*(a.execute_task(t) for a, t in zip(agents, tasks)))
+        return res, lookup, mem, llm
+
+    res, lookup, mem, llm = asyncio.run(go())
+    assert all(r.success for r in res)
+    # 8 agents x 2 step-planning calls each; concurrent lookups share index passes
+    assert lookup.stats["lookups"] == 16
+    assert lookup.stats["passes"] < lookup.stats["lookups"]
+    assert lookup.stats["max_batch_seen"] >= 2
+    mem_prompts = [p for p in llm.prompts if "Relevant memory:" in p]
+    assert len(mem_prompts) == 16
+    assert any("quarterly revenue" in p for p in mem_prompts)
+    # every finished task was written back (batched stores)
+    assert lookup.stats["stores"] == 8 and len(mem) == 48
+    assert lookup.stats["store_batches"] < 8
+
+
+def test_memory_off_keeps_default_prompt():
+    async def go():
+        llm = _RecordingLLM()
+        a = BaseAgent(AgentConfig(role="worker", goal="g", max_iterations=1), llm=llm,
+                      tools=[Tool(name="echo", description="identity", function=echo_tool)],
+                      policy=ControlPolicy("fixed", 1))
+        await a.start()
+        r = await a.execute_task(Task(description="Summarize the document"))
+        return r, llm
+
+    r, llm = asyncio.run(go())
+    assert r.success and not any("Relevant memory" in p for p in llm.prompts)
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _rows(n, dim, seed=0):
+    g = np.random.default_rng(seed)
+    return g.standard_normal((n, dim)).astype(np.float32)
+
+
+def _shard_entry(rank, world, port, n, dim, q):
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        vecs = _rows(n, dim)
+        prio = [int(i % 5) for i in range(n)]
+        tags = [{"even"} if i % 2 == 0 else {"odd"} for i in range(n)]
+        local = SemanticIndex(dim=dim, capacity=64, device="cpu")
+        sh = ShardedSemanticIndex(local)
+        mine = list(range(rank, n, world))  # global row g = local_row * world + rank
+        ids = sh.add_local(vecs[mine], [prio[i] for i in mine], [tags[i] for i in mine], [None] * len(mine))
+        assert ids == mine
+        queries = _rows(6, dim, seed=1)
+        res = sh.search(queries, 5, [0, 0, 2, 0, 3, 0], [(), ("even",), (), ("odd",), ("even",), ()], now=None)
+        q.put((rank, res))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_sharded_index_topk_equals_single_index(world):
+    n, dim = 203, 64
+    vecs = _rows(n, dim)
+    single = SemanticIndex(dim=dim, capacity=256, device="cpu")
+    single.add(vecs, [int(i % 5) for i in range(n)], [{"even"} if i % 2 == 0 else {"odd"} for i in range(n)],
+               [None] * n)
+    queries = _rows(6, dim, seed=1)
+    ref = single.search(queries, 5, [0, 0, 2, 0, 3, 0], [(), ("even",), (), ("odd",), ("even",), ()])
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_shard_entry, args=(r, world, port, n, dim, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=30)
+        assert p.exitcode == 0
+    for r in range(world):  # every rank gets the same merged answer ...
+        assert [[row for row, _ in lst] for lst in got[r]] == [[row for row, _ in lst] for lst in got[0]]
+    for lst_s, lst_r in zip(got[0], ref):  # ... equal to one index holding all rows
+        assert [row for row, _ in lst_s] == [row for row, _ in lst_r]
+        np.testing.assert_allclose([s for _, s in lst_s], [s for _, s in lst_r], rtol=1e-5, atol=1e-5)

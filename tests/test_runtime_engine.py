@@ -70,6 +70,38 @@ def test_all_schemas_produce_valid_json_under_random_sampling(gc, tok):
         assert set(obj) == set(schemas[name]), name
 
 
+def test_reply_tokens_fix_the_free_text_length(tok):
+    """bench.py --reply-tokens N: each schema's free-text slot (or an added "notes" field)
+    is exactly N sampled tokens under random sampling — the quote is masked until N."""
+    from pilottai_amd.engine.grammar import REPLY_SLOTS
+
+    N = 40
+    gcr = GrammarCompiler(tok, reply_tokens=N)
+    masks = gcr.reg.packed().view(np.uint32)
+    rng = np.random.default_rng(1)
+    for name in ("agent.task_analysis", "agent.step_planning", "agent.result_evaluation",
+                 "orchestrator.task_analysis", "orchestrator.result_evaluation", "agent.tool_selection"):
+        segs = gcr.compile(name)
+        g = _runtime.Grammar(segs)
+        out, sampled = [], 0
+        while not g.done():
+            cls, f = g.next()
+            if f < 0:
+                allowed = np.nonzero(np.unpackbits(masks[cls].view(np.uint8), bitorder="little"))[0]
+                f = int(rng.choice(allowed))
+                sampled += 1
+            g.advance(f)
+            out.append(f)
+        obj = json.loads(tok.decode(out))
+        path = REPLY_SLOTS.get(name, "notes")
+        v = obj
+        for k in path.split("."):
+            v = v[k]
+        assert isinstance(v, str) and sampled >= N, (name, sampled)
+        assert len(tok.encode(v)) >= N - 2, name  # re-tokenisation may merge a few pieces
+        assert ("notes" in obj) == (name not in REPLY_SLOTS)
+
+
 def test_scheduler_prefix_cache_preemption_and_layout():
     L_cfg = {"num_blocks": 12, "block_size": 16, "max_num_seqs": 4, "max_num_batched_tokens": 64,
              "max_prefill_tokens": 64, "max_model_len": 128, "gqa_group": 4, "eos_ids": [128009]}
