@@ -428,7 +428,7 @@ class BaseAgent:
                 if lock is not None and lock.locked():
                     lock.release()
 
-    def prefetch_opening(self, task: Task, _store: bool = True) -> "asyncio.Future":
+    def prefetch_opening(self, task: Task, _store: bool = True) -> Optional["asyncio.Future"]:
         """Start a task's two opening LLM calls — task analysis and tool selection.
 
         They are independent (the reference's _select_tools, pilott/core/agent.py:
@@ -436,6 +436,11 @@ class BaseAgent:
         so both go into the continuous batch at once. Neither has side effects: the
         orchestrator may start them speculatively while it analyses the task itself
         (Serve._submit) and drop them (drop_opening) if it decomposes the task."""
+        if _store and type(self)._execute_task_internal is not BaseAgent._execute_task_internal:
+            # a subclass with its own execution path never consumes the opening: starting
+            # it would spend two LLM calls per task (and resolve a default LLM) for nothing
+            return None
+
         async def both():
             sel = asyncio.ensure_future(self._select_tools(task))
             try:

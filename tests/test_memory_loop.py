@@ -138,3 +138,28 @@ def test_sharded_index_topk_equals_single_index(world):
     for lst_s, lst_r in zip(got[0], ref):  # ... equal to one index holding all rows
         assert [row for row, _ in lst_s] == [row for row, _ in lst_r]
         np.testing.assert_allclose([s for _, s in lst_s], [s for _, s in lst_r], rtol=1e-5, atol=1e-5)
+
+
+def test_serve_does_not_start_openings_for_custom_agents():
+    """Serve's speculative opening (task analysis + tool selection) is only started for
+    agents that run the standard protocol; a subclass with its own execution path must
+    not have its LLM resolved (that once built a default engine per plumbing run)."""
+    import sys
+
+    sys.path.insert(0, str(__import__("pathlib").Path(__file__).resolve().parent.parent))
+    from benchmarks.plumbing import InstantLLM, make_echo_agent_cls
+    from pilottai_amd.serve import Serve
+
+    Echo = make_echo_agent_cls()
+
+    async def go():
+        agents = [Echo(AgentConfig(role=f"echo-{i}", goal="echo")) for i in range(2)]
+        serve = Serve(agents=agents, manager_llm=InstantLLM(), config={"max_concurrent_tasks": 2})
+        await serve.start()
+        rs = await asyncio.gather(*(serve.execute_task(Task(description=f"echo {i}")) for i in range(6)))
+        await serve.stop()
+        return agents, rs
+
+    agents, rs = asyncio.run(go())
+    assert all(r.success for r in rs)
+    assert all(a._llm is None for a in agents)
