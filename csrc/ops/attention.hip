@@ -623,7 +623,8 @@ __global__ __launch_bounds__(256, 2) void paged_attn_kernel(
     const bf16* __restrict__ v_cache, const int4* __restrict__ items,
     const int* __restrict__ n_items, const int* __restrict__ part_size, const int* __restrict__ q_start,
     const int* __restrict__ q_len, const int* __restrict__ ctx_len,
-    const int* __restrict__ block_table, int max_blocks, int H, int KV, float scale_log2) {
+    const int* __restrict__ block_table, int max_blocks, int H, int KV, float scale_log2,
+    const u32x4* __restrict__ pf, long long pf_lines, u32x4* __restrict__ pf_sink) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int TPW = 16 / G;
   // The first item is loaded together with the item count, not after it: one dependent
@@ -632,6 +633,23 @@ __global__ __launch_bounds__(256, 2) void paged_attn_kernel(
   // length of `items`.
   int4 it_next = items[blockIdx.x];
   const int n = n_items[0];
+  if ((int)blockIdx.x >= n) {
+    // A workgroup without an item (the grid is sized for the bucket's largest item
+    // list; a decode step of 8 rows uses ~1/70 of it): read a slice of the next
+    // projection's weights so they are in the Infinity Cache when it starts (the
+    // attention K/V stream leaves most of HBM's bandwidth idle at small batch).
+    if (pf_lines > 0) {
+      const long long idle = (long long)(gridDim.x - n) * gridDim.y;
+      const long long me = (long long)blockIdx.y * (gridDim.x - n) + (blockIdx.x - n);
+      const long long per = (pf_lines + idle - 1) / idle;
+      const long long l1 = min(pf_lines, (me + 1) * per);
+      u32x4 acc = {0u, 0u, 0u, 0u};
+      for (long long l = me * per + threadIdx.x; l < l1; l += blockDim.x) acc ^= pf[4 * l];  // 16 B per 64-B line
+      if (acc.x == 0x9E3779B9u && acc.y == 0x7F4A7C15u && acc.z == 0xF39CC060u && acc.w == 0x5CEDC834u)
+        pf_sink[threadIdx.x] = acc;  // never in practice: keeps the loads
+    }
+    return;
+  }
   const int psz = part_size ? part_size[0] : ATT_PART;  // decode partition (keys), per step
   const int kvh = blockIdx.y;
   for (int item = blockIdx.x; item < n; item += gridDim.x) {
@@ -659,8 +677,11 @@ extern "C" int pa_paged_attention(void* out, float* part_o, float* part_ml, cons
                                   const int* q_start,
                                   const int* q_len, const int* ctx_len, const int* block_table,
                                   int max_blocks, int H, int KV, float scale_log2,
+                                  const void* pf, long long pf_bytes, void* pf_sink,
                                   hipStream_t st) {
   if (H % KV != 0) return -1;
+  if (pf_bytes > 0 && (pf == nullptr || pf_sink == nullptr || (reinterpret_cast<uintptr_t>(pf) & 15))) return -1;
+  const long long pf_lines = pf_bytes > 0 ? pf_bytes / 64 : 0;
   const int G = H / KV;
   // items are strided over the grid: ~8 resident workgroups per CU over all KV heads
   const int gx = max_items < 1 ? 1 : (max_items < 2048 / KV ? max_items : (2048 / KV > 0 ? 2048 / KV : 1));
@@ -680,7 +701,8 @@ extern "C" int pa_paged_attention(void* out, float* part_o, float* part_ml, cons
                          (const pa::bf16*)k_cache, (const pa::bf16*)v_cache,                \
                          (const int4*)items, n_items, part_size, q_start, q_len, ctx_len,    \
                          block_table,                                                       \
-                         max_blocks, H, KV, scale_log2);                                    \
+                         max_blocks, H, KV, scale_log2, (const pa::u32x4*)pf, pf_lines,     \
+                         (pa::u32x4*)pf_sink);                                              \
   } while (0)
   switch (G) {
     case 1: PA_ATT(1); break;

@@ -18,7 +18,8 @@ int pa_paged_attention(void* out, float* part_o, float* part_ml, const void* q, 
                        const void* v_cache, const int* items, const int* n_items, int max_items,
                        const int* part_size, int* counters, const int* q_start,
                        const int* q_len, const int* ctx_len, const int* block_table,
-                       int max_blocks, int H, int KV, float scale_log2, hipStream_t st);
+                       int max_blocks, int H, int KV, float scale_log2, const void* pf, long long pf_bytes,
+                       void* pf_sink, hipStream_t st);
 int pa_sample_workspace_floats(int rows, int V);
 int pa_sample(int* out_tokens, float* out_keys, float* workspace, const void* logits, int rows,
               int V, int ld, int vocab_offset, const float* temperature, const int* mask_class,
@@ -48,6 +49,7 @@ int pa_mid_gemm(void* y, const void* x, const void* wp, const void* resid, float
                 void* q_out, void* k_cache, void* v_cache, const int* positions, const int* slots,
                 const float* cos_sin, int H, int KV, hipStream_t st);
 int pa_row_sumsq(float* out, const void* x, int M, int K, int ldx, hipStream_t st);
+int pa_prefetch(const void* p, long long bytes, void* sink, int wgs, hipStream_t st);
 long long pa_cosine_topk_workspace_bytes(int Q, int N, int K);
 int pa_cosine_topk(float* out_scores, int* out_rows, void* workspace, const void* queries,
                    const void* index, int Q, int N, int D, int K, const int* row_priority,
@@ -78,6 +80,14 @@ void check_dtype(const at::Tensor& t, at::ScalarType dt, const char* name) {
 void check_rc(int rc, const char* what) {
   TORCH_CHECK(rc == 0, what, " launch failed with code ", rc, " (",
               rc > 0 ? hipGetErrorString((hipError_t)rc) : "bad arguments", ")");
+}
+
+void prefetch(at::Tensor t, at::Tensor sink, int64_t wgs) {
+  check_gpu(t, "t"); check_gpu(sink, "sink");
+  TORCH_CHECK(sink.numel() * sink.element_size() >= 256 * 16, "prefetch sink must hold 4 KiB");
+  check_rc(pa_prefetch(t.data_ptr(), (long long)t.numel() * t.element_size(), sink.data_ptr(), (int)wgs,
+                       cur_stream()),
+           "prefetch");
 }
 
 void rmsnorm(at::Tensor out, at::Tensor x, at::Tensor w, double eps) {
@@ -144,7 +154,8 @@ void paged_attention(at::Tensor out, at::Tensor part_o, at::Tensor part_ml, at::
                      at::Tensor k_cache, at::Tensor v_cache, at::Tensor items, at::Tensor n_items,
                      at::Tensor counters, at::Tensor q_start, at::Tensor q_len,
                      at::Tensor ctx_len, at::Tensor block_table, double scale,
-                     c10::optional<at::Tensor> part_size) {
+                     c10::optional<at::Tensor> part_size, c10::optional<at::Tensor> prefetch,
+                     c10::optional<at::Tensor> prefetch_sink) {
   for (auto* t : {&out, &part_o, &part_ml, &q, &k_cache, &v_cache, &items, &n_items, &counters,
                   &q_start, &q_len, &ctx_len, &block_table})
     check_gpu(*t, "paged_attention arg");
@@ -167,6 +178,18 @@ void paged_attention(at::Tensor out, at::Tensor part_o, at::Tensor part_ml, at::
   TORCH_CHECK(counters.numel() >= block_table.size(0) * KV,
               "counters must hold one zero-initialised int per (sequence, KV head)");
   const float scale_log2 = (float)(scale * 1.4426950408889634);
+  const void* pf = nullptr;
+  long long pf_bytes = 0;
+  void* pf_sink = nullptr;
+  if (prefetch.has_value()) {  // weights to warm with the idle workgroups (see attention.hip)
+    check_gpu(*prefetch, "prefetch");
+    TORCH_CHECK(prefetch_sink.has_value() && prefetch_sink->is_cuda() &&
+                    prefetch_sink->numel() * prefetch_sink->element_size() >= 256 * 16,
+                "prefetch needs a >= 4 KiB prefetch_sink");
+    pf = prefetch->data_ptr();
+    pf_bytes = (long long)prefetch->numel() * prefetch->element_size();
+    pf_sink = prefetch_sink->data_ptr();
+  }
   check_rc(pa_paged_attention(out.data_ptr(), part_o.data_ptr<float>(), part_ml.data_ptr<float>(),
                               q.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(),
                               items.data_ptr<int>(), n_items.data_ptr<int>(), max_items,
@@ -174,7 +197,7 @@ void paged_attention(at::Tensor out, at::Tensor part_o, at::Tensor part_ml, at::
                               counters.data_ptr<int>(),
                               q_start.data_ptr<int>(), q_len.data_ptr<int>(),
                               ctx_len.data_ptr<int>(), block_table.data_ptr<int>(),
-                              block_table.size(1), H, KV, scale_log2, cur_stream()),
+                              block_table.size(1), H, KV, scale_log2, pf, pf_bytes, pf_sink, cur_stream()),
            "paged_attention");
 }
 
@@ -576,6 +599,7 @@ void car_all_reduce(std::vector<int64_t> bases, int64_t rank0, std::vector<at::T
 
 PYBIND11_MODULE(_C, m) {
   m.doc() = "pilottai_amd CDNA4 (gfx950) HIP kernels";
+  m.def("prefetch", &prefetch, py::arg("t"), py::arg("sink"), py::arg("wgs") = 64);
   m.def("rmsnorm", &rmsnorm);
   m.def("fused_add_rmsnorm", &fused_add_rmsnorm);
   m.def("rope_cache", &rope_cache);
@@ -605,7 +629,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("paged_attention", &paged_attention, py::arg("out"), py::arg("part_o"), py::arg("part_ml"), py::arg("q"),
         py::arg("k_cache"), py::arg("v_cache"), py::arg("items"), py::arg("n_items"), py::arg("counters"),
         py::arg("q_start"), py::arg("q_len"), py::arg("ctx_len"), py::arg("block_table"), py::arg("scale"),
-        py::arg("part_size") = py::none());
+        py::arg("part_size") = py::none(), py::arg("prefetch") = py::none(), py::arg("prefetch_sink") = py::none());
   m.def("sample_workspace_floats", &sample_workspace_floats);
   m.def("sample", &sample, py::arg("out_tokens"), py::arg("out_keys"), py::arg("workspace"),
         py::arg("logits"), py::arg("vocab_offset"), py::arg("temperature"), py::arg("mask_class"),

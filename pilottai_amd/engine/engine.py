@@ -82,6 +82,7 @@ class EngineConfig:
     mid_max_t: Optional[int] = None  # largest step on the LDS-DMA tiled mid-size path; None = model default
     att_qcols: int = 128  # prefill attention item width in MFMA columns (128: LDS-staged 4-wave items)
     att_wide_min_tokens: int = 2048  # ... used only for steps with at least this many prefill tokens
+    prefetch_weights: Optional[bool] = None  # decode-step MALL prefetch on a side stream (None: model default)
     reply_tokens: Optional[int] = None  # fixed length of every reply schema's free-text slot (grammar.py)
 
 
@@ -169,6 +170,8 @@ class LLMEngine:
             self.model.WIDE_MAX_T = int(cfg.wide_max_t)
         if cfg.mid_max_t is not None:
             self.model.MID_MAX_T = int(cfg.mid_max_t)
+        if cfg.prefetch_weights is not None:
+            self.model.PREFETCH_WEIGHTS = bool(cfg.prefetch_weights)
         self.load_time = time.time() - t0
         self.max_model_len = min(cfg.max_model_len, mc.max_position)
         # ---- KV cache sizing (288 GB HBM: the default leaves room for graphs/activations)

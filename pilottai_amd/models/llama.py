@@ -133,6 +133,14 @@ class LlamaModel:
     # steps of up to this many tokens (above WIDE_MAX_T) run the LDS-DMA tiled projections
     # (csrc/ops/gemm_mid.hip) with every norm / SwiGLU / residual / RoPE + KV write fused
     MID_MAX_T = 256
+    # decode/small steps: let the attention launch's idle workgroups read the O
+    # projection's weights into the Infinity Cache (MALL-resident weights run the 34 MB
+    # O projection at M=8 in 8.7 us vs 12.8 us cold, profiles/r2_mall_warm.jsonl). Off by
+    # default: end to end it did not pay (8-row steps 3.67 -> 3.72 ms, 16-row 4.01 -> 4.10:
+    # the prefetching workgroups compete with the K/V stream), and a side-stream prefetch
+    # inside the graph was worse still (+1 ms per step from the fork/join nodes);
+    # profiles/r2_prefetch_ab.jsonl. EngineConfig.prefetch_weights turns it on.
+    PREFETCH_WEIGHTS = False
     # (largest M, fm, fn, K-slices) per projection, best of tools/mid_gemm_bench.py on MI355X
     # (profiles/r2_mid_gemm_sweep.jsonl); the first row whose M covers the step is used
     MID_CFG = {
@@ -195,6 +203,8 @@ class LlamaModel:
             ops.mid_workspace(self.device)
         # RMSNorm row statistics handed from each residual epilogue to the next projection
         self._ss = torch.zeros(2, 1 << 14, dtype=torch.float32, device=self.device)
+        if self.device.type == "cuda":
+            ops.kernels._prefetch_sink(self.device)  # before any graph capture
         self.decode_packed = True
 
     # -- weights -----------------------------------------------------------------
@@ -366,14 +376,18 @@ class LlamaModel:
         h = self._embed(ids)
         if not h.is_contiguous():
             h = h.contiguous()
+        pf = self.PREFETCH_WEIGHTS and self.device.type == "cuda"
         for li, L in enumerate(self.layers):
             q = torch.empty(T, H, hd, dtype=self.dtype, device=self.device)
             ops.decode_qkv_rope(h, L["wqkv_p"], eps, q, kv.k[li], kv.v[li], meta.positions, meta.slots,
                                 self.cos_sin, H, KVh)
             attn = torch.empty(T, H, hd, dtype=self.dtype, device=self.device)
+            # the attention grid's idle workgroups read the O projection's weights into
+            # the Infinity Cache while the K/V stream runs (csrc/ops/attention.hip)
             ops.paged_attention(attn, part_o, part_ml, q, kv.k[li], kv.v[li], meta.items, meta.n_items,
                                 meta.att_counters, meta.q_start, meta.q_len, meta.ctx_len,
-                                meta.block_table, self.scale, num_seqs=meta.num_seqs, part_size=meta.part_size)
+                                meta.block_table, self.scale, num_seqs=meta.num_seqs, part_size=meta.part_size,
+                                prefetch=L["wo_p"] if pf else None)
             a2 = attn.view(T, H * hd)
             if tp:
                 o = ops.decode_gemm(a2, L["wo_p"], "plain")
@@ -423,7 +437,8 @@ class LlamaModel:
             attn = torch.empty(T, H, hd, dtype=self.dtype, device=self.device)
             ops.paged_attention(attn, part_o, part_ml, q, kv.k[li], kv.v[li], meta.items, meta.n_items,
                                 meta.att_counters, meta.q_start, meta.q_len, meta.ctx_len,
-                                meta.block_table, self.scale, num_seqs=meta.num_seqs, part_size=meta.part_size)
+                                meta.block_table, self.scale, num_seqs=meta.num_seqs, part_size=meta.part_size,
+                                prefetch=L["wo_p"] if self.PREFETCH_WEIGHTS and self.device.type == "cuda" else None)
             a2 = attn.view(T, H * hd)
             if tp:
                 o = ops.wide_gemm(a2, L["wo_p"], "plain")

@@ -56,6 +56,28 @@ def _on_gpu(t: torch.Tensor) -> bool:
 # ---------------------------------------------------------------------------
 
 
+_PF_SINKS: dict = {}
+
+
+def _prefetch_sink(device) -> torch.Tensor:
+    """A 4 KiB device buffer per device that prefetching kernels could write (never do in
+    practice). Allocated on first use — the model calls it at load time, outside any
+    graph capture."""
+    key = str(device)
+    t = _PF_SINKS.get(key)
+    if t is None:
+        t = _PF_SINKS[key] = torch.zeros(1024, dtype=torch.int32, device=device)
+    return t
+
+
+def prefetch(t: torch.Tensor, sink: torch.Tensor, wgs: int = 64):
+    """Read `t` once so its lines land in the Infinity Cache (csrc/ops/prefetch.hip); meant
+    for a side stream while a latency-bound kernel runs. `sink` (>= 4 KiB, on t's device)
+    is never written in practice. No-op off the GPU."""
+    if _on_gpu(t):
+        require_native().prefetch(t, sink, int(wgs))
+
+
 def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float, out: Optional[torch.Tensor] = None):
     if _on_gpu(x):
         out = torch.empty_like(x) if out is None else out
@@ -109,15 +131,18 @@ def rope_cache(q_out, k_cache, v_cache, qkv, positions, slot_mapping, cos_sin, H
 
 def paged_attention(out, part_o, part_ml, q, k_cache, v_cache, items, n_items, counters,
                     q_start, q_len, ctx_len, block_table, scale: float, num_seqs: Optional[int] = None,
-                    part_size: Optional[torch.Tensor] = None):
+                    part_size: Optional[torch.Tensor] = None, prefetch: Optional[torch.Tensor] = None):
     """Attention over the paged cache. On GPU `items` must be a device int32
     [max, 4] tensor with a device count (graph-capturable) and `counters` a
     zero-initialised int32 tensor of >= seqs * KV entries (partition tickets; the
-    kernel leaves it zeroed); on CPU the reference path ignores both."""
+    kernel leaves it zeroed); on CPU the reference path ignores both. `prefetch`: a
+    tensor (e.g. the next projection's packed weights) that the grid's idle workgroups
+    read into the Infinity Cache."""
     if _on_gpu(q):
+        sink = _prefetch_sink(q.device) if prefetch is not None else None
         require_native().paged_attention(out, part_o, part_ml, q, k_cache, v_cache, items, n_items,
                                          counters, q_start, q_len, ctx_len, block_table,
-                                         float(scale), part_size)
+                                         float(scale), part_size, prefetch, sink)
         return out
     ns = len(q_len) if num_seqs is None else num_seqs
     r = ref.paged_attention(q, k_cache, v_cache, q_start[:ns], q_len[:ns], ctx_len[:ns],

@@ -69,7 +69,8 @@ def test_rope_cache(gpu):
     torch.testing.assert_close(vc.cpu().float(), vc_r.float(), atol=0, rtol=0)
 
 
-def _run_attention(gpu, H, KV, q_lens, ctx_lens, seed=0, split=True, part=512, qcols=128):
+def _run_attention(gpu, H, KV, q_lens, ctx_lens, seed=0, split=True, part=512, qcols=128, pad=1,
+                   prefetch=None):
     torch.manual_seed(seed)
     G = H // KV
     blk = 16
@@ -89,7 +90,7 @@ def _run_attention(gpu, H, KV, q_lens, ctx_lens, seed=0, split=True, part=512, q
     q = _bf(T, H, 128, dev=gpu)
     items, nslots = ops.build_attention_items(q_lens, ctx_lens, G, split=split, part=part,
                                                qcols=qcols, wide_min_tokens=0)
-    it = torch.tensor(items + [(0, 0, 0, 0)], dtype=torch.int32, device=gpu)
+    it = torch.tensor(items + [(0, 0, 0, 0)] * pad, dtype=torch.int32, device=gpu)
     cnt = torch.zeros(ns * KV, dtype=torch.int32, device=gpu)
     n_it = torch.tensor([len(items)], dtype=torch.int32, device=gpu)
     maxit = it.shape[0]
@@ -99,7 +100,8 @@ def _run_attention(gpu, H, KV, q_lens, ctx_lens, seed=0, split=True, part=512, q
     scale = 1.0 / math.sqrt(128)
     dev_i = lambda a: torch.tensor(a, dtype=torch.int32, device=gpu)  # noqa: E731
     ops.paged_attention(out, part_o, part_ml, q, kc, vc, it, n_it, cnt, dev_i(q_start),
-                        dev_i(q_lens), dev_i(ctx_lens), bt.to(gpu), scale, part_size=dev_i([part]))
+                        dev_i(q_lens), dev_i(ctx_lens), bt.to(gpu), scale, part_size=dev_i([part]),
+                        prefetch=prefetch)
     torch.cuda.synchronize()
     assert int(cnt.abs().sum()) == 0, "partition tickets must be left zeroed"
     r = ref.paged_attention(q.cpu(), kc.cpu(), vc.cpu(), q_start, q_lens, ctx_lens, bt, scale)
@@ -111,6 +113,20 @@ def test_attention_decode(gpu, H, KV):
     ctx = [1, 15, 16, 17, 33, 100, 511, 512, 513, 1500, 2049, 64]
     o, r = _run_attention(gpu, H, KV, [1] * len(ctx), ctx)
     torch.testing.assert_close(o, r, atol=2e-2, rtol=2e-2)
+
+
+def test_attention_idle_workgroups_prefetch(gpu):
+    """The engine's decode graphs size the attention grid for the bucket's largest item
+    list; the idle workgroups read the next projection's weights (MALL prefetch). The
+    attention result must be bit-identical with and without it, and equal to fp32."""
+    ctx = [1, 15, 100, 511, 513, 1500, 2049, 64]
+    w = torch.randn(4096 * 4096 + 24, device=gpu).to(torch.bfloat16)  # 34 MB, not a multiple of 64 B
+    o0, r = _run_attention(gpu, 32, 8, [1] * len(ctx), ctx, seed=3, pad=140)
+    o1, _ = _run_attention(gpu, 32, 8, [1] * len(ctx), ctx, seed=3, pad=140, prefetch=w)
+    torch.testing.assert_close(o1, r, atol=2e-2, rtol=2e-2)
+    assert torch.equal(o0, o1)
+    with pytest.raises(RuntimeError):  # a prefetch tensor on the wrong device fails loudly
+        _run_attention(gpu, 32, 8, [1], [10], pad=4, prefetch=w.cpu())
 
 
 @pytest.mark.parametrize("qcols", [32, 128])
