@@ -138,6 +138,57 @@ static void stress_scheduler(uint32_t seed) {
               steps, finished.size(), (long long)sch.total_preemptions(), (long long)sch.total_cached_tokens());
 }
 
+// Long contexts, few sequences, GQA groups 4 and 8: the item list of
+// every step (prefill tiles + flash-decoding partitions, both partition sizes, both
+// prefill item widths) must fit max_items, which the scheduler now checks itself.
+static void stress_long_context_items(uint32_t seed) {
+  std::mt19937 rng(seed);
+  for (int32_t group : {4, 8}) {
+    SchedulerConfig cfg;
+    cfg.block_size = 16;
+    cfg.max_num_seqs = 4;
+    cfg.max_model_len = 8192;
+    cfg.num_blocks = 4 * 8192 / 16 + 8;
+    cfg.max_num_batched_tokens = 2048;
+    cfg.max_prefill_tokens = 2048;
+    cfg.gqa_group = group;
+    cfg.kv_heads = 8;
+    cfg.att_wide_min_tokens = (seed % 2) ? 0 : 2048;
+    cfg.eos_ids = {2};
+    Scheduler sch(cfg);
+    const StepLayout& L = sch.layout();
+    std::vector<int32_t> buf(L.total + 16, 0);
+    int64_t id = 1;
+    // three long decoders (~7.9k context) plus a 4k prompt arriving later
+    for (int i = 0; i < 3; ++i) {
+      std::vector<int32_t> prompt;
+      for (int j = 0; j < 7800 + (int)(rng() % 64); ++j) prompt.push_back(10 + rng() % 900);
+      sch.add_request(id++, prompt, 0.7f, 200, id, true, {}, nullptr, 0, 1.0f);
+    }
+    int steps = 0, max_it = 0;
+    while (sch.has_work() && steps < 600) {
+      if (steps == 8) {
+        std::vector<int32_t> prompt;
+        for (int j = 0; j < 4096; ++j) prompt.push_back(10 + rng() % 900);
+        sch.add_request(id++, prompt, 0.7f, 16, id, true, {}, nullptr, 0, 1.0f);
+      }
+      const int32_t T = sch.schedule(buf.data());
+      ++steps;
+      if (T == 0) continue;
+      const int32_t nit = buf[L.n_items];
+      CHECK(nit > 0 && nit <= L.max_items);
+      CHECK(buf[L.part_size] == 256 || buf[L.part_size] == 512);
+      max_it = std::max(max_it, nit);
+      const int32_t nsamp = buf[L.counts + 2];
+      std::vector<int32_t> sampled(nsamp, 11);
+      sch.commit(sampled.data(), nsamp);
+    }
+    CHECK(!sch.has_work());
+    std::printf("long-context items seed %u group %d: %d steps, max %d of %d items\n", seed, group, steps, max_it,
+                L.max_items);
+  }
+}
+
 static void fuzz_block_manager(uint32_t seed) {
   std::mt19937 rng(seed);
   BlockManager bm(64, 16, true);
@@ -190,6 +241,7 @@ int main(int argc, char** argv) {
   const int seeds = argc > 1 ? std::atoi(argv[1]) : 6;
   for (int s = 1; s <= seeds; ++s) {
     stress_scheduler((uint32_t)s);
+    if (s <= 2) stress_long_context_items((uint32_t)s);
     fuzz_block_manager((uint32_t)s);
     roundtrip_tokenizer((uint32_t)s);
   }

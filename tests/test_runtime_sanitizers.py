@@ -34,4 +34,5 @@ def test_runtime_stress_under_asan_ubsan():
         r = subprocess.run([exe, "4"], capture_output=True, text=True, timeout=300, env=env)
         assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-4000:])
         assert "runtime stress: ok" in r.stdout
+        assert r.stdout.count("long-context items") == 4  # seeds 1-2 x GQA groups 4 and 8
         assert "preemptions" in r.stdout and " 0 preemptions" not in r.stdout
