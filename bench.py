@@ -66,6 +66,8 @@ def parse():
                     help="largest step on the packed small-batch path (default: the model's)")
     ap.add_argument("--mid-max-t", type=int, default=None,
                     help="largest step on the LDS-DMA tiled mid-size path (default: the model's; 0 = off)")
+    ap.add_argument("--att-wide-min-tokens", type=int, default=None,
+                    help="prefill tokens per step from which attention uses the 4-wave LDS-staged items")
     ap.add_argument("--no-prefetch", action="store_true", help="decode steps without the side-stream weight prefetch")
     ap.add_argument("--token-align", type=int, default=256, help="GEMM-friendly step sizes (0 = off)")
     ap.add_argument("--align-slack", type=int, default=96)
@@ -111,7 +113,9 @@ async def run_rank(a, rank: int, world: int, device):
                                  token_align=a.token_align, align_slack=a.align_slack,
                                  decode_fused_max_t=a.fused_max_t, wide_max_t=a.wide_max_t,
                                  mid_max_t=a.mid_max_t, reply_tokens=a.reply_tokens,
-                                 prefetch_weights=False if a.no_prefetch else None), device=device)
+                                 prefetch_weights=False if a.no_prefetch else None,
+                                 **({"att_wide_min_tokens": a.att_wide_min_tokens}
+                                    if a.att_wide_min_tokens is not None else {})), device=device)
     register_engine(eng.model_cfg.name, eng)
     eng.start()
     llm = LocalLLM(LLMConfig(model_name=eng.model_cfg.name, temperature=a.temperature, max_tokens=1024,

@@ -253,10 +253,17 @@ int32_t Scheduler::schedule(int32_t* buf) {
   // the step has enough prefill work to fill the chip with 4x fewer items (tools/
   // attn_bench.py --scan: 8 x 512 tokens 50.8 us wide vs 68.8 narrow, 8 x 128 14.8 vs
   // 13.8, a single 512-token chunk 19.5 vs 12.7)
+  // (a single long chunk gains nothing: its causal imbalance makes the longest item the
+  // critical path, 4x longer per workgroup with the wide items; --scan pf2048: 79.6 vs 79.0)
   int64_t prefill_tokens = 0;
+  int32_t prefill_seqs = 0;
   for (const Planned& p : last_plan_)
-    if (p.n > tpw) prefill_tokens += p.n;
-  const int32_t qcols = prefill_tokens >= cfg_.att_wide_min_tokens ? std::max(32, cfg_.att_qcols) : 32;
+    if (p.n > tpw) {
+      prefill_tokens += p.n;
+      ++prefill_seqs;
+    }
+  const bool wide = prefill_tokens >= cfg_.att_wide_min_tokens && prefill_seqs >= 2;
+  const int32_t qcols = wide ? std::max(32, cfg_.att_qcols) : 32;
   const int32_t qtile = std::max(1, qcols / std::max(1, cfg_.gqa_group));
   int32_t psz = 512;
   if (cfg_.split_decode) {

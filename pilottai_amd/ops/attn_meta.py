@@ -23,7 +23,8 @@ def build_attention_items(q_lens: Sequence[int], ctx_lens: Sequence[int], group:
     # tokens per prefill item: qcols MFMA columns (128: the LDS-staged 4-wave path of
     # csrc/ops/attention.hip; 32: one wave per item)
     # (wide items only when the step's prefill tokens reach wide_min_tokens, as the scheduler)
-    if sum(ql for ql in q_lens if ql > tpw) < wide_min_tokens:
+    pre = [ql for ql in q_lens if ql > tpw]
+    if sum(pre) < wide_min_tokens or (wide_min_tokens > 0 and len(pre) < 2):
         qcols = 32
     qtile = max(1, max(32, qcols) // group)
     items: List[Tuple[int, int, int, int]] = []
