@@ -35,7 +35,7 @@ py::list outputs_to_py(const std::vector<SeqOutput>& outs) {
   py::list l;
   for (const auto& o : outs)
     l.append(py::make_tuple(o.id, o.tokens, o.finish_reason, o.prompt_len, o.cached_prompt_tokens,
-                            o.num_sampled, o.num_forced, o.t_first_token, o.t_finish));
+                            o.num_sampled, o.num_forced, o.t_first_token, o.t_finish, o.embed_slot));
   return l;
 }
 
@@ -115,7 +115,7 @@ PYBIND11_MODULE(_runtime, m) {
         d["offsets"] = L.offsets; d["temperature"] = L.temperature; d["seeds"] = L.seeds;
         d["top_k"] = L.top_k; d["top_p"] = L.top_p;
         d["items"] = L.items; d["n_items"] = L.n_items; d["part_size"] = L.part_size;
-        d["counts"] = L.counts; d["block_table"] = L.block_table;
+        d["counts"] = L.counts; d["block_table"] = L.block_table; d["embed_rows"] = L.embed_rows;
         d["total"] = L.total;
         return d;
       })
@@ -123,13 +123,13 @@ PYBIND11_MODULE(_runtime, m) {
            [](Scheduler& s, int64_t id, const std::vector<int32_t>& prompt, float temperature,
               int32_t max_tokens, int64_t seed, bool ignore_eos,
               const std::vector<int32_t>& stop_ids, const py::object& grammar, int32_t top_k,
-              float top_p) {
+              float top_p, bool embed) {
              s.add_request(id, prompt, temperature, max_tokens, seed, ignore_eos, stop_ids,
-                           make_grammar(grammar), top_k, top_p);
+                           make_grammar(grammar), top_k, top_p, embed);
            },
            py::arg("id"), py::arg("prompt"), py::arg("temperature"), py::arg("max_tokens"),
            py::arg("seed"), py::arg("ignore_eos"), py::arg("stop_ids"), py::arg("grammar"),
-           py::arg("top_k") = 0, py::arg("top_p") = 1.0f)
+           py::arg("top_k") = 0, py::arg("top_p") = 1.0f, py::arg("embed") = false)
       .def("schedule", [](Scheduler& s, uintptr_t buf) {
         py::gil_scoped_release nogil;
         return s.schedule(reinterpret_cast<int32_t*>(buf));
@@ -143,6 +143,7 @@ PYBIND11_MODULE(_runtime, m) {
         return outputs_to_py(outs);
       })
       .def("abort", &Scheduler::abort)
+      .def("take_embed_resets", &Scheduler::take_embed_resets)
       .def("drain_aborted", [](Scheduler& s) { return outputs_to_py(s.drain_aborted()); })
       .def("has_work", &Scheduler::has_work)
       .def("reset_prefix_cache", &Scheduler::reset_prefix_cache)

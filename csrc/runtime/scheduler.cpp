@@ -48,13 +48,15 @@ Scheduler::Scheduler(const SchedulerConfig& cfg)
   L.seeds = take(2 * L.max_seqs);
   L.items = take(4 * L.max_items);
   L.block_table = take(L.max_seqs * L.max_blocks);
+  L.embed_rows = take(L.max_tokens);
   L.total = o;
+  for (int32_t r = L.max_seqs; r-- > 0;) embed_free_.push_back(r);
 }
 
 void Scheduler::add_request(int64_t id, std::vector<int32_t> prompt, float temperature,
                             int32_t max_tokens, int64_t seed, bool ignore_eos,
                             std::vector<int32_t> stop_ids, std::unique_ptr<Grammar> grammar,
-                            int32_t top_k, float top_p) {
+                            int32_t top_k, float top_p, bool embed) {
   auto s = std::make_unique<Sequence>();
   s->id = id;
   if ((int32_t)prompt.size() >= cfg_.max_model_len)
@@ -69,7 +71,8 @@ void Scheduler::add_request(int64_t id, std::vector<int32_t> prompt, float tempe
   s->seed = seed;
   s->ignore_eos = ignore_eos;
   s->stop_ids = std::move(stop_ids);
-  s->grammar = std::move(grammar);
+  s->grammar = embed ? nullptr : std::move(grammar);
+  s->embed = embed;
   s->arrival = arrival_counter_++;
   // a grammar that starts with forced text (e.g. '{"key": ') is jump-forwarded into the prompt
   if (s->grammar) {
@@ -83,14 +86,21 @@ void Scheduler::add_request(int64_t id, std::vector<int32_t> prompt, float tempe
   waiting_.push_back(raw);
 }
 
-void Scheduler::free_seq(Sequence* s) {
+void Scheduler::free_seq(Sequence* s, bool keep_embed_slot) {
+  if (s->embed_slot >= 0 && !keep_embed_slot) {
+    embed_free_.push_back(s->embed_slot);
+    s->embed_slot = -1;
+  }
   for (int32_t b : s->blocks) bm_.release(b);
   s->blocks.clear();
   s->block_hashes.clear();
 }
 
 void Scheduler::preempt(Sequence* s) {
-  free_seq(s);
+  // an embedding request keeps its pooling row, but restarts from token 0: the row's
+  // partial sums must be cleared before the next step runs (take_embed_resets)
+  if (s->embed_slot >= 0) embed_resets_.push_back(s->embed_slot);
+  free_seq(s, true);
   s->num_computed = 0;
   s->running = false;
   waiting_.push_front(s);
@@ -106,7 +116,7 @@ bool Scheduler::ensure_blocks(Sequence* s, int32_t upto_tokens) {
 
 void Scheduler::match_prefix(Sequence* s) {
   const int32_t B = cfg_.block_size;
-  if (cfg_.prefix_caching) {
+  if (cfg_.prefix_caching && !s->embed) {
     const int32_t n_full = ((int32_t)s->tokens.size() - 1) / B;  // never reuse the last token
     uint64_t parent = 0;
     for (int32_t b = 0; b < n_full; ++b) {
@@ -172,7 +182,7 @@ int32_t Scheduler::schedule(int32_t* buf) {
       preempt(s);
       continue;
     }
-    last_plan_.push_back({s, n, s->num_computed + n == (int32_t)s->tokens.size()});
+    last_plan_.push_back({s, n, !s->embed && s->num_computed + n == (int32_t)s->tokens.size()});
     tok_budget -= n;
   }
   running_.erase(std::remove_if(running_.begin(), running_.end(),
@@ -184,6 +194,11 @@ int32_t Scheduler::schedule(int32_t* buf) {
   while (!waiting_.empty() && (int32_t)last_plan_.size() < cfg_.max_num_seqs &&
          (int32_t)running_.size() < cfg_.max_num_seqs && tok_budget > 0 && prefill_budget > 0) {
     Sequence* s = waiting_.front();
+    if (s->embed && s->embed_slot < 0) {
+      if (embed_free_.empty()) break;  // every pooling row is in use: wait
+      s->embed_slot = embed_free_.back();
+      embed_free_.pop_back();
+    }
     if (s->blocks.empty()) match_prefix(s);
     const int32_t pending = (int32_t)s->tokens.size() - s->num_computed;
     const int32_t n = std::min(pending, std::min(tok_budget, prefill_budget));
@@ -194,7 +209,7 @@ int32_t Scheduler::schedule(int32_t* buf) {
     waiting_.pop_front();
     s->running = true;
     running_.push_back(s);
-    last_plan_.push_back({s, n, s->num_computed + n == (int32_t)s->tokens.size()});
+    last_plan_.push_back({s, n, !s->embed && s->num_computed + n == (int32_t)s->tokens.size()});
     tok_budget -= n;
     prefill_budget -= n;
   }
@@ -215,7 +230,7 @@ int32_t Scheduler::schedule(int32_t* buf) {
           const int32_t cut = std::min(left, p.n - 1);
           p.n -= cut;
           left -= cut;
-          p.sample = p.s->num_computed + p.n == (int32_t)p.s->tokens.size();
+          p.sample = !p.s->embed && p.s->num_computed + p.n == (int32_t)p.s->tokens.size();
         }
         ++stat_aligned_steps_;
       }
@@ -241,6 +256,8 @@ int32_t Scheduler::schedule(int32_t* buf) {
   int64_t* seeds = reinterpret_cast<int64_t*>(buf + L.seeds);
   int32_t* items = buf + L.items;
   int32_t* bt = buf + L.block_table;
+  int32_t* er = buf + L.embed_rows;
+  int32_t nembed = 0;
   const int32_t tpw = 16 / std::max(1, cfg_.gqa_group);
 
   int32_t T = 0, ns = 0, nsamp = 0, nit = 0, nparted = 0, pslot = 0;
@@ -298,12 +315,15 @@ int32_t Scheduler::schedule(int32_t* buf) {
     qs[ns] = T;
     ql[ns] = n;
     cl[ns] = ctx;
+    const int32_t erow = s->embed_slot >= 0 ? s->embed_slot : L.max_seqs;
     for (int32_t j = 0; j < n; ++j) {
       const int32_t ppos = c0 + j;
       ids[T + j] = s->tokens[ppos];
       pos[T + j] = ppos;
       slots[T + j] = s->blocks[ppos / B] * B + ppos % B;
+      er[T + j] = erow;
     }
+    if (s->embed_slot >= 0) nembed += n;
     const int32_t nb = (ctx + B - 1) / B;
     std::memcpy(bt + (size_t)ns * L.max_blocks, s->blocks.data(), sizeof(int32_t) * nb);
     if (p.sample) {
@@ -344,6 +364,7 @@ int32_t Scheduler::schedule(int32_t* buf) {
     ids[t] = 0;
     pos[t] = 0;
     slots[t] = -1;
+    er[t] = L.max_seqs;
   }
   for (int32_t r = nsamp; r < L.max_seqs; ++r) {
     lr[r] = 0;
@@ -367,6 +388,7 @@ int32_t Scheduler::schedule(int32_t* buf) {
   counts[4] = nparted;
   counts[5] = pslot;
   counts[6] = ntrunc;  // rows that need the top-k / top-p threshold pass
+  counts[7] = nembed;  // tokens whose hidden states are pooled (embedding requests)
   if (nit > L.max_items)  // by construction (psz guard above, max_items sizing) this cannot happen
     throw std::logic_error("scheduler: attention item list overflows max_items");
   buf[L.n_items] = nit;
@@ -385,6 +407,7 @@ SeqOutput Scheduler::finish(Sequence* s, int32_t reason, double now) {
   o.num_forced = s->num_forced;
   o.t_first_token = s->t_first_token;
   o.t_finish = now;
+  o.embed_slot = s->embed_slot;  // FINISH_EMBED: read it; otherwise: clear it before reuse
   free_seq(s);
   s->running = false;
   return o;
@@ -399,6 +422,10 @@ std::vector<SeqOutput> Scheduler::commit(const int32_t* sampled, int32_t n) {
     Sequence* s = p.s;
     if (!p.sample) {
       register_full_blocks(s);
+      if (s->embed && s->num_computed == (int32_t)s->tokens.size()) {
+        outs.push_back(finish(s, FINISH_EMBED, now));  // frees the row: the caller reads it first
+        done.push_back(s);
+      }
       continue;
     }
     if (idx >= n) break;
@@ -458,6 +485,12 @@ std::vector<SeqOutput> Scheduler::drain_aborted() {
   std::vector<SeqOutput> o;
   o.swap(aborted_);
   return o;
+}
+
+std::vector<int32_t> Scheduler::take_embed_resets() {
+  std::vector<int32_t> r;
+  r.swap(embed_resets_);
+  return r;
 }
 
 void Scheduler::reset_prefix_cache() {

@@ -52,9 +52,13 @@ struct StepLayout {
   int32_t max_tokens, max_seqs, max_blocks, max_items;
   int32_t input_ids, positions, slots, q_start, q_len, ctx_len, logit_rows, mask_class, forced,
       offsets, temperature, top_k, top_p, seeds, items, n_items, part_size, counts, block_table, total;
+  int32_t embed_rows;  // [max_tokens]: pooling row of each token (embedding requests), max_seqs = none
 };
 
-enum FinishReason : int32_t { NOT_FINISHED = -1, FINISH_STOP = 0, FINISH_LENGTH = 1, FINISH_ABORT = 2 };
+enum FinishReason : int32_t {
+  NOT_FINISHED = -1, FINISH_STOP = 0, FINISH_LENGTH = 1, FINISH_ABORT = 2,
+  FINISH_EMBED = 3  // embedding request: prompt fully prefilled, pooled hidden state ready
+};
 
 struct SeqOutput {
   int64_t id;
@@ -66,6 +70,7 @@ struct SeqOutput {
   int32_t num_forced;
   double t_first_token;
   double t_finish;
+  int32_t embed_slot = -1;  // pooling row of an embedding request (FINISH_EMBED: holds the sums)
 };
 
 struct Sequence {
@@ -90,6 +95,10 @@ struct Sequence {
   int64_t arrival = 0;
   double t_first_token = -1.0;
   bool running = false;
+  // embedding request: the whole prompt is computed (no prefix-cache reuse: every token's
+  // final hidden state is summed into pooling row embed_slot), nothing is sampled
+  bool embed = false;
+  int32_t embed_slot = -1;
 };
 
 class Scheduler {
@@ -100,7 +109,8 @@ class Scheduler {
 
   void add_request(int64_t id, std::vector<int32_t> prompt, float temperature, int32_t max_tokens,
                    int64_t seed, bool ignore_eos, std::vector<int32_t> stop_ids,
-                   std::unique_ptr<Grammar> grammar, int32_t top_k = 0, float top_p = 1.0f);
+                   std::unique_ptr<Grammar> grammar, int32_t top_k = 0, float top_p = 1.0f,
+                   bool embed = false);
   bool abort(int64_t id);
   // Fill `buf` (layout()) for the next step. Returns the number of tokens in the
   // step (0 = nothing to run).
@@ -121,6 +131,9 @@ class Scheduler {
   int64_t aligned_steps() const { return stat_aligned_steps_; }
   bool has_work() const { return !running_.empty() || !waiting_.empty(); }
   void reset_prefix_cache();
+  // Pooling rows whose embedding request was preempted in the last schedule() (it restarts
+  // from token 0): the caller clears them before running the step.
+  std::vector<int32_t> take_embed_resets();
 
  private:
   bool ensure_blocks(Sequence* s, int32_t upto_tokens);
@@ -128,7 +141,7 @@ class Scheduler {
   void match_prefix(Sequence* s);
   void register_full_blocks(Sequence* s);
   SeqOutput finish(Sequence* s, int32_t reason, double now);
-  void free_seq(Sequence* s);
+  void free_seq(Sequence* s, bool keep_embed_slot = false);
 
   SchedulerConfig cfg_;
   StepLayout lay_;
@@ -143,6 +156,8 @@ class Scheduler {
   };
   std::vector<Planned> last_plan_;
   std::vector<SeqOutput> aborted_;
+  std::vector<int32_t> embed_free_;    // free pooling rows (0 .. max_seqs - 1)
+  std::vector<int32_t> embed_resets_;  // rows of preempted embedding requests, to be cleared
   int64_t arrival_counter_ = 0;
   int64_t stat_prompt_tokens_ = 0, stat_cached_tokens_ = 0, stat_preemptions_ = 0, stat_steps_ = 0;
   int64_t stat_aligned_steps_ = 0;

@@ -94,8 +94,9 @@ static void stress_scheduler(uint32_t seed) {
       std::vector<int32_t> prompt = prefixes[rng() % prefixes.size()];
       for (int j = 0, m = 1 + rng() % 40; j < m; ++j) prompt.push_back(10 + rng() % 900);
       std::unique_ptr<Grammar> g = (rng() % 3 == 0) ? random_grammar(rng) : nullptr;
+      const bool embed = rng() % 7 == 0;  // embedding request: prefill only, pooled rows
       sch.add_request(next_id, prompt, 0.7f, 1 + rng() % 48, next_id, rng() % 4 == 0, {3},
-                      std::move(g), rng() % 5, 1.0f);
+                      std::move(g), rng() % 5, 1.0f, embed);
       live.insert(next_id++);
     }
     if (!live.empty() && rng() % 17 == 0) {
@@ -110,21 +111,34 @@ static void stress_scheduler(uint32_t seed) {
     }
     const int32_t T = sch.schedule(buf.data());
     ++steps;
+    for (int32_t r : sch.take_embed_resets()) CHECK(r >= 0 && r < L.max_seqs);
     if (T == 0) continue;
     CHECK(T <= L.max_tokens);
     const int32_t* counts = buf.data() + L.counts;
     const int32_t ns = counts[1], nsamp = counts[2];
     CHECK(ns >= 0 && ns <= L.max_seqs && nsamp >= 0 && nsamp <= ns);
     CHECK(buf[L.n_items] >= 0 && buf[L.n_items] <= L.max_items);
+    int32_t nemb = 0;
+    std::set<int32_t> rows_used;
     for (int32_t t = 0; t < T; ++t) {
       const int32_t slot = buf[L.slots + t];
       CHECK(slot >= -1 && slot < cfg.num_blocks * cfg.block_size);
+      const int32_t er = buf[L.embed_rows + t];
+      CHECK(er >= 0 && er <= L.max_seqs);
+      if (er < L.max_seqs) {
+        ++nemb;
+        rows_used.insert(er);
+      }
     }
+    CHECK(nemb == counts[7]);
+    CHECK(buf[L.embed_rows + T] == L.max_seqs || T == L.max_tokens);
     std::vector<int32_t> sampled(nsamp);
     for (auto& s : sampled) s = (rng() % 20 == 0) ? 2 : (rng() % 10 == 0 ? 7 : 10 + rng() % 900);
     for (const SeqOutput& o : sch.commit(sampled.data(), nsamp)) {
       CHECK(live.count(o.id) && !finished.count(o.id));
-      CHECK(o.finish_reason >= 0 && o.finish_reason <= 2);
+      CHECK(o.finish_reason >= 0 && o.finish_reason <= 3);
+      if (o.finish_reason == 3) CHECK(o.embed_slot >= 0);
+      if (o.finish_reason == 3) CHECK(o.tokens.empty() && o.embed_slot < L.max_seqs);
       live.erase(o.id);
       finished.insert(o.id);
     }

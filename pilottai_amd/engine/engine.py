@@ -86,7 +86,7 @@ class EngineConfig:
     reply_tokens: Optional[int] = None  # fixed length of every reply schema's free-text slot (grammar.py)
 
 
-# TP step header: [op, T, ns, nsamp, bucket, masks_changed, n_copy, truncate]
+# TP step header: [op, T, ns, nsamp, bucket, masks_changed, n_copy, truncate, embed]
 _OP_STOP, _OP_STEP = 0, 1
 
 
@@ -104,6 +104,7 @@ class GenerationOutput:
     t_first_token: float
     t_finish: float
     _tok: Optional[Tokenizer] = field(default=None, repr=False)
+    embedding: Optional[np.ndarray] = field(default=None, repr=False)  # embedding requests: mean final hidden
 
     @property
     def text(self) -> str:
@@ -118,7 +119,7 @@ class GenerationOutput:
         return max(0.0, self.t_finish - self.t_arrival)
 
 
-_REASONS = {0: "stop", 1: "length", 2: "abort"}
+_REASONS = {0: "stop", 1: "length", 2: "abort", 3: "embed"}
 
 
 @dataclass
@@ -135,6 +136,7 @@ class _Request:
     t_arrival: float
     top_k: int = 0
     top_p: float = 1.0
+    embed: bool = False
 
 
 class LLMEngine:
@@ -224,6 +226,10 @@ class LLMEngine:
         self._sampled_dev = torch.zeros(S, dtype=torch.int32, device=self.device)
         self._sampled_host = torch.zeros(S, dtype=torch.int32, pin_memory=pin)
         self._keys_dev = torch.zeros(S, dtype=torch.float32, device=self.device)
+        # embedding requests: per-request pooling rows (+ one row that collects every other
+        # token), summed in the step graph, read and cleared when the request finishes
+        self._embed_pool = torch.zeros(L["max_seqs"] + 1, mc.hidden_size, dtype=torch.float32, device=self.device)
+        self._embed_rows = self._dev_meta[L["embed_rows"]:L["embed_rows"] + L["max_tokens"]]
         tpw = 16 // (self.model.h_local // self.model.kv_local)
         self._tpw = tpw
         self._max_parts = (self.max_model_len + ops.ATT_PART - 1) // ops.ATT_PART
@@ -241,7 +247,7 @@ class LLMEngine:
         self._graph_pool = None
         self.use_graphs = cfg.use_graphs and self.on_gpu
         self.is_driver = self.tp.rank == 0
-        self._tp_header = torch.zeros(8, dtype=torch.int64)
+        self._tp_header = torch.zeros(9, dtype=torch.int64)
         self._tp_closed = False
         # ---- request plumbing
         self._inbox: "queue.SimpleQueue" = queue.SimpleQueue()
@@ -317,9 +323,10 @@ class LLMEngine:
                         m.block_table, m.items[:n_it], m.n_items, m.att_counters, m.logit_rows, num_seqs=ns,
                         part_size=m.part_size)
 
-    def _forward_and_sample(self, bucket: int, s_b: int, ns: int, trunc: bool = False):
+    def _forward_and_sample(self, bucket: int, s_b: int, ns: int, trunc: bool = False, embed: bool = False):
         meta = self._meta_for(bucket, s_b, ns)
-        logits = self.model.forward(meta, self.kv, bucket, s_b, self._part_o, self._part_ml)
+        logits = self.model.forward(meta, self.kv, bucket, s_b, self._part_o, self._part_ml,
+                                    embed=(self._embed_rows, self._embed_pool) if embed else None)
         tau = None
         if trunc:
             # exact top-k / top-p threshold on the full vocabulary (TP: all-gathered)
@@ -343,17 +350,19 @@ class LLMEngine:
             best = keys.argmax(0, keepdim=True)
             self._sampled_dev[:s_b].copy_(toks.gather(0, best).squeeze(0))
 
-    def _run(self, bucket: int, ns: int, trunc: bool, n_copy: int):
-        """Replay the (bucket, trunc) graph — capturing it first if needed — or run eagerly."""
+    def _run(self, bucket: int, ns: int, trunc: bool, n_copy: int, embed: bool = False):
+        """Replay the (bucket, trunc, embed) graph — capturing it first if needed — or run eagerly."""
         if not self.use_graphs:
-            self._forward_and_sample(bucket, self._seq_bucket(bucket), ns, trunc)
+            self._forward_and_sample(bucket, self._seq_bucket(bucket), ns, trunc, embed)
             return
-        g = self._graphs.get((bucket, trunc))
+        g = self._graphs.get((bucket, trunc, embed))
         if g is None:
             saved = self._dev_meta[:n_copy].clone()
-            self.capture_graphs([bucket], trunc=trunc)  # clobbers the device metadata
+            pool = self._embed_pool.clone()
+            self.capture_graphs([bucket], trunc=trunc, embed=embed)  # clobbers the device metadata
             self._dev_meta[:n_copy].copy_(saved)
-            g = self._graphs[(bucket, trunc)]
+            self._embed_pool.copy_(pool)
+            g = self._graphs[(bucket, trunc, embed)]
         g.replay()
         self.stats["graph_replays"] += 1
 
@@ -365,10 +374,12 @@ class LLMEngine:
         L = self.L
         d = torch.zeros(L["total"], dtype=torch.int32)
         d[L["slots"]:L["slots"] + L["max_tokens"]] = -1
+        d[L["embed_rows"]:L["embed_rows"] + L["max_tokens"]] = L["max_seqs"]
         self._dev_meta.copy_(d.to(self.device))
 
-    def capture_graphs(self, buckets: Optional[Sequence[int]] = None, trunc: bool = False):
-        """Capture one hipGraph per token bucket (shared memory pool)."""
+    def capture_graphs(self, buckets: Optional[Sequence[int]] = None, trunc: bool = False, embed: bool = False):
+        """Capture one hipGraph per token bucket (shared memory pool); the top-k/top-p and
+        embedding-pooling variants are captured on first use."""
         if not self.use_graphs:
             return
         self._dummy_meta()
@@ -376,19 +387,21 @@ class LLMEngine:
             self._graph_pool = torch.cuda.graph_pool_handle()
         t0 = time.time()
         for b in sorted(buckets or self.buckets, reverse=True):
-            if (b, trunc) in self._graphs:
+            if (b, trunc, embed) in self._graphs:
                 continue
             s_b = self._seq_bucket(b)
             st = torch.cuda.Stream(device=self.device)
             st.wait_stream(torch.cuda.current_stream())
             with torch.cuda.stream(st):
                 for _ in range(2):
-                    self._forward_and_sample(b, s_b, 0, trunc)
+                    self._forward_and_sample(b, s_b, 0, trunc, embed)
             torch.cuda.current_stream().wait_stream(st)
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, pool=self._graph_pool):
-                self._forward_and_sample(b, s_b, 0, trunc)
-            self._graphs[(b, trunc)] = g
+                self._forward_and_sample(b, s_b, 0, trunc, embed)
+            self._graphs[(b, trunc, embed)] = g
+        if embed:
+            self._embed_pool.zero_()  # the capture's dummy steps pooled into row max_seqs only
         torch.cuda.synchronize()
         log.info("captured %d hipGraphs in %.1fs", len(self._graphs), time.time() - t0)
 
@@ -402,11 +415,13 @@ class LLMEngine:
     def submit(self, prompt_ids: Sequence[int], callback: Callable[[GenerationOutput], None], *,
                temperature: float = 0.7, max_tokens: int = 256, seed: Optional[int] = None,
                ignore_eos: bool = False, stop_ids: Sequence[int] = (), grammar: Optional[list] = None,
-               request_id: Optional[int] = None, top_k: int = 0, top_p: float = 1.0) -> int:
+               request_id: Optional[int] = None, top_k: int = 0, top_p: float = 1.0, embed: bool = False) -> int:
         """Thread-safe; `callback` runs on the engine thread when the request finishes.
 
         top_k > 0 / top_p < 1 truncate the (grammar-masked) distribution before
-        sampling (exact threshold kernel, csrc/ops/sampling.hip)."""
+        sampling (exact threshold kernel, csrc/ops/sampling.hip). embed=True: an embedding
+        request — the prompt is prefilled in the continuous batch (no prefix-cache reuse),
+        nothing is sampled, and the output carries the mean final-norm hidden state."""
         if self._err is not None:
             raise RuntimeError(f"engine failed: {self._err!r}")
         rid = request_id if request_id is not None else self.new_request_id()
@@ -414,7 +429,7 @@ class LLMEngine:
             seed = (self.cfg.seed * 0x9E3779B1 + rid * 0x85EBCA77) & 0x7FFFFFFFFFFFFFFF
         req = _Request(rid, list(prompt_ids), float(temperature), int(max_tokens), int(seed),
                        bool(ignore_eos), list(stop_ids), grammar, callback, self._rt.now(),
-                       int(top_k or 0), float(1.0 if top_p is None else top_p))
+                       int(top_k or 0), float(1.0 if top_p is None else top_p), bool(embed))
         self._inbox.put(req)
         self._wake.set()
         return rid
@@ -448,6 +463,16 @@ class LLMEngine:
         if self._err is not None:
             raise RuntimeError(f"engine failed: {self._err!r}")
         return [results[i] for i in ids]
+
+    def embed(self, prompts: Sequence[Sequence[int]]) -> np.ndarray:
+        """Mean final-norm hidden state of each prompt, [B, hidden] fp32, computed as
+        embedding requests inside the continuous batch (the engine's own kernels and
+        graphs, batched with whatever else is running). Blocking; thread-safe."""
+        outs = self.generate([list(p) or [0] for p in prompts], embed=True, temperature=0.0, max_tokens=1)
+        bad = [o.finish_reason for o in outs if o.embedding is None]
+        if bad:
+            raise RuntimeError(f"embedding requests did not complete: {bad}")
+        return np.stack([o.embedding for o in outs]) if outs else np.zeros((0, self.model_cfg.hidden_size), np.float32)
 
     def prewarm(self, prompt_ids: Sequence[int], timeout: float = 300.0) -> int:
         """Compute and cache the KV of `prompt_ids` (prefix cache) without keeping
@@ -510,13 +535,13 @@ class LLMEngine:
         with torch.inference_mode():
             while True:
                 self.tp.broadcast(h, cpu=True)
-                op, T, ns, nsamp, bucket, masks_changed, n_copy, trunc = (int(v) for v in h.tolist())
+                op, T, ns, nsamp, bucket, masks_changed, n_copy, trunc, embed = (int(v) for v in h.tolist())
                 if op == _OP_STOP:
                     break
                 if masks_changed:
                     self.tp.broadcast(self._class_masks)
                 self.tp.broadcast(self._dev_meta[:n_copy])
-                self._run(bucket, ns, bool(trunc), n_copy)
+                self._run(bucket, ns, bool(trunc), n_copy, bool(embed))
                 self._car_fetch()
                 if self.on_gpu:
                     torch.cuda.current_stream().synchronize()
@@ -547,7 +572,7 @@ class LLMEngine:
                 break
             self._reqs[req.rid] = req
             self.sched.add_request(req.rid, req.prompt_ids, req.temperature, req.max_tokens, req.seed,
-                                   req.ignore_eos, req.stop_ids, req.grammar, req.top_k, req.top_p)
+                                   req.ignore_eos, req.stop_ids, req.grammar, req.top_k, req.top_p, req.embed)
             self.stats["requests"] += 1
         while True:
             try:
@@ -559,13 +584,18 @@ class LLMEngine:
             self._deliver(o)
 
     def _deliver(self, o):
-        rid, toks, reason, plen, cached, nsamp, nforced, t_first, t_fin = o
+        rid, toks, reason, plen, cached, nsamp, nforced, t_first, t_fin, eslot = o
+        emb = None
+        if eslot >= 0:  # the request's pooling row: read it (finished) and clear it for reuse
+            if reason == 3:
+                emb = (self._embed_pool[eslot] / max(1, plen)).cpu().numpy()
+            self._embed_pool[eslot].zero_()
         req = self._reqs.pop(rid, None)
         self.stats["finished"] += 1
         if req is None:
             return
         out = GenerationOutput(rid, list(toks), _REASONS.get(reason, "stop"), plen, cached, len(toks),
-                               nsamp, nforced, req.t_arrival, t_first, t_fin, self.tok)
+                               nsamp, nforced, req.t_arrival, t_first, t_fin, self.tok, emb)
         # per-request timings: TTFT = arrival -> first token, TPOT = later tokens' mean gap
         if t_first > 0:
             n_out = max(1, len(toks))
@@ -590,20 +620,23 @@ class LLMEngine:
                 raise RuntimeError("KV cache too small for the head request")
             return False
         c = self._host_np[L["counts"]:L["counts"] + 8]
-        ns, nsamp, trunc = int(c[1]), int(c[2]), int(c[6]) > 0
+        ns, nsamp, trunc, embed = int(c[1]), int(c[2]), int(c[6]) > 0, int(c[7]) > 0
         bucket = next(b for b in self.buckets if b >= T)
         s_b = self._seq_bucket(bucket)
         masks_changed = self._sync_masks()
-        n_copy = L["block_table"] + ns * L["max_blocks"]
+        n_copy = L["embed_rows"] + bucket if embed else L["block_table"] + ns * L["max_blocks"]
+        resets = self.sched.take_embed_resets()
+        if resets:  # preempted embedding requests restart from token 0
+            self._embed_pool[torch.tensor(resets, dtype=torch.long, device=self.device)] = 0.0
         if self.on_gpu:
             self._dev_meta[:n_copy].copy_(self._host_meta[:n_copy], non_blocking=True)
         if self.tp.size > 1:
-            self._tp_send(_OP_STEP, T, ns, nsamp, bucket, int(masks_changed), n_copy, int(trunc))
+            self._tp_send(_OP_STEP, T, ns, nsamp, bucket, int(masks_changed), n_copy, int(trunc), int(embed))
             if masks_changed:
                 self.tp.broadcast(self._class_masks)
             self.tp.broadcast(self._dev_meta[:n_copy])
         with torch.inference_mode(), trace_range("engine.forward"):
-            self._run(bucket, ns, trunc, n_copy)
+            self._run(bucket, ns, trunc, n_copy, embed)
         if nsamp:
             self._sampled_host[:nsamp].copy_(self._sampled_dev[:nsamp], non_blocking=self.on_gpu)
         self._car_fetch()

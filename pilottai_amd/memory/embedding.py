@@ -6,8 +6,10 @@ deterministic, needs no weights, and makes cosine similarity track lexical
 overlap — a strict generalisation of the reference's case-insensitive
 substring search (pilott/memory/enhanced_memory.py:110), which it replaces.
 
-`EngineEmbedder`: mean-pooled token embeddings of the local Llama engine's model,
-projected to D by a fixed random orthogonal map (meaningful with real weights).
+`EngineEmbedder`: mean-pooled final hidden states of the local Llama engine's model,
+projected to D by a fixed random orthogonal map (meaningful with real weights). By
+default (`pool="engine"`) the texts go through the serving engine itself as embedding
+requests — same kernels, same continuous batch as the agents' calls.
 """
 from __future__ import annotations
 
@@ -55,13 +57,17 @@ class HashingEmbedder:
 
 
 class EngineEmbedder:
-    """Embeddings from the serving model itself: final hidden states of
-    a dense forward (LlamaModel.hidden_states) mean-pooled over the text's tokens,
-    projected to `dim` by a fixed orthonormal matrix and L2-normalised. Texts are
-    embedded in batches of up to `batch_size`, truncated to `max_tokens`. With
-    `pool="tokens"` the (much cheaper) mean of input token embeddings is used."""
+    """Embeddings from the serving model itself: final-norm hidden states
+    mean-pooled over the text's tokens, projected to `dim` by a fixed orthonormal matrix
+    and L2-normalised; texts truncated to `max_tokens`.
 
-    def __init__(self, engine, dim: int = 1024, seed: int = 0, pool: str = "hidden", batch_size: int = 16,
+    pool="engine" (default): embedding requests through `LLMEngine.embed` — prefilled by
+    the engine's kernels inside its continuous batch, pooled in the step graph.
+    pool="hidden": a separate dense PyTorch forward (LlamaModel.hidden_states), the
+    reference the engine path is tested against. pool="tokens": the (much cheaper) mean
+    of the input token embeddings."""
+
+    def __init__(self, engine, dim: int = 1024, seed: int = 0, pool: str = "engine", batch_size: int = 16,
                  max_tokens: int = 512):
         import torch
 
@@ -71,7 +77,7 @@ class EngineEmbedder:
         g = torch.Generator().manual_seed(seed)
         q, _ = torch.linalg.qr(torch.randn(d, max(d, dim), generator=g))
         self.proj = q[:, :dim].contiguous().to(engine.device, torch.float32)
-        self.pool = pool if getattr(engine.model.tp, "size", 1) == 1 else "tokens"
+        self.pool = pool if (pool == "engine" or getattr(engine.model.tp, "size", 1) == 1) else "tokens"
         self.batch_size = batch_size
         self.max_tokens = max_tokens
 
@@ -81,6 +87,12 @@ class EngineEmbedder:
 
         m = self.engine.model
         rows: List[np.ndarray] = []
+        if self.pool == "engine":
+            ids = [self.engine.tok.encode(t)[: self.max_tokens] or [0] for t in texts]
+            if not ids:
+                return np.zeros((0, self.dim), np.float32)
+            h = torch.from_numpy(self.engine.embed(ids)).to(self.proj.device)
+            return F.normalize(h @ self.proj, dim=1).cpu().numpy()
         with torch.inference_mode():
             if self.pool == "hidden":
                 for i in range(0, len(texts), self.batch_size):

@@ -324,16 +324,19 @@ class LlamaModel:
         return h
 
     def forward(self, meta: StepMeta, kv: KVCache, num_tokens: int, num_logit_rows: int,
-                part_o: torch.Tensor, part_ml: torch.Tensor) -> torch.Tensor:
-        """Returns local-vocab logits [num_logit_rows, V/tp] (bf16)."""
+                part_o: torch.Tensor, part_ml: torch.Tensor, embed=None) -> torch.Tensor:
+        """Returns local-vocab logits [num_logit_rows, V/tp] (bf16).
+
+        embed = (rows [>= T] int32, pool [R + 1, d] fp32): every token's final-norm hidden
+        state is added to pool[rows[t]] (embedding requests; row R collects the others)."""
         cfg = self.cfg
         T = num_tokens
         if self.decode_packed and T <= self.DECODE_FUSED_MAX_T:
-            return self._forward_decode(meta, kv, T, num_logit_rows, part_o, part_ml)
+            return self._forward_decode(meta, kv, T, num_logit_rows, part_o, part_ml, embed)
         if self.decode_packed and T <= self.WIDE_MAX_T:
-            return self._forward_wide(meta, kv, T, num_logit_rows, part_o, part_ml)
+            return self._forward_wide(meta, kv, T, num_logit_rows, part_o, part_ml, embed)
         if self.decode_packed and T <= self.MID_MAX_T:
-            return self._forward_mid(meta, kv, T, num_logit_rows, part_o, part_ml)
+            return self._forward_mid(meta, kv, T, num_logit_rows, part_o, part_ml, embed)
         H, KVh, hd = self.h_local, self.kv_local, cfg.head_dim
         ids = meta.input_ids[:T].long() if self.device.type == "cpu" else meta.input_ids[:T]
         h = self._embed(ids)
@@ -358,13 +361,15 @@ class LlamaModel:
                 self.tp.all_reduce(d)
             nxt = self.layers[li + 1]["ln1"] if li + 1 < len(self.layers) else self.norm
             x = ops.fused_add_rmsnorm(resid, d, nxt, cfg.rms_eps)
+        if embed is not None:
+            self._pool_embed(x, T, embed)
         rows = meta.logit_rows[:num_logit_rows]
         rows = rows.long() if self.device.type == "cpu" else rows
         xs = x.index_select(0, rows)
         return ops.linear(xs, self.lm_head, "lm_head")
 
     def _forward_decode(self, meta: StepMeta, kv: KVCache, T: int, num_logit_rows: int,
-                        part_o: torch.Tensor, part_ml: torch.Tensor) -> torch.Tensor:
+                        part_o: torch.Tensor, part_ml: torch.Tensor, embed=None) -> torch.Tensor:
         """Decode-sized step on the packed weights: 5 launches per layer
         (norm+QKV+RoPE+KV write, attention, O+residual, norm+gate_up+SwiGLU,
         down+residual) instead of 9; the residual stream h is updated in place."""
@@ -402,6 +407,8 @@ class LlamaModel:
                 h.add_(d)
             else:
                 ops.decode_gemm(a, L["w2_p"], "resid", resid=h, out=h, **self._down_cfg(T))
+        if embed is not None:
+            self._pool_embed(ops.rmsnorm(h, self.norm, eps), T, embed)
         rows = meta.logit_rows[:num_logit_rows]
         rows = rows.long() if self.device.type == "cpu" else rows
         xs = ops.rmsnorm(h.index_select(0, rows), self.norm, eps)
@@ -416,7 +423,7 @@ class LlamaModel:
         return {"nt": 2, "waves": 16, "splits": 2} if T > 8 else {}
 
     def _forward_wide(self, meta: StepMeta, kv: KVCache, T: int, num_logit_rows: int,
-                      part_o: torch.Tensor, part_ml: torch.Tensor) -> torch.Tensor:
+                      part_o: torch.Tensor, part_ml: torch.Tensor, embed=None) -> torch.Tensor:
         """Small-batch step (DECODE_FUSED_MAX_T < T <= WIDE_MAX_T: decode rows plus
         grammar jump-forward runs or a short prefill chunk) on the packed weights:
         x staged once per workgroup through LDS, split-K for the narrow projections,
@@ -453,12 +460,21 @@ class LlamaModel:
                 h.add_(d)
             else:
                 ops.wide_gemm(a, L["w2_p"], "resid", resid=h, out=h)
+        if embed is not None:
+            self._pool_embed(ops.rmsnorm(h, self.norm, eps), T, embed)
         rows = meta.logit_rows[:num_logit_rows]
         rows = rows.long() if self.device.type == "cpu" else rows
         xs = ops.rmsnorm(h.index_select(0, rows), self.norm, eps)
         if num_logit_rows <= 16:  # decode_gemm beats hipBLASLt on the LM head only up to 16 rows
             return ops.decode_gemm(xs, self.lm_head_p, "plain")
         return ops.linear(xs, self.lm_head, "lm_head")
+
+    @staticmethod
+    def _pool_embed(hn: torch.Tensor, T: int, embed):
+        """Sum each token's final-norm hidden state into its pooling row (graph-capturable)."""
+        rows, pool = embed
+        pool[-1].zero_()  # the row collecting non-embedding tokens holds one step's sums only
+        pool.index_add_(0, rows[:T].long(), hn[:T].float())
 
     def _mid_cfg(self, kind: str, T: int) -> dict:
         for mmax, fm, fn, S in self.MID_CFG[kind]:
@@ -467,7 +483,7 @@ class LlamaModel:
         return {}
 
     def _forward_mid(self, meta: StepMeta, kv: KVCache, T: int, num_logit_rows: int,
-                     part_o: torch.Tensor, part_ml: torch.Tensor) -> torch.Tensor:
+                     part_o: torch.Tensor, part_ml: torch.Tensor, embed=None) -> torch.Tensor:
         """Mid-size step (WIDE_MAX_T < T <= MID_MAX_T: decode rows plus prefill chunks) on
         the packed weights, 4 projection launches + attention per layer
         (csrc/ops/gemm_mid.hip):
@@ -517,6 +533,8 @@ class LlamaModel:
                 ops.row_sumsq(h, out=ss_a)
             else:
                 ops.mid_gemm(a, L["w2_p"], "resid", resid=h, out=h, ss_out=ss_a, ss_zero=ss_b, **c_dn)
+        if embed is not None:
+            self._pool_embed(ops.rmsnorm(h, self.norm, eps), T, embed)
         rows = meta.logit_rows[:num_logit_rows]
         rows = rows.long() if self.device.type == "cpu" else rows
         xs = ops.rmsnorm(h.index_select(0, rows), self.norm, eps)

@@ -153,3 +153,25 @@ def _eng8b(gpu):
                                              token_buckets=[16, 48, 128, 256, 512], token_align=0),
                                 device=gpu)
     return _ENG8B["e"]
+
+
+def test_embedding_requests_on_the_gpu_engine(engine):
+    """Embedding requests run through the engine's kernels and graphs (every forward path:
+    a short prompt alone takes the packed decode/wide path, a long one chunked prefill on
+    the library path) and pool the same final hidden state as the dense forward."""
+    tok = engine.tok
+    prompts = [tok.encode("alpha beta"), tok.encode("The orchestrator delegates a task to worker agents " * 20),
+               tok.encode("memory lookup for agent step " * 5)]
+    v = torch.from_numpy(engine.embed(prompts))
+    ref = torch.cat([engine.model.hidden_states([p]).float().cpu() for p in prompts])
+    rel = (v - ref).norm(dim=1) / ref.norm(dim=1)
+    assert float(rel.max()) < 3e-2, rel
+    # beside generation in the same batch, and again (pool rows are reused cleanly)
+    outs = {}
+    gen = engine.submit(prompts[1] + [11, 12], lambda o: outs.setdefault(o.request_id, o), temperature=0.0,
+                        max_tokens=4, ignore_eos=True)
+    v2 = torch.from_numpy(engine.embed(prompts))
+    while gen not in outs:
+        engine.step()
+    assert float(((v2 - v).norm(dim=1) / v.norm(dim=1)).max()) < 1e-2
+    assert float(engine._embed_pool[:-1].abs().sum()) == 0.0

@@ -171,6 +171,38 @@ def test_engine_cpu_tiny_end_to_end(tok):
         assert row[t] >= row.max() - 0.05
 
 
+def test_engine_embedding_requests_match_dense_forward(tok):
+    """Embedding requests inside the continuous batch (engine.embed): the pooled final
+    hidden state equals the dense reference forward's, for prompts that span several
+    prefill chunks, share a cached prefix with a generation request (embeddings never
+    reuse the prefix cache), and run beside that request."""
+    from pilottai_amd.engine.engine import EngineConfig, LLMEngine
+    from pilottai_amd.memory.embedding import EngineEmbedder
+
+    e = LLMEngine(EngineConfig(model="tiny", max_num_seqs=8, max_num_batched_tokens=64, max_model_len=512,
+                               num_kv_blocks=128), device="cpu")
+    p_long = tok.encode("Task: summarize the quarterly report. " * 12)[:150]  # 3 chunks of <= 64
+    p_short = tok.encode("alpha beta gamma")
+    e.generate([p_long], temperature=0.0, max_tokens=2, ignore_eos=True)  # p_long now in the prefix cache
+    outs = {}
+
+    def cb(o):
+        outs[o.request_id] = o
+
+    gen = e.submit(p_long + [5, 6, 7], cb, temperature=0.0, max_tokens=3, ignore_eos=True)
+    v = e.embed([p_long, p_short])
+    while gen not in outs:
+        e.step()
+    ref = e.model.hidden_states([p_long, p_short]).float()
+    rel = (torch.from_numpy(v) - ref).norm(dim=1) / ref.norm(dim=1)
+    assert float(rel.max()) < 2e-2, rel  # bf16 paths: ~0.5 % (chunking changes nothing)
+    assert outs[gen].finish_reason == "length" and len(outs[gen].token_ids) == 3
+    assert float(e._embed_pool[:-1].abs().sum()) == 0.0  # request rows cleared after delivery
+    emb = EngineEmbedder(e, dim=64)  # default: through the engine
+    w = emb.embed(["alpha beta", "alpha beta"])
+    assert w.shape == (2, 64) and abs(float((w[0] * w[1]).sum()) - 1.0) < 1e-4
+
+
 def test_reference_sampler_masks_and_forced():
     V = 256
     logits = torch.randn(3, V).to(torch.bfloat16)
@@ -253,7 +285,7 @@ def test_hidden_states_match_reference_forward():
             def encode(t):
                 return [ord(c) % 1000 for c in t]
 
-    emb = EngineEmbedder(_E(), dim=64)
+    emb = EngineEmbedder(_E(), dim=64, pool="hidden")
     v = emb.embed(["alpha beta", "alpha beta", "unrelated text here"])
     assert v.shape == (3, 64) and abs(float((v[0] * v[1]).sum()) - 1.0) < 1e-4
 
