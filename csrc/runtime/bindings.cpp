@@ -144,6 +144,14 @@ PYBIND11_MODULE(_runtime, m) {
       })
       .def("abort", &Scheduler::abort)
       .def("take_embed_resets", &Scheduler::take_embed_resets)
+      .def("num_free_embed_rows", &Scheduler::num_free_embed_rows)
+      .def("debug_state", [](const Scheduler& s) {
+        py::list l;
+        for (const auto& x : s.debug_state())
+          l.append(py::make_tuple(x.id, x.running, x.embed, x.embed_slot, x.num_computed, x.num_tokens,
+                                  x.num_blocks));
+        return l;
+      })
       .def("drain_aborted", [](Scheduler& s) { return outputs_to_py(s.drain_aborted()); })
       .def("has_work", &Scheduler::has_work)
       .def("reset_prefix_cache", &Scheduler::reset_prefix_cache)

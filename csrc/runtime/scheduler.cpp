@@ -487,6 +487,16 @@ std::vector<SeqOutput> Scheduler::drain_aborted() {
   return o;
 }
 
+std::vector<Scheduler::SeqState> Scheduler::debug_state() const {
+  std::vector<SeqState> out;
+  for (const auto& kv : seqs_) {
+    const Sequence* s = kv.second.get();
+    out.push_back({s->id, s->running, s->embed, s->embed_slot, s->num_computed, (int32_t)s->tokens.size(),
+                   (int32_t)s->blocks.size()});
+  }
+  return out;
+}
+
 std::vector<int32_t> Scheduler::take_embed_resets() {
   std::vector<int32_t> r;
   r.swap(embed_resets_);

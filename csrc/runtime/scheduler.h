@@ -134,6 +134,13 @@ class Scheduler {
   // Pooling rows whose embedding request was preempted in the last schedule() (it restarts
   // from token 0): the caller clears them before running the step.
   std::vector<int32_t> take_embed_resets();
+  struct SeqState {
+    int64_t id;
+    bool running, embed;
+    int32_t embed_slot, num_computed, num_tokens, num_blocks;
+  };
+  std::vector<SeqState> debug_state() const;  // every live sequence (diagnostics)
+  int32_t num_free_embed_rows() const { return (int32_t)embed_free_.size(); }
 
  private:
   bool ensure_blocks(Sequence* s, int32_t upto_tokens);

@@ -171,7 +171,18 @@ def test_embedding_requests_on_the_gpu_engine(engine):
     gen = engine.submit(prompts[1] + [11, 12], lambda o: outs.setdefault(o.request_id, o), temperature=0.0,
                         max_tokens=4, ignore_eos=True)
     v2 = torch.from_numpy(engine.embed(prompts))
-    while gen not in outs:
-        engine.step()
+    import time
+
+    t0 = time.time()
+    while gen not in outs and time.time() - t0 < 60:
+        if engine._thread is None:  # no engine thread (an earlier test may have started one)
+            if not engine.step():
+                s = engine.sched
+                raise AssertionError(f"scheduler stalled: running={s.num_running} waiting={s.num_waiting} "
+                                     f"free_blocks={s.num_free_blocks()} free_rows={s.num_free_embed_rows()} "
+                                     f"seqs={s.debug_state()}")
+        else:
+            time.sleep(0.01)
+    assert gen in outs and engine.failed is None
     assert float(((v2 - v).norm(dim=1) / v.norm(dim=1)).max()) < 1e-2
     assert float(engine._embed_pool[:-1].abs().sum()) == 0.0
