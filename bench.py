@@ -68,6 +68,8 @@ def parse():
                     help="largest step on the LDS-DMA tiled mid-size path (default: the model's; 0 = off)")
     ap.add_argument("--att-wide-min-tokens", type=int, default=None,
                     help="prefill tokens per step from which attention uses the 4-wave LDS-staged items")
+    ap.add_argument("--no-prefix-dedup", action="store_true",
+                    help="admit requests whose prefix another request is prefilling right away (no deferral)")
     ap.add_argument("--no-prefetch", action="store_true", help="decode steps without the side-stream weight prefetch")
     ap.add_argument("--token-align", type=int, default=256, help="GEMM-friendly step sizes (0 = off)")
     ap.add_argument("--align-slack", type=int, default=96)
@@ -114,6 +116,7 @@ async def run_rank(a, rank: int, world: int, device):
                                  decode_fused_max_t=a.fused_max_t, wide_max_t=a.wide_max_t,
                                  mid_max_t=a.mid_max_t, reply_tokens=a.reply_tokens,
                                  prefetch_weights=False if a.no_prefetch else None,
+                                 dedup_inflight_prefix=not a.no_prefix_dedup,
                                  **({"att_wide_min_tokens": a.att_wide_min_tokens}
                                     if a.att_wide_min_tokens is not None else {})), device=device)
     register_engine(eng.model_cfg.name, eng)
@@ -249,6 +252,7 @@ async def run_rank(a, rank: int, world: int, device):
         "prompt_tokens": u1["prompt_tokens"] - u0["prompt_tokens"],
         "completion_tokens": u1["completion_tokens"] - u0["completion_tokens"],
         "busy_s": st1["busy_s"] - st0["busy_s"], "prefix_hit": em["prefix_cache_hit_tokens"],
+        "prefix_defers": em["prefix_defers"],
         "host_phases": {k: st1[k] - st0[k] for k in ("host_sched_s", "host_launch_s", "device_wait_s",
                                                      "host_commit_s", "host_deliver_s")},
         "bucket_tokens": st1["bucket_tokens"] - st0["bucket_tokens"],
@@ -379,6 +383,7 @@ def main():
             "llm_calls_per_rank": [g["calls"] for g in gathered],
             "engine_busy_frac": round(tot("busy_s") / (dt * len(gathered)), 3),
             "prefix_cache_hit_frac": round(tot("prefix_hit") / max(1, tot("prompt_total")), 3),
+            "prefix_defers": tot("prefix_defers"),
             "graph_pad_frac": round(1 - tot("tokens") / max(1, tot("bucket_tokens")), 3),
             # rank 0's engine thread, ms per step: schedule / copy+launch / wait for the device /
             # commit / deliver (the host phases are the device's idle time between steps)

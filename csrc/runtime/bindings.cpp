@@ -97,6 +97,8 @@ PYBIND11_MODULE(_runtime, m) {
         if (d.contains("att_qcols")) c.att_qcols = d["att_qcols"].cast<int32_t>();
         if (d.contains("att_wide_min_tokens")) c.att_wide_min_tokens = d["att_wide_min_tokens"].cast<int32_t>();
         if (d.contains("prefix_caching")) c.prefix_caching = d["prefix_caching"].cast<bool>();
+        if (d.contains("dedup_inflight_prefix")) c.dedup_inflight_prefix = d["dedup_inflight_prefix"].cast<bool>();
+        if (d.contains("max_prefix_defer")) c.max_prefix_defer = d["max_prefix_defer"].cast<int32_t>();
         if (d.contains("split_decode")) c.split_decode = d["split_decode"].cast<bool>();
         if (d.contains("token_align")) c.token_align = d["token_align"].cast<int32_t>();
         if (d.contains("kv_heads")) c.kv_heads = d["kv_heads"].cast<int32_t>();
@@ -145,6 +147,7 @@ PYBIND11_MODULE(_runtime, m) {
       .def("abort", &Scheduler::abort)
       .def("take_embed_resets", &Scheduler::take_embed_resets)
       .def("num_free_embed_rows", &Scheduler::num_free_embed_rows)
+      .def_property_readonly("prefix_defers", &Scheduler::prefix_defers)
       .def("debug_state", [](const Scheduler& s) {
         py::list l;
         for (const auto& x : s.debug_state())

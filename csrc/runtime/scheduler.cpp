@@ -4,6 +4,7 @@
 #include <chrono>
 #include <cstring>
 #include <stdexcept>
+#include <unordered_set>
 
 namespace rt {
 
@@ -84,6 +85,14 @@ void Scheduler::add_request(int64_t id, std::vector<int32_t> prompt, float tempe
   Sequence* raw = s.get();
   seqs_.emplace(id, std::move(s));
   waiting_.push_back(raw);
+}
+
+uint64_t Scheduler::prefix_key(const Sequence* s) const {
+  // hash chain of the first two full blocks (what match_prefix would look up first)
+  const int32_t B = cfg_.block_size;
+  if ((int32_t)s->tokens.size() <= 2 * B) return 0;
+  const uint64_t h1 = hash_block(0, s->tokens.data(), B);
+  return hash_block(h1, s->tokens.data() + B, B) | 1ull;
 }
 
 void Scheduler::free_seq(Sequence* s, bool keep_embed_slot) {
@@ -189,11 +198,32 @@ int32_t Scheduler::schedule(int32_t* buf) {
                                 [](Sequence* s) { return !s->running; }),
                  running_.end());
 
-  // 2) admit waiting sequences (FCFS) into the remaining budget
+  // 2) admit waiting sequences (FCFS) into the remaining budget. A request whose
+  //    leading blocks another sequence is prefilling right now (same prefix_key) is
+  //    deferred (at most max_prefix_defer steps) so it reuses them once registered:
+  //    an agent task's orchestrator analysis, agent analysis and tool selection arrive
+  //    together and all start with the task text.
   const int32_t watermark = std::max(1, cfg_.num_blocks / 100);
+  const bool dedup = cfg_.prefix_caching && cfg_.dedup_inflight_prefix;
+  std::unordered_set<uint64_t> inflight;
+  if (dedup)
+    for (const Sequence* r : running_)
+      if (r->running && !r->embed && r->num_computed < 2 * B) {
+        const uint64_t k = prefix_key(r);
+        if (k) inflight.insert(k);
+      }
+  std::vector<Sequence*> deferred;
   while (!waiting_.empty() && (int32_t)last_plan_.size() < cfg_.max_num_seqs &&
          (int32_t)running_.size() < cfg_.max_num_seqs && tok_budget > 0 && prefill_budget > 0) {
     Sequence* s = waiting_.front();
+    const uint64_t key = (dedup && !s->embed && s->blocks.empty()) ? prefix_key(s) : 0;
+    if (key && inflight.count(key) && s->defer_count < cfg_.max_prefix_defer) {
+      waiting_.pop_front();
+      ++s->defer_count;
+      ++stat_prefix_defers_;
+      deferred.push_back(s);
+      continue;
+    }
     if (s->embed && s->embed_slot < 0) {
       if (embed_free_.empty()) break;  // every pooling row is in use: wait
       s->embed_slot = embed_free_.back();
@@ -209,10 +239,12 @@ int32_t Scheduler::schedule(int32_t* buf) {
     waiting_.pop_front();
     s->running = true;
     running_.push_back(s);
+    if (key && s->num_computed < 2 * B) inflight.insert(key);  // its leading blocks are computed now
     last_plan_.push_back({s, n, !s->embed && s->num_computed + n == (int32_t)s->tokens.size()});
     tok_budget -= n;
     prefill_budget -= n;
   }
+  waiting_.insert(waiting_.begin(), deferred.begin(), deferred.end());  // keep arrival order
 
   // 2b) align the step size (see SchedulerConfig::token_align): trim chunk tails,
   //     newest entries first, never below one token per entry

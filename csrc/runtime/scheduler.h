@@ -37,6 +37,12 @@ struct SchedulerConfig {
   int32_t att_wide_min_tokens = 2048;  // ... used only when the step's prefill tokens reach this
                                        // (fewer, 4x wider items underfill the chip below it)
   bool prefix_caching = true;
+  // A request whose first two blocks are being prefilled right now by another sequence
+  // (the calls of one agent task all start with the task text and arrive together)
+  // waits up to max_prefix_defer steps for them and then reuses them from the prefix
+  // cache instead of computing the same KV again.
+  bool dedup_inflight_prefix = true;
+  int32_t max_prefix_defer = 4;
   bool split_decode = true;            // flash-decoding partitions for long contexts
   // GEMM-friendly step sizes: when a step has T > token_align tokens and
   // T % token_align <= align_slack, the tail of the multi-token chunks (prefill /
@@ -99,6 +105,7 @@ struct Sequence {
   // final hidden state is summed into pooling row embed_slot), nothing is sampled
   bool embed = false;
   int32_t embed_slot = -1;
+  int32_t defer_count = 0;  // steps deferred waiting for an in-flight identical prefix
 };
 
 class Scheduler {
@@ -129,6 +136,7 @@ class Scheduler {
   int64_t total_preemptions() const { return stat_preemptions_; }
   int64_t steps() const { return stat_steps_; }
   int64_t aligned_steps() const { return stat_aligned_steps_; }
+  int64_t prefix_defers() const { return stat_prefix_defers_; }
   bool has_work() const { return !running_.empty() || !waiting_.empty(); }
   void reset_prefix_cache();
   // Pooling rows whose embedding request was preempted in the last schedule() (it restarts
@@ -168,6 +176,8 @@ class Scheduler {
   int64_t arrival_counter_ = 0;
   int64_t stat_prompt_tokens_ = 0, stat_cached_tokens_ = 0, stat_preemptions_ = 0, stat_steps_ = 0;
   int64_t stat_aligned_steps_ = 0;
+  int64_t stat_prefix_defers_ = 0;
+  uint64_t prefix_key(const Sequence* s) const;
 };
 
 double now_seconds();

@@ -68,6 +68,7 @@ class EngineConfig:
     kv_cache_gb: Optional[float] = None
     kv_cache_fraction: float = 0.5
     prefix_caching: bool = True
+    dedup_inflight_prefix: bool = True  # requests wait for an identical prefix another request is prefilling
     split_decode: bool = True
     use_graphs: bool = True
     token_buckets: Optional[List[int]] = None
@@ -205,6 +206,7 @@ class LLMEngine:
             "att_qcols": cfg.att_qcols,
             "att_wide_min_tokens": cfg.att_wide_min_tokens,
             "prefix_caching": cfg.prefix_caching, "split_decode": cfg.split_decode,
+            "dedup_inflight_prefix": cfg.dedup_inflight_prefix,
             "token_align": cfg.token_align, "align_slack": cfg.align_slack,
             "kv_heads": self.model.kv_local,
             "eos_ids": list(self.tok.eos_ids)})
@@ -708,6 +710,7 @@ class LLMEngine:
             "total_kv_blocks": self.num_kv_blocks, "cached_kv_blocks": s.num_cached_blocks,
             "prompt_tokens": s.total_prompt_tokens, "prefix_cache_hit_tokens": s.total_cached_tokens,
             "preemptions": s.total_preemptions, "graphs": len(self._graphs), "aligned_steps": s.aligned_steps,
+            "prefix_defers": s.prefix_defers,
             "kv_cache_gb": self.kv.k.numel() * 2 * 2 / 2**30,
             "weights_gb": self.model.weight_bytes() / 2**30,
         })
