@@ -118,10 +118,10 @@ __global__ __launch_bounds__(WAVES * 64) void decode_gemm_kernel(const DgArgs A)
     xr[i] = x + (size_t)(m < M ? m : 0) * ldx + 8 * g;
   }
 
-  auto step = [&](const bf16x8 (&bw)[NT], int ks) {
+  auto step = [&](const bf16x8 (&bw)[NT], const bf16x8 (&ax)[MT]) {
 #pragma unroll
     for (int i = 0; i < MT; ++i) {
-      const bf16x8 a = *reinterpret_cast<const bf16x8*>(xr[i] + 32 * ks);
+      const bf16x8 a = ax[i];
       if constexpr (NORM) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
@@ -135,21 +135,45 @@ __global__ __launch_bounds__(WAVES * 64) void decode_gemm_kernel(const DgArgs A)
     }
   };
 
+  // Every load of a round (U chunks of W from HBM and the matching x fragments from L2)
+  // is issued before the first MFMA: left to itself the scheduler interleaved them with
+  // the MFMAs and kept only 2-5 loads in flight per wave, so each round paid several
+  // dependent L2 round trips for x (down_proj at M=8 streamed 4.6 TB/s). Loads are
+  // ordered chunk by chunk, so chunk u waits only for its own operands.
+  auto load_x = [&](bf16x8 (&ax)[MT], int k) {
+#pragma unroll
+    for (int i = 0; i < MT; ++i) ax[i] = *reinterpret_cast<const bf16x8*>(xr[i] + 32 * k);
+  };
+  // (sub-batches of UB chunks where a whole round would not fit the wave's registers:
+  // 16-wave workgroups leave 128 VGPRs per wave)
+  constexpr int LOAD_REGS = WAVES >= 16 ? 80 : 192;
+  constexpr int UB0 = LOAD_REGS / (4 * (NT + MT));
+  constexpr int UB = UB0 >= U ? U : (UB0 < 1 ? 1 : UB0);
   int ks = ks0;
   for (; ks + U <= ks1; ks += U) {
-    bf16x8 bw[U][NT];
 #pragma unroll
-    for (int u = 0; u < U; ++u)
+    for (int u0 = 0; u0 < U; u0 += UB) {
+      bf16x8 bw[UB][NT], ax[UB][MT];
 #pragma unroll
-      for (int j = 0; j < NT; ++j) bw[u][j] = wt[j][(size_t)(ks + u) * 64];
+      for (int u = 0; u < UB; ++u) {
+        if (u0 + u < U) {
 #pragma unroll
-    for (int u = 0; u < U; ++u) step(bw[u], ks + u);
+          for (int j = 0; j < NT; ++j) bw[u][j] = wt[j][(size_t)(ks + u0 + u) * 64];
+          load_x(ax[u], ks + u0 + u);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int u = 0; u < UB; ++u)
+        if (u0 + u < U) step(bw[u], ax[u]);
+    }
   }
   for (; ks < ks1; ++ks) {
-    bf16x8 bw[NT];
+    bf16x8 bw[NT], ax[MT];
 #pragma unroll
     for (int j = 0; j < NT; ++j) bw[j] = wt[j][(size_t)ks * 64];
-    step(bw, ks);
+    load_x(ax, ks);
+    step(bw, ax);
   }
 
   // C layout of a 16x16 tile: lane (g, c) holds rows 4g + r, column c.
@@ -280,7 +304,7 @@ __global__ __launch_bounds__(WAVES * 64) void decode_gemm_kernel(const DgArgs A)
 
 template <int MT, int NT, int WAVES, int EPI, bool NORM>
 static int launch_dg(const DgArgs& a, hipStream_t st) {
-  constexpr int U = MT == 1 ? 8 : (MT == 2 ? 4 : 2);
+  constexpr int U = MT == 1 ? 8 : (MT == 2 ? 4 : 2);  // chunks per round (16 per round for 8-wave groups was slower)
   const size_t lds = ((size_t)(WAVES + 1) * MT * 16 * (NT * 16 + 1) + 16) * sizeof(float);
   auto kern = decode_gemm_kernel<MT, NT, WAVES, U, EPI, NORM>;
   static bool attr = false;
