@@ -56,7 +56,10 @@ def parse():
     ap.add_argument("--workers", type=int, default=64)
     ap.add_argument("--model", default="llama-3-8b")
     ap.add_argument("--doc-words", type=int, default=120)
-    ap.add_argument("--kv-gb", type=float, default=48.0)
+    ap.add_argument("--kv-gb", type=float, default=None,
+                    help="KV-cache size per GPU (default: 85%% of the HBM left after the weights; 48 GB "
+                         "with --share-gpu). 288 GB per MI355X: a large pool keeps the prefix cache "
+                         "hitting over long runs (48 GB: 59.7%% hits over 20 steps vs 64.8%% at 160 GB)")
     ap.add_argument("--max-batched-tokens", type=int, default=2048)
     ap.add_argument("--temperature", type=float, default=0.7)
     ap.add_argument("--steps-per-task", type=int, default=1)
@@ -110,7 +113,10 @@ async def run_rank(a, rank: int, world: int, device):
         # before the engine sizes its KV pool: the index is resident beside the model
         memory, lookup = build_memory(a, device)
     eng = LLMEngine(EngineConfig(model=a.model if not a.cpu else "tiny", max_num_seqs=max(64, 2 * n_local),
-                                 max_num_batched_tokens=a.max_batched_tokens, kv_cache_gb=a.kv_gb if not a.cpu else None,
+                                 max_num_batched_tokens=a.max_batched_tokens,
+                                 kv_cache_gb=None if a.cpu else (a.kv_gb if a.kv_gb is not None else
+                                                                 (48.0 / max(1, world) if a.share_gpu else None)),
+                                 kv_cache_fraction=0.85,
                                  num_kv_blocks=4096 if a.cpu else None, seed=1234 + rank,
                                  token_align=a.token_align, align_slack=a.align_slack,
                                  decode_fused_max_t=a.fused_max_t, wide_max_t=a.wide_max_t,

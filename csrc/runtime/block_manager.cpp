@@ -29,22 +29,37 @@ void BlockManager::reset() {
   hash_.assign(num_blocks_, 0);
   hashed_.assign(num_blocks_, 0);
   tokens_.assign(num_blocks_, {});
-  lru_.clear();
-  lru_pos_.assign(num_blocks_, lru_.end());
+  lru_[0].clear();
+  lru_[1].clear();
+  lru_pos_.assign(num_blocks_, lru_[0].end());
   in_lru_.assign(num_blocks_, 0);
+  reused_.assign(num_blocks_, 0);
   cache_.clear();
   free_list_.clear();
   free_list_.reserve(num_blocks_);
   for (int32_t b = num_blocks_ - 1; b >= 0; --b) free_list_.push_back(b);
 }
 
-void BlockManager::evict_one() {
-  const int32_t b = lru_.front();
-  lru_.pop_front();
+void BlockManager::lru_remove(int32_t b) {
+  if (!in_lru_[b]) return;
+  lru_[in_lru_[b] - 1].erase(lru_pos_[b]);
   in_lru_[b] = 0;
+}
+
+void BlockManager::lru_push(int32_t b, int list) {
+  lru_[list].push_back(b);
+  lru_pos_[b] = std::prev(lru_[list].end());
+  in_lru_[b] = (char)(list + 1);
+}
+
+void BlockManager::evict_one() {
+  const int list = lru_[0].empty() ? 1 : 0;  // never-reused blocks first
+  const int32_t b = lru_[list].front();
+  lru_remove(b);
   auto it = cache_.find(hash_[b]);
   if (it != cache_.end() && it->second == b) cache_.erase(it);
   hashed_[b] = 0;
+  reused_[b] = 0;
   tokens_[b].clear();
   free_list_.push_back(b);
 }
@@ -66,11 +81,19 @@ void BlockManager::release(int32_t b) {
   if (b < 0 || b >= num_blocks_ || ref_[b] <= 0) return;
   if (--ref_[b] > 0) return;
   if (hashed_[b] && prefix_caching_) {
-    lru_.push_back(b);
-    lru_pos_[b] = std::prev(lru_.end());
-    in_lru_[b] = 1;
+    if (reused_[b]) {
+      lru_push(b, 1);
+      if ((int32_t)lru_[1].size() > num_blocks_ / 2) {  // protected segment full: demote its oldest
+        const int32_t d = lru_[1].front();
+        lru_remove(d);
+        lru_push(d, 0);
+      }
+    } else {
+      lru_push(b, 0);
+    }
   } else {
     hashed_[b] = 0;
+    reused_[b] = 0;
     tokens_[b].clear();
     free_list_.push_back(b);
   }
@@ -84,10 +107,8 @@ int32_t BlockManager::lookup(uint64_t hash, const int32_t* tokens) {
   if ((int32_t)tokens_[b].size() != block_size_ ||
       std::memcmp(tokens_[b].data(), tokens, sizeof(int32_t) * block_size_) != 0)
     return -1;
-  if (in_lru_[b]) {
-    lru_.erase(lru_pos_[b]);
-    in_lru_[b] = 0;
-  }
+  lru_remove(b);
+  reused_[b] = 1;
   ++ref_[b];
   return b;
 }
