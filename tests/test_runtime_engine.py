@@ -428,3 +428,53 @@ def test_engine_fails_on_custom_allreduce_timeout():
     with pytest.raises(RuntimeError, match="custom all-reduce"):
         for _ in range(4):
             eng.step()
+
+
+def _sched_run(s, L, reqs, max_steps=200):
+    """Add (id, prompt) requests, step until all finish; returns {id: output tuple}."""
+    import numpy as np
+
+    buf = np.zeros(L["total"], dtype=np.int32)
+    for rid, p in reqs:
+        s.add_request(rid, p, 0.0, 1, rid, True, [], None)
+    outs = {}
+    for _ in range(max_steps):
+        if not s.has_work():
+            break
+        T = s.schedule(buf.ctypes.data)
+        c = buf[L["counts"]:L["counts"] + 8]
+        nsamp = int(c[2]) if T else 0
+        for o in s.commit(np.full(max(1, nsamp), 7, np.int32).ctypes.data, nsamp):
+            outs[o[0]] = o
+    return outs
+
+
+def test_scheduler_inflight_prefix_dedup():
+    """Two requests sharing a 64-token prefix arrive together: the second waits one step
+    and then takes the first's prefix blocks from the cache instead of recomputing them."""
+    cfg = {"num_blocks": 64, "block_size": 16, "max_num_seqs": 8, "max_num_batched_tokens": 256,
+           "max_prefill_tokens": 256, "max_model_len": 512, "gqa_group": 4, "eos_ids": [2]}
+    P = list(range(1000, 1064))
+    for dedup in (True, False):
+        s = _runtime.Scheduler(dict(cfg, dedup_inflight_prefix=dedup))
+        outs = _sched_run(s, s.layout(), [(1, P + [5] * 16), (2, P + [6] * 16)])
+        assert set(outs) == {1, 2}
+        if dedup:
+            assert s.prefix_defers == 1 and outs[2][4] == 64  # cached_prompt_tokens
+        else:
+            assert s.prefix_defers == 0 and outs[2][4] == 0
+
+
+def test_prefix_cache_protects_reused_blocks_under_eviction():
+    """Segmented LRU: a prefix that was reused survives a burst of one-off prompts that
+    overflows the pool (plain LRU evicted it first: it was released earliest)."""
+    cfg = {"num_blocks": 40, "block_size": 16, "max_num_seqs": 4, "max_num_batched_tokens": 256,
+           "max_prefill_tokens": 256, "max_model_len": 512, "gqa_group": 4, "eos_ids": [2]}
+    s = _runtime.Scheduler(cfg)
+    L = s.layout()
+    P = list(range(2000, 2064))
+    _sched_run(s, L, [(1, P + [11] * 16)])
+    assert _sched_run(s, L, [(2, P + [12] * 16)])[2][4] == 64  # reused once -> protected
+    for i in range(10):  # 10 one-off prompts of 5 blocks: more than the pool holds
+        _sched_run(s, L, [(10 + i, [3000 + 100 * i + t for t in range(80)])])
+    assert _sched_run(s, L, [(99, P + [13] * 16)])[99][4] == 64
