@@ -32,7 +32,7 @@ def main():
     eng = Engine(EngineConfig(model=a.model, capture_on_start=False, max_num_seqs=64))
     eng.capture_graphs(bks)
     for b in bks:
-        g = eng._graphs[(b, False)]
+        g = eng._graphs[(b, False, False)]
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         host, dev = [], []
         for i in range(a.iters):
