@@ -29,7 +29,9 @@ nothing on the host has to be kept consistent between ranks.
 from __future__ import annotations
 
 import logging
+import os
 import queue
+import sys
 from collections import deque
 import threading
 import time
@@ -85,6 +87,9 @@ class EngineConfig:
     att_wide_min_tokens: int = 2048  # ... used only for steps with at least this many prefill tokens
     prefetch_weights: Optional[bool] = None  # decode-step MALL prefetch on a side stream (None: model default)
     reply_tokens: Optional[int] = None  # fixed length of every reply schema's free-text slot (grammar.py)
+    # interpreter thread-switch interval while the engine thread runs (sys.setswitchinterval);
+    # None = env PILOTTAI_GIL_SWITCH_S or the interpreter default (5 ms)
+    gil_switch_interval: Optional[float] = None
 
 
 # TP step header: [op, T, ns, nsamp, bucket, masks_changed, n_copy, truncate, embed]
@@ -497,6 +502,11 @@ class LLMEngine:
     def start(self):
         if self._thread is not None:
             return
+        sw = self.cfg.gil_switch_interval
+        if sw is None and os.environ.get("PILOTTAI_GIL_SWITCH_S"):
+            sw = float(os.environ["PILOTTAI_GIL_SWITCH_S"])
+        if sw is not None and sw > 0:
+            sys.setswitchinterval(sw)
         self._stop = False
         self._thread = threading.Thread(target=self._loop, name="pilottai-engine", daemon=True)
         self._thread.start()
