@@ -6,66 +6,57 @@ carries both field families, with `max_iter`/`max_iterations` and
 `allow_delegation`/`can_delegate` kept in sync, so BaseAgent and the control-plane
 services read the same object. Save/load round-trips (App. A #37).
 
-`SecureConfig` provides the reference's encrypt/decrypt contract without the
-`cryptography` dependency (not installable here): an HMAC-SHA256 keystream
-cipher with an HMAC-SHA256 authentication tag (encrypt-then-MAC), stdlib only.
+`SecureConfig` is the reference's Fernet store: the same key-file format and the same
+tokens (AES-128-CBC + HMAC-SHA256), implemented in the standard library by
+`core/fernet.py` because `cryptography` is not importable here, so key files and
+encrypted values move between the two frameworks unchanged.
 """
 from __future__ import annotations
 
 import base64
-import hashlib
-import hmac
 import json
-import secrets
 import shutil
 from pathlib import Path
 from typing import Any, Dict, List, Optional
 
 from pydantic import BaseModel, ConfigDict, Field, SecretStr, field_validator, model_validator
 
+from .fernet import Fernet, InvalidToken
 from .role import AgentRole
 
 
 class SecureConfig:
-    """Authenticated symmetric encryption of sensitive config values."""
+    """Fernet-encrypted sensitive config values (reference: pilott/core/config.py:10-38).
+
+    The key file holds a Fernet key (44 url-safe base64 bytes), as the reference writes
+    it. A 32-byte raw key (this class's pre-Fernet format) is read as the same 32 key
+    bytes."""
 
     def __init__(self, key_path: Optional[Path] = None):
         self._key_path = Path(key_path) if key_path else None
         if self._key_path and self._key_path.exists():
-            self.key = self._key_path.read_bytes()
+            self.key = self._key_path.read_bytes().strip()
+            if len(self.key) == 32:
+                self.key = base64.urlsafe_b64encode(self.key)
         else:
-            self.key = secrets.token_bytes(32)
+            self.key = Fernet.generate_key()
             if self._key_path:
                 self._key_path.parent.mkdir(parents=True, exist_ok=True)
                 self._key_path.write_bytes(self.key)
-        self._enc_key = hmac.new(self.key, b"enc", hashlib.sha256).digest()
-        self._mac_key = hmac.new(self.key, b"mac", hashlib.sha256).digest()
-
-    def _stream(self, nonce: bytes, n: int) -> bytes:
-        out = bytearray()
-        ctr = 0
-        while len(out) < n:
-            out += hmac.new(self._enc_key, nonce + ctr.to_bytes(8, "big"), hashlib.sha256).digest()
-            ctr += 1
-        return bytes(out[:n])
+        self.cipher = Fernet(self.key)
 
     def encrypt(self, value: str) -> bytes:
         if not value:
             raise ValueError("Cannot encrypt empty value")
-        nonce = secrets.token_bytes(16)
-        pt = value.encode()
-        ct = bytes(a ^ b for a, b in zip(pt, self._stream(nonce, len(pt))))
-        tag = hmac.new(self._mac_key, nonce + ct, hashlib.sha256).digest()
-        return base64.urlsafe_b64encode(nonce + ct + tag)
+        return self.cipher.encrypt(value.encode())
 
     def decrypt(self, token: bytes) -> str:
         if not token:
             raise ValueError("Cannot decrypt empty value")
-        raw = base64.urlsafe_b64decode(token)
-        nonce, ct, tag = raw[:16], raw[16:-32], raw[-32:]
-        if not hmac.compare_digest(tag, hmac.new(self._mac_key, nonce + ct, hashlib.sha256).digest()):
-            raise ValueError("Invalid token (authentication failed)")
-        return bytes(a ^ b for a, b in zip(ct, self._stream(nonce, len(ct)))).decode()
+        try:
+            return self.cipher.decrypt(token).decode()
+        except InvalidToken as e:
+            raise ValueError(f"Invalid token: {e}") from e
 
     def cleanup(self):
         try:

@@ -105,6 +105,35 @@ def test_secure_config_roundtrip(tmp_path):
         sc.decrypt(bytes(bad))
 
 
+def test_aes128_fips197_known_answer():
+    from pilottai_amd.core.fernet import aes128_encrypt_block
+
+    ct = aes128_encrypt_block(bytes(range(16)), bytes.fromhex("00112233445566778899aabbccddeeff"))
+    assert ct.hex() == "69c4e0d86a7b0430d8cdb78070b4c55a"  # FIPS-197 Appendix C.1
+
+
+# The Fernet specification's published vector (github.com/fernet/spec, generate.json):
+# key, IV 00..0f, time 1985-10-26T01:20:00-07:00, message "hello".
+_SPEC_KEY = "cw_0x689RpI-jtRR7oE8h_eQsKImvJapLeSbXpwF4e4="
+_SPEC_TOKEN = (b"gAAAAAAdwJ6wAAECAwQFBgcICQoLDA0ODy021cpGVWKZ_eEwCGM4BLLF_5CV9dOPmrhuVUPgJobwOz7JcbmrR64jVmpU4IwqDA==")
+
+
+def test_fernet_spec_vector_and_reference_key_file(tmp_path):
+    from pilottai_amd.core.fernet import Fernet, InvalidToken
+
+    f = Fernet(_SPEC_KEY)
+    assert f.encrypt_at_time(b"hello", 499162800, iv=bytes(range(16))) == _SPEC_TOKEN
+    assert f.decrypt_at_time(_SPEC_TOKEN, 60, 499162800 + 30) == b"hello"
+    with pytest.raises(InvalidToken):
+        f.decrypt_at_time(_SPEC_TOKEN, 60, 499162800 + 61)
+    # a key file as the reference's SecureConfig writes it (Fernet.generate_key bytes)
+    (tmp_path / "ref.key").write_bytes(_SPEC_KEY.encode())
+    sc = SecureConfig(tmp_path / "ref.key")
+    assert sc.decrypt(_SPEC_TOKEN) == "hello"
+    assert Fernet(_SPEC_KEY).decrypt(sc.encrypt("api-key-123")) == b"api-key-123"
+    assert len(Fernet.generate_key()) == 44
+
+
 def test_llm_config_defaults_local():
     c = LLMConfig()
     assert c.provider == "local" and c.model_name == "llama-3-8b"
