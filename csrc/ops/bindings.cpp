@@ -31,6 +31,7 @@ int pa_topkp_threshold(float* tau, const void* logits, int rows, int V, int ld, 
                        int mask_words, hipStream_t st);
 void pa_skinny_set_variant(int v);
 int pa_skinny_gemm(void* y, const void* x, const void* w, int M, int N, int K, int ldy, hipStream_t st);
+void pa_decode_set_variant(int v);
 int pa_decode_gemm(void* y, const void* x, const void* wp, const void* resid, int M, int N, int K,
                    int ldx, int ldy, int ldr, int epi, int norm, float eps, int nt, int waves, int splits,
                    float* ws, long long ws_floats, int* counters, int n_counters, hipStream_t st);
@@ -606,6 +607,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("silu_mul", &silu_mul);
   m.def("skinny_gemm", &skinny_gemm);
   m.def("skinny_set_variant", [](int v) { pa_skinny_set_variant(v); });
+  m.def("decode_set_variant", [](int v) { pa_decode_set_variant(v); });
   m.def("decode_gemm", &decode_gemm, py::arg("y"), py::arg("x"), py::arg("wp"), py::arg("resid") = py::none(),
         py::arg("epi") = 0, py::arg("norm") = false, py::arg("eps") = 1e-5, py::arg("nt") = 0,
         py::arg("waves") = 0, py::arg("splits") = 0, py::arg("ws") = py::none(), py::arg("counters") = py::none());

@@ -9,6 +9,7 @@ how the control-plane tests execute the whole engine without a GPU.
 from __future__ import annotations
 
 import importlib
+import os
 from typing import Optional
 
 import torch
@@ -25,6 +26,8 @@ def _load():
         return _C
     try:
         _C = importlib.import_module("pilottai_amd._C")
+        if os.environ.get("PILOTTAI_DECODE_VARIANT"):  # A/B switch of the packed decode GEMM
+            _C.decode_set_variant(int(os.environ["PILOTTAI_DECODE_VARIANT"]))
     except BaseException as e:  # noqa: BLE001 — surfaced by require_native()
         _LOAD_ERROR = e
     return _C
