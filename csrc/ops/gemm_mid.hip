@@ -86,6 +86,13 @@ __device__ __forceinline__ void raw_barrier() {
 __device__ __forceinline__ void glds16(const bf16* src, char* lds) {
   __builtin_amdgcn_global_load_lds((gbl_t*)src, (lds_t*)lds, 16, 0, 0);
 }
+// gate_up's weight stream when one row tile covers M (each weight byte read once per step):
+// non-temporal, 1-3 % faster at M = 64-256. The other projections keep the default policy:
+// with nt o_proj at M = 256 ran 34.4 -> 37.9 us, down and qkv 1-3 % slower
+// (profiles/r2_nt_weights_ab.jsonl).
+__device__ __forceinline__ void glds16_nt(const bf16* src, char* lds) {
+  __builtin_amdgcn_global_load_lds((gbl_t*)src, (lds_t*)lds, 16, 0, 2);
+}
 
 // packed rope-QKV tile -> first column of its original tile
 __device__ __forceinline__ int ropeperm_tile(int tile) {
@@ -165,7 +172,7 @@ __device__ __forceinline__ float store_quad(const Args& A, int m, int tile, int 
 template <int EPI>
 constexpr bool pair_epi() { return EPI == EP_SILU || EPI == EP_ROPEKV; }
 
-template <int FM, int FN, int EPI, bool NORM>
+template <int FM, int FN, int EPI, bool NORM, bool WNT>
 __global__ __launch_bounds__(256) void mid_gemm_kernel(const Args A) {
   constexpr int BM = 32 * FM, BN = 32 * FN, NTL = BN / 16;  // tiles per block
   constexpr int XB = BM * 128, WB = BN * 128, SB = XB + WB;  // bytes per stage
@@ -212,8 +219,13 @@ __global__ __launch_bounds__(256) void mid_gemm_kernel(const Args A) {
     char* st = smem + b * SB;
 #pragma unroll
     for (int i = 0; i < FM; ++i) glds16(xsrc[i] + c * 64, st + (wid * FM + i) * 1024);
+    if constexpr (WNT) {
 #pragma unroll
-    for (int i = 0; i < FN; ++i) glds16(wsrc[i] + (size_t)c * 1024, st + XB + (wid * FN + i) * 1024);
+      for (int i = 0; i < FN; ++i) glds16_nt(wsrc[i] + (size_t)c * 1024, st + XB + (wid * FN + i) * 1024);
+    } else {
+#pragma unroll
+      for (int i = 0; i < FN; ++i) glds16(wsrc[i] + (size_t)c * 1024, st + XB + (wid * FN + i) * 1024);
+    }
   };
 
   f32x4 acc[FM][FN];
@@ -399,7 +411,11 @@ __global__ __launch_bounds__(256) void mid_gemm_kernel(const Args A) {
 // ---------------------------------------------------------------------------------
 template <int FM, int FN>
 static int launch_f(const Args& a, int epi, bool norm, int grid, hipStream_t st) {
-#define PA_MID(E, NRM) hipLaunchKernelGGL((mid_gemm_kernel<FM, FN, E, NRM>), dim3(grid), dim3(256), 0, st, a)
+#define PA_MID(E, NRM)                                                                                \
+  do {                                                                                                \
+    if (E == EP_SILU && a.MT == 1) hipLaunchKernelGGL((mid_gemm_kernel<FM, FN, E, NRM, true>), dim3(grid), dim3(256), 0, st, a); \
+    else hipLaunchKernelGGL((mid_gemm_kernel<FM, FN, E, NRM, false>), dim3(grid), dim3(256), 0, st, a);          \
+  } while (0)
   switch (epi) {
     case EP_PLAIN:
       if (norm) PA_MID(EP_PLAIN, true); else PA_MID(EP_PLAIN, false);

@@ -117,11 +117,12 @@ __global__ __launch_bounds__(WAVES * 64) void wide_gemm_kernel(const WgArgs A) {
       }
     }
   };
+  // weights: non-temporal (streamed once per step by one wave; as in gemm_decode.hip)
   auto load_w = [&](int ch, bf16x8 (&dst)[KC][NTW]) {
 #pragma unroll
     for (int kk = 0; kk < KC; ++kk)
 #pragma unroll
-      for (int j = 0; j < NTW; ++j) dst[kk][j] = wsrc[j][(size_t)(ks0 + KC * ch + kk) * 64];
+      for (int j = 0; j < NTW; ++j) dst[kk][j] = __builtin_nontemporal_load(wsrc[j] + (size_t)(ks0 + KC * ch + kk) * 64);
   };
 
 #pragma unroll
