@@ -358,8 +358,11 @@ static void wide_default(int M, int N, int K, int epi, int& ntw, int& waves, int
   if (epi != WG_SILU && M <= 128 && tiles / 8 >= 256 && tiles % 8 == 0) ntw = 2;
   const int G = tiles / (waves * ntw);
   S = G >= 192 ? 1 : std::max(1, (256 + G - 1) / G);
+  // down_proj (K = 14,336) at M <= 32: 512 workgroups (8 K-slices) beat 256 with the
+  // non-temporal weight stream, 25.8 vs 28.0 us at M = 24 (profiles/r2_nt_weights_ab.jsonl
+  // sweep); at M = 48 the two tie.
+  if (K >= 8192 && M <= 32) S = std::max(S, (512 + G - 1) / G);
   S = std::min(S, std::max(1, K / 64 / 8));  // keep >= 8 chunks per slice
-  (void)M;
 }
 
 }  // namespace pa
