@@ -22,7 +22,8 @@
 //     per wave load) straight into registers one chunk ahead, so every weight byte
 //     is read from HBM exactly once;
 //   * epilogues as the decode kernel: plain, RoPE-permuted QKV columns restored,
-//     SwiGLU over interleaved gate/up tiles, residual add.
+//     SwiGLU over interleaved gate/up tiles (in registers with two tiles per wave, or
+//     handed from the up wave to the gate wave through LDS with one), residual add.
 #include "common.h"
 
 #include <algorithm>
@@ -63,6 +64,7 @@ __global__ __launch_bounds__(WAVES * 64) void wide_gemm_kernel(const WgArgs A) {
   constexpr int XPT = (XU + NTH - 1) / NTH;      // units per thread
   constexpr int TPG = WAVES * NTW;               // tiles per column group
   __shared__ __attribute__((aligned(16))) bf16x8 xs[2][ROWS][UPR];  // the only LDS object (guide §5 trap 4a)
+  static_assert(sizeof(xs) >= (256 + WAVES / 2 * ROWS * 16) * sizeof(float), "SiLU hand-off must fit the x staging");
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int g = lane >> 4, c = lane & 15;
   const int M = A.M, K = A.K, S = A.S;
@@ -200,6 +202,32 @@ __global__ __launch_bounds__(WAVES * 64) void wide_gemm_kernel(const WgArgs A) {
       if constexpr (NORM) return rsqrtf(lds_f[16 + m] * inv_k + A.eps);
       else return 1.f;
     };
+    if constexpr (EPI == WG_SILU && NTW == 1) {
+      // one tile per wave: odd waves hold the up tiles of their even neighbours' gate
+      // tiles (interleaved packing) and hand them over through LDS (x staging is dead;
+      // [256, 256 + WAVES / 2 * ROWS * 16) floats, clear of the flag and row sums)
+      float* xch = lds_f + 256 + (wid >> 1) * ROWS * 16;
+      if (wid & 1) {
+#pragma unroll
+        for (int i = 0; i < MT; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) xch[(16 * i + 4 * g + r) * 16 + c] = acc[i][0][r];
+      }
+      __syncthreads();
+      if (wid & 1) return;
+#pragma unroll
+      for (int i = 0; i < MT; ++i) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = 16 * i + 4 * g + r;
+          if (m >= M) continue;
+          const float rs = rsf(m);
+          const float gv = acc[i][0][r] * rs, uv = xch[m * 16 + c] * rs;
+          A.y[(size_t)m * A.ldy + (tile0 >> 1) * 16 + c] = (bf16)(gv / (1.f + __expf(-gv)) * uv);
+        }
+      }
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < MT; ++i) {
 #pragma unroll
@@ -209,7 +237,7 @@ __global__ __launch_bounds__(WAVES * 64) void wide_gemm_kernel(const WgArgs A) {
         const float rs = rsf(m);
         if constexpr (EPI == WG_SILU) {
 #pragma unroll
-          for (int j = 0; j < NTW; j += 2) {
+          for (int j = 0; j + 1 < NTW; j += 2) {
             const float gv = acc[i][j][r] * rs, uv = acc[i][j + 1][r] * rs;
             const int col = ((tile0 + j) >> 1) * 16 + c;
             A.y[(size_t)m * A.ldy + col] = (bf16)(gv / (1.f + __expf(-gv)) * uv);
@@ -325,16 +353,16 @@ static int launch_wg_e(const WgArgs& a, int epi, bool norm, hipStream_t st) {
       case WG_RESID: PA_WG(WG_RESID, false); return 0;
       case WG_ROPEPERM: PA_WG(WG_ROPEPERM, false); return 0;
       default:
-        if constexpr (NTW % 2 == 0) { PA_WG(WG_SILU, false); return 0; }
-        return 1;
+        PA_WG(WG_SILU, false);
+        return 0;
     }
   }
   switch (epi) {
     case WG_PLAIN: PA_WG(WG_PLAIN, true); return 0;
     case WG_ROPEPERM: PA_WG(WG_ROPEPERM, true); return 0;
     case WG_SILU:
-      if constexpr (NTW % 2 == 0) { PA_WG(WG_SILU, true); return 0; }
-      return 1;
+      PA_WG(WG_SILU, true);
+      return 0;
     default: return 1;
   }
 #undef PA_WG
@@ -354,7 +382,9 @@ static int launch_wg_mt(const WgArgs& a, int epi, bool norm, int ntw, int waves,
 static void wide_default(int M, int N, int K, int epi, int& ntw, int& waves, int& S) {
   const int tiles = N / 16;
   waves = M > 128 ? 8 : 4;
-  ntw = (epi == WG_SILU) ? 2 : 1;
+  // SiLU on one tile per wave too (gate/up pairs meet through LDS): twice the workgroups
+  // of the paired form, 1792 / 4 = 448 for gate_up
+  ntw = 1;
   if (epi != WG_SILU && M <= 128 && tiles / 8 >= 256 && tiles % 8 == 0) ntw = 2;
   const int G = tiles / (waves * ntw);
   S = G >= 192 ? 1 : std::max(1, (256 + G - 1) / G);
@@ -387,7 +417,7 @@ extern "C" int pa_wide_gemm(void* y, const void* x, const void* wp, const void* 
   if (ntw <= 0) ntw = dn;
   if (waves <= 0) waves = dw;
   int S = splits > 0 ? splits : dS;
-  if (epi == WG_SILU && ntw % 2) return 1;
+  if (epi == WG_SILU && (waves * ntw) % 2) return 1;  // gate/up tile pairs within a group
   const int TPG = waves * ntw;
   if ((N / 16) % TPG) return 1;
   const int G = N / 16 / TPG;

@@ -381,7 +381,10 @@ def test_decode_qkv_rope(gpu, M, H, KV, K, splits):
     (128, 28672, 4096, "silu", True, 0, 0, 0), (64, 4096, 14336, "resid", False, 0, 0, 0),
     (33, 1024, 512, "silu", True, 2, 4, 2), (100, 768, 512, "rope_perm", False, 1, 4, 1),
     (120, 4096, 4096, "resid", False, 1, 8, 3), (90, 6144, 4096, "plain", True, 2, 4, 5),
-    (64, 2048, 1024, "plain", False, 2, 8, 1), (29, 4096, 4096, "plain", True, 1, 4, 4)])
+    (64, 2048, 1024, "plain", False, 2, 8, 1), (29, 4096, 4096, "plain", True, 1, 4, 4),
+    # SwiGLU with one tile per wave (gate/up handed over through LDS), split-K and 8 waves
+    (24, 28672, 4096, "silu", True, 1, 4, 0), (33, 1024, 512, "silu", True, 1, 4, 3),
+    (40, 1024, 512, "silu", False, 1, 8, 0)])
 def test_wide_gemm(gpu, M, N, K, epi, norm, ntw, waves, splits):
     """Small-batch packed-weight GEMM (csrc/ops/gemm_wide.hip) vs fp32, every epilogue
     and the folded row norm, with and without split-K; run twice so the
