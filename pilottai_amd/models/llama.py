@@ -469,7 +469,8 @@ class LlamaModel:
         rows = meta.logit_rows[:num_logit_rows]
         rows = rows.long() if self.device.type == "cpu" else rows
         xs = ops.rmsnorm(h.index_select(0, rows), self.norm, eps)
-        if num_logit_rows <= 16:  # decode_gemm beats hipBLASLt on the LM head only up to 16 rows
+        if num_logit_rows <= 32:  # decode_gemm beats hipBLASLt on the LM head up to 32 rows (24: 180 vs
+            # 191 us, 32: 184.5 vs 196; 48: 221 vs 204; profiles/r2_decode_sweep_nt*.jsonl)
             return ops.decode_gemm(xs, self.lm_head_p, "plain")
         return ops.linear(xs, self.lm_head, "lm_head")
 
@@ -542,7 +543,7 @@ class LlamaModel:
         rows = meta.logit_rows[:num_logit_rows]
         rows = rows.long() if self.device.type == "cpu" else rows
         xs = ops.rmsnorm(h.index_select(0, rows), self.norm, eps)
-        if num_logit_rows <= 16:
+        if num_logit_rows <= 32:
             return ops.decode_gemm(xs, self.lm_head_p, "plain")
         return ops.linear(xs, self.lm_head, "lm_head")
 
