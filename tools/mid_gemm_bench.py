@@ -2,7 +2,7 @@
 hipBLASLt (shipped tuned solutions) vs csrc/ops/gemm_mid.hip over its (fm, fn, splits)
 configurations, with an fp32 check of every configuration.
 
-    python tools/mid_gemm_bench.py [M list] [--quick] > out.jsonl
+    python tools/mid_gemm_bench.py [M list] [--quick] [--fused-sweep] > out.jsonl
 
 Each row: M, shape, lib (us), every config "f{fm}x{fn}s{S}" (us), auto (the default
 plan), fused (the engine's epilogue: norm + rope_perm / silu / resid), err of the worst
@@ -39,6 +39,7 @@ def timeit(fn, ncopies, iters=20):
 
 args = [a for a in sys.argv[1:] if not a.startswith("--")]
 quick = "--quick" in sys.argv
+fused_sweep = "--fused-sweep" in sys.argv  # time every config in the engine's epilogue form
 Ms = [int(v) for v in (args[0] if args else "64,96,128,192,256,384,512").split(",")]
 CFGS = [(1, fm, fn, 4, S) for fm in (2, 4, 8) for fn in (2, 4) for S in (1, 2, 3, 4, 6)]
 torch.manual_seed(0)
@@ -56,6 +57,9 @@ for N, K, name in shapes:
         row = {"M": M, "shape": name}
         row["lib"] = round(timeit(lambda i: torch.nn.functional.linear(x, ws[i]), ncopies), 1)
         ref = x.float() @ ws[0].float().T
+        resid = torch.randn(M, N, device="cuda").to(torch.bfloat16) if epi == "resid" else None
+        yo = torch.empty(M, N // 2 if epi == "silu" else N, dtype=torch.bfloat16, device="cuda")
+        ssv = kernels.row_sumsq(x)
         best, worst_err = None, 0.0
         for var, fm, fn, wv, S in ([] if quick else CFGS):
             bm = (32 if var == 1 else 16) * fm
@@ -67,16 +71,17 @@ for N, K, name in shapes:
             except (ValueError, RuntimeError):
                 continue
             worst_err = max(worst_err, float((got - ref).abs().max() / ref.abs().max()))
-            t = timeit(lambda i: kernels.mid_gemm(x, wps[i], out=y, fm=fm, fn=fn, splits=S), ncopies)
+            if fused_sweep:
+                t = timeit(lambda i: kernels.mid_gemm(x, fps[i], epi, resid=resid, norm=nrm, out=yo, ss_in=ssv,
+                                                      fm=fm, fn=fn, splits=S), ncopies)
+            else:
+                t = timeit(lambda i: kernels.mid_gemm(x, wps[i], out=y, fm=fm, fn=fn, splits=S), ncopies)
             row[key] = round(t, 1)
             best = (t, key) if best is None or t < best[0] else best
         row["plan"] = kernels.require_native().mid_gemm_plan(M, N, K, kernels.MID_EPI["plain"])
         got = kernels.mid_gemm(x, wps[0], out=y).float()
         worst_err = max(worst_err, float((got - ref).abs().max() / ref.abs().max()))
         row["auto"] = round(timeit(lambda i: kernels.mid_gemm(x, wps[i], out=y), ncopies), 1)
-        resid = torch.randn(M, N, device="cuda").to(torch.bfloat16) if epi == "resid" else None
-        yo = torch.empty(M, N // 2 if epi == "silu" else N, dtype=torch.bfloat16, device="cuda")
-        ssv = kernels.row_sumsq(x)
         bfm, bfn, bS = (int(v) for v in re.match(r"v1f(\d+)x(\d+)w4s(\d+)", best[1]).groups()) if best else (0, 0, 0)
         row["fused"] = round(timeit(lambda i: kernels.mid_gemm(x, fps[i], epi, resid=resid, norm=nrm, out=yo,
                                                                ss_in=ssv, fm=bfm, fn=bfn, splits=bS), ncopies), 1)
