@@ -129,7 +129,10 @@ class LlamaModel:
     DECODE_FUSED_MAX_T = 16
     # steps of up to this many tokens (above DECODE_FUSED_MAX_T) run the packed-weight
     # small-batch kernels (csrc/ops/gemm_wide.hip; tools/wide_gemm_bench.py)
-    WIDE_MAX_T = 48  # measured: the packed path wins the 48-token bucket, loses at 64 (BENCHMARKS.md)
+    # (off by default since the mid path and the nt weight streams landed: 48-token steps run
+    # 4.07-4.34 ms on the mid path against 4.6-4.7 on this one, 32-token steps 3.83-3.90 against
+    # 3.92-3.97; profiles/r2_wide_max_t_ab.jsonl. EngineConfig.wide_max_t = 48 turns it back on)
+    WIDE_MAX_T = 16
     # steps of up to this many tokens (above WIDE_MAX_T) run the LDS-DMA tiled projections
     # (csrc/ops/gemm_mid.hip) with every norm / SwiGLU / residual / RoPE + KV write fused
     MID_MAX_T = 256

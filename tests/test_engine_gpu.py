@@ -124,8 +124,8 @@ def test_http_server_on_gpu_engine(engine):
 @pytest.mark.parametrize("n_prompt", [5, 30, 100, 200, 400])
 def test_llama3_8b_layer_dims_every_path(gpu, n_prompt):
     """Two layers with the exact Llama-3-8B dimensions through every forward path: the
-    prompt's prefill step runs the packed decode (<= 16 tokens), small-batch (17-48),
-    LDS-DMA tiled mid-size (49-256, fused norm / RoPE + KV write / SwiGLU / residual with
+    prompt's prefill step runs the packed decode (<= 16 tokens), LDS-DMA tiled mid-size
+    (17-256, fused norm / RoPE + KV write / SwiGLU / residual with
     the producer-side norm statistics) or library (> 256) path, and every later token the
     decode path; greedy tokens must match the dense fp32 reference forward."""
     from pilottai_amd.engine.engine import EngineConfig, LLMEngine
@@ -139,6 +139,22 @@ def test_llama3_8b_layer_dims_every_path(gpu, n_prompt):
     assert len(out.token_ids) == 6
     _check_greedy(eng, prompt, out.token_ids)
     _ = EngineConfig, LLMEngine
+
+
+def test_llama3_8b_layer_dims_small_batch_path(gpu):
+    """The packed small-batch path (csrc/ops/gemm_wide.hip; off by default, EngineConfig
+    wide_max_t turns it on) on a 17-48-token prefill step at the exact Llama-3-8B dims."""
+    from pilottai_amd.engine.engine import EngineConfig, LLMEngine
+
+    eng = LLMEngine(EngineConfig(model="llama-3-8b-2l", max_num_seqs=8, max_num_batched_tokens=512,
+                                 max_model_len=1024, num_kv_blocks=256, prefix_caching=False,
+                                 token_buckets=[16, 48, 128, 256, 512], token_align=0, wide_max_t=48),
+                    device=gpu)
+    assert eng.model.WIDE_MAX_T == 48
+    tok = eng.tok
+    prompt = tok.encode(("agents plan tasks and tools while the orchestrator checks every result " * 8))[:30]
+    out = eng.generate([prompt], temperature=0.0, max_tokens=6, ignore_eos=True)[0]
+    _check_greedy(eng, prompt, out.token_ids)
 
 
 _ENG8B = {}
