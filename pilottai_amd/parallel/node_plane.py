@@ -135,7 +135,7 @@ class PlaneServer:
         for r, st in list(self.ranks.items()):
             if r != 0 and st.alive and st.writer is not None:
                 try:
-                    await _send(st.writer, {"op": "stop"})
+                    await _send(st.writer, {"op": "shutdown"})
                 except Exception:  # noqa: BLE001
                     pass
         if self._monitor:
@@ -361,7 +361,8 @@ class PlaneWorker:
             while True:
                 msg = await _recv(self._reader)
                 op = msg.get("op")
-                if op == "stop":
+                # the plane's shutdown; an agent-level "stop" (it names an agent_id) is a request
+                if op == "shutdown" or (op == "stop" and "agent_id" not in msg):
                     break
                 if op == "reply":
                     fut = self._pending.pop(msg["id"], None)

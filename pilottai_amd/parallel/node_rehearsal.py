@@ -101,6 +101,13 @@ async def _rank0(world: int, port: int, scenario: str, per_rank: int, n_tasks: i
             out["src_queue"] = await p1.remote_queue()
             out["dst_queue"] = await p2.remote_queue()
             out["queued_ids"] = ids
+            # stopping ONE remote agent is an agent request, not the plane's shutdown: its rank
+            # keeps serving (scale-down of a remote worker)
+            await p1.stop()
+            await asyncio.sleep(0.3)
+            out["lost_after_agent_stop"] = list(plane.lost)
+            out["rank1_alive"] = bool(plane.ranks[1].alive)
+            out["rank1_serving"] = isinstance(await p1.remote_queue(), list)
         elif scenario == "scale":
             before = {r: 0 for r in range(world)}
             for aid, r in node.rank_of.items():

@@ -32,6 +32,8 @@ def test_load_balancer_moves_queued_task_across_ranks():
     moved = [t for t in r["queued_ids"] if t in r["dst_queue"]]
     assert len(moved) == 2 and len(r["src_queue"]) == 1
     assert not set(moved) & set(r["src_queue"])
+    # an agent-level stop leaves the worker rank serving (it used to end the rank's plane loop)
+    assert r["lost_after_agent_stop"] == [] and r["rank1_alive"] and r["rank1_serving"]
 
 
 def test_dynamic_scaling_creates_agent_on_least_loaded_rank():
