@@ -413,7 +413,10 @@ def test_wide_gemm(gpu, M, N, K, epi, norm, ntw, waves, splits):
     (100, 1024, 512, "silu", True, 4, 2, 2), (77, 768, 512, "rope_perm", False, 2, 2, 1),
     (300, 4096, 4096, "resid", False, 8, 4, 3), (512, 6144, 4096, "plain", True, 8, 2, 1),
     (49, 2048, 1024, "plain", False, 2, 4, 8), (250, 4096, 4096, "plain", True, 4, 4, 4),
-    (130, 1024, 1024, "silu", False, 8, 4, 2), (33, 512, 2048, "resid", False, 4, 2, 6)])
+    (130, 1024, 1024, "silu", False, 8, 4, 2), (33, 512, 2048, "resid", False, 4, 2, 6),
+    # 32-row tiles (17-32-token steps)
+    (24, 4096, 4096, "resid", False, 1, 2, 4), (32, 28672, 4096, "silu", True, 1, 4, 1),
+    (20, 6144, 4096, "rope_perm", True, 1, 2, 2), (48, 4096, 14336, "resid", False, 1, 2, 3)])
 def test_mid_gemm(gpu, M, N, K, epi, norm, fm, fn, splits):
     _check_mid(gpu, M, N, K, epi, norm, fm, fn, splits)
 

@@ -41,7 +41,7 @@ args = [a for a in sys.argv[1:] if not a.startswith("--")]
 quick = "--quick" in sys.argv
 fused_sweep = "--fused-sweep" in sys.argv  # time every config in the engine's epilogue form
 Ms = [int(v) for v in (args[0] if args else "64,96,128,192,256,384,512").split(",")]
-CFGS = [(1, fm, fn, 4, S) for fm in (2, 4, 8) for fn in (2, 4) for S in (1, 2, 3, 4, 6)]
+CFGS = [(1, fm, fn, 4, S) for fm in (1, 2, 4, 8) for fn in (2, 4) for S in (1, 2, 3, 4, 6)]
 torch.manual_seed(0)
 for N, K, name in shapes:
     gb = N * K * 2 / 1e9
