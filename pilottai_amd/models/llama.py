@@ -151,7 +151,7 @@ class LlamaModel:
         "qkv": [(32, 1, 2, 2), (64, 1, 2, 1), (128, 2, 2, 1), (256, 4, 2, 1), (1 << 30, 4, 4, 1)],
         "o": [(32, 1, 2, 4), (64, 1, 2, 2), (128, 2, 2, 2), (256, 2, 2, 1), (1 << 30, 4, 2, 1)],
         "gate_up": [(32, 1, 4, 1), (64, 2, 4, 1), (128, 4, 4, 1), (256, 8, 4, 1), (1 << 30, 8, 4, 1)],
-        "down": [(32, 1, 2, 4), (64, 2, 2, 4), (96, 4, 2, 4), (128, 2, 2, 2), (256, 4, 2, 2), (1 << 30, 4, 4, 2)],
+        "down": [(32, 1, 2, 4), (64, 2, 2, 4), (128, 2, 2, 2), (256, 4, 2, 2), (1 << 30, 4, 4, 2)],
     }
 
     def __init__(self, cfg: LlamaConfig, device, dtype=torch.bfloat16, tp: Optional[TPGroup] = None,
