@@ -52,9 +52,10 @@ from .tokenizer import Tokenizer, get_tokenizer
 log = logging.getLogger("pilottai_amd.engine")
 
 # hipGraph token buckets: a step of T tokens replays the smallest bucket >= T, so
-# the spacing bounds the padded (wasted) work: 32-token steps up to 512, 64 up to
-# 2048 (prefill-heavy agent steps sit at 400-1000 tokens).
-DEFAULT_BUCKETS = ([8, 16, 32, 48, 64] + list(range(96, 513, 32)) + list(range(576, 2049, 64))
+# the spacing bounds the padded (wasted) work: 16-token steps up to 512 (graph padding 1.9 ->
+# 1.1 % of step tokens at 64 workers; profiles/r2_buckets16_ab.jsonl), 64 up to 2048
+# (prefill-heavy agent steps sit at 400-1000 tokens).
+DEFAULT_BUCKETS = ([8, 16, 32, 48, 64, 80] + list(range(96, 513, 16)) + list(range(576, 2049, 64))
                    + [3072, 4096, 6144, 8192])
 
 
