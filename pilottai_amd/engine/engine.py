@@ -85,7 +85,9 @@ class EngineConfig:
     wide_max_t: Optional[int] = None  # largest step on the packed small-batch path; None = model default
     mid_max_t: Optional[int] = None  # largest step on the LDS-DMA tiled mid-size path; None = model default
     att_qcols: int = 128  # prefill attention item width in MFMA columns (128: LDS-staged 4-wave items)
-    att_wide_min_tokens: int = 2048  # ... used only for steps with at least this many prefill tokens
+    # ... used only for steps with at least this many prefill tokens (1,024: 1,024-2,048-token steps
+    # 1-2 % faster than with 2,048, which most mixed steps never reached; profiles/r2_att_wide_min_ab.jsonl)
+    att_wide_min_tokens: int = 1024
     prefetch_weights: Optional[bool] = None  # decode-step MALL prefetch on a side stream (None: model default)
     reply_tokens: Optional[int] = None  # fixed length of every reply schema's free-text slot (grammar.py)
     # interpreter thread-switch interval while the engine thread runs (sys.setswitchinterval);
