@@ -221,11 +221,17 @@ __global__ __launch_bounds__(WAVES * 64) void decode_gemm_kernel(const DgArgs A)
   if (S > 1) {
     // split-K hand-off (cdna_hip_programming.md §5 item 2, sc1 form): publish the
     // slice's partial tile write-through, take a ticket; the last slice reduces.
-    constexpr int SLAB = TM * TN + TM;
+    // slabs padded to 64 floats: each wave's b32 store instruction then writes two whole
+    // 128-B lines and no line is shared by two instructions, waves or slabs. (This did NOT
+    // cure the rare qkv_rope mismatch at M = 9, S = 3 -- only the rotated second half of a
+    // row, so not a stale slab read; profiles/r2_splitk_qkv_rope_flake.jsonl. The engine runs
+    // qkv_rope unsplit; split-K here is used for down_proj, which never mismatched.)
+    constexpr int SLAB = (TM * TN + TM + 63) / 64 * 64;
     float* gslab = A.ws + (size_t)grp * S * SLAB;
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(gslab + (size_t)sl * SLAB, 0, SLAB * 4, 0x00020000);
     for (int e = threadIdx.x; e < SLAB; e += WAVES * 64)
-      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(e < TM * TN ? fin[e] : fss[e - TM * TN]), rs, e * 4, 0, 16);
+      __builtin_amdgcn_raw_buffer_store_b32(
+          __float_as_uint(e < TM * TN ? fin[e] : (e < TM * TN + TM ? fss[e - TM * TN] : 0.f)), rs, e * 4, 0, 16);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -239,7 +245,7 @@ __global__ __launch_bounds__(WAVES * 64) void decode_gemm_kernel(const DgArgs A)
     if (!*lflag) return;
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(gslab, 0, S * SLAB * 4, 0x00020000);
-    for (int e = threadIdx.x; e < SLAB; e += WAVES * 64) {
+    for (int e = threadIdx.x; e < TM * TN + TM; e += WAVES * 64) {  // (padding not read)
       float t = 0.f;
       for (int p = 0; p < S; ++p) t += __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(ra, (p * SLAB + e) * 4, 0, 16));
       if (e < TM * TN) fin[e] = t;
@@ -383,7 +389,7 @@ static int dispatch(DgArgs a, int epi, int norm, int nt, int waves, int splits, 
   S = std::max(1, std::min(S, a.K / 32));
   const int G = N / 16 / nt;
   if (S > 1) {
-    const long long slab = (long long)MT * 16 * (nt * 16 + 1);
+    const long long slab = ((long long)MT * 16 * (nt * 16 + 1) + 63) / 64 * 64;  // kernel's padded SLAB
     if (!a.ws || !a.counters || n_counters < G || (long long)G * S * slab > ws_floats) {
       if (splits > 0) return 1;
       S = 1;  // default split without a workspace: run unsplit
