@@ -30,6 +30,7 @@ import asyncio
 import json
 import os
 import random
+import secrets
 import sys
 import time
 
@@ -69,6 +70,8 @@ def parse():
                     help="largest step on the packed small-batch path (default: the model's)")
     ap.add_argument("--mid-max-t", type=int, default=None,
                     help="largest step on the LDS-DMA tiled mid-size path (default: the model's; 0 = off)")
+    ap.add_argument("--prefill-max-t", type=int, default=None,
+                    help="largest step on the fused packed path with the 256x256 prefill GEMMs; 0 = library path")
     ap.add_argument("--att-wide-min-tokens", type=int, default=None,
                     help="prefill tokens per step from which attention uses the 4-wave LDS-staged items")
     ap.add_argument("--no-prefix-dedup", action="store_true",
@@ -120,7 +123,8 @@ async def run_rank(a, rank: int, world: int, device):
                                  num_kv_blocks=4096 if a.cpu else None, seed=1234 + rank,
                                  token_align=a.token_align, align_slack=a.align_slack,
                                  decode_fused_max_t=a.fused_max_t, wide_max_t=a.wide_max_t,
-                                 mid_max_t=a.mid_max_t, reply_tokens=a.reply_tokens,
+                                 mid_max_t=a.mid_max_t, prefill_max_t=a.prefill_max_t,
+                                 reply_tokens=a.reply_tokens,
                                  prefetch_weights=False if a.no_prefetch else None,
                                  dedup_inflight_prefix=not a.no_prefix_dedup,
                                  **({"att_wide_min_tokens": a.att_wide_min_tokens}
@@ -141,7 +145,19 @@ async def run_rank(a, rank: int, world: int, device):
     node = a.dp_mode == "node" and world > 1
     serve_cfg = {"name": f"bench-r{rank}", "policy": "fixed", "steps_per_task": a.steps_per_task,
                  "max_queue_size": 100000, "task_timeout": 900, "agent_wait_timeout": 900}
+    async def coll(fn, *args):
+        """A blocking collective off the event loop (worker ranks keep serving the control
+        plane meanwhile); the thread binds this rank's GPU first (RCCL uses the current device)."""
+        def run():
+            if device.type == "cuda":
+                torch.cuda.set_device(device)
+            return fn(*args)
+        return await asyncio.to_thread(run)
+
     serve = plane = worker = None
+    if node:  # the control plane's shared secret: drawn on rank 0, broadcast to the job's ranks
+        os.environ["PILOTTAI_PLANE_SECRET"] = await coll(
+            comm.broadcast_object, secrets.token_hex(16) if rank == 0 else None)
     if node and rank > 0:
         # worker rank: host this shard's agents (and this GPU's engine) for the manager
         from pilottai_amd.parallel.node_plane import PlaneWorker
@@ -169,15 +185,6 @@ async def run_rank(a, rank: int, world: int, device):
     else:
         serve = Serve(agents=agents, manager_llm=llm, config={**serve_cfg, "max_concurrent_tasks": n_local})
         await serve.start()
-    async def coll(fn, *args):
-        """A blocking collective off the event loop (worker ranks keep serving the control
-        plane meanwhile); the thread binds this rank's GPU first (RCCL uses the current device)."""
-        def run():
-            if device.type == "cuda":
-                torch.cuda.set_device(device)
-            return fn(*args)
-        return await asyncio.to_thread(run)
-
     # shared-context broadcast (SURVEY N14): rank 0 fixes the workload seed for every rank
     seed = await coll(comm.broadcast_object, int(time.time()) & 0xFFFF if rank == 0 else None)
     init_s = time.time() - t_init

@@ -54,7 +54,7 @@ __device__ __forceinline__ void decode_item(
     float* __restrict__ part_ml, int* __restrict__ counters, const bf16* __restrict__ q, const bf16* __restrict__ k_cache,
     const bf16* __restrict__ v_cache, const int* __restrict__ q_start, const int* __restrict__ q_len,
     const int* __restrict__ ctx_len, const int* __restrict__ block_table, int max_blocks, int H,
-    int KV, int kvh, float scale_log2, int psz) {
+    int KV, int kvh, float scale_log2, int psz, int acq) {
   const int s = it.x, qb = it.y;
   const int nq = it.z & 0xff, part = (it.z >> 8) & 0xfff, nparts = it.z >> 20;
   const int pidx = it.w;
@@ -232,17 +232,7 @@ __device__ __forceinline__ void decode_item(
     }
     int* lflag = reinterpret_cast<int*>(smem + ATT_LDS_DECODE_BYTES);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      gi32* c = (gi32*)(counters + (size_t)s * KV + kvh);
-      const int tk = __hip_atomic_fetch_add(c, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const int last = tk == nparts - 1;
-      if (last) __hip_atomic_store(c, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
-      *lflag = last;
-    }
-    __syncthreads();
-    if (!*lflag || ctq >= nq) return;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // orders the loads below the ticket only
+    if (!handoff_last(counters + (size_t)s * KV + kvh, nparts, lflag, acq) || ctq >= nq) return;
     const int p0 = pidx - part;
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
         part_o + (size_t)p0 * KV * 16 * ATT_HD, 0, nparts * KV * 16 * ATT_HD * 4, 0x00020000);
@@ -624,7 +614,7 @@ __global__ __launch_bounds__(256, 2) void paged_attn_kernel(
     const int* __restrict__ n_items, const int* __restrict__ part_size, const int* __restrict__ q_start,
     const int* __restrict__ q_len, const int* __restrict__ ctx_len,
     const int* __restrict__ block_table, int max_blocks, int H, int KV, float scale_log2,
-    const u32x4* __restrict__ pf, long long pf_lines, u32x4* __restrict__ pf_sink) {
+    const u32x4* __restrict__ pf, long long pf_lines, u32x4* __restrict__ pf_sink, int acq) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int TPW = 16 / G;
   // The first item is loaded together with the item count, not after it: one dependent
@@ -658,7 +648,7 @@ __global__ __launch_bounds__(256, 2) void paged_attn_kernel(
     const int nq = it.z & 0xff;
     if (nq <= TPW)
       decode_item<G>(it, smem, out, part_o, part_ml, counters, q, k_cache, v_cache, q_start, q_len, ctx_len,
-                     block_table, max_blocks, H, KV, kvh, scale_log2, psz);
+                     block_table, max_blocks, H, KV, kvh, scale_log2, psz, acq);
     else if (nq <= 32 / G)
       prefill_item<G>(it, smem, out, q, k_cache, v_cache, q_start, q_len, ctx_len, block_table,
                       max_blocks, H, KV, kvh, scale_log2);
@@ -702,7 +692,7 @@ extern "C" int pa_paged_attention(void* out, float* part_o, float* part_ml, cons
                          (const int4*)items, n_items, part_size, q_start, q_len, ctx_len,    \
                          block_table,                                                       \
                          max_blocks, H, KV, scale_log2, (const pa::u32x4*)pf, pf_lines,     \
-                         (pa::u32x4*)pf_sink);                                              \
+                         (pa::u32x4*)pf_sink, pa::g_handoff_acquire);                        \
   } while (0)
   switch (G) {
     case 1: PA_ATT(1); break;

@@ -32,6 +32,7 @@ int pa_topkp_threshold(float* tau, const void* logits, int rows, int V, int ld, 
 void pa_skinny_set_variant(int v);
 int pa_skinny_gemm(void* y, const void* x, const void* w, int M, int N, int K, int ldy, hipStream_t st);
 void pa_decode_set_variant(int v);
+void pa_handoff_set_acquire(int v);
 int pa_decode_gemm(void* y, const void* x, const void* wp, const void* resid, int M, int N, int K,
                    int ldx, int ldy, int ldr, int epi, int norm, float eps, int nt, int waves, int splits,
                    float* ws, long long ws_floats, int* counters, int n_counters, hipStream_t st);
@@ -50,6 +51,13 @@ int pa_mid_gemm(void* y, const void* x, const void* wp, const void* resid, float
                 void* q_out, void* k_cache, void* v_cache, const int* positions, const int* slots,
                 const float* cos_sin, int H, int KV, hipStream_t st);
 int pa_row_sumsq(float* out, const void* x, int M, int K, int ldx, hipStream_t st);
+void pa_prefill_gemm_plan(int M, int N, int K, int* full, int* S);
+long long pa_prefill_gemm_ws_floats(int M, int N, int full, int S);
+int pa_prefill_gemm(void* y, const void* x, const void* wp, const void* resid, float* ws, long long ws_floats,
+                    int* counters, int n_counters, int M, int N, int K, int ldx, int ldy, int ldr, int epi,
+                    const float* ss_in, float* ss_out, float* ss_zero, float eps, int full, int splits,
+                    void* q_out, void* k_cache, void* v_cache, const int* positions, const int* slots,
+                    const float* cos_sin, int H, int KV, hipStream_t st);
 int pa_prefetch(const void* p, long long bytes, void* sink, int wgs, hipStream_t st);
 long long pa_cosine_topk_workspace_bytes(int Q, int N, int K);
 int pa_cosine_topk(float* out_scores, int* out_rows, void* workspace, const void* queries,
@@ -416,6 +424,85 @@ bool mid_qkv_rope(at::Tensor x, at::Tensor wp, at::Tensor ss_in, double eps, at:
   return rc == 0;
 }
 
+// Large-M projections (csrc/ops/gemm_prefill.hip): 256x256 MFMA tiles on the packed
+// weights with the same epilogues as mid_gemm (0 plain, 1 SwiGLU, 2 residual, 3 rope-perm).
+bool prefill_gemm(at::Tensor y, at::Tensor x, at::Tensor wp, c10::optional<at::Tensor> resid, at::Tensor ws,
+                  at::Tensor counters, int64_t epi, c10::optional<at::Tensor> ss_in, c10::optional<at::Tensor> ss_out,
+                  c10::optional<at::Tensor> ss_zero, double eps, int64_t full, int64_t splits) {
+  check_gpu(wp, "wp"); check_gpu(ws, "ws"); check_gpu(counters, "counters");
+  TORCH_CHECK(x.is_cuda() && x.dim() == 2 && x.stride(1) == 1, "x must be a 2-D GPU tensor, unit inner stride");
+  TORCH_CHECK(y.is_cuda() && y.dim() == 2 && y.stride(1) == 1, "y must be a 2-D GPU tensor, unit inner stride");
+  check_dtype(x, at::kBFloat16, "x"); check_dtype(wp, at::kBFloat16, "wp"); check_dtype(y, at::kBFloat16, "y");
+  check_dtype(ws, at::kFloat, "ws"); check_dtype(counters, at::kInt, "counters");
+  TORCH_CHECK(epi >= 0 && epi <= 3, "prefill_gemm epi must be 0..3 (RoPE + KV write: prefill_qkv_rope)");
+  TORCH_CHECK(wp.dim() == 4 && wp.size(2) == 64 && wp.size(3) == 8, "wp must be packed [N/16, K/32, 64, 8]");
+  const int M = x.size(0), K = x.size(1), N = wp.size(0) * 16;
+  TORCH_CHECK(wp.size(1) * 32 == K, "packed weight K mismatch");
+  TORCH_CHECK(x.stride(0) % 8 == 0 && y.stride(0) % 4 == 0, "x rows must be 16-byte, y rows 8-byte aligned");
+  const int NO = epi == 1 ? N / 2 : N;
+  TORCH_CHECK(y.size(0) == M && y.size(1) == NO, "y shape mismatch");
+  const void* rp = nullptr;
+  int ldr = 0;
+  if (epi == 2) {
+    TORCH_CHECK(resid.has_value(), "epi=2 needs resid");
+    const auto& r = *resid;
+    TORCH_CHECK(r.is_cuda() && r.dim() == 2 && r.stride(1) == 1 && r.size(0) == M && r.size(1) == N &&
+                    r.stride(0) % 4 == 0,
+                "resid must be [M, N] with unit inner stride");
+    check_dtype(r, at::kBFloat16, "resid");
+    rp = r.data_ptr();
+    ldr = r.stride(0);
+  }
+  const int rc = pa_prefill_gemm(y.data_ptr(), x.data_ptr(), wp.data_ptr(), rp, ws.data_ptr<float>(), ws.numel(),
+                                 counters.data_ptr<int>(), counters.numel(), M, N, K, x.stride(0), y.stride(0), ldr,
+                                 (int)epi, opt_rows(ss_in, M, "ss_in"), const_cast<float*>(opt_rows(ss_out, M, "ss_out")),
+                                 const_cast<float*>(opt_rows(ss_zero, M, "ss_zero")), (float)eps, (int)full,
+                                 (int)splits, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0, cur_stream());
+  TORCH_CHECK(rc >= 0, "prefill_gemm launch failed");
+  return rc == 0;
+}
+
+bool prefill_qkv_rope(at::Tensor x, at::Tensor wp, at::Tensor ss_in, double eps, at::Tensor q_out, at::Tensor k_cache,
+                      at::Tensor v_cache, at::Tensor positions, at::Tensor slots, at::Tensor cos_sin, int64_t H,
+                      int64_t KV, at::Tensor ws, at::Tensor counters, int64_t full, int64_t splits) {
+  check_gpu(wp, "wp"); check_gpu(q_out, "q_out"); check_gpu(k_cache, "k_cache"); check_gpu(v_cache, "v_cache");
+  check_gpu(positions, "positions"); check_gpu(slots, "slots"); check_gpu(cos_sin, "cos_sin");
+  check_gpu(ws, "ws"); check_gpu(counters, "counters");
+  TORCH_CHECK(x.is_cuda() && x.dim() == 2 && x.stride(1) == 1, "x must be a 2-D GPU tensor, unit inner stride");
+  check_dtype(x, at::kBFloat16, "x"); check_dtype(wp, at::kBFloat16, "wp"); check_dtype(q_out, at::kBFloat16, "q_out");
+  check_dtype(k_cache, at::kBFloat16, "k_cache"); check_dtype(v_cache, at::kBFloat16, "v_cache");
+  check_dtype(positions, at::kInt, "positions"); check_dtype(slots, at::kInt, "slots");
+  check_dtype(cos_sin, at::kFloat, "cos_sin");
+  check_dtype(ws, at::kFloat, "ws"); check_dtype(counters, at::kInt, "counters");
+  TORCH_CHECK(wp.dim() == 4 && wp.size(2) == 64 && wp.size(3) == 8, "wp must be packed [N/16, K/32, 64, 8]");
+  const int M = x.size(0), K = x.size(1), N = wp.size(0) * 16;
+  TORCH_CHECK(wp.size(1) * 32 == K, "packed weight K mismatch");
+  TORCH_CHECK(x.stride(0) % 8 == 0, "x rows must be 16-byte aligned");
+  TORCH_CHECK(N == (H + 2 * KV) * 128, "QKV width must be (H + 2 KV) * 128");
+  TORCH_CHECK(q_out.numel() >= (int64_t)M * H * 128, "q_out too small");
+  TORCH_CHECK(positions.numel() >= M && slots.numel() >= M, "positions/slots shorter than x");
+  TORCH_CHECK(cos_sin.dim() == 2 && cos_sin.size(1) == 128, "cos_sin must be [max_pos, 128]");
+  TORCH_CHECK(k_cache.dim() == 5 && k_cache.size(1) == KV && k_cache.size(2) == 16 && k_cache.size(3) == 16 &&
+                  k_cache.size(4) == 8, "k_cache must be [NB, KV, 16, 16, 8]");
+  TORCH_CHECK(v_cache.dim() == 4 && v_cache.size(1) == KV && v_cache.size(2) == 128 && v_cache.size(3) == 16,
+              "v_cache must be [NB, KV, 128, 16]");
+  TORCH_CHECK(ss_in.is_cuda() && ss_in.numel() >= M, "ss_in must hold M row statistics");
+  check_dtype(ss_in, at::kFloat, "ss_in");
+  const int rc = pa_prefill_gemm(nullptr, x.data_ptr(), wp.data_ptr(), nullptr, ws.data_ptr<float>(), ws.numel(),
+                                 counters.data_ptr<int>(), counters.numel(), M, N, K, x.stride(0), 0, 0, 4,
+                                 ss_in.data_ptr<float>(), nullptr, nullptr, (float)eps, (int)full, (int)splits,
+                                 q_out.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(), positions.data_ptr<int>(),
+                                 slots.data_ptr<int>(), cos_sin.data_ptr<float>(), (int)H, (int)KV, cur_stream());
+  TORCH_CHECK(rc >= 0, "prefill_qkv_rope launch failed");
+  return rc == 0;
+}
+
+std::vector<int64_t> prefill_gemm_plan(int64_t M, int64_t N, int64_t K) {
+  int full, S;
+  pa_prefill_gemm_plan((int)M, (int)N, (int)K, &full, &S);
+  return {full, S, pa_prefill_gemm_ws_floats((int)M, (int)N, full, S)};
+}
+
 // out[m] = sum_k x[m, k]^2 (fp32)
 void row_sumsq(at::Tensor out, at::Tensor x) {
   check_gpu(out, "out");
@@ -608,6 +695,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("skinny_gemm", &skinny_gemm);
   m.def("skinny_set_variant", [](int v) { pa_skinny_set_variant(v); });
   m.def("decode_set_variant", [](int v) { pa_decode_set_variant(v); });
+  m.def("handoff_set_acquire", [](int v) { pa_handoff_set_acquire(v); },
+        "consumer mode of the in-launch split-K / partition hand-offs: 1 = agent acquire (default)");
   m.def("decode_gemm", &decode_gemm, py::arg("y"), py::arg("x"), py::arg("wp"), py::arg("resid") = py::none(),
         py::arg("epi") = 0, py::arg("norm") = false, py::arg("eps") = 1e-5, py::arg("nt") = 0,
         py::arg("waves") = 0, py::arg("splits") = 0, py::arg("ws") = py::none(), py::arg("counters") = py::none());
@@ -626,6 +715,14 @@ PYBIND11_MODULE(_C, m) {
         py::arg("q_out"), py::arg("k_cache"), py::arg("v_cache"), py::arg("positions"), py::arg("slots"),
         py::arg("cos_sin"), py::arg("H"), py::arg("KV"), py::arg("ws"), py::arg("counters"), py::arg("fm") = 0,
         py::arg("fn") = 0, py::arg("splits") = 0);
+  m.def("prefill_gemm", &prefill_gemm, py::arg("y"), py::arg("x"), py::arg("wp"), py::arg("resid"), py::arg("ws"),
+        py::arg("counters"), py::arg("epi") = 0, py::arg("ss_in") = py::none(), py::arg("ss_out") = py::none(),
+        py::arg("ss_zero") = py::none(), py::arg("eps") = 1e-5, py::arg("full") = -1, py::arg("splits") = 0);
+  m.def("prefill_qkv_rope", &prefill_qkv_rope, py::arg("x"), py::arg("wp"), py::arg("ss_in"), py::arg("eps"),
+        py::arg("q_out"), py::arg("k_cache"), py::arg("v_cache"), py::arg("positions"), py::arg("slots"),
+        py::arg("cos_sin"), py::arg("H"), py::arg("KV"), py::arg("ws"), py::arg("counters"), py::arg("full") = -1,
+        py::arg("splits") = 0);
+  m.def("prefill_gemm_plan", &prefill_gemm_plan, "default (full tiles, splits, workspace floats) of prefill_gemm");
   m.def("row_sumsq", &row_sumsq, py::arg("out"), py::arg("x"));
   m.def("mid_gemm_plan", &mid_gemm_plan, "default (fm, fn, splits, workspace floats) of mid_gemm");
   m.def("paged_attention", &paged_attention, py::arg("out"), py::arg("part_o"), py::arg("part_ml"), py::arg("q"),

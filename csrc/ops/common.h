@@ -51,6 +51,48 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
   return t;
 }
 
+// In-launch split-K / partition hand-off (cdna_hip_programming.md §6 Guideline 16 and §5
+// "In-launch split-K reduction"). Protocol, in this order:
+//   producer  every wave stores its partial write-through (sc1 buffer stores), then
+//             runs asm `s_waitcnt vmcnt(0)` (EVERY storing wave drains: Pitfall 14),
+//             then calls handoff_last();
+//   ticket    one lane takes a relaxed agent-scope ticket after a workgroup barrier;
+//   consumer  the workgroup that drew ticket n-1 resets the counter for the next launch and
+//             runs ONE agent-scope acquire (`buffer_inv sc1`, completion awaited by an asm
+//             vmcnt(0)) before the barrier that releases its readers.
+// The acquire makes the hand-off placement-independent for ANY number of workgroups per CU
+// (the sc1-loads-only form is validated only at one workgroup per CU: MI355X_MICROARCH.md
+// "Valid forms", condition (4)); the readers may then use plain or sc1 loads.
+// `acquire` = 0 keeps the old sc1-only consumer, 2 adds a producer-side agent release
+// (diagnostics: tools/splitk_check.py).
+// Every thread of the workgroup must call it; it returns true in all of them for the last
+// arriver. `lflag` is an int in the kernel's single LDS array.
+typedef __attribute__((address_space(1))) int handoff_gi32;
+__device__ __forceinline__ bool handoff_last(int* counter, int n, int* lflag, int acquire) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    if (acquire >= 2) {  // diagnostic: an agent-scope release (L2 write-back) on top of the sc1 stores
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    const int tk = __hip_atomic_fetch_add((handoff_gi32*)counter, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = tk == n - 1;
+    if (last) {
+      __hip_atomic_store((handoff_gi32*)counter, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (acquire) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+    }
+    *lflag = last;
+  }
+  __syncthreads();
+  return *lflag != 0;
+}
+
+// host-side hand-off mode passed to every kernel with an in-launch hand-off (default 1)
+extern int g_handoff_acquire;
+
 // Cheap stateless 32-bit hash (splitmix-style finaliser) used as a counter-based
 // RNG for sampling: u = hash(seed, row, col) -> uniform in (0, 1).
 __device__ __forceinline__ uint32_t mix32(uint32_t x) {

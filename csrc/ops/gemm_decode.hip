@@ -64,9 +64,8 @@ struct DgArgs {
   int S;          // K slices (split-K across workgroups; 1 = none)
   float* ws;      // split-K slabs [groups][S][TM*TN + TM] fp32
   int* counters;  // [groups] arrival tickets, zero between launches
+  int acq;        // hand-off consumer mode (common.h handoff_last)
 };
-
-typedef __attribute__((address_space(1))) int dg_gi32;
 
 template <int MT, int NT, int WAVES, int U, int EPI, bool NORM, bool NTW>
 __global__ __launch_bounds__(WAVES * 64) void decode_gemm_kernel(const DgArgs A) {
@@ -219,13 +218,9 @@ __global__ __launch_bounds__(WAVES * 64) void decode_gemm_kernel(const DgArgs A)
   }
   __syncthreads();
   if (S > 1) {
-    // split-K hand-off (cdna_hip_programming.md §5 item 2, sc1 form): publish the
-    // slice's partial tile write-through, take a ticket; the last slice reduces.
-    // slabs padded to 64 floats: each wave's b32 store instruction then writes two whole
-    // 128-B lines and no line is shared by two instructions, waves or slabs. (This did NOT
-    // cure the rare qkv_rope mismatch at M = 9, S = 3 -- only the rotated second half of a
-    // row, so not a stale slab read; profiles/r2_splitk_qkv_rope_flake.jsonl. The engine runs
-    // qkv_rope unsplit; split-K here is used for down_proj, which never mismatched.)
+    // split-K hand-off (common.h handoff_last): publish the slice's partial tile
+    // write-through, take a ticket; the last slice acquires at agent scope and reduces.
+    // Slabs padded to 64 floats: each wave's b32 store instruction writes two whole 128-B lines.
     constexpr int SLAB = (TM * TN + TM + 63) / 64 * 64;
     float* gslab = A.ws + (size_t)grp * S * SLAB;
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(gslab + (size_t)sl * SLAB, 0, SLAB * 4, 0x00020000);
@@ -233,17 +228,7 @@ __global__ __launch_bounds__(WAVES * 64) void decode_gemm_kernel(const DgArgs A)
       __builtin_amdgcn_raw_buffer_store_b32(
           __float_as_uint(e < TM * TN ? fin[e] : (e < TM * TN + TM ? fss[e - TM * TN] : 0.f)), rs, e * 4, 0, 16);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      dg_gi32* cp = (dg_gi32*)(A.counters + grp);
-      const int tk = __hip_atomic_fetch_add(cp, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const int last = tk == S - 1;
-      if (last) __hip_atomic_store(cp, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      *lflag = last;
-    }
-    __syncthreads();
-    if (!*lflag) return;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (!handoff_last(A.counters + grp, S, lflag, A.acq)) return;
     const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(gslab, 0, S * SLAB * 4, 0x00020000);
     for (int e = threadIdx.x; e < TM * TN + TM; e += WAVES * 64) {  // (padding not read)
       float t = 0.f;
@@ -317,6 +302,10 @@ __global__ __launch_bounds__(WAVES * 64) void decode_gemm_kernel(const DgArgs A)
 // wave, so it should not displace x and the KV cache in L2 / MALL; 5-9 % faster on every
 // projection at M = 8-32, 8-token decode steps 3.49 -> 3.33 ms: profiles/r2_decode_nt_ab.jsonl)
 static int g_dg_variant = 1;
+
+// consumer side of every in-launch hand-off (decode / wide / mid GEMM split-K, attention
+// partition merge): 1 = agent-scope acquire by the last arriver (common.h handoff_last)
+int g_handoff_acquire = 1;
 
 template <int MT, int NT, int WAVES, int EPI, bool NORM>
 static int launch_dg(const DgArgs& a, hipStream_t st) {
@@ -396,6 +385,7 @@ static int dispatch(DgArgs a, int epi, int norm, int nt, int waves, int splits, 
     }
   }
   a.S = S;
+  a.acq = g_handoff_acquire;
   int rc = 1;
 #define PA_DGE(MT_)                                                                 \
   switch (epi * 2 + (norm ? 1 : 0)) {                                               \
@@ -422,6 +412,7 @@ static int dispatch(DgArgs a, int epi, int norm, int nt, int waves, int splits, 
 // epi: 0 plain, 1 silu(gate)*up over interleaved tile pairs, 2 residual add.
 // nt/waves/splits <= 0 pick the defaults; ws/counters: split-K slabs and zeroed tickets.
 extern "C" void pa_decode_set_variant(int v) { pa::g_dg_variant = v; }
+extern "C" void pa_handoff_set_acquire(int v) { pa::g_handoff_acquire = v; }
 
 extern "C" int pa_decode_gemm(void* y, const void* x, const void* wp, const void* resid, int M, int N, int K,
                               int ldx, int ldy, int ldr, int epi, int norm, float eps, int nt, int waves,

@@ -34,13 +34,18 @@
 //   * split-K partials go to fp32 slabs with write-through (sc1) stores; the last
 //     slice to take the tile's ticket reduces them and runs the epilogue — one launch.
 #include "common.h"
+#include "packed_epi.h"
 
 #include <algorithm>
 
 namespace pa {
 namespace mid {
 
-enum { EP_PLAIN = 0, EP_SILU = 1, EP_RESID = 2, EP_ROPEPERM = 3, EP_ROPEKV = 4 };
+using pk::EP_PLAIN;
+using pk::EP_SILU;
+using pk::EP_RESID;
+using pk::EP_ROPEPERM;
+using pk::EP_ROPEKV;
 
 struct Args {
   bf16* y;
@@ -64,11 +69,11 @@ struct Args {
   const int* slots;      // [M], < 0 = no cache write
   const float* cos_sin;  // [max_pos, 128] (cos | sin)
   int H, KV;
+  int acq;  // hand-off consumer mode (common.h handoff_last)
 };
 
 typedef __attribute__((address_space(3))) void lds_t;
 typedef __attribute__((address_space(1))) void gbl_t;
-typedef __attribute__((address_space(1))) int gi32_t;
 
 // s_waitcnt vmcnt(N) only (expcnt / lgkmcnt left at "no wait"); gfx9 encoding.
 template <int N>
@@ -94,83 +99,9 @@ __device__ __forceinline__ void glds16_nt(const bf16* src, char* lds) {
   __builtin_amdgcn_global_load_lds((gbl_t*)src, (lds_t*)lds, 16, 0, 2);
 }
 
-// packed rope-QKV tile -> first column of its original tile
-__device__ __forceinline__ int ropeperm_tile(int tile) {
-  const int p = tile & 7;  // packed position inside a head -> original tile (0,4,1,5,2,6,3,7)
-  return (tile & ~7) + ((p & 1) ? 4 + (p >> 1) : (p >> 1));
-}
-
-// Epilogue for one token row m and 4 consecutive columns [cq, cq + 4) of packed tile
-// `tile` (and, for the pair epilogues, the same 4 columns of tile + 1).
-// Returns, for EP_RESID, the sum of squares of the 4 written (bf16-rounded) values.
-template <int EPI>
-__device__ __forceinline__ float store_quad(const Args& A, int m, int tile, int cq, f32x4 v, f32x4 v2) {
-  if constexpr (EPI == EP_SILU) {
-    bf16x4 o;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) o[r] = (bf16)(v[r] / (1.f + __expf(-v[r])) * v2[r]);
-    *reinterpret_cast<bf16x4*>(A.y + (size_t)m * A.ldy + (tile >> 1) * 16 + cq) = o;
-    return 0.f;
-  } else if constexpr (EPI == EP_ROPEKV) {
-    // tile even: original tile i (dims 16i + cq ..), tile + 1: original tile i + 4 (dims + 64)
-    const int hh = tile >> 3;
-    const int d = 16 * ((tile & 7) >> 1) + cq;
-    f32x4 o1 = v, o2 = v2;
-    if (hh < A.H + A.KV) {
-      const float* cs = A.cos_sin + (size_t)A.positions[m] * 128;
-      const f32x4 c = *reinterpret_cast<const f32x4*>(cs + d);
-      const f32x4 s = *reinterpret_cast<const f32x4*>(cs + 64 + d);
-      o1 = v * c - v2 * s;
-      o2 = v2 * c + v * s;
-    }
-    bf16x4 b1, b2;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) { b1[r] = (bf16)o1[r]; b2[r] = (bf16)o2[r]; }
-    if (hh < A.H) {
-      bf16* dst = A.q_out + ((size_t)m * A.H + hh) * 128;
-      *reinterpret_cast<bf16x4*>(dst + d) = b1;
-      *reinterpret_cast<bf16x4*>(dst + d + 64) = b2;
-    } else {
-      const int slot = A.slots[m];
-      if (slot >= 0) {
-        const int blk = slot >> 4, off = slot & 15;
-        if (hh < A.H + A.KV) {
-          bf16* page = A.k_cache + ((size_t)blk * A.KV + (hh - A.H)) * 128 * 16;
-          *reinterpret_cast<bf16x4*>(page + ((size_t)(d >> 3) * 16 + off) * 8 + (d & 7)) = b1;
-          *reinterpret_cast<bf16x4*>(page + ((size_t)((d + 64) >> 3) * 16 + off) * 8 + (d & 7)) = b2;
-        } else {
-          bf16* page = A.v_cache + ((size_t)blk * A.KV + (hh - A.H - A.KV)) * 128 * 16 + off;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            page[(size_t)(d + r) * 16] = b1[r];
-            page[(size_t)(d + 64 + r) * 16] = b2[r];
-          }
-        }
-      }
-    }
-    return 0.f;
-  } else {
-    const int col = (EPI == EP_ROPEPERM ? ropeperm_tile(tile) * 16 : tile * 16) + cq;
-    if constexpr (EPI == EP_RESID) {
-      const bf16x4 rv = *reinterpret_cast<const bf16x4*>(A.resid + (size_t)m * A.ldr + col);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] += (float)rv[r];
-    }
-    bf16x4 o;
-    float sq = 0.f;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      o[r] = (bf16)v[r];
-      const float f = (float)o[r];
-      sq = fmaf(f, f, sq);
-    }
-    *reinterpret_cast<bf16x4*>(A.y + (size_t)m * A.ldy + col) = o;
-    return sq;
-  }
-}
-
-template <int EPI>
-constexpr bool pair_epi() { return EPI == EP_SILU || EPI == EP_ROPEKV; }
+using pk::ropeperm_tile;
+using pk::store_quad;
+using pk::pair_epi;
 
 template <int FM, int FN, int EPI, bool NORM, bool WNT>
 __global__ __launch_bounds__(256) void mid_gemm_kernel(const Args A) {
@@ -359,21 +290,12 @@ __global__ __launch_bounds__(256) void mid_gemm_kernel(const Args A) {
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();  // also: every wave is past its last LDS read of the stages
+  __syncthreads();  // every wave is past its last LDS read of the stages
   int* lflag = reinterpret_cast<int*>(smem);
   float* rsq = reinterpret_cast<float*>(smem) + 4;  // [BM] row sum(y^2) of this tile (EP_RESID)
-  if (threadIdx.x == 0) {
-    gi32_t* cp = (gi32_t*)(A.counters + tile_id);
-    const int tk = __hip_atomic_fetch_add(cp, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int last = tk == A.S - 1;
-    if (last) __hip_atomic_store(cp, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    *lflag = last;
-  }
   if constexpr (EPI == EP_RESID)
     for (int i = threadIdx.x; i < BM; i += 256) rsq[i] = 0.f;
-  __syncthreads();
-  if (!*lflag) return;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  if (!pa::handoff_last(A.counters + tile_id, A.S, lflag, A.acq)) return;
   const __amdgpu_buffer_rsrc_t rall =
       __builtin_amdgcn_make_buffer_rsrc(slab_base, 0, A.S * BM * BN * 4, 0x00020000);
   // thread -> (token row, 4 consecutive columns of one tile; pair epilogues: of an even tile)
@@ -536,7 +458,7 @@ extern "C" int pa_mid_gemm(void* y, const void* x, const void* wp, const void* r
   }
   Args a{(pa::bf16*)y, (const pa::bf16*)x, (const pa::bf16*)wp, (const pa::bf16*)resid, ws, counters, M, N, K,
          ldx, ldy, ldr, S, per, MT, NT, eps, ss_in, ss_out, ss_zero, (pa::bf16*)q_out, (pa::bf16*)k_cache, (pa::bf16*)v_cache, positions,
-         slots, cos_sin, H, KV};
+         slots, cos_sin, H, KV, pa::g_handoff_acquire};
   const int grid = MT * NT * S;
   int rc;
   if (fm == 1 && fn == 2) rc = launch_f<1, 2>(a, epi, norm != 0, grid, st);

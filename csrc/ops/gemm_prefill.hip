@@ -1,0 +1,404 @@
+// Large-M projections (prefill-heavy steps, M > 256 tokens) on the packed weights
+// (replaces hipBLASLt + rmsnorm + silu_mul + rope_cache on those steps).
+//
+//     y[M, N] = epi( rownorm(x)[M, K] · W[N, K]^T )      bf16 in/out, fp32 accumulate
+//
+// At 64 concurrent agents most engine time sits in 512-2,048-token steps (prefill chunks
+// beside the decode rows). Their projections are compute-bound: 2·M·N·K FLOPs on MFMA.
+// The kernel is the CDNA4 256x256 tile of cdna_hip_programming.md §5, built around the
+// operands this engine already has in memory:
+//
+//   * 512 threads = 8 waves as 2 (rows) x 4 (columns); a wave owns 128 x 64 outputs
+//     (8 x 4 tiles of v_mfma_f32_16x16x32_bf16, 128 accumulator VGPRs). The MFMA runs as
+//     C^T = W · x^T, so each lane ends with 4 consecutive output columns of one token:
+//     the norm / SwiGLU / residual / RoPE + KV-write epilogues of packed_epi.h run on
+//     registers (no separate rmsnorm / silu_mul / rope_cache launches);
+//   * W is the fragment-major packed copy (ops.pack_decode_weight): a 16-column x 32-k
+//     chunk is 1 KiB contiguous, so one global_load_lds wave instruction moves one chunk
+//     and the LDS image is lane-linear and conflict-free for the B-fragment ds_read_b128;
+//   * x rows are staged in full 128-B lines (64 k); the 16-B units are XOR-swizzled by
+//     (row >> 1) on the SOURCE address (LDS-DMA writes lane-linear), which makes every
+//     16-row fragment read conflict-free under the ds_read_b128 lane groups;
+//   * a 64-k tile is four 16-KiB "pieces" [x rows lo | x rows hi | W k0 | W k1] in one of
+//     two buffers (128 KiB LDS, one workgroup per CU). Each of the tile's four phases
+//     (rows lo/hi x k halves, 16 MFMAs per wave) issues one piece of a LATER tile and waits
+//     with a counted vmcnt(8) — four pieces (8 LDS-DMA loads per lane) stay in flight
+//     across the raw s_barrier of every phase; a piece is overwritten only two barriers
+//     after its last read (one barrier per phase, no vmcnt(0) inside the loop);
+//   * s_setprio(1) around each MFMA cluster keeps hipcc from moving the MFMAs across the
+//     barriers (guide §5.5 T5);
+//   * tiles are numbered row-tile fastest and mapped XCD-aware, so the 8 row tiles that
+//     share a W panel at M = 2,048 run on one XCD (W read once from HBM per panel);
+//   * wave quantisation: tiles [0, full) run whole, the remaining tiles are split over S
+//     K-slices (one more round of shorter items instead of a half-empty round). The slices
+//     publish fp32 partials write-through in the accumulators' own fragment order and the
+//     last arriver adds them to its registers after the agent-scope acquire of
+//     common.h handoff_last.
+#include "common.h"
+#include "packed_epi.h"
+
+#include <algorithm>
+#include <type_traits>
+
+namespace pa {
+namespace pf {
+
+using namespace pk;
+
+struct Args {
+  bf16* y;
+  const bf16* x;
+  const bf16* wp;
+  const bf16* resid;
+  float* ws;      // split slabs: [(tiles - full) * S][256 * 256] fp32, fragment order
+  int* counters;  // [tiles - full] arrival tickets, zero between launches
+  int M, N, K, ldx, ldy, ldr;
+  int MT, NT;     // 256-row / 256-column tiles
+  int full;       // tiles [0, full) run whole
+  int S, per;     // tiles [full, MT * NT): S K-slices of `per` 64-k tiles
+  float eps;
+  const float* ss_in;  // NORM: [M] row sum(x^2) over K
+  float* ss_out;       // EP_RESID (optional): [M] += row sum(y^2) of the written bf16 output
+  float* ss_zero;      // optional: [M] zeroed by workgroup 0
+  bf16* q_out;
+  bf16* k_cache;
+  bf16* v_cache;
+  const int* positions;
+  const int* slots;
+  const float* cos_sin;
+  int H, KV;
+  int acq;
+};
+
+typedef __attribute__((address_space(3))) void lds_t;
+typedef __attribute__((address_space(1))) void gbl_t;
+
+// s_waitcnt vmcnt(N) only (expcnt / lgkmcnt left at "no wait"); gfx9 encoding.
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  static_assert(N >= 0 && N < 64, "vmcnt is 6 bits");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+}
+
+__device__ __forceinline__ void raw_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+__device__ __forceinline__ void glds16(const bf16* src, char* lds) {
+  __builtin_amdgcn_global_load_lds((gbl_t*)src, (lds_t*)lds, 16, 0, 0);
+}
+
+constexpr int PIECE = 16384;          // bytes
+constexpr int BUF = 4 * PIECE;        // one 64-k tile: [A-p0 | A-p1 | B-k0 | B-k1]
+constexpr int OFF_B = 2 * PIECE;
+constexpr int SLAB = 256 * 256;       // floats per split slab
+
+template <int V>
+using ic = std::integral_constant<int, V>;
+
+template <int EPI, bool NORM>
+__global__ __launch_bounds__(512) void prefill_gemm_kernel(const Args A) {
+  // the only LDS object (guide §5 trap 4a): two tile buffers, reused by the hand-off flag
+  __shared__ __attribute__((aligned(1024))) char smem[2 * BUF];
+
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wid >> 2, wc = wid & 3;
+  const int g = lane >> 4, c = lane & 15;
+
+  // ---- work item: a whole tile, or one K-slice of a tail tile
+  const int bid = blockIdx.x;
+  const int KT = A.K >> 6;
+  int tile, kt0, kt1, slice = -1;
+  if (bid < A.full) {  // XCD-aware bijective remap: consecutive tiles share an XCD
+    const int q8 = A.full >> 3, r8 = A.full & 7, xcd = bid & 7;
+    tile = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+    kt0 = 0;
+    kt1 = KT;
+  } else {
+    const int w2 = bid - A.full;
+    tile = A.full + w2 / A.S;
+    slice = w2 % A.S;
+    kt0 = slice * A.per;
+    kt1 = min(KT, kt0 + A.per);
+  }
+  const int mt = tile % A.MT, nt = tile / A.MT;
+  const int row0 = mt * 256;
+  const int nk = kt1 - kt0;
+
+  if (A.ss_zero && blockIdx.x == 0)
+    for (int i = threadIdx.x; i < A.M; i += 512) A.ss_zero[i] = 0.f;
+
+  // ---- per-lane LDS-DMA sources
+  // x piece p (rows lo / hi of each wave row): LDS row lr = (2 wid + q) * 8 + (lane >> 3)
+  // holds tile row (lr >> 6) * 128 + 64 p + (lr & 63); its 16-B unit (lane & 7) is the
+  // row's logical unit (lane & 7) ^ ((lr >> 1) & 7).
+  const bf16* xs[2][2];
+#pragma unroll
+  for (int p = 0; p < 2; ++p)
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int lr = (wid * 2 + q) * 8 + (lane >> 3);
+      const int trow = (lr >> 6) * 128 + p * 64 + (lr & 63);
+      const int gr = min(row0 + trow, A.M - 1);
+      const int unit = (lane & 7) ^ ((lr >> 1) & 7);
+      xs[p][q] = A.x + (size_t)gr * A.ldx + unit * 8;
+    }
+  const int KS = A.K >> 5;
+  const bf16* wsrc[2];
+#pragma unroll
+  for (int q = 0; q < 2; ++q) wsrc[q] = A.wp + ((size_t)(nt * 16 + wid * 2 + q) * KS) * 512 + lane * 8;
+
+  auto issue_a = [&](int p, int kt, char* buf) {
+#pragma unroll
+    for (int q = 0; q < 2; ++q) glds16(xs[p][q] + (size_t)kt * 64, buf + p * PIECE + (wid * 2 + q) * 1024);
+  };
+  auto issue_b = [&](int kh, int kt, char* buf) {
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+      glds16(wsrc[q] + (size_t)(2 * kt + kh) * 512, buf + OFF_B + kh * PIECE + (wid * 2 + q) * 1024);
+  };
+  auto read_b = [&](const char* buf, int kh, bf16x8(&bf)[4]) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      bf[j] = *reinterpret_cast<const bf16x8*>(buf + OFF_B + kh * PIECE + (wc * 4 + j) * 1024 + lane * 16);
+  };
+  auto read_a = [&](const char* buf, int p, int kh, bf16x8(&af)[4]) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int lr = wr * 64 + 16 * i + c;
+      const int u = 4 * kh + g;
+      af[i] = *reinterpret_cast<const bf16x8*>(buf + p * PIECE + lr * 128 + ((u ^ ((lr >> 1) & 7)) << 4));
+    }
+  };
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto mma = [&](auto half, const bf16x8(&af)[4], const bf16x8(&bf)[4]) {
+    constexpr int h = decltype(half)::value;
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[h * 4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j], af[i], acc[h * 4 + i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  char* const b0 = smem;
+  char* const b1 = smem + BUF;
+  bf16x8 bk0[4], bk1[4], af[4];
+
+  // One 64-k tile in four phases. ISS: pieces of the next tiles are issued (main loop:
+  // B-k1 and x-hi of tile i + 1 in phases 0/1, B-k0 and x-lo of tile i + 2 in phases 2/3);
+  // W0/W1/W3: the counted vmcnt of phases 0, 1 and 3 (-1 = none).
+  auto tile_body = [&](int i, auto iss1, auto iss2, auto w0, auto w1, auto w3) {
+    char* cur = (i & 1) ? b1 : b0;
+    char* oth = (i & 1) ? b0 : b1;
+    // phase 0: rows lo, k 0-31
+    read_b(cur, 0, bk0);
+    read_a(cur, 0, 0, af);
+    if constexpr (decltype(iss1)::value) issue_b(1, kt0 + i + 1, oth);
+    if constexpr (decltype(w0)::value >= 0) wait_vm<decltype(w0)::value>();
+    raw_barrier();
+    mma(ic<0>{}, af, bk0);
+    // phase 1: rows lo, k 32-63
+    read_b(cur, 1, bk1);
+    read_a(cur, 0, 1, af);
+    if constexpr (decltype(iss1)::value) issue_a(1, kt0 + i + 1, oth);
+    if constexpr (decltype(w1)::value >= 0) wait_vm<decltype(w1)::value>();
+    raw_barrier();
+    mma(ic<0>{}, af, bk1);
+    // phase 2: rows hi, k 0-31
+    read_a(cur, 1, 0, af);
+    if constexpr (decltype(iss2)::value) issue_b(0, kt0 + i + 2, cur);
+    raw_barrier();
+    mma(ic<1>{}, af, bk0);
+    // phase 3: rows hi, k 32-63
+    read_a(cur, 1, 1, af);
+    if constexpr (decltype(iss2)::value) issue_a(0, kt0 + i + 2, cur);
+    if constexpr (decltype(w3)::value >= 0) wait_vm<decltype(w3)::value>();
+    raw_barrier();
+    mma(ic<1>{}, af, bk1);
+  };
+
+  if (nk >= 2) {
+    issue_b(0, kt0, b0);
+    issue_a(0, kt0, b0);
+    issue_b(1, kt0, b0);
+    issue_a(1, kt0, b0);
+    issue_b(0, kt0 + 1, b1);
+    issue_a(0, kt0 + 1, b1);
+    wait_vm<8>();
+    raw_barrier();
+    int i = 0;
+    for (; i + 2 < nk; ++i) tile_body(i, ic<1>{}, ic<1>{}, ic<8>{}, ic<8>{}, ic<8>{});
+    tile_body(i, ic<1>{}, ic<0>{}, ic<8>{}, ic<8>{}, ic<4>{});  // tile nk - 2
+    tile_body(i + 1, ic<0>{}, ic<0>{}, ic<2>{}, ic<0>{}, ic<-1>{});  // tile nk - 1
+  } else if (nk == 1) {
+    issue_b(0, kt0, b0);
+    issue_a(0, kt0, b0);
+    issue_b(1, kt0, b0);
+    issue_a(1, kt0, b0);
+    wait_vm<4>();
+    raw_barrier();
+    tile_body(0, ic<0>{}, ic<0>{}, ic<2>{}, ic<0>{}, ic<-1>{});
+  }
+
+  // ---- split tiles: publish, last arriver sums the other slices into its registers
+  if (slice >= 0) {
+    float* base = A.ws + (size_t)(tile - A.full) * A.S * SLAB;
+    {
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(base + (size_t)slice * SLAB, 0, SLAB * 4, 0x00020000);
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i][j]), rs,
+                                                 (((wid * 8 + i) * 4 + j) * 64 + lane) * 16, 0, 16);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (!handoff_last(A.counters + (tile - A.full), A.S, reinterpret_cast<int*>(smem), A.acq)) return;
+    for (int p = 0; p < A.S; ++p) {
+      if (p == slice) continue;
+      const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(base + (size_t)p * SLAB, 0, SLAB * 4, 0x00020000);
+#pragma unroll
+      for (int i = 0; i < 8; i += 2) {  // 8 loads in flight per lane (the accumulators hold the rest)
+        f32x4 t[2][4];
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            t[h][j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                    rp, (((wid * 8 + i + h) * 4 + j) * 64 + lane) * 16, 0, 16));
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[i + h][j] += t[h][j];
+      }
+    }
+  }
+
+  // ---- register epilogue: lane (g, c) of tile (i, j) holds token row 16 i + c (of its
+  // wave's 128), columns 4 g .. 4 g + 3 of 16-column tile nt * 16 + wc * 4 + j
+  const float inv_k = 1.f / (float)A.K;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int m = row0 + wr * 128 + 16 * i + c;
+    const bool ok = m < A.M;
+    float sq = 0.f;
+    if (ok) {
+      float rs = 1.f;
+      if constexpr (NORM) rs = rsqrtf(A.ss_in[m] * inv_k + A.eps);
+      if constexpr (pair_epi<EPI>()) {
+#pragma unroll
+        for (int j = 0; j < 4; j += 2)
+          store_quad<EPI>(A, m, nt * 16 + wc * 4 + j, 4 * g, acc[i][j] * rs, acc[i][j + 1] * rs);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) sq += store_quad<EPI>(A, m, nt * 16 + wc * 4 + j, 4 * g, acc[i][j] * rs, acc[i][j]);
+      }
+    }
+    if constexpr (EPI == EP_RESID) {
+      if (A.ss_out) {
+        sq += __shfl_xor(sq, 16, 64);
+        sq += __shfl_xor(sq, 32, 64);
+        if (ok && g == 0) atomicAdd(A.ss_out + m, sq);
+      }
+    }
+  }
+}
+
+// Default decomposition: whole tiles while they fill complete rounds of 256 CUs; the
+// remainder is split over K so that the last round is (nearly) full.
+static void plan_default(int M, int N, int K, int& full, int& S) {
+  const int tiles = ((M + 255) / 256) * (N / 256);
+  const int KT = K / 64;
+  const int rem = tiles % 256;
+  full = tiles - rem;
+  S = 1;
+  if (rem) {
+    S = std::max(1, std::min(4, 256 / rem));
+    while (S > 1 && KT / S < 8) --S;
+    if (S == 1) full = tiles;
+  }
+}
+
+}  // namespace pf
+}  // namespace pa
+
+extern "C" void pa_prefill_gemm_plan(int M, int N, int K, int* full, int* S) {
+  pa::pf::plan_default(M, N, K, *full, *S);
+}
+
+extern "C" long long pa_prefill_gemm_ws_floats(int M, int N, int full, int S) {
+  const long long tiles = (long long)((M + 255) / 256) * (N / 256);
+  return S > 1 ? (tiles - full) * S * (long long)pa::pf::SLAB : 0;
+}
+
+// Returns 1 if the shape/config is not handled, 0 on success, -2 on a launch error.
+// full < 0 / splits <= 0 pick the defaults. For epi 4 (RoPE + paged KV write) y is unused.
+extern "C" int pa_prefill_gemm(void* y, const void* x, const void* wp, const void* resid, float* ws,
+                               long long ws_floats, int* counters, int n_counters, int M, int N, int K, int ldx,
+                               int ldy, int ldr, int epi, const float* ss_in, float* ss_out, float* ss_zero,
+                               float eps, int full, int splits, void* q_out, void* k_cache, void* v_cache,
+                               const int* positions, const int* slots, const float* cos_sin, int H, int KV,
+                               hipStream_t st) {
+  using namespace pa::pf;
+  if (M <= 0) return 0;
+  if (K % 64 != 0 || N % 256 != 0 || epi < 0 || epi > 4 || ldx % 8 != 0) return 1;
+  const int norm = ss_in != nullptr;
+  if (epi == EP_RESID && (!resid || norm)) return 1;
+  if (ss_out && epi != EP_RESID) return 1;
+  if (epi == EP_ROPEKV && (!q_out || !k_cache || !v_cache || !positions || !slots || !cos_sin ||
+                           N != (H + 2 * KV) * 128))
+    return 1;
+  const int MT = (M + 255) / 256, NT = N / 256, tiles = MT * NT;
+  int dfull, dS;
+  plan_default(M, N, K, dfull, dS);
+  if (full < 0) full = dfull;
+  int S = splits > 0 ? splits : (full == dfull ? dS : 1);
+  full = std::min(std::max(full, 0), tiles);
+  const int KT = K / 64;
+  S = std::max(1, std::min(S, KT));
+  int per = (KT + S - 1) / S;
+  S = (KT + per - 1) / per;  // no empty slices
+  if (S == 1) full = tiles;
+  if (full < tiles) {
+    const long long need = (long long)(tiles - full) * S * SLAB;
+    if (!ws || !counters || n_counters < tiles - full || need > ws_floats) return 1;
+  }
+  Args a{(pa::bf16*)y, (const pa::bf16*)x, (const pa::bf16*)wp, (const pa::bf16*)resid, ws, counters,
+         M, N, K, ldx, ldy, ldr, MT, NT, full, S, per, eps, ss_in, ss_out, ss_zero,
+         (pa::bf16*)q_out, (pa::bf16*)k_cache, (pa::bf16*)v_cache, positions, slots, cos_sin, H, KV,
+         pa::g_handoff_acquire};
+  const int grid = full + (tiles - full) * S;
+#define PA_PF(E, NRM) hipLaunchKernelGGL((prefill_gemm_kernel<E, NRM>), dim3(grid), dim3(512), 0, st, a)
+  switch (epi) {
+    case EP_PLAIN:
+      if (norm) PA_PF(EP_PLAIN, true); else PA_PF(EP_PLAIN, false);
+      break;
+    case EP_RESID:
+      PA_PF(EP_RESID, false);
+      break;
+    case EP_ROPEPERM:
+      if (norm) PA_PF(EP_ROPEPERM, true); else PA_PF(EP_ROPEPERM, false);
+      break;
+    case EP_SILU:
+      if (norm) PA_PF(EP_SILU, true); else PA_PF(EP_SILU, false);
+      break;
+    case EP_ROPEKV:
+      if (norm) PA_PF(EP_ROPEKV, true); else PA_PF(EP_ROPEKV, false);
+      break;
+    default:
+      return 1;
+  }
+#undef PA_PF
+  return (int)hipGetLastError() == 0 ? 0 : -2;
+}

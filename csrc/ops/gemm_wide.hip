@@ -32,8 +32,6 @@ namespace pa {
 
 enum { WG_PLAIN = 0, WG_SILU = 1, WG_RESID = 2, WG_ROPEPERM = 3 };
 
-typedef __attribute__((address_space(1))) int wg_gi32;
-
 struct WgArgs {
   bf16* y;
   const bf16* x;
@@ -43,6 +41,7 @@ struct WgArgs {
   int* counters;  // [groups], zero between launches
   int M, N, K, ldx, ldy, ldr, S, per;  // per = k-steps per slice (multiple of the chunk's k-steps)
   float eps;                           // NORM: rows scaled by rsqrt(mean(x^2) + eps)
+  int acq;                             // hand-off consumer mode (common.h handoff_last)
 };
 
 __device__ __forceinline__ int ropeperm_col(int tile, int c) {
@@ -286,18 +285,8 @@ __global__ __launch_bounds__(WAVES * 64) void wide_gemm_kernel(const WgArgs A) {
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
   int* lflag = reinterpret_cast<int*>(lds_f);
-  if (threadIdx.x == 0) {
-    wg_gi32* cp = (wg_gi32*)(A.counters + grp);
-    const int tk = __hip_atomic_fetch_add(cp, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int last = tk == S - 1;
-    if (last) __hip_atomic_store(cp, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    *lflag = last;
-  }
-  __syncthreads();
-  if (!*lflag) return;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  if (!handoff_last(A.counters + grp, S, lflag, A.acq)) return;
   const __amdgpu_buffer_rsrc_t rall =
       __builtin_amdgcn_make_buffer_rsrc(slab_base, 0, S * ROWS * GC * 4, 0x00020000);
   const __amdgpu_buffer_rsrc_t rqall = __builtin_amdgcn_make_buffer_rsrc(ss_base, 0, S * ROWS * 4, 0x00020000);
@@ -443,7 +432,7 @@ extern "C" int pa_wide_gemm(void* y, const void* x, const void* wp, const void* 
     if (ws_need(S) > ws_floats) return 1;
   }
   WgArgs a{(bf16*)y, (const bf16*)x, (const bf16*)wp, (const bf16*)resid, ws, counters, M, N, K, ldx, ldy, ldr,
-           S, per, eps};
+           S, per, eps, g_handoff_acquire};
   int rc;
   switch (MTp) {
     case 2: rc = launch_wg_mt<2>(a, epi, norm != 0, ntw, waves, st); break;

@@ -4,6 +4,7 @@
 
 #include "grammar.h"
 #include "scheduler.h"
+#include "shm_ring.h"
 #include "tokenizer.h"
 
 namespace py = pybind11;
@@ -47,6 +48,31 @@ PYBIND11_MODULE(_runtime, m) {
   m.def("hash_block", [](uint64_t parent, const std::vector<int32_t>& toks) {
     return hash_block(parent, toks.data(), (int)toks.size());
   });
+
+  py::class_<ShmRing>(m, "ShmRing")
+      .def(py::init<const std::string&, int, int, int, bool, double>(), py::arg("name"), py::arg("ints"),
+           py::arg("slots"), py::arg("consumers"), py::arg("create"), py::arg("attach_timeout_s") = 60.0)
+      .def("put", [](ShmRing& r, const std::vector<int64_t>& rec, double timeout_s) {
+             if ((int)rec.size() != r.ints()) throw std::invalid_argument("record length mismatch");
+             bool ok;
+             {
+               py::gil_scoped_release nogil;
+               ok = r.put(rec.data(), timeout_s);
+             }
+             return ok;
+           }, py::arg("rec"), py::arg("timeout_s") = 600.0)
+      .def("get", [](ShmRing& r, int c, double timeout_s) -> py::object {
+             std::vector<int64_t> rec(r.ints());
+             bool ok;
+             {
+               py::gil_scoped_release nogil;
+               ok = r.get(c, rec.data(), timeout_s);
+             }
+             if (!ok) return py::none();
+             return py::cast(rec);
+           }, py::arg("consumer"), py::arg("timeout_s") = 600.0)
+      .def("published", &ShmRing::published)
+      .def("unlink", &ShmRing::unlink);
 
   py::class_<Tokenizer>(m, "Tokenizer")
       .def(py::init([](const std::vector<py::bytes>& vocab) {

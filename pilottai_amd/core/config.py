@@ -35,9 +35,11 @@ class SecureConfig:
     def __init__(self, key_path: Optional[Path] = None):
         self._key_path = Path(key_path) if key_path else None
         if self._key_path and self._key_path.exists():
-            self.key = self._key_path.read_bytes().strip()
-            if len(self.key) == 32:
-                self.key = base64.urlsafe_b64encode(self.key)
+            raw = self._key_path.read_bytes()
+            if len(raw) == 32:  # legacy raw key: check the length BEFORE any strip (a random
+                self.key = base64.urlsafe_b64encode(raw)  # key may start/end with a whitespace byte)
+            else:
+                self.key = raw.strip()  # Fernet key (44 url-safe base64 bytes, maybe + newline)
         else:
             self.key = Fernet.generate_key()
             if self._key_path:

@@ -84,6 +84,9 @@ class EngineConfig:
     decode_fused_max_t: Optional[int] = None  # largest step (tokens) on that path; None = model default
     wide_max_t: Optional[int] = None  # largest step on the packed small-batch path; None = model default
     mid_max_t: Optional[int] = None  # largest step on the LDS-DMA tiled mid-size path; None = model default
+    # largest step on the fused packed-weight path with the 256 x 256 prefill kernels (above
+    # mid_max_t); 0 = such steps take the library (hipBLASLt) path; None = model default
+    prefill_max_t: Optional[int] = None
     att_qcols: int = 128  # prefill attention item width in MFMA columns (128: LDS-staged 4-wave items)
     # ... used only for steps with at least this many prefill tokens (1,024: 1,024-2,048-token steps
     # 1-2 % faster than with 2,048, which most mixed steps never reached; profiles/r2_att_wide_min_ab.jsonl)
@@ -181,6 +184,8 @@ class LLMEngine:
             self.model.WIDE_MAX_T = int(cfg.wide_max_t)
         if cfg.mid_max_t is not None:
             self.model.MID_MAX_T = int(cfg.mid_max_t)
+        if cfg.prefill_max_t is not None:
+            self.model.PREFILL_MAX_T = int(cfg.prefill_max_t)
         if cfg.prefetch_weights is not None:
             self.model.PREFETCH_WEIGHTS = bool(cfg.prefetch_weights)
         self.load_time = time.time() - t0
@@ -280,6 +285,9 @@ class LLMEngine:
         # step's synchronize, failing the engine rather than continuing on partial sums
         self._car = getattr(self.tp, "custom", None) if self.tp.size > 1 else None
         self._car_err_host = torch.zeros(1, dtype=torch.int32, pin_memory=pin) if self._car is not None else None
+        self._tp_ring = None
+        if self.tp.size > 1:
+            self._open_tp_ring()
         if self.tp.size > 1:  # ranks reach graph capture together (their init times differ)
             torch.distributed.barrier(group=self.tp.cpu_group)
         # graphs contain the TP collectives, so every rank captures every bucket up front
@@ -523,13 +531,52 @@ class LLMEngine:
         self.release_followers()
 
     # ------------------------------------------------------------------ TP
+    def _open_tp_ring(self):
+        """The per-step TP header travels through a shared-memory ring (csrc/runtime/shm_ring.cpp;
+        SURVEY §5: shared-memory rings, not sockets, for the node-local control hop): the
+        driver publishes, every follower polls its own read position. PILOTTAI_TP_HEADER=gloo
+        (or a node without POSIX shared memory) keeps the gloo broadcast."""
+        if os.environ.get("PILOTTAI_TP_HEADER", "shm") == "gloo":
+            return
+        box = [f"pilottai_tp_{os.getpid()}_{self.tp.root}_{os.urandom(4).hex()}" if self.is_driver else None]
+        torch.distributed.broadcast_object_list(box, src=self.tp.root, group=self.tp.cpu_group)
+        ok = torch.zeros(1, dtype=torch.int32)
+        try:
+            from pilottai_amd import _runtime
+
+            # driver first (creates), then the followers attach
+            if self.is_driver:
+                self._tp_ring = _runtime.ShmRing(box[0], 9, 64, self.tp.size - 1, True)
+            torch.distributed.barrier(group=self.tp.cpu_group)
+            if not self.is_driver:
+                self._tp_ring = _runtime.ShmRing(box[0], 9, 64, self.tp.size - 1, False, 120.0)
+        except Exception as e:  # noqa: BLE001 — fall back to the gloo broadcast on every rank
+            log.warning("TP header ring unavailable (%s): using the gloo broadcast", e)
+            ok[0] = 1
+        torch.distributed.all_reduce(ok, group=self.tp.cpu_group)
+        if int(ok[0]):
+            self._tp_ring = None
+
     def _tp_send(self, op: int, *vals: int):
         h = self._tp_header
         h.zero_()
         h[0] = op
         for i, v in enumerate(vals):
             h[1 + i] = int(v)
-        self.tp.broadcast(h, cpu=True)
+        if self._tp_ring is not None:
+            if not self._tp_ring.put(h.tolist(), 600.0):
+                raise RuntimeError("TP follower stopped reading step headers (ring full for 600 s)")
+        else:
+            self.tp.broadcast(h, cpu=True)
+
+    def _tp_recv(self):
+        if self._tp_ring is not None:
+            rec = self._tp_ring.get(self.tp.rank - 1, 3600.0)
+            if rec is None:
+                raise RuntimeError("no TP step header from the driver for an hour")
+            return rec
+        self.tp.broadcast(self._tp_header, cpu=True)
+        return self._tp_header.tolist()
 
     def release_followers(self):
         """Driver: tell the follower ranks to leave `follow()` (idempotent)."""
@@ -546,11 +593,9 @@ class LLMEngine:
         if self.on_gpu:
             torch.cuda.set_device(self.device)
         n = 0
-        h = self._tp_header
         with torch.inference_mode():
             while True:
-                self.tp.broadcast(h, cpu=True)
-                op, T, ns, nsamp, bucket, masks_changed, n_copy, trunc, embed = (int(v) for v in h.tolist())
+                op, T, ns, nsamp, bucket, masks_changed, n_copy, trunc, embed = (int(v) for v in self._tp_recv())
                 if op == _OP_STOP:
                     break
                 if masks_changed:

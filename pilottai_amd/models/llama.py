@@ -136,6 +136,19 @@ class LlamaModel:
     # steps of up to this many tokens (above WIDE_MAX_T) run the LDS-DMA tiled projections
     # (csrc/ops/gemm_mid.hip) with every norm / SwiGLU / residual / RoPE + KV write fused
     MID_MAX_T = 256
+    # steps above MID_MAX_T and up to this many tokens run the same fused packed-weight layer
+    # with the 256 x 256 prefill kernels (csrc/ops/gemm_prefill.hip) for the projections that
+    # PF_CFG assigns to them; larger steps (and PREFILL_MAX_T = 0) take the library path
+    PREFILL_MAX_T = 1 << 30
+    # per projection: (largest M, path, config); the first row whose M covers the step is used.
+    # "pf": prefill kernel (full = whole tiles, -1 = the kernel's plan; splits of the rest),
+    # "mid": mid kernel (fm, fn, splits as MID_CFG)
+    PF_CFG = {
+        "qkv": [(1 << 30, "pf", {"full": -1, "splits": 0})],
+        "o": [(1 << 30, "pf", {"full": -1, "splits": 0})],
+        "gate_up": [(1 << 30, "pf", {"full": -1, "splits": 0})],
+        "down": [(1 << 30, "pf", {"full": -1, "splits": 0})],
+    }
     # decode/small steps: let the attention launch's idle workgroups read the O
     # projection's weights into the Infinity Cache (MALL-resident weights run the 34 MB
     # O projection at M=8 in 8.7 us vs 12.8 us cold, profiles/r2_mall_warm.jsonl). Off by
@@ -205,8 +218,9 @@ class LlamaModel:
         if self.device.type == "cuda":
             ops.wide_workspace(self.device)  # split-K slabs + tickets, before any graph capture
             ops.mid_workspace(self.device)
+            ops.prefill_workspace(self.device)
         # RMSNorm row statistics handed from each residual epilogue to the next projection
-        self._ss = torch.zeros(2, 1 << 14, dtype=torch.float32, device=self.device)
+        self._ss = torch.zeros(2, 1 << 15, dtype=torch.float32, device=self.device)
         if self.device.type == "cuda":
             ops.kernels._prefetch_sink(self.device)  # before any graph capture
         self.decode_packed = True
@@ -339,7 +353,7 @@ class LlamaModel:
             return self._forward_decode(meta, kv, T, num_logit_rows, part_o, part_ml, embed)
         if self.decode_packed and T <= self.WIDE_MAX_T:
             return self._forward_wide(meta, kv, T, num_logit_rows, part_o, part_ml, embed)
-        if self.decode_packed and T <= self.MID_MAX_T:
+        if self.decode_packed and (T <= self.MID_MAX_T or T <= self.PREFILL_MAX_T):
             return self._forward_mid(meta, kv, T, num_logit_rows, part_o, part_ml, embed)
         H, KVh, hd = self.h_local, self.kv_local, cfg.head_dim
         ids = meta.input_ids[:T].long() if self.device.type == "cpu" else meta.input_ids[:T]
@@ -491,11 +505,32 @@ class LlamaModel:
                 return {"fm": fm, "fn": fn, "splits": S}
         return {}
 
+    def _proj_path(self, kind: str, T: int):
+        """("mid", cfg) or ("pf", cfg) for projection `kind` on a T-token step."""
+        if T > self.MID_MAX_T and self.device.type == "cuda":
+            for mmax, path, cfg in self.PF_CFG[kind]:
+                if T <= mmax:
+                    return path, (dict(cfg) if path == "pf" else self._mid_cfg(kind, T) | dict(cfg))
+        return "mid", self._mid_cfg(kind, T)
+
+    def _gemm(self, kind: str, T: int, x, wp, epi: str, **kw):
+        path, cfg = self._proj_path(kind, T)
+        fn = ops.prefill_gemm if path == "pf" else ops.mid_gemm
+        return fn(x, wp, epi, **cfg, **kw)
+
+    def _qkv_rope(self, T: int, x, wp, eps, q, k_cache, v_cache, meta, ss_in):
+        H, KVh = self.h_local, self.kv_local
+        path, cfg = self._proj_path("qkv", T)
+        fn = ops.prefill_qkv_rope if path == "pf" else ops.mid_qkv_rope
+        return fn(x, wp, eps, q, k_cache, v_cache, meta.positions, meta.slots, self.cos_sin, H, KVh,
+                  ss_in=ss_in, **cfg)
+
     def _forward_mid(self, meta: StepMeta, kv: KVCache, T: int, num_logit_rows: int,
                      part_o: torch.Tensor, part_ml: torch.Tensor, embed=None) -> torch.Tensor:
-        """Mid-size step (WIDE_MAX_T < T <= MID_MAX_T: decode rows plus prefill chunks) on
-        the packed weights, 4 projection launches + attention per layer
-        (csrc/ops/gemm_mid.hip):
+        """Mid-size and prefill-heavy steps (T > WIDE_MAX_T: decode rows plus prefill chunks)
+        on the packed weights, 4 projection launches + attention per layer
+        (csrc/ops/gemm_mid.hip up to MID_MAX_T tokens; above it the 256 x 256 tiles of
+        csrc/ops/gemm_prefill.hip for the projections PF_CFG assigns to them):
 
           QKV (RMSNorm folded, RoPE + paged KV write in the epilogue) -> attention ->
           O (+ residual, accumulating the next norm's row statistics) ->
@@ -516,32 +551,29 @@ class LlamaModel:
         ss_a, ss_b = self._ss[0, :T], self._ss[1, :T]
         ops.row_sumsq(h, out=ss_a)
         ss_b.zero_()
-        c_qkv, c_o = self._mid_cfg("qkv", T), self._mid_cfg("o", T)
-        c_gu, c_dn = self._mid_cfg("gate_up", T), self._mid_cfg("down", T)
         for li, L in enumerate(self.layers):
             q = torch.empty(T, H, hd, dtype=self.dtype, device=self.device)
-            ops.mid_qkv_rope(h, L["wqkv_p"], eps, q, kv.k[li], kv.v[li], meta.positions, meta.slots,
-                             self.cos_sin, H, KVh, ss_in=ss_a, **c_qkv)
+            self._qkv_rope(T, h, L["wqkv_p"], eps, q, kv.k[li], kv.v[li], meta, ss_a)
             attn = torch.empty(T, H, hd, dtype=self.dtype, device=self.device)
             ops.paged_attention(attn, part_o, part_ml, q, kv.k[li], kv.v[li], meta.items, meta.n_items,
                                 meta.att_counters, meta.q_start, meta.q_len, meta.ctx_len,
                                 meta.block_table, self.scale, num_seqs=meta.num_seqs, part_size=meta.part_size)
             a2 = attn.view(T, H * hd)
             if tp:
-                o = ops.mid_gemm(a2, L["wo_p"], "plain", **c_o)
+                o = self._gemm("o", T, a2, L["wo_p"], "plain")
                 self.tp.all_reduce(o)
                 h.add_(o)
                 ops.row_sumsq(h, out=ss_b)
             else:  # ss_b was zeroed by the previous down launch (or above)
-                ops.mid_gemm(a2, L["wo_p"], "resid", resid=h, out=h, ss_out=ss_b, ss_zero=ss_a, **c_o)
-            a = ops.mid_gemm(h, L["w13_p"], "silu", norm=True, eps=eps, ss_in=ss_b, **c_gu)
+                self._gemm("o", T, a2, L["wo_p"], "resid", resid=h, out=h, ss_out=ss_b, ss_zero=ss_a)
+            a = self._gemm("gate_up", T, h, L["w13_p"], "silu", norm=True, eps=eps, ss_in=ss_b)
             if tp:
-                d = ops.mid_gemm(a, L["w2_p"], "plain", **c_dn)
+                d = self._gemm("down", T, a, L["w2_p"], "plain")
                 self.tp.all_reduce(d)
                 h.add_(d)
                 ops.row_sumsq(h, out=ss_a)
             else:
-                ops.mid_gemm(a, L["w2_p"], "resid", resid=h, out=h, ss_out=ss_a, ss_zero=ss_b, **c_dn)
+                self._gemm("down", T, a, L["w2_p"], "resid", resid=h, out=h, ss_out=ss_a, ss_zero=ss_b)
         if embed is not None:
             self._pool_embed(ops.rmsnorm(h, self.norm, eps), T, embed)
         rows = meta.logit_rows[:num_logit_rows]

@@ -70,14 +70,15 @@ def env_rank_world():
     return rank, world, local
 
 
-def init_distributed(backend: Optional[str] = None, timeout_s: int = 600) -> tuple:
+def init_distributed(backend: Optional[str] = None, timeout_s: int = 600, single: bool = False) -> tuple:
     """Initialise the default process group from torchrun-style env vars.
 
     Returns (rank, world_size, local_rank). backend defaults to "nccl" (RCCL)
-    when a GPU is visible, else "gloo". Safe to call twice.
+    when a GPU is visible, else "gloo". Safe to call twice. A world of one rank
+    creates no group unless `single` (a one-process group, e.g. to exercise RCCL).
     """
     rank, world, local = env_rank_world()
-    if world <= 1:
+    if world <= 1 and not single:
         return 0, 1, 0
     if not dist.is_initialized():
         if backend is None:

@@ -26,10 +26,12 @@ declared lost is ignored).
 from __future__ import annotations
 
 import asyncio
+import hmac
 import itertools
 import json
 import logging
 import os
+import secrets
 import struct
 import time
 from datetime import datetime
@@ -50,6 +52,29 @@ def plane_port() -> int:
     if os.environ.get("PILOTTAI_PLANE_PORT"):
         return int(os.environ["PILOTTAI_PLANE_PORT"])
     return int(os.environ.get("MASTER_PORT", "29511")) + 7
+
+
+def plane_secret() -> str:
+    """Shared secret every worker's hello must carry (the plane had no
+    authentication). PILOTTAI_PLANE_SECRET when set (launchers export it to every rank);
+    otherwise, inside an initialised torch.distributed job, a token that rank 0 draws and
+    broadcasts to the job's ranks; otherwise a per-process token (a lone rank 0)."""
+    env = os.environ.get("PILOTTAI_PLANE_SECRET")
+    if env:
+        return env
+    try:
+        import torch.distributed as dist
+
+        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+            box = [secrets.token_hex(16) if dist.get_rank() == 0 else None]
+            dist.broadcast_object_list(box, src=0)
+            os.environ["PILOTTAI_PLANE_SECRET"] = box[0]
+            return box[0]
+    except Exception:  # noqa: BLE001 — no usable process group: fall through
+        pass
+    tok = secrets.token_hex(16)
+    os.environ["PILOTTAI_PLANE_SECRET"] = tok
+    return tok
 
 
 async def _send(writer: asyncio.StreamWriter, obj: Dict[str, Any]):
@@ -106,8 +131,11 @@ class PlaneServer:
     """Rank 0 side: accepts the worker ranks, routes requests, detects lost ranks."""
 
     def __init__(self, world: int, host: str = "127.0.0.1", port: Optional[int] = None,
-                 hb_timeout: float = 5.0, local_load: Optional[Callable[[], Dict[str, float]]] = None):
+                 hb_timeout: float = 5.0, local_load: Optional[Callable[[], Dict[str, float]]] = None,
+                 secret: Optional[str] = None):
         self.world = world
+        self._secret = secret or plane_secret()
+        self.rejected = 0  # hellos refused (bad secret, rank out of range or already alive)
         self.host = host
         self.port = port or plane_port()
         self.hb_timeout = hb_timeout
@@ -150,9 +178,19 @@ class PlaneServer:
     # ---------------------------------------------------------------- connections
     async def _handle(self, reader: asyncio.StreamReader, writer: asyncio.StreamWriter):
         rank = None
+        st = None
         try:
             hello = await _recv(reader)
-            rank = int(hello["rank"])
+            r = hello.get("rank") if hello.get("op") == "hello" else None
+            ok = (isinstance(r, int) and 0 < r < self.world
+                  and hmac.compare_digest(str(hello.get("secret", "")), self._secret)
+                  and not (r in self.ranks and self.ranks[r].alive))
+            if not ok:
+                self.rejected += 1
+                log.warning("control plane: refused a hello (rank %r)", r)
+                writer.close()
+                return
+            rank = r
             st = RankState(rank, writer)
             st.load = hello.get("load", {})
             self.ranks[rank] = st
@@ -181,7 +219,8 @@ class PlaneServer:
         except (asyncio.IncompleteReadError, ConnectionError, OSError):
             pass
         finally:
-            if rank is not None:
+            # only the connection that owns the rank's live state can declare it lost
+            if rank is not None and self.ranks.get(rank) is st:
                 self._declare_lost(rank, "connection closed")
 
     @property
@@ -310,8 +349,9 @@ class PlaneWorker:
     def __init__(self, rank: int, agents: Sequence[Any], llm: Any = None, host: str = "127.0.0.1",
                  port: Optional[int] = None, hb_interval: float = 0.5,
                  load_fn: Optional[Callable[[], Dict[str, float]]] = None,
-                 agent_factory: Optional[Callable[..., Any]] = None):
+                 agent_factory: Optional[Callable[..., Any]] = None, secret: Optional[str] = None):
         self.rank = rank
+        self._secret = secret or plane_secret()
         self.agents: Dict[str, Any] = {a.id: a for a in agents}
         self.llm = llm
         self.host = host
@@ -337,7 +377,7 @@ class PlaneWorker:
                 if time.monotonic() - t0 > timeout:
                     raise
                 await asyncio.sleep(0.1)
-        await _send(self._writer, {"op": "hello", "rank": self.rank, "load": self._load(),
+        await _send(self._writer, {"op": "hello", "rank": self.rank, "secret": self._secret, "load": self._load(),
                                    "agents": [agent_descriptor(a) for a in self.agents.values()]})
 
     def _load(self) -> Dict[str, float]:

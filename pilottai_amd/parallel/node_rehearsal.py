@@ -21,6 +21,7 @@ import asyncio
 import json
 import multiprocessing as mp
 import os
+import secrets
 import socket
 import sys
 import time
@@ -182,6 +183,8 @@ def run(world: int, scenario: str, per_rank: int = 2, n_tasks: int = 0, latency:
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = free_port()
+    # the control plane's shared secret reaches every spawned rank through the environment
+    os.environ.setdefault("PILOTTAI_PLANE_SECRET", secrets.token_hex(16))
     # balance: one wave — half the pool's worth submitted at rank 0, half forwarded from
     # the last rank, all at once — must land one task per agent
     n_tasks = n_tasks or (world * per_rank * (1 if scenario == "balance" else 5))

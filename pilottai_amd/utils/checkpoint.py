@@ -64,10 +64,12 @@ def save_serve_checkpoint(serve, path) -> str:
     # one is in place; a crash between the two renames leaves it at <path>.bak, which
     # load_checkpoint falls back to
     bak = path.with_name(path.name + ".bak")
-    if bak.exists():
-        shutil.rmtree(bak)
     if path.exists():
+        if bak.exists():
+            shutil.rmtree(bak)  # <path> is a complete checkpoint: the older .bak is redundant
         os.replace(path, bak)
+    # else: an earlier save was interrupted between its renames and <path>.bak is the only good
+    # checkpoint -- keep it until the new one is in place
     os.replace(tmp, path)
     if bak.exists():
         shutil.rmtree(bak)

@@ -177,3 +177,18 @@ def test_parse_json_response_variants():
     assert parse_json_response({"content": '{"c": 3}'}) == {"c": 3}
     with pytest.raises(ValueError):
         parse_json_response("no json here")
+
+
+def test_legacy_raw_key_with_whitespace_bytes(tmp_path):
+    """a 32-byte raw key whose first / last byte is whitespace must stay 32 bytes
+    (the length check runs before any strip); Fernet keys may carry a trailing newline."""
+    import base64
+
+    raw = b"\n" + bytes(range(1, 30)) + b" \t"
+    assert len(raw) == 32
+    (tmp_path / "raw.key").write_bytes(raw)
+    sc = SecureConfig(tmp_path / "raw.key")
+    assert sc.key == base64.urlsafe_b64encode(raw)
+    assert sc.decrypt(sc.encrypt("v")) == "v"
+    (tmp_path / "nl.key").write_bytes(_SPEC_KEY.encode() + b"\n")
+    assert SecureConfig(tmp_path / "nl.key").decrypt(_SPEC_TOKEN) == "hello"

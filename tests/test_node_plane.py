@@ -53,3 +53,47 @@ def test_rank_loss_requeues_and_completes_every_task_exactly_once():
     assert r["completed_ids"] == r["unique_completed"] == 40
     assert r["requeued"] >= 1
     assert r["agents_after"] == 6
+
+
+async def test_plane_refuses_unauthenticated_and_duplicate_hellos():
+    """a hello must carry the job's shared secret and claim a rank that is in range
+    and not already alive; a refused duplicate must not take down the live rank's state."""
+    import asyncio
+
+    from pilottai_amd.parallel.node_plane import PlaneServer, PlaneWorker, _recv, _send
+    from pilottai_amd.parallel.node_rehearsal import free_port
+
+    port = free_port()
+    srv = PlaneServer(3, port=port, hb_timeout=30.0, secret="s3cret")
+    srv._server = await asyncio.start_server(srv._handle, srv.host, srv.port)
+
+    async def raw_hello(**hello):
+        r, w = await asyncio.open_connection("127.0.0.1", port)
+        await _send(w, {"op": "hello", **hello})
+        try:
+            await asyncio.wait_for(_recv(r), 1.0)
+            return "open"
+        except (asyncio.IncompleteReadError, ConnectionError):
+            return "closed"
+        except asyncio.TimeoutError:
+            return "open"
+        finally:
+            w.close()
+
+    assert await raw_hello(rank=1, secret="wrong") == "closed"
+    assert await raw_hello(rank=7, secret="s3cret") == "closed"  # outside the world
+    assert await raw_hello(rank=0, secret="s3cret") == "closed"  # rank 0 is the server
+    good = PlaneWorker(1, [], port=port, secret="s3cret")
+    await good.connect(timeout=5)
+    for _ in range(50):
+        if 1 in srv.ranks and srv.ranks[1].alive:
+            break
+        await asyncio.sleep(0.02)
+    live = srv.ranks[1]
+    assert live.alive
+    assert await raw_hello(rank=1, secret="s3cret") == "closed"  # duplicate of a live rank
+    await asyncio.sleep(0.1)
+    assert srv.ranks[1] is live and live.alive and srv.lost == []
+    assert srv.rejected == 4
+    good._writer.close()
+    srv._server.close()

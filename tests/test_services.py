@@ -275,3 +275,30 @@ async def test_checkpoint_and_resume(tmp_path):
     assert n == 1 and len(s2.completed_tasks) == 1 and len(s2.memory) == 1
     assert (await s2.wait_for(pending.id, timeout=20)).success
     await s2.stop()
+
+
+async def test_checkpoint_save_after_interrupted_swap_keeps_a_good_copy(tmp_path, monkeypatch):
+    """when an earlier save died between its renames (<path> missing, <path>.bak
+    holding the last checkpoint), the next save must not delete .bak before the new
+    checkpoint is in place: a crash in that window still leaves a loadable checkpoint."""
+    import os
+    import shutil
+
+    from pilottai_amd.utils import checkpoint as ck
+
+    s = Serve(agents=[agent("w")], manager_llm=SchemaLLM(), config={"policy": "fixed"})
+    path = tmp_path / "ckpt"
+    s.checkpoint(path)
+    os.replace(path, path.with_name("ckpt.bak"))  # the interrupted state
+    real_replace = os.replace
+
+    def crash_on_publish(src, dst):
+        if str(dst) == str(path):
+            raise OSError("simulated crash before the new checkpoint is published")
+        return real_replace(src, dst)
+    monkeypatch.setattr(ck.os, "replace", crash_on_publish)
+    with pytest.raises(OSError):
+        s.checkpoint(path)
+    monkeypatch.setattr(ck.os, "replace", real_replace)
+    assert ck.load_checkpoint(path)["format_version"] == ck.FORMAT_VERSION  # from .bak
+    shutil.rmtree(path.with_name("ckpt.bak"))

@@ -51,7 +51,8 @@ def _worker(rank, world, port, out_path, model="tiny-gqa4"):
     torch.distributed.destroy_process_group()
     with open(out_path, "w") as f:
         json.dump({"greedy": [o.token_ids for o in greedy], "json": js.text,
-                   "steps": e.stats["steps"]}, f)
+                   "steps": e.stats["steps"], "header": "shm" if e._tp_ring is not None else "gloo",
+                   "published": e._tp_ring.published() if e._tp_ring is not None else 0}, f)
 
 
 @pytest.mark.parametrize("world,model", [(2, "tiny-gqa4"), (4, "tiny-kv8"), (8, "tiny-kv8")])
@@ -65,6 +66,9 @@ def test_tp_engine_matches_tp1(tmp_path, world, model):
     # structured output is valid JSON of the schema under TP sampling
     obj = json.loads(res["json"])
     assert set(obj) == {"success", "quality", "requires_retry"}
+    # the per-step header went through the shared-memory ring (csrc/runtime/shm_ring.cpp):
+    # one record per step plus the stop record
+    assert res["header"] == "shm" and res["published"] == res["steps"] + 1
 
     from pilottai_amd.engine.engine import LLMEngine
 

@@ -1,0 +1,62 @@
+# One parameterised runner for the GPU-box jobs of this repo (replaces the round-1/2
+# one-off tools/gpu_*.sh scripts; they are in git history). Run through gpurun:
+#
+#   gpurun --timeout 900 -- 'bash tools/gpu_tasks.sh OUT_DIR TASK [TASK ...]'
+#
+# Every task writes under gpurun_out/OUT_DIR, runs under its own timeout, and the chain
+# stops at the first failing task (no GPU step runs after a fault, abort or time-out).
+# Knobs (environment): REPS, WORKERS, STEPS, WARMUP, MLIST, BENCH_ARGS.
+#
+# tasks:
+#   tests          python -m pytest tests -m gpu (all GPU tests)
+#   tests:<file>   one GPU test file, e.g. tests:tests/test_prefill_gemm_gpu.py
+#   smoke          __graft_entry__.smoke()
+#   bench          bench.py (driver shape: --gpus 1 --steps $STEPS --warmup $WARMUP)
+#   bench_w        bench.py --workers $WORKERS (one per-rank load of the multi-GPU runs)
+#   prof           rocprofv3 --kernel-trace --stats of bench.py --workers $WORKERS, summarised
+#   splitk         tools/splitk_check.py --reps $REPS (hand-off stress, both consumer modes)
+#   handoff_cost   tools/handoff_cost.py
+#   pfbench        tools/prefill_gemm_bench.py --M $MLIST
+#   anatomy        tools/step_anatomy.py
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" || exit 2
+OUT=gpurun_out/$1
+shift
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+REPS=${REPS:-3000}
+WORKERS=${WORKERS:-64}
+STEPS=${STEPS:-3}
+WARMUP=${WARMUP:-1}
+MLIST=${MLIST:-512,768,1024,1536,2048}
+run() {  # run NAME SECONDS CMD...
+  local name=$1 secs=$2
+  shift 2
+  echo "[gpu_tasks] $name: $*"
+  timeout -k 10 "$secs" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "[gpu_tasks] $name rc=$rc"
+  tail -3 "$OUT/$name.log"
+  return $rc
+}
+for t in "$@"; do
+  case "$t" in
+    tests) run tests 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread || exit $? ;;
+    tests:*) f=${t#tests:}; run "tests_$(basename "$f" .py)" 600 python -u -m pytest "$f" -m gpu -x -v --timeout 120 --timeout-method thread || exit $? ;;
+    smoke) run smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" || exit $? ;;
+    bench) run bench 900 python -u bench.py --gpus 1 --steps "$STEPS" --warmup "$WARMUP" $BENCH_ARGS || exit $? ;;
+    bench_w) run "bench_w$WORKERS" 600 python -u bench.py --workers "$WORKERS" --steps "$STEPS" --warmup "$WARMUP" $BENCH_ARGS || exit $? ;;
+    prof)
+      P=/tmp/pilottai_prof_$WORKERS
+      rm -rf "$P" && mkdir -p "$P"
+      run "prof_w$WORKERS" 600 rocprofv3 --kernel-trace --stats -d "$P" -o w -- python3 bench.py --steps "$STEPS" --warmup "$WARMUP" --workers "$WORKERS" $BENCH_ARGS || exit $?
+      python3 tools/prof_summary.py "$P"/*/*.db "$P"/*.db --after-frac 0.3 --top 40 > "$OUT/w${WORKERS}_kernels.md" 2>&1 || exit $?
+      ;;
+    splitk) run splitk 900 python -u tools/splitk_check.py --reps "$REPS" --out "$OUT/splitk.jsonl" $SPLITK_ARGS || exit $? ;;
+    handoff_cost) run handoff_cost 300 python -u tools/handoff_cost.py --out "$OUT/handoff_cost.jsonl" || exit $? ;;
+    pfbench) run pfbench 900 python -u tools/prefill_gemm_bench.py --M "$MLIST" --out "$OUT/pfbench.jsonl" $PF_ARGS || exit $? ;;
+    anatomy) run anatomy 600 python -u tools/step_anatomy.py $ANATOMY_ARGS || exit $? ;;
+    *) echo "[gpu_tasks] unknown task $t"; exit 2 ;;
+  esac
+done
+echo "[gpu_tasks] done"

@@ -1,45 +1,105 @@
-"""Prefill-shape GEMM survey (Llama-3-8B projections) on hipBLASLt: TFLOP/s per M.
+"""Large-M projection benchmark (Llama-3-8B shapes, prefill-heavy steps): tuned hipBLASLt vs
+the mid path (csrc/ops/gemm_mid.hip) vs the 256 x 256 prefill kernel
+(csrc/ops/gemm_prefill.hip) over its (whole tiles, K-slices) decompositions, each checked
+against fp32. Variants are timed in interleaved rounds in one process (guide §5.4 rule 24).
 
-    python tools/prefill_gemm_bench.py [M list] > out.jsonl
+    python tools/prefill_gemm_bench.py [--M 512,1024,2048] [--rounds 3] [--out file.jsonl]
 
-For each projection and token count M it times F.linear(x, W) with W stored
-[N, K] (the engine's layout) and x @ Wt with W stored [K, N], so the table
-shows both which M the library handles well and whether the layout matters.
+Row: M, shape, us per variant (median of rounds), TFLOP/s of the best, err of pf_default.
+"fused" variants run the engine's epilogue (norm + rope_perm / silu / resid).
 """
+import argparse
 import json
 import os
+import statistics
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 
-shapes = [(6144, 4096, "qkv"), (4096, 4096, "o"), (28672, 4096, "gate_up"), (4096, 14336, "down")]
+from pilottai_amd.engine.gemm_tuning import load_tuned_gemms  # noqa: E402
+from pilottai_amd.ops import kernels  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--M", default="512,768,1024,1536,2048")
+ap.add_argument("--rounds", type=int, default=3)
+ap.add_argument("--iters", type=int, default=10)
+ap.add_argument("--shapes", default="qkv,o,gate_up,down")
+ap.add_argument("--variants", default="")
+ap.add_argument("--out", default="")
+a = ap.parse_args()
+load_tuned_gemms("llama-3-8b", 1)
+SHAPES = {"qkv": (6144, 4096), "o": (4096, 4096), "gate_up": (28672, 4096), "down": (4096, 14336)}
+FUSED = {"qkv": ("rope_perm", True), "o": ("resid", False), "gate_up": ("silu", True), "down": ("resid", False)}
+out_f = open(a.out, "a") if a.out else None
 
 
-def timeit(fn, iters=20):
-    for _ in range(3):
-        fn()
-    torch.cuda.synchronize()
+def timeit(fn, ncopies):
+    for i in range(2):
+        fn(i % ncopies)
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     s.record()
-    for _ in range(iters):
-        fn()
+    for i in range(a.iters):
+        fn(i % ncopies)
     e.record()
-    torch.cuda.synchronize()
-    return s.elapsed_time(e) * 1000 / iters
+    e.synchronize()
+    return s.elapsed_time(e) * 1000 / a.iters
 
 
-Ms = [int(x) for x in (sys.argv[1] if len(sys.argv) > 1 else "128,256,512,768,1024,2048").split(",")]
-for N, K, name in shapes:
-    w = (torch.randn(N, K, device="cuda") * 0.02).to(torch.bfloat16)
-    wt = w.t().contiguous()
-    for M in Ms:
+torch.manual_seed(0)
+for name in a.shapes.split(","):
+    N, K = SHAPES[name]
+    gb = N * K * 2 / 1e9
+    ncopies = 2
+    ws = [(torch.randn(N, K, device="cuda") * 0.02).to(torch.bfloat16) for _ in range(ncopies)]
+    wps = [kernels.pack_decode_weight(w) for w in ws]
+    epi, nrm = FUSED[name]
+    fpack = {"silu": kernels.pack_decode_gate_up, "rope_perm": kernels.pack_decode_qkv_rope}.get(epi)
+    fps = [fpack(w) for w in ws] if fpack else wps
+    for M in [int(v) for v in a.M.split(",")]:
         x = torch.randn(M, K, device="cuda").to(torch.bfloat16)
-        t_nk = timeit(lambda: torch.nn.functional.linear(x, w))
-        t_kn = timeit(lambda: x @ wt)
-        t_sw = timeit(lambda: torch.nn.functional.linear(w, x))  # C^T = W X^T (M <-> N swapped)
-        fl = 2.0 * M * N * K
-        print(json.dumps({"shape": name, "M": M, "us_NK": round(t_nk, 1), "us_KN": round(t_kn, 1),
-                          "us_swap": round(t_sw, 1),
-                          "TF_NK": round(fl / t_nk / 1e6, 1), "TF_KN": round(fl / t_kn / 1e6, 1),
-                          "TF_swap": round(fl / t_sw / 1e6, 1)}), flush=True)
+        y = torch.empty(M, N, dtype=torch.bfloat16, device="cuda")
+        NO = N // 2 if epi == "silu" else N
+        yf = torch.empty(M, NO, dtype=torch.bfloat16, device="cuda")
+        resid = torch.randn(M, N, device="cuda").to(torch.bfloat16) if epi == "resid" else None
+        ss = kernels.row_sumsq(x)
+        full_default, s_default, _ = kernels.require_native().prefill_gemm_plan(M, N, K)
+        variants = {
+            "lib": lambda i: torch.nn.functional.linear(x, ws[i]),
+            "mid": lambda i: kernels.mid_gemm(x, wps[i], "plain", out=y),
+            "pf_default": lambda i: kernels.prefill_gemm(x, wps[i], "plain", out=y),
+            "pf_whole": lambda i: kernels.prefill_gemm(x, wps[i], "plain", out=y, full=-1, splits=1),
+            "pf_s2": lambda i: kernels.prefill_gemm(x, wps[i], "plain", out=y, full=0, splits=2),
+            "pf_s3": lambda i: kernels.prefill_gemm(x, wps[i], "plain", out=y, full=0, splits=3),
+            "pf_s4": lambda i: kernels.prefill_gemm(x, wps[i], "plain", out=y, full=0, splits=4),
+            "pf_fused": lambda i: kernels.prefill_gemm(x, fps[i], epi, out=yf if epi == "silu" else y, resid=resid,
+                                                       norm=nrm, ss_in=ss if nrm else None),
+            "mid_fused": lambda i: kernels.mid_gemm(x, fps[i], epi, out=yf if epi == "silu" else y, resid=resid,
+                                                    norm=nrm, ss_in=ss if nrm else None),
+        }
+        if a.variants:
+            variants = {k: v for k, v in variants.items() if k in a.variants.split(",")}
+        times = {k: [] for k in variants}
+        for _ in range(a.rounds):
+            for k, fn in variants.items():
+                try:
+                    times[k].append(timeit(fn, ncopies))
+                except (ValueError, RuntimeError):
+                    times[k].append(float("nan"))
+        row = {"M": M, "shape": name, "plan": [full_default, s_default]}
+        for k in variants:
+            row[k] = round(statistics.median(times[k]), 1)
+        flop = 2.0 * M * N * K
+        best = min((v, k) for k, v in row.items() if k in variants and v == v)
+        row["best"] = best[1]
+        row["tflops_best"] = round(flop / best[0] / 1e6, 1)
+        row["tflops_lib"] = round(flop / row["lib"] / 1e6, 1) if "lib" in row else None
+        if "pf_default" in row:
+            row["tflops_pf"] = round(flop / row["pf_default"] / 1e6, 1)
+            yy = kernels.prefill_gemm(x, wps[0], "plain", out=y)
+            ref = x.float() @ ws[0].float().T
+            row["err_pf"] = float(((yy.float() - ref).abs().max() / ref.abs().max()))
+        print(json.dumps(row), flush=True)
+        if out_f:
+            out_f.write(json.dumps(row) + "\n")
+            out_f.flush()
