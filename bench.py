@@ -87,6 +87,9 @@ def parse():
     ap.add_argument("--memory-rows", type=int, default=0,
                     help="semantic memory on the engine's GPU with this many rows; every agent step looks it up")
     ap.add_argument("--memory-top-k", type=int, default=3)
+    ap.add_argument("--embedder", default="hashing", choices=["hashing", "engine"],
+                    help="memory text encoder: feature hashing, or the serving model itself (embedding "
+                         "requests in the engine's continuous batch, SURVEY N11)")
     ap.add_argument("--share-gpu", action="store_true",
                     help="rehearsal: every rank on GPU 0 (use with PILOTTAI_DIST_BACKEND=gloo)")
     return ap.parse_args()
@@ -130,6 +133,12 @@ async def run_rank(a, rank: int, world: int, device):
                                  **({"att_wide_min_tokens": a.att_wide_min_tokens}
                                     if a.att_wide_min_tokens is not None else {})), device=device)
     register_engine(eng.model_cfg.name, eng)
+    if memory is not None and a.embedder == "engine":
+        # queries and write-backs are encoded by the serving model: mean-pooled final hidden
+        # states of embedding requests inside the engine's continuous batch
+        from pilottai_amd.memory.embedding import EngineEmbedder
+
+        memory.embedder = EngineEmbedder(eng, dim=memory.index.dim, pool="engine", max_tokens=256)
     eng.start()
     llm = LocalLLM(LLMConfig(model_name=eng.model_cfg.name, temperature=a.temperature, max_tokens=1024,
                              retry_attempts=1), engine=eng)

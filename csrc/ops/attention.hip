@@ -34,6 +34,8 @@
 // shape-stable under hipGraph capture.
 #include "common.h"
 
+#include <algorithm>
+
 namespace pa {
 
 constexpr int ATT_HD = 128;
@@ -606,7 +608,12 @@ constexpr int ATT_LDS_BYTES = ATT_LDS_BYTES0 > PW_NBUF * PW_TILE ? ATT_LDS_BYTES
 // One launch serves a whole ragged step: items (seq, q_begin, nq | part<<8 |
 // nparts<<20, partial slot) are strided over the grid, so the shape-stable
 // (graph-captured) grid can be sized to the chip rather than to the worst case.
-template <int G>
+// MODE 0: every item of the step (one launch); MODE 1: the decode / short items only,
+// items [n_items[1], n_items[0]); MODE 2: the prefill (q-split) items only, items
+// [0, n_items[1]) -- the scheduler lists them first. Split into two launches, each kernel
+// gets the register budget of its own paths (the mixed kernel carries 254 VGPRs, 2 waves
+// per SIMD, for the wide prefill path's sake).
+template <int G, int MODE>
 __global__ __launch_bounds__(256, 2) void paged_attn_kernel(
     bf16* __restrict__ out, float* __restrict__ part_o, float* __restrict__ part_ml,
     int* __restrict__ counters, const bf16* __restrict__ q, const bf16* __restrict__ k_cache,
@@ -621,16 +628,18 @@ __global__ __launch_bounds__(256, 2) void paged_attn_kernel(
   // memory round trip less before the K/V stream starts (decode steps with few rows are
   // latency-bound). In bounds: the host sizes the grid to gridDim.x <= max_items, the
   // length of `items`.
-  int4 it_next = items[blockIdx.x];
-  const int n = n_items[0];
-  if ((int)blockIdx.x >= n) {
+  const int i0 = MODE == 1 ? n_items[1] : 0;
+  const int n = MODE == 2 ? n_items[1] : n_items[0];
+  int4 it_next = items[min((int)blockIdx.x + i0, max(n - 1, 0))];
+  if (MODE == 2 && (int)blockIdx.x + i0 >= n) return;
+  if ((int)blockIdx.x + i0 >= n) {
     // A workgroup without an item (the grid is sized for the bucket's largest item
     // list; a decode step of 8 rows uses ~1/70 of it): read a slice of the next
     // projection's weights so they are in the Infinity Cache when it starts (the
     // attention K/V stream leaves most of HBM's bandwidth idle at small batch).
     if (pf_lines > 0) {
-      const long long idle = (long long)(gridDim.x - n) * gridDim.y;
-      const long long me = (long long)blockIdx.y * (gridDim.x - n) + (blockIdx.x - n);
+      const long long idle = (long long)(gridDim.x - (n - i0)) * gridDim.y;
+      const long long me = (long long)blockIdx.y * (gridDim.x - (n - i0)) + (blockIdx.x - (n - i0));
       const long long per = (pf_lines + idle - 1) / idle;
       const long long l1 = min(pf_lines, (me + 1) * per);
       u32x4 acc = {0u, 0u, 0u, 0u};
@@ -642,17 +651,17 @@ __global__ __launch_bounds__(256, 2) void paged_attn_kernel(
   }
   const int psz = part_size ? part_size[0] : ATT_PART;  // decode partition (keys), per step
   const int kvh = blockIdx.y;
-  for (int item = blockIdx.x; item < n; item += gridDim.x) {
+  for (int item = blockIdx.x + i0; item < n; item += gridDim.x) {
     const int4 it = it_next;
     if (item + (int)gridDim.x < n) it_next = items[item + gridDim.x];
     const int nq = it.z & 0xff;
-    if (nq <= TPW)
+    if (MODE != 2 && nq <= TPW)
       decode_item<G>(it, smem, out, part_o, part_ml, counters, q, k_cache, v_cache, q_start, q_len, ctx_len,
                      block_table, max_blocks, H, KV, kvh, scale_log2, psz, acq);
-    else if (nq <= 32 / G)
+    else if (MODE != 1 && nq <= 32 / G)
       prefill_item<G>(it, smem, out, q, k_cache, v_cache, q_start, q_len, ctx_len, block_table,
                       max_blocks, H, KV, kvh, scale_log2);
-    else
+    else if (MODE != 1)
       prefill_item_wg<G>(it, smem, out, q, k_cache, v_cache, q_start, q_len, ctx_len, block_table,
                          max_blocks, H, KV, kvh, scale_log2);
     __syncthreads();  // LDS reuse by the next item
@@ -661,9 +670,12 @@ __global__ __launch_bounds__(256, 2) void paged_attn_kernel(
 
 }  // namespace pa
 
+// split_prefill > 0: two launches -- the prefill items [0, n_items[1]) on their own kernel
+// with a grid of split_prefill workgroups per KV head, then the decode items.
 extern "C" int pa_paged_attention(void* out, float* part_o, float* part_ml, const void* q,
                                   const void* k_cache, const void* v_cache, const int* items,
-                                  const int* n_items, int max_items, const int* part_size, int* counters,
+                                  const int* n_items, int max_items, int split_prefill, const int* part_size,
+                                  int* counters,
                                   const int* q_start,
                                   const int* q_len, const int* ctx_len, const int* block_table,
                                   int max_blocks, int H, int KV, float scale_log2,
@@ -676,23 +688,30 @@ extern "C" int pa_paged_attention(void* out, float* part_o, float* part_ml, cons
   // items are strided over the grid: ~8 resident workgroups per CU over all KV heads
   const int gx = max_items < 1 ? 1 : (max_items < 2048 / KV ? max_items : (2048 / KV > 0 ? 2048 / KV : 1));
   dim3 grid(gx, KV);
-#define PA_ATT(GG)                                                                          \
-  do {                                                                                      \
-    static bool attr_##GG = false;                                                          \
-    if (!attr_##GG) {                                                                       \
-      (void)hipFuncSetAttribute((const void*)pa::paged_attn_kernel<GG>,                           \
-                          hipFuncAttributeMaxDynamicSharedMemorySize, pa::ATT_LDS_BYTES);   \
-      attr_##GG = true;                                                                     \
-    }                                                                                       \
-    if (max_items > 0)                                                                      \
-      hipLaunchKernelGGL(pa::paged_attn_kernel<GG>, grid, dim3(256), pa::ATT_LDS_BYTES, st, \
-                         (pa::bf16*)out,                                                    \
-                         part_o, part_ml, counters, (const pa::bf16*)q,                      \
-                         (const pa::bf16*)k_cache, (const pa::bf16*)v_cache,                \
-                         (const int4*)items, n_items, part_size, q_start, q_len, ctx_len,    \
-                         block_table,                                                       \
-                         max_blocks, H, KV, scale_log2, (const pa::u32x4*)pf, pf_lines,     \
-                         (pa::u32x4*)pf_sink, pa::g_handoff_acquire);                        \
+#define PA_ATT1(GG, MD, GRID, PFP, PFL)                                                         \
+  do {                                                                                          \
+    static bool attr_##GG##_##MD = false;                                                       \
+    if (!attr_##GG##_##MD) {                                                                    \
+      (void)hipFuncSetAttribute((const void*)pa::paged_attn_kernel<GG, MD>,                     \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, pa::ATT_LDS_BYTES); \
+      attr_##GG##_##MD = true;                                                                  \
+    }                                                                                           \
+    hipLaunchKernelGGL((pa::paged_attn_kernel<GG, MD>), GRID, dim3(256), pa::ATT_LDS_BYTES, st,  \
+                       (pa::bf16*)out, part_o, part_ml, counters, (const pa::bf16*)q,          \
+                       (const pa::bf16*)k_cache, (const pa::bf16*)v_cache, (const int4*)items, \
+                       n_items, part_size, q_start, q_len, ctx_len, block_table, max_blocks, H, \
+                       KV, scale_log2, (const pa::u32x4*)PFP, PFL, (pa::u32x4*)pf_sink,        \
+                       pa::g_handoff_attn);                                                  \
+  } while (0)
+#define PA_ATT(GG)                                                                              \
+  do {                                                                                          \
+    if (max_items <= 0) break;                                                                  \
+    if (split_prefill > 0) {                                                                    \
+      PA_ATT1(GG, 2, dim3(std::min(split_prefill, max_items), KV), nullptr, 0LL);              \
+      PA_ATT1(GG, 1, grid, pf, pf_lines);                                                       \
+    } else {                                                                                    \
+      PA_ATT1(GG, 0, grid, pf, pf_lines);                                                       \
+    }                                                                                           \
   } while (0)
   switch (G) {
     case 1: PA_ATT(1); break;
@@ -703,5 +722,6 @@ extern "C" int pa_paged_attention(void* out, float* part_o, float* part_ml, cons
     default: return -2;
   }
 #undef PA_ATT
+#undef PA_ATT1
   return (int)hipGetLastError();
 }

@@ -16,7 +16,7 @@ int pa_rope_cache(void* q_out, void* k_cache, void* v_cache, const void* qkv, co
 int pa_silu_mul(void* out, const void* in, int T, int F, hipStream_t st);
 int pa_paged_attention(void* out, float* part_o, float* part_ml, const void* q, const void* k_cache,
                        const void* v_cache, const int* items, const int* n_items, int max_items,
-                       const int* part_size, int* counters, const int* q_start,
+                       int split_prefill, const int* part_size, int* counters, const int* q_start,
                        const int* q_len, const int* ctx_len, const int* block_table,
                        int max_blocks, int H, int KV, float scale_log2, const void* pf, long long pf_bytes,
                        void* pf_sink, hipStream_t st);
@@ -33,6 +33,7 @@ void pa_skinny_set_variant(int v);
 int pa_skinny_gemm(void* y, const void* x, const void* w, int M, int N, int K, int ldy, hipStream_t st);
 void pa_decode_set_variant(int v);
 void pa_handoff_set_acquire(int v);
+void pa_handoff_set_modes(int gemm, int attn);
 int pa_decode_gemm(void* y, const void* x, const void* wp, const void* resid, int M, int N, int K,
                    int ldx, int ldy, int ldr, int epi, int norm, float eps, int nt, int waves, int splits,
                    float* ws, long long ws_floats, int* counters, int n_counters, hipStream_t st);
@@ -52,6 +53,7 @@ int pa_mid_gemm(void* y, const void* x, const void* wp, const void* resid, float
                 const float* cos_sin, int H, int KV, hipStream_t st);
 int pa_row_sumsq(float* out, const void* x, int M, int K, int ldx, hipStream_t st);
 void pa_prefill_gemm_plan(int M, int N, int K, int* full, int* S);
+void pa_prefill_set_variant(int v);
 long long pa_prefill_gemm_ws_floats(int M, int N, int full, int S);
 int pa_prefill_gemm(void* y, const void* x, const void* wp, const void* resid, float* ws, long long ws_floats,
                     int* counters, int n_counters, int M, int N, int K, int ldx, int ldy, int ldr, int epi,
@@ -164,7 +166,7 @@ void paged_attention(at::Tensor out, at::Tensor part_o, at::Tensor part_ml, at::
                      at::Tensor counters, at::Tensor q_start, at::Tensor q_len,
                      at::Tensor ctx_len, at::Tensor block_table, double scale,
                      c10::optional<at::Tensor> part_size, c10::optional<at::Tensor> prefetch,
-                     c10::optional<at::Tensor> prefetch_sink) {
+                     c10::optional<at::Tensor> prefetch_sink, int64_t split_prefill) {
   for (auto* t : {&out, &part_o, &part_ml, &q, &k_cache, &v_cache, &items, &n_items, &counters,
                   &q_start, &q_len, &ctx_len, &block_table})
     check_gpu(*t, "paged_attention arg");
@@ -202,6 +204,7 @@ void paged_attention(at::Tensor out, at::Tensor part_o, at::Tensor part_ml, at::
   check_rc(pa_paged_attention(out.data_ptr(), part_o.data_ptr<float>(), part_ml.data_ptr<float>(),
                               q.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(),
                               items.data_ptr<int>(), n_items.data_ptr<int>(), max_items,
+                              n_items.numel() >= 2 ? (int)split_prefill : 0,
                               part_size.has_value() ? part_size->data_ptr<int>() : nullptr,
                               counters.data_ptr<int>(),
                               q_start.data_ptr<int>(), q_len.data_ptr<int>(),
@@ -696,7 +699,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("skinny_set_variant", [](int v) { pa_skinny_set_variant(v); });
   m.def("decode_set_variant", [](int v) { pa_decode_set_variant(v); });
   m.def("handoff_set_acquire", [](int v) { pa_handoff_set_acquire(v); },
-        "consumer mode of the in-launch split-K / partition hand-offs: 1 = agent acquire (default)");
+        "protocol of every in-launch hand-off (diagnostics): 0 sc1 only, 1 acquire, 2 release + acquire");
+  m.def("handoff_set_modes", [](int gemm, int attn) { pa_handoff_set_modes(gemm, attn); },
+        "hand-off protocols of the GEMM split-K slabs and of the attention merge (defaults 2, 1)");
   m.def("decode_gemm", &decode_gemm, py::arg("y"), py::arg("x"), py::arg("wp"), py::arg("resid") = py::none(),
         py::arg("epi") = 0, py::arg("norm") = false, py::arg("eps") = 1e-5, py::arg("nt") = 0,
         py::arg("waves") = 0, py::arg("splits") = 0, py::arg("ws") = py::none(), py::arg("counters") = py::none());
@@ -722,13 +727,15 @@ PYBIND11_MODULE(_C, m) {
         py::arg("q_out"), py::arg("k_cache"), py::arg("v_cache"), py::arg("positions"), py::arg("slots"),
         py::arg("cos_sin"), py::arg("H"), py::arg("KV"), py::arg("ws"), py::arg("counters"), py::arg("full") = -1,
         py::arg("splits") = 0);
+  m.def("prefill_set_variant", [](int v) { pa_prefill_set_variant(v); });
   m.def("prefill_gemm_plan", &prefill_gemm_plan, "default (full tiles, splits, workspace floats) of prefill_gemm");
   m.def("row_sumsq", &row_sumsq, py::arg("out"), py::arg("x"));
   m.def("mid_gemm_plan", &mid_gemm_plan, "default (fm, fn, splits, workspace floats) of mid_gemm");
   m.def("paged_attention", &paged_attention, py::arg("out"), py::arg("part_o"), py::arg("part_ml"), py::arg("q"),
         py::arg("k_cache"), py::arg("v_cache"), py::arg("items"), py::arg("n_items"), py::arg("counters"),
         py::arg("q_start"), py::arg("q_len"), py::arg("ctx_len"), py::arg("block_table"), py::arg("scale"),
-        py::arg("part_size") = py::none(), py::arg("prefetch") = py::none(), py::arg("prefetch_sink") = py::none());
+        py::arg("part_size") = py::none(), py::arg("prefetch") = py::none(), py::arg("prefetch_sink") = py::none(),
+        py::arg("split_prefill") = 0);
   m.def("sample_workspace_floats", &sample_workspace_floats);
   m.def("sample", &sample, py::arg("out_tokens"), py::arg("out_keys"), py::arg("workspace"),
         py::arg("logits"), py::arg("vocab_offset"), py::arg("temperature"), py::arg("mask_class"),

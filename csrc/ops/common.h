@@ -56,6 +56,8 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
 //   producer  every wave stores its partial write-through (sc1 buffer stores), then
 //             runs asm `s_waitcnt vmcnt(0)` (EVERY storing wave drains: Pitfall 14),
 //             then calls handoff_last();
+//   release   (acquire >= 2, the default) one lane runs an agent-scope release
+//             (buffer_wbl2 sc1) and drains it, behind the workgroup barrier;
 //   ticket    one lane takes a relaxed agent-scope ticket after a workgroup barrier;
 //   consumer  the workgroup that drew ticket n-1 resets the counter for the next launch and
 //             runs ONE agent-scope acquire (`buffer_inv sc1`, completion awaited by an asm
@@ -63,15 +65,15 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
 // The acquire makes the hand-off placement-independent for ANY number of workgroups per CU
 // (the sc1-loads-only form is validated only at one workgroup per CU: MI355X_MICROARCH.md
 // "Valid forms", condition (4)); the readers may then use plain or sc1 loads.
-// `acquire` = 0 keeps the old sc1-only consumer, 2 adds a producer-side agent release
-// (diagnostics: tools/splitk_check.py).
+// `acquire` = 0 keeps the old sc1-only consumer and 1 the acquire without the release
+// (diagnostics: tools/splitk_check.py, tools/handoff_cost.py).
 // Every thread of the workgroup must call it; it returns true in all of them for the last
 // arriver. `lflag` is an int in the kernel's single LDS array.
 typedef __attribute__((address_space(1))) int handoff_gi32;
 __device__ __forceinline__ bool handoff_last(int* counter, int n, int* lflag, int acquire) {
   __syncthreads();
   if (threadIdx.x == 0) {
-    if (acquire >= 2) {  // diagnostic: an agent-scope release (L2 write-back) on top of the sc1 stores
+    if (acquire >= 2) {  // agent-scope release (L2 write-back) on top of the sc1 stores
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
@@ -90,8 +92,10 @@ __device__ __forceinline__ bool handoff_last(int* counter, int n, int* lflag, in
   return *lflag != 0;
 }
 
-// host-side hand-off mode passed to every kernel with an in-launch hand-off (default 1)
+// host-side hand-off modes passed to the kernels with an in-launch hand-off: the GEMM
+// split-K slabs (decode / wide / mid / prefill) and the attention partition merge
 extern int g_handoff_acquire;
+extern int g_handoff_attn;
 
 // Cheap stateless 32-bit hash (splitmix-style finaliser) used as a counter-based
 // RNG for sampling: u = hash(seed, row, col) -> uniform in (0, 1).

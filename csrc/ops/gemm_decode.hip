@@ -303,9 +303,17 @@ __global__ __launch_bounds__(WAVES * 64) void decode_gemm_kernel(const DgArgs A)
 // projection at M = 8-32, 8-token decode steps 3.49 -> 3.33 ms: profiles/r2_decode_nt_ab.jsonl)
 static int g_dg_variant = 1;
 
-// consumer side of every in-launch hand-off (decode / wide / mid GEMM split-K, attention
-// partition merge): 1 = agent-scope acquire by the last arriver (common.h handoff_last)
-int g_handoff_acquire = 1;
+// protocol of the in-launch hand-offs, common.h handoff_last (tools/splitk_check.py: fresh
+// inputs, NaN-poisoned slabs and outputs; tools/handoff_cost.py; profiles/r3_splitk_handoff.md):
+//   GEMM split-K slabs (decode / wide / mid / prefill): 2 = producer agent release + last-arriver
+//     agent acquire. Decode qkv_rope at M = 9 with 3 K-slices mismatched in 46 of 3,000 runs
+//     with the round-2 sc1-only form (mode 0) and in 4 of 10,000 with the acquire alone
+//     (mode 1); none with mode 2 (+2-3 us per split launch).
+//   attention partition merge: 1 = last-arriver agent acquire (0 mismatches in 3,000 poisoned
+//     runs in every mode; the release costs +77 us at 64 rows x 1,000 keys there: it writes
+//     back every dirty L2 line of the XCD, and this launch leaves many).
+int g_handoff_acquire = 2;
+int g_handoff_attn = 1;
 
 template <int MT, int NT, int WAVES, int EPI, bool NORM>
 static int launch_dg(const DgArgs& a, hipStream_t st) {
@@ -412,7 +420,11 @@ static int dispatch(DgArgs a, int epi, int norm, int nt, int waves, int splits, 
 // epi: 0 plain, 1 silu(gate)*up over interleaved tile pairs, 2 residual add.
 // nt/waves/splits <= 0 pick the defaults; ws/counters: split-K slabs and zeroed tickets.
 extern "C" void pa_decode_set_variant(int v) { pa::g_dg_variant = v; }
-extern "C" void pa_handoff_set_acquire(int v) { pa::g_handoff_acquire = v; }
+extern "C" void pa_handoff_set_acquire(int v) { pa::g_handoff_acquire = pa::g_handoff_attn = v; }
+extern "C" void pa_handoff_set_modes(int gemm, int attn) {
+  pa::g_handoff_acquire = gemm;
+  pa::g_handoff_attn = attn;
+}
 
 extern "C" int pa_decode_gemm(void* y, const void* x, const void* wp, const void* resid, int M, int N, int K,
                               int ldx, int ldy, int ldr, int epi, int norm, float eps, int nt, int waves,

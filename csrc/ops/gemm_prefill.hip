@@ -98,7 +98,7 @@ constexpr int SLAB = 256 * 256;       // floats per split slab
 template <int V>
 using ic = std::integral_constant<int, V>;
 
-template <int EPI, bool NORM>
+template <int EPI, bool NORM, bool RA>
 __global__ __launch_bounds__(512) void prefill_gemm_kernel(const Args A) {
   // the only LDS object (guide §5 trap 4a): two tile buffers, reused by the hand-off flag
   __shared__ __attribute__((aligned(1024))) char smem[2 * BUF];
@@ -228,7 +228,82 @@ __global__ __launch_bounds__(512) void prefill_gemm_kernel(const Args A) {
     mma(ic<1>{}, af, bk1);
   };
 
-  if (nk >= 2) {
+  if constexpr (RA) {
+    // Read-ahead schedule: each phase's window (between two barriers) issues the LDS reads
+    // of the NEXT phase into the other register set, one piece of tile i + 2 (into the
+    // current buffer: its region's last reads completed before the window's barrier), then
+    // the phase's 16 MFMAs on registers read one window earlier; every wave retires its
+    // LDS reads (lgkmcnt(0)) and the counted vmcnt before the barrier. Pieces stay in flight
+    // ~5 phases (vmcnt(10): 5 pieces x 2 LDS-DMA loads per lane).
+    //   window  reads (for next phase)        MFMA          issue           wait
+    //   ph0     B-k1(i) -> bk1, x-lo k1 -> afB  afA x bk0    B-k0(i + 2)     10
+    //   ph1     x-hi k0 -> afA                  afB x bk1    x-lo(i + 2)     -
+    //   ph2     x-hi k1 -> afB                  afA x bk0    B-k1(i + 2)     10
+    //   ph3     B-k0(i+1) -> bk0, x-lo(i+1) -> afA  afB x bk1  x-hi(i + 2)   10
+    bf16x8 afA[4], afB[4];
+    auto body = [&](int i, auto iss, auto nxt, auto w0, auto w2, auto w3) {
+      char* cur = (i & 1) ? b1 : b0;
+      char* oth = (i & 1) ? b0 : b1;
+      // ph0
+      read_b(cur, 1, bk1);
+      read_a(cur, 0, 1, afB);
+      if constexpr (decltype(iss)::value) issue_b(0, kt0 + i + 2, cur);
+      mma(ic<0>{}, afA, bk0);
+      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this window's LDS reads are done
+      if constexpr (decltype(w0)::value >= 0) wait_vm<decltype(w0)::value>();
+      raw_barrier();
+      // ph1
+      read_a(cur, 1, 0, afA);
+      if constexpr (decltype(iss)::value) issue_a(0, kt0 + i + 2, cur);
+      mma(ic<0>{}, afB, bk1);
+      __builtin_amdgcn_s_waitcnt(0xC07F);
+      raw_barrier();
+      // ph2
+      read_a(cur, 1, 1, afB);
+      if constexpr (decltype(iss)::value) issue_b(1, kt0 + i + 2, cur);
+      mma(ic<1>{}, afA, bk0);
+      __builtin_amdgcn_s_waitcnt(0xC07F);
+      if constexpr (decltype(w2)::value >= 0) wait_vm<decltype(w2)::value>();
+      raw_barrier();
+      // ph3
+      if constexpr (decltype(nxt)::value) {
+        read_b(oth, 0, bk0);
+        read_a(oth, 0, 0, afA);
+      }
+      if constexpr (decltype(iss)::value) issue_a(1, kt0 + i + 2, cur);
+      mma(ic<1>{}, afB, bk1);
+      __builtin_amdgcn_s_waitcnt(0xC07F);
+      if constexpr (decltype(w3)::value >= 0) wait_vm<decltype(w3)::value>();
+      raw_barrier();
+    };
+    // prologue: the pieces of tiles 0 and 1 in steady-state order, then phase 0's registers
+    issue_b(0, kt0, b0);
+    issue_a(0, kt0, b0);
+    issue_b(1, kt0, b0);
+    issue_a(1, kt0, b0);
+    if (nk >= 2) {
+      issue_b(0, kt0 + 1, b1);
+      issue_a(0, kt0 + 1, b1);
+      issue_b(1, kt0 + 1, b1);
+      issue_a(1, kt0 + 1, b1);
+      wait_vm<10>();  // tile 0's B-k0, x-lo and B-k1 landed
+    } else {
+      wait_vm<2>();
+    }
+    raw_barrier();
+    read_b(b0, 0, bk0);
+    read_a(b0, 0, 0, afA);
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // no LDS read pending at the loop head (else hipcc waits
+                                         // lgkmcnt(0) before phase 0's MFMAs on every iteration)
+    if (nk >= 2) {
+      int i = 0;
+      for (; i + 2 < nk; ++i) body(i, ic<1>{}, ic<1>{}, ic<10>{}, ic<10>{}, ic<10>{});
+      body(i, ic<0>{}, ic<1>{}, ic<8>{}, ic<4>{}, ic<2>{});       // tile nk - 2: nothing left to issue
+      body(i + 1, ic<0>{}, ic<0>{}, ic<0>{}, ic<-1>{}, ic<-1>{});  // tile nk - 1
+    } else {
+      body(0, ic<0>{}, ic<0>{}, ic<0>{}, ic<-1>{}, ic<-1>{});
+    }
+  } else if (nk >= 2) {
     issue_b(0, kt0, b0);
     issue_a(0, kt0, b0);
     issue_b(1, kt0, b0);
@@ -315,6 +390,9 @@ __global__ __launch_bounds__(512) void prefill_gemm_kernel(const Args A) {
   }
 }
 
+// main-loop schedule: 1 = read-ahead (default), 0 = reads in the phase they feed
+static int g_pf_variant = 1;
+
 // Default decomposition: whole tiles while they fill complete rounds of 256 CUs; the
 // remainder is split over K so that the last round is (nearly) full.
 static void plan_default(int M, int N, int K, int& full, int& S) {
@@ -332,6 +410,8 @@ static void plan_default(int M, int N, int K, int& full, int& S) {
 
 }  // namespace pf
 }  // namespace pa
+
+extern "C" void pa_prefill_set_variant(int v) { pa::pf::g_pf_variant = v; }
 
 extern "C" void pa_prefill_gemm_plan(int M, int N, int K, int* full, int* S) {
   pa::pf::plan_default(M, N, K, *full, *S);
@@ -379,7 +459,11 @@ extern "C" int pa_prefill_gemm(void* y, const void* x, const void* wp, const voi
          (pa::bf16*)q_out, (pa::bf16*)k_cache, (pa::bf16*)v_cache, positions, slots, cos_sin, H, KV,
          pa::g_handoff_acquire};
   const int grid = full + (tiles - full) * S;
-#define PA_PF(E, NRM) hipLaunchKernelGGL((prefill_gemm_kernel<E, NRM>), dim3(grid), dim3(512), 0, st, a)
+#define PA_PF(E, NRM)                                                                                \
+  do {                                                                                               \
+    if (g_pf_variant == 1) hipLaunchKernelGGL((prefill_gemm_kernel<E, NRM, true>), dim3(grid), dim3(512), 0, st, a); \
+    else hipLaunchKernelGGL((prefill_gemm_kernel<E, NRM, false>), dim3(grid), dim3(512), 0, st, a);                 \
+  } while (0)
   switch (epi) {
     case EP_PLAIN:
       if (norm) PA_PF(EP_PLAIN, true); else PA_PF(EP_PLAIN, false);

@@ -54,3 +54,12 @@ class ControlPolicy:
 
 
 DEFAULT_POLICY = ControlPolicy()
+
+
+# The agent a task is bound to (speculatively reserved or executing), visible to the
+# manager-side LLM calls the orchestrator makes for that task (its analysis and its
+# evaluation): the node plane's DistributedLLM sends them to that agent's rank, where the
+# task's prompt prefix is already in the engine's prefix cache.
+from contextvars import ContextVar  # noqa: E402
+
+TASK_AGENT: ContextVar = ContextVar("pilottai_task_agent", default=None)

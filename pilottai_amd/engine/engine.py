@@ -269,6 +269,7 @@ class LLMEngine:
         self._aborts: "queue.SimpleQueue" = queue.SimpleQueue()
         self._wake = threading.Event()
         self._reqs: Dict[int, _Request] = {}
+        self._pending_out: list = []  # finished outputs delivered during the next step's GPU time
         self._next_id = 1
         self._id_lock = threading.Lock()
         self._thread: Optional[threading.Thread] = None
@@ -669,6 +670,7 @@ class LLMEngine:
         """Run one engine step. Returns False when there was nothing to run."""
         self._drain_inbox()
         if not self.sched.has_work():
+            self._flush_deliveries()
             return False
         L = self.L
         t0 = time.perf_counter()
@@ -676,6 +678,7 @@ class LLMEngine:
             T = self.sched.schedule(self._host_ptr)
         t_sched = time.perf_counter()
         if T == 0:
+            self._flush_deliveries()
             if self.sched.num_running == 0 and self.sched.num_waiting > 0:
                 raise RuntimeError("KV cache too small for the head request")
             return False
@@ -701,6 +704,10 @@ class LLMEngine:
             self._sampled_host[:nsamp].copy_(self._sampled_dev[:nsamp], non_blocking=self.on_gpu)
         self._car_fetch()
         t_launch = time.perf_counter()
+        # the previous step's finished requests are handed to their callers while this step
+        # runs on the GPU (host/device overlap): delivery needs nothing from it
+        self._flush_deliveries()
+        t_flush = time.perf_counter()
         if self.on_gpu:
             torch.cuda.current_stream().synchronize()
         self._car_check()
@@ -721,12 +728,18 @@ class LLMEngine:
         bh = self.bucket_hist.setdefault(bucket, [0, 0.0])
         bh[0] += 1
         bh[1] += dt
-        t_deliver = time.perf_counter()
-        for o in outs:
-            self._deliver(o)
-        st["host_commit_s"] += t_deliver - t_sync
-        st["host_deliver_s"] += time.perf_counter() - t_deliver
+        st["host_commit_s"] += time.perf_counter() - t_sync
+        st["host_deliver_s"] += t_flush - t_launch  # overlapped with the device
+        self._pending_out.extend(outs)
+        if not self.sched.has_work():
+            self._flush_deliveries()  # nothing to overlap with: deliver now
         return True
+
+    def _flush_deliveries(self):
+        if self._pending_out:
+            outs, self._pending_out = self._pending_out, []
+            for o in outs:
+                self._deliver(o)
 
     def _loop(self):
         if self.on_gpu:

@@ -75,8 +75,11 @@ class EngineEmbedder:
         self.dim = dim
         d = engine.model_cfg.hidden_size
         g = torch.Generator().manual_seed(seed)
-        q, _ = torch.linalg.qr(torch.randn(d, max(d, dim), generator=g))
-        self.proj = q[:, :dim].contiguous().to(engine.device, torch.float32)
+        if d >= dim:  # [d, dim] with orthonormal columns
+            q, _ = torch.linalg.qr(torch.randn(d, dim, generator=g))
+        else:  # a model narrower than the index (test shapes): orthonormal rows
+            q = torch.linalg.qr(torch.randn(dim, d, generator=g))[0].T
+        self.proj = q.contiguous().to(engine.device, torch.float32)
         self.pool = pool if (pool == "engine" or getattr(engine.model.tp, "size", 1) == 1) else "tokens"
         self.batch_size = batch_size
         self.max_tokens = max_tokens

@@ -97,10 +97,19 @@ class EnhancedMemory:
         if any(not t for t in texts):
             raise ValueError("Text cannot be empty")
         async with self._semantic_lock:
-            return self._store_items(items) if n else []
+            if not n:
+                return []
+            if getattr(self.index.device, "type", "cpu") == "cuda":
+                # the embedder may be the serving engine itself (EngineEmbedder): embed in a
+                # worker thread so the event loop keeps serving the agents meanwhile
+                vecs = await asyncio.get_running_loop().run_in_executor(
+                    None, self.embedder, [it.text for it in items])
+                return self._store_items(items, vecs)
+            return self._store_items(items)
 
-    def _store_items(self, items: List[MemoryItem]) -> List[int]:
-        vecs = self.embedder([it.text for it in items])
+    def _store_items(self, items: List[MemoryItem], vecs=None) -> List[int]:
+        if vecs is None:
+            vecs = self.embedder([it.text for it in items])
         rows = self.index.add(vecs, [it.priority for it in items], [it.tags for it in items],
                               [it.expires_at.timestamp() if it.expires_at else None for it in items])
         for r, it in zip(rows, items):

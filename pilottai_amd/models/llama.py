@@ -138,8 +138,10 @@ class LlamaModel:
     MID_MAX_T = 256
     # steps above MID_MAX_T and up to this many tokens run the same fused packed-weight layer
     # with the 256 x 256 prefill kernels (csrc/ops/gemm_prefill.hip) for the projections that
-    # PF_CFG assigns to them; larger steps (and PREFILL_MAX_T = 0) take the library path
-    PREFILL_MAX_T = 1 << 30
+    # PF_CFG assigns to them; larger steps (and PREFILL_MAX_T = 0, the default while the
+    # library GEMMs + elementwise kernels are faster: profiles/r3_prefill_gemm_bench.jsonl)
+    # take the library path. EngineConfig.prefill_max_t / bench.py --prefill-max-t turn it on.
+    PREFILL_MAX_T = 0
     # per projection: (largest M, path, config); the first row whose M covers the step is used.
     # "pf": prefill kernel (full = whole tiles, -1 = the kernel's plan; splits of the rest),
     # "mid": mid kernel (fm, fn, splits as MID_CFG)

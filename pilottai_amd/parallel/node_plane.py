@@ -38,6 +38,7 @@ from datetime import datetime
 from typing import Any, Callable, Dict, List, Optional, Sequence
 
 from ..core.errors import AgentLostError
+from ..core.policy import TASK_AGENT
 from ..core.role import AgentStatus
 from ..core.task import Task, TaskResult
 
@@ -136,6 +137,7 @@ class PlaneServer:
         self.world = world
         self._secret = secret or plane_secret()
         self.rejected = 0  # hellos refused (bad secret, rank out of range or already alive)
+        self.agent_rank: Dict[Any, int] = {}  # agent id -> rank (NodeManager keeps it current)
         self.host = host
         self.port = port or plane_port()
         self.hb_timeout = hb_timeout
@@ -637,9 +639,10 @@ class DistributedLLM:
 
     provider = "distributed"
 
-    def __init__(self, plane: PlaneServer, local_llm: Any):
+    def __init__(self, plane: PlaneServer, local_llm: Any, affinity: bool = True):
         self.plane = plane
         self.local = local_llm
+        self.affinity = affinity and os.environ.get("PILOTTAI_LLM_AFFINITY", "1") != "0"
         self.model_name = getattr(local_llm, "model_name", "llama-3-8b")
         self.usage = {"calls": 0, "prompt_tokens": 0, "completion_tokens": 0}
         self.calls_by_rank: Dict[int, int] = {}
@@ -647,8 +650,14 @@ class DistributedLLM:
 
     async def generate_response(self, messages: List[Dict[str, str]], tools: Optional[List[Dict]] = None,
                                 response_format: Optional[Dict[str, Any]] = None) -> Dict[str, Any]:
+        aff = self.plane.agent_rank.get(TASK_AGENT.get()) if self.affinity else None
         while True:
-            r = self.plane.least_loaded_rank(extra={0: float(self._local_inflight)})
+            # the rank of the task's own agent (its prompt prefix is cached there), else the
+            # least-loaded live rank
+            if aff is not None and self.plane.ranks.get(aff) is not None and self.plane.ranks[aff].alive:
+                r = aff
+            else:
+                r = self.plane.least_loaded_rank(extra={0: float(self._local_inflight)})
             # (remote ranks' in-flight count already includes their routed calls)
             self.calls_by_rank[r] = self.calls_by_rank.get(r, 0) + 1
             try:
@@ -663,6 +672,7 @@ class DistributedLLM:
                                                 response_format=response_format)
                 break
             except AgentLostError:
+                aff = None
                 continue  # that rank died under the call: send it elsewhere
         u = out.get("usage", {})
         self.usage["calls"] += 1
@@ -689,6 +699,7 @@ class NodeManager:
         self.serve = serve
         self.proxies: Dict[str, RemoteAgent] = {}
         self.rank_of: Dict[str, int] = {}
+        plane.agent_rank = self.rank_of  # DistributedLLM's task -> rank affinity
         plane.on_rank_lost.append(self._rank_lost)
         plane.on_submit = self._remote_submit
         serve.node = self

@@ -11,6 +11,12 @@ report:
   scale    DynamicScaling's create_agent places a new worker on the least-loaded rank
   kill     rank 2 dies (os._exit) in the middle of the run: every submitted task still
            completes exactly once (its in-flight tasks are re-queued on survivors)
+  throughput / throughput_indep
+           capacity of the plane: world x per_rank closed-loop clients
+           for `duration` seconds, every LLM call taking `latency` s (the measured per-call
+           latency of a rank). "throughput": all clients talk to rank 0's one manager Serve over
+           the node-wide pool; "throughput_indep": every rank runs its own Serve over its own
+           agents. Reports tasks/s and rank 0's event-loop lag (a 10 ms sleep probe).
 
     python -m pilottai_amd.parallel.node_rehearsal --world 8 --scenario balance
 """
@@ -109,6 +115,8 @@ async def _rank0(world: int, port: int, scenario: str, per_rank: int, n_tasks: i
             out["lost_after_agent_stop"] = list(plane.lost)
             out["rank1_alive"] = bool(plane.ranks[1].alive)
             out["rank1_serving"] = isinstance(await p1.remote_queue(), list)
+        elif scenario == "throughput":
+            out.update(await _closed_loop(serve, world * per_rank, latency))
         elif scenario == "scale":
             before = {r: 0 for r in range(world)}
             for aid, r in node.rank_of.items():
@@ -125,6 +133,62 @@ async def _rank0(world: int, port: int, scenario: str, per_rank: int, n_tasks: i
         await serve.stop()
         await plane.stop()
     return out
+
+
+THROUGHPUT_S = 8.0  # measured window of the throughput scenarios (after a 1 s warm-up)
+
+
+async def _closed_loop(serve, n_clients: int, latency: float) -> Dict[str, Any]:
+    """n_clients closed-loop clients on `serve`; tasks/s over the window + event-loop lag."""
+    from ..core.task import Task
+
+    loop = asyncio.get_running_loop()
+    t_start = time.time() + 1.0
+    t_end = t_start + THROUGHPUT_S
+    done = [0]
+    lags: List[float] = []
+
+    async def client(i):
+        k = 0
+        while time.time() < t_end:
+            r = await serve.execute_task(Task(description=f"Summarize the document and list its findings: {i}/{k}"))
+            k += 1
+            if r.success and t_start <= time.time() < t_end:
+                done[0] += 1
+
+    async def probe():
+        while time.time() < t_end:
+            t0 = loop.time()
+            await asyncio.sleep(0.01)
+            if time.time() >= t_start:
+                lags.append(loop.time() - t0 - 0.01)
+
+    await asyncio.gather(probe(), *(client(i) for i in range(n_clients)))
+    lags.sort()
+    pct = lambda q: round(1e3 * lags[min(len(lags) - 1, int(q * len(lags)))], 2) if lags else None  # noqa: E731
+    return {"clients": n_clients, "latency_s": latency, "window_s": THROUGHPUT_S,
+            "tasks_per_s": round(done[0] / THROUGHPUT_S, 2),
+            "loop_lag_ms_p50": pct(0.5), "loop_lag_ms_p99": pct(0.99), "loop_lag_ms_max": pct(1.0)}
+
+
+async def _independent(rank: int, per_rank: int, latency: float) -> Dict[str, Any]:
+    from ..engine.local_llm import SchemaLLM
+    from ..serve import Serve
+
+    llm = SchemaLLM(seed=rank, latency_s=latency)
+    agents = _agents(rank, per_rank, llm)
+    serve = Serve(agents=agents, manager_llm=llm,
+                  config={"name": f"indep-{rank}", "max_concurrent_tasks": 4 * per_rank, "policy": "fixed",
+                          "max_queue_size": 100000, "task_timeout": 120, "agent_wait_timeout": 120})
+    await serve.start()
+    try:
+        res = await _closed_loop(serve, per_rank, latency)
+    finally:
+        await serve.stop()
+    res["rank"] = rank
+    if rank == 0:
+        res["scenario"] = "throughput_indep"
+    return res
 
 
 async def _worker(rank: int, world: int, port: int, scenario: str, per_rank: int, latency: float,
@@ -165,7 +229,9 @@ async def _worker(rank: int, world: int, port: int, scenario: str, per_rank: int
 
 def _entry(rank, world, port, scenario, per_rank, n_tasks, latency, q):
     try:
-        if rank == 0:
+        if scenario == "throughput_indep":
+            res = asyncio.run(_independent(rank, per_rank, latency))
+        elif rank == 0:
             fwd = n_tasks // 2 if scenario == "balance" and world > 1 else 0
             res = asyncio.run(_rank0(world, port, scenario, per_rank, n_tasks - fwd, latency, fwd))
         else:
@@ -210,17 +276,24 @@ def run(world: int, scenario: str, per_rank: int = 2, n_tasks: int = 0, latency:
     main = next((r for r in reports if "scenario" in r), {})
     main["ranks"] = sorted((r for r in reports if "scenario" not in r), key=lambda r: r.get("rank", 0))
     main["exitcodes"] = [p.exitcode for p in procs]
+    if scenario == "throughput_indep":  # rank 0's report holds its own rate: add the others'
+        main["rank0_tasks_per_s"] = main.get("tasks_per_s", 0.0)
+        main["tasks_per_s"] = round(main.get("tasks_per_s", 0.0) + sum(r.get("tasks_per_s", 0.0)
+                                                                        for r in main["ranks"]), 2)
+        main["clients"] = world * per_rank
     return main
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--world", type=int, default=4)
-    ap.add_argument("--scenario", default="balance", choices=["balance", "lb_move", "scale", "kill"])
+    ap.add_argument("--scenario", default="balance",
+                    choices=["balance", "lb_move", "scale", "kill", "throughput", "throughput_indep"])
     ap.add_argument("--per-rank", type=int, default=2)
     ap.add_argument("--tasks", type=int, default=0)
+    ap.add_argument("--latency", type=float, default=0.01, help="seconds per LLM call")
     a = ap.parse_args()
-    print(json.dumps(run(a.world, a.scenario, a.per_rank, a.tasks)))
+    print(json.dumps(run(a.world, a.scenario, a.per_rank, a.tasks, latency=a.latency)))
     return 0
 
 

@@ -35,7 +35,7 @@ from .core.config import AgentConfig, LLMConfig
 from .core.errors import AgentLostError
 from .core.factory import AgentFactory
 from .core.memory import Memory
-from .core.policy import DEFAULT_POLICY, ControlPolicy
+from .core.policy import DEFAULT_POLICY, TASK_AGENT, ControlPolicy
 from .core.prompts import PromptManager, parse_json_response
 from .core.role import AgentStatus
 from .core.router import TaskRouter
@@ -309,11 +309,14 @@ class Serve:
         self._futures.setdefault(task.id, asyncio.get_running_loop().create_future())
         task.metadata.setdefault("_t_submit", time.perf_counter())
         spec = await self._speculative_agent(task) if inline else None
+        tok = TASK_AGENT.set(spec.id if spec is not None else None)
         try:
             analysis = await self._analyze_task(task) if self.config.analyze_tasks else {}
         except BaseException:
             await self._drop_speculation(task, spec)
             raise
+        finally:
+            TASK_AGENT.reset(tok)
         if analysis.get("requires_decomposition", False):
             await self._drop_speculation(task, spec)
             spec = None
@@ -502,6 +505,7 @@ class Serve:
                 agent = await self._acquire_agent(task, prefer=prefer)
             try:
                 self.running_tasks[task.id] = agent.id
+                task.metadata["_agent_id"] = agent.id
                 return await agent.execute_task(task)
             except AgentLostError as e:
                 self.metrics["requeued_tasks"] += 1
@@ -515,8 +519,12 @@ class Serve:
         """`agent`: already reserved (speculative start in _submit)."""
         task.mark_started() if task.status in (TaskStatus.PENDING, TaskStatus.RETRY) else None
         result = await self._run_on_agent(task, agent)
-        evaluation = await self._evaluate_result(task, result) if self.config.evaluate_results else \
-            {"success": result.success, "requires_retry": not result.success}
+        tok = TASK_AGENT.set(task.metadata.get("_agent_id"))
+        try:
+            evaluation = await self._evaluate_result(task, result) if self.config.evaluate_results else \
+                {"success": result.success, "requires_retry": not result.success}
+        finally:
+            TASK_AGENT.reset(tok)
         if not evaluation.get("success", result.success):
             if evaluation.get("requires_retry", False) and task.retry_count < max(1, self.config.max_retry_attempts):
                 self.metrics["retried_tasks"] += 1

@@ -346,10 +346,9 @@ def test_decode_gemm_configs(gpu, nt, waves, splits):
 
 @pytest.mark.parametrize("M,H,KV,K,splits", [
     (7, 32, 8, 4096, 0), (16, 4, 1, 512, 0), (1, 8, 2, 1024, 0), (9, 32, 8, 4096, 2),
-    # open item (BENCHMARKS.md "Next steps"): 3 slices at 9 rows mismatch in ~1 % of runs;
-    # the engine never splits this kernel
-    pytest.param(9, 32, 8, 4096, 3, marks=pytest.mark.xfail(strict=False, reason="rare split-3 mismatch")),
-    (16, 4, 1, 512, 2)])
+    # round 2's rare split-3 mismatch: fixed by the release + acquire hand-off (common.h
+    # handoff_last); stressed with poisoned slabs in tests/test_handoff_gpu.py
+    (9, 32, 8, 4096, 3), (16, 4, 1, 512, 2)])
 def test_decode_qkv_rope(gpu, M, H, KV, K, splits):
     """Norm-folded QKV projection with RoPE + paged KV write in the epilogue vs the
     fp32 projection followed by the reference rope_cache."""

@@ -18,6 +18,9 @@
 #   handoff_cost   tools/handoff_cost.py
 #   pfbench        tools/prefill_gemm_bench.py --M $MLIST
 #   anatomy        tools/step_anatomy.py
+#   midsweep       tools/mid_gemm_bench.py $MLIST --fused-sweep (mid-path configs, engine epilogues)
+#   pmc            rocprofv3 --pmc passes over $PMC_SCRIPT, one pass per ';'-separated set in
+#                  $PMC_SETS (each set within the per-block slot limits), summarised per kernel
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 2
 OUT=gpurun_out/$1
@@ -55,7 +58,19 @@ for t in "$@"; do
     splitk) run splitk 900 python -u tools/splitk_check.py --reps "$REPS" --out "$OUT/splitk.jsonl" $SPLITK_ARGS || exit $? ;;
     handoff_cost) run handoff_cost 300 python -u tools/handoff_cost.py --out "$OUT/handoff_cost.jsonl" || exit $? ;;
     pfbench) run pfbench 900 python -u tools/prefill_gemm_bench.py --M "$MLIST" --out "$OUT/pfbench.jsonl" $PF_ARGS || exit $? ;;
+    midsweep) run midsweep 900 python -u tools/mid_gemm_bench.py "$MLIST" --fused-sweep || exit $? ;;
     anatomy) run anatomy 600 python -u tools/step_anatomy.py $ANATOMY_ARGS || exit $? ;;
+    pmc)
+      i=0
+      IFS=';' read -ra SETS <<< "$PMC_SETS"
+      for cs in "${SETS[@]}"; do
+        i=$((i + 1))
+        rm -rf "/tmp/pmc_$i"
+        echo "[gpu_tasks] pmc pass $i: $cs"
+        timeout -s KILL 180 rocprofv3 --pmc $cs --output-format csv -d "/tmp/pmc_$i" -- python3 "$PMC_SCRIPT" > "$OUT/pmc_$i.log" 2>&1 || exit $?
+        python3 tools/pmc_summary.py "/tmp/pmc_$i" > "$OUT/pmc_$i.json" || exit $?
+      done
+      ;;
     *) echo "[gpu_tasks] unknown task $t"; exit 2 ;;
   esac
 done

@@ -1,6 +1,7 @@
-"""What the agent-scope acquire of the in-launch hand-offs costs (common.h handoff_last):
-times the engine's split-K / partition-merge launches with the acquire (mode 1) and with
-the round-2 sc1-only consumer (mode 0), interleaved in one process (guide §5.4 rule 24).
+"""What the agent-scope fences of the in-launch hand-offs cost (common.h handoff_last):
+times the engine's split-K / partition-merge launches with the round-2 sc1-only consumer
+(mode 0), the acquire by the last arriver (mode 1) and producer release + acquire
+(mode 2), interleaved in one process (guide §5.4 rule 24).
 
     python tools/handoff_cost.py [--rounds 15] [--out file.jsonl]
 """
@@ -78,18 +79,19 @@ cases = {
     "attention decode 64 x ctx 1000 part 256": attention(64, 1000, 256),
     "attention decode 8 x ctx 2000 part 512": attention(8, 2000, 512),
 }
-res = {k: {0: [], 1: []} for k in cases}
+MODES = (0, 1, 2)
+res = {k: {m: [] for m in MODES} for k in cases}
 for _ in range(a.rounds):
     for k, fn in cases.items():
-        for mode in (0, 1):
+        for mode in MODES:
             C.handoff_set_acquire(mode)
             res[k][mode].append(timer(fn))
-C.handoff_set_acquire(1)
+C.handoff_set_modes(2, 1)
 f = open(a.out, "a") if a.out else None
 for k in cases:
-    m0, m1 = statistics.median(res[k][0]), statistics.median(res[k][1])
-    rec = {"case": k, "sc1_only_us": round(m0, 2), "acquire_us": round(m1, 2), "delta_us": round(m1 - m0, 2),
-           "min_sc1_only": round(min(res[k][0]), 2), "min_acquire": round(min(res[k][1]), 2)}
+    m0, m1, m2 = (statistics.median(res[k][m]) for m in MODES)
+    rec = {"case": k, "sc1_only_us": round(m0, 2), "acquire_us": round(m1, 2), "release_acquire_us": round(m2, 2),
+           "delta_acquire_us": round(m1 - m0, 2), "delta_release_acquire_us": round(m2 - m0, 2)}
     print(json.dumps(rec), flush=True)
     if f:
         f.write(json.dumps(rec) + "\n")

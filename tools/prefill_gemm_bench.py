@@ -46,6 +46,17 @@ def timeit(fn, ncopies):
     return s.elapsed_time(e) * 1000 / a.iters
 
 
+C = kernels.require_native()
+
+
+def v0(fn):  # the round-3 first schedule (reads in the phase they feed), for A/B
+    C.prefill_set_variant(0)
+    try:
+        return fn()
+    finally:
+        C.prefill_set_variant(1)
+
+
 torch.manual_seed(0)
 for name in a.shapes.split(","):
     N, K = SHAPES[name]
@@ -68,6 +79,7 @@ for name in a.shapes.split(","):
             "lib": lambda i: torch.nn.functional.linear(x, ws[i]),
             "mid": lambda i: kernels.mid_gemm(x, wps[i], "plain", out=y),
             "pf_default": lambda i: kernels.prefill_gemm(x, wps[i], "plain", out=y),
+            "pf_v0": lambda i: v0(lambda: kernels.prefill_gemm(x, wps[i], "plain", out=y)),
             "pf_whole": lambda i: kernels.prefill_gemm(x, wps[i], "plain", out=y, full=-1, splits=1),
             "pf_s2": lambda i: kernels.prefill_gemm(x, wps[i], "plain", out=y, full=0, splits=2),
             "pf_s3": lambda i: kernels.prefill_gemm(x, wps[i], "plain", out=y, full=0, splits=3),

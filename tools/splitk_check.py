@@ -11,8 +11,10 @@ The check is built so that it CAN fail:
 
     python tools/splitk_check.py [--reps 300] [--modes 0,1] [--out file.jsonl]
 
-Modes: 1 = agent-scope acquire by the last arriver (the default, common.h handoff_last),
-0 = the round-2 sc1-loads-only consumer. Both run interleaved in one process.
+Modes (common.h handoff_last): "default" = the shipped protocols (GEMM slabs: producer
+release + last-arriver acquire; attention merge: acquire), or one protocol for every
+hand-off: 2 = release + acquire, 1 = acquire only, 0 = the round-2 sc1-loads-only consumer;
+--modes 0,1,2,default runs them all.
 """
 import argparse
 import json
@@ -31,11 +33,11 @@ from pilottai_amd.ops import kernels, reference as ref  # noqa: E402
 C = kernels.require_native()
 ap = argparse.ArgumentParser()
 ap.add_argument("--reps", type=int, default=300)
-ap.add_argument("--modes", default="0,1")
+ap.add_argument("--modes", default="default")
 ap.add_argument("--only", default="")
 ap.add_argument("--out", default="")
 a = ap.parse_args()
-modes = [int(m) for m in a.modes.split(",")]
+modes = [m if m == "default" else int(m) for m in a.modes.split(",")]
 dev = torch.device("cuda")
 NAN = float("nan")
 side = torch.cuda.Stream()
@@ -55,6 +57,7 @@ def emit(rec):
 def poison_ws():
     kernels.wide_workspace(dev)[0].fill_(NAN)
     kernels.mid_workspace(dev)[0].fill_(NAN)
+    kernels.prefill_workspace(dev)[0].fill_(NAN)
 
 
 def load(rep):
@@ -72,7 +75,10 @@ def compare(got, base):
 def run_cfg(name, make, call, reps):
     """make() -> state with fresh inputs; call(state, splits, mode) -> output tensor."""
     for mode in modes:
-        C.handoff_set_acquire(mode)
+        if mode == "default":
+            C.handoff_set_modes(2, 1)
+        else:
+            C.handoff_set_acquire(mode)
         bad_runs = bad_elems = nan_elems = 0
         t0 = time.time()
         for rep in range(reps):
@@ -89,7 +95,7 @@ def run_cfg(name, make, call, reps):
                 nan_elems += nn
         emit({"case": name, "mode": mode, "reps": reps, "bad_runs": bad_runs, "bad_elems": bad_elems,
               "nan_elems": nan_elems, "s": round(time.time() - t0, 1)})
-    C.handoff_set_acquire(1)
+    C.handoff_set_modes(2, 1)
 
 
 H, KV, D = 32, 8, 4096
@@ -143,6 +149,9 @@ def gemm_case(M, N, K, epi, splits, kind, **cfg):
         if kind == "decode":
             ops.decode_gemm(x, wp, epi, norm=(epi == "silu"), resid=r if epi == "resid" else None, out=out,
                             splits=s, **kw)
+        elif kind == "prefill":
+            ops.prefill_gemm(x, wp, epi, resid=r if epi == "resid" else None, out=out, norm=(epi == "silu"),
+                             splits=s, full=kw.get("full", -1) if s != 1 else -1)
         elif kind == "wide":
             ops.wide_gemm(x, wp, epi, resid=r if epi == "resid" else None, out=out, norm=(epi == "silu"),
                           splits=s, **kw)
@@ -214,6 +223,10 @@ for M, fm, fn, S in ((32, 1, 2, 4), (64, 1, 2, 2), (128, 2, 2, 2)):
 for M, fm, fn, S in ((32, 1, 2, 4), (64, 2, 2, 4), (128, 2, 2, 2), (256, 4, 2, 2)):
     cases.append((f"mid_down_resid M{M} fm{fm} fn{fn} S{S} (engine)",
                   lambda M=M, fm=fm, fn=fn, S=S: gemm_case(M, 4096, 14336, "resid", S, "mid", fm=fm, fn=fn)))
+cases.append(("prefill o_resid M2048 S2 (256x256 tiles, every tile split)",
+              lambda: gemm_case(2048, 4096, 4096, "resid", 2, "prefill", full=0)))
+cases.append(("prefill gate_up_silu M2048 (768 whole + 128 tiles x S2)",
+              lambda: gemm_case(2048, 28672, 4096, "silu", 2, "prefill", full=768)))
 cases.append(("attention decode 48 seqs part256", lambda: attention_case(48, 3000, 256)))
 cases.append(("attention decode 8 seqs part512", lambda: attention_case(8, 4000, 512)))
 
