@@ -241,6 +241,13 @@ async def run_rank(a, rank: int, world: int, device):
         dev_s = lookup.lookup_device_seconds()
         mem = {"rows": memory.index.count, "index_gb": round(memory.index.memory_bytes() / 2**30, 2),
                "lookups": lookup.stats["lookups"] - mem0["lookups"],
+               # the encoder's work when the serving model embeds (--embedder engine):
+               # embedding requests and their prefilled tokens inside the continuous batch
+               "embedder": a.embedder,
+               "embed_requests": st1["embed_requests"] - st0["embed_requests"],
+               "embed_tokens": st1["embed_tokens"] - st0["embed_tokens"],
+               "embed_token_share": round((st1["embed_tokens"] - st0["embed_tokens"]) /
+                                          max(1, st1["tokens"] - st0["tokens"]), 4),
                "passes": lookup.stats["passes"] - mem0["passes"],
                "stores": lookup.stats["stores"] - mem0["stores"],
                # HIP events around each pass on the lookup stream (includes any wait for

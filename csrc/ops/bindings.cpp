@@ -52,12 +52,13 @@ int pa_mid_gemm(void* y, const void* x, const void* wp, const void* resid, float
                 void* q_out, void* k_cache, void* v_cache, const int* positions, const int* slots,
                 const float* cos_sin, int H, int KV, hipStream_t st);
 int pa_row_sumsq(float* out, const void* x, int M, int K, int ldx, hipStream_t st);
-void pa_prefill_gemm_plan(int M, int N, int K, int* full, int* S);
+void pa_prefill_gemm_plan(int M, int N, int K, int bn, int* full, int* S);
+int pa_prefill_pick_bn(int M, int N);
 void pa_prefill_set_variant(int v);
-long long pa_prefill_gemm_ws_floats(int M, int N, int full, int S);
+long long pa_prefill_gemm_ws_floats(int M, int N, int bn, int full, int S);
 int pa_prefill_gemm(void* y, const void* x, const void* wp, const void* resid, float* ws, long long ws_floats,
                     int* counters, int n_counters, int M, int N, int K, int ldx, int ldy, int ldr, int epi,
-                    const float* ss_in, float* ss_out, float* ss_zero, float eps, int full, int splits,
+                    const float* ss_in, float* ss_out, float* ss_zero, float eps, int full, int splits, int bn,
                     void* q_out, void* k_cache, void* v_cache, const int* positions, const int* slots,
                     const float* cos_sin, int H, int KV, hipStream_t st);
 int pa_prefetch(const void* p, long long bytes, void* sink, int wgs, hipStream_t st);
@@ -431,7 +432,7 @@ bool mid_qkv_rope(at::Tensor x, at::Tensor wp, at::Tensor ss_in, double eps, at:
 // weights with the same epilogues as mid_gemm (0 plain, 1 SwiGLU, 2 residual, 3 rope-perm).
 bool prefill_gemm(at::Tensor y, at::Tensor x, at::Tensor wp, c10::optional<at::Tensor> resid, at::Tensor ws,
                   at::Tensor counters, int64_t epi, c10::optional<at::Tensor> ss_in, c10::optional<at::Tensor> ss_out,
-                  c10::optional<at::Tensor> ss_zero, double eps, int64_t full, int64_t splits) {
+                  c10::optional<at::Tensor> ss_zero, double eps, int64_t full, int64_t splits, int64_t bn) {
   check_gpu(wp, "wp"); check_gpu(ws, "ws"); check_gpu(counters, "counters");
   TORCH_CHECK(x.is_cuda() && x.dim() == 2 && x.stride(1) == 1, "x must be a 2-D GPU tensor, unit inner stride");
   TORCH_CHECK(y.is_cuda() && y.dim() == 2 && y.stride(1) == 1, "y must be a 2-D GPU tensor, unit inner stride");
@@ -460,14 +461,15 @@ bool prefill_gemm(at::Tensor y, at::Tensor x, at::Tensor wp, c10::optional<at::T
                                  counters.data_ptr<int>(), counters.numel(), M, N, K, x.stride(0), y.stride(0), ldr,
                                  (int)epi, opt_rows(ss_in, M, "ss_in"), const_cast<float*>(opt_rows(ss_out, M, "ss_out")),
                                  const_cast<float*>(opt_rows(ss_zero, M, "ss_zero")), (float)eps, (int)full,
-                                 (int)splits, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0, cur_stream());
+                                 (int)splits, (int)bn, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0,
+                                 cur_stream());
   TORCH_CHECK(rc >= 0, "prefill_gemm launch failed");
   return rc == 0;
 }
 
 bool prefill_qkv_rope(at::Tensor x, at::Tensor wp, at::Tensor ss_in, double eps, at::Tensor q_out, at::Tensor k_cache,
                       at::Tensor v_cache, at::Tensor positions, at::Tensor slots, at::Tensor cos_sin, int64_t H,
-                      int64_t KV, at::Tensor ws, at::Tensor counters, int64_t full, int64_t splits) {
+                      int64_t KV, at::Tensor ws, at::Tensor counters, int64_t full, int64_t splits, int64_t bn) {
   check_gpu(wp, "wp"); check_gpu(q_out, "q_out"); check_gpu(k_cache, "k_cache"); check_gpu(v_cache, "v_cache");
   check_gpu(positions, "positions"); check_gpu(slots, "slots"); check_gpu(cos_sin, "cos_sin");
   check_gpu(ws, "ws"); check_gpu(counters, "counters");
@@ -494,16 +496,17 @@ bool prefill_qkv_rope(at::Tensor x, at::Tensor wp, at::Tensor ss_in, double eps,
   const int rc = pa_prefill_gemm(nullptr, x.data_ptr(), wp.data_ptr(), nullptr, ws.data_ptr<float>(), ws.numel(),
                                  counters.data_ptr<int>(), counters.numel(), M, N, K, x.stride(0), 0, 0, 4,
                                  ss_in.data_ptr<float>(), nullptr, nullptr, (float)eps, (int)full, (int)splits,
-                                 q_out.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(), positions.data_ptr<int>(),
+                                 (int)bn, q_out.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(), positions.data_ptr<int>(),
                                  slots.data_ptr<int>(), cos_sin.data_ptr<float>(), (int)H, (int)KV, cur_stream());
   TORCH_CHECK(rc >= 0, "prefill_qkv_rope launch failed");
   return rc == 0;
 }
 
-std::vector<int64_t> prefill_gemm_plan(int64_t M, int64_t N, int64_t K) {
+std::vector<int64_t> prefill_gemm_plan(int64_t M, int64_t N, int64_t K, int64_t bn) {
   int full, S;
-  pa_prefill_gemm_plan((int)M, (int)N, (int)K, &full, &S);
-  return {full, S, pa_prefill_gemm_ws_floats((int)M, (int)N, full, S)};
+  if (bn <= 0) bn = pa_prefill_pick_bn((int)M, (int)N);
+  pa_prefill_gemm_plan((int)M, (int)N, (int)K, (int)bn, &full, &S);
+  return {full, S, pa_prefill_gemm_ws_floats((int)M, (int)N, (int)bn, full, S), bn};
 }
 
 // out[m] = sum_k x[m, k]^2 (fp32)
@@ -722,13 +725,15 @@ PYBIND11_MODULE(_C, m) {
         py::arg("fn") = 0, py::arg("splits") = 0);
   m.def("prefill_gemm", &prefill_gemm, py::arg("y"), py::arg("x"), py::arg("wp"), py::arg("resid"), py::arg("ws"),
         py::arg("counters"), py::arg("epi") = 0, py::arg("ss_in") = py::none(), py::arg("ss_out") = py::none(),
-        py::arg("ss_zero") = py::none(), py::arg("eps") = 1e-5, py::arg("full") = -1, py::arg("splits") = 0);
+        py::arg("ss_zero") = py::none(), py::arg("eps") = 1e-5, py::arg("full") = -1, py::arg("splits") = 0,
+        py::arg("bn") = 0);
   m.def("prefill_qkv_rope", &prefill_qkv_rope, py::arg("x"), py::arg("wp"), py::arg("ss_in"), py::arg("eps"),
         py::arg("q_out"), py::arg("k_cache"), py::arg("v_cache"), py::arg("positions"), py::arg("slots"),
         py::arg("cos_sin"), py::arg("H"), py::arg("KV"), py::arg("ws"), py::arg("counters"), py::arg("full") = -1,
-        py::arg("splits") = 0);
+        py::arg("splits") = 0, py::arg("bn") = 0);
   m.def("prefill_set_variant", [](int v) { pa_prefill_set_variant(v); });
-  m.def("prefill_gemm_plan", &prefill_gemm_plan, "default (full tiles, splits, workspace floats) of prefill_gemm");
+  m.def("prefill_gemm_plan", &prefill_gemm_plan, py::arg("M"), py::arg("N"), py::arg("K"), py::arg("bn") = 0,
+        "default (full tiles, splits, workspace floats, tile width) of prefill_gemm");
   m.def("row_sumsq", &row_sumsq, py::arg("out"), py::arg("x"));
   m.def("mid_gemm_plan", &mid_gemm_plan, "default (fm, fn, splits, workspace floats) of mid_gemm");
   m.def("paged_attention", &paged_attention, py::arg("out"), py::arg("part_o"), py::arg("part_ml"), py::arg("q"),

@@ -98,14 +98,21 @@ constexpr int SLAB = 256 * 256;       // floats per split slab
 template <int V>
 using ic = std::integral_constant<int, V>;
 
-template <int EPI, bool NORM, bool RA>
-__global__ __launch_bounds__(512) void prefill_gemm_kernel(const Args A) {
+template <int EPI, bool NORM, bool RA, int NW>
+__global__ __launch_bounds__(NW * 64) void prefill_gemm_kernel(const Args A) {
+  // NW = 8: 2 x 4 waves of 128 x 64 outputs; NW = 4: 2 x 2 waves of 128 x 128 (one wave per
+  // SIMD, 256 accumulator registers, half the fragment reads per MFMA)
+  static_assert(NW == 4 || NW == 8, "4 or 8 waves");
+  constexpr int WCN = NW / 2;     // wave columns
+  constexpr int CPW = 16 / WCN;   // 16-column fragments per wave
+  constexpr int LPW = 16 / NW;    // LDS-DMA loads per lane per 16-KiB piece
+  constexpr int NTH = NW * 64;
   // the only LDS object (guide §5 trap 4a): two tile buffers, reused by the hand-off flag
   __shared__ __attribute__((aligned(1024))) char smem[2 * BUF];
 
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wr = wid >> 2, wc = wid & 3;
+  const int wr = wid / WCN, wc = wid % WCN;
   const int g = lane >> 4, c = lane & 15;
 
   // ---- work item: a whole tile, or one K-slice of a tail tile
@@ -118,9 +125,16 @@ __global__ __launch_bounds__(512) void prefill_gemm_kernel(const Args A) {
     kt0 = 0;
     kt1 = KT;
   } else {
+    // split items, remapped the same way: logical item L = slice * ntail + t runs the
+    // tail tiles row-tile fastest per slice, so the row tiles that share a W panel and a
+    // K-slice sit on one XCD (consecutive blockIdx alternate XCDs; without the remap every
+    // tail item fetched its panel slice from HBM)
     const int w2 = bid - A.full;
-    tile = A.full + w2 / A.S;
-    slice = w2 % A.S;
+    const int ntail = A.MT * A.NT - A.full, nitems = ntail * A.S;
+    const int q8 = nitems >> 3, r8 = nitems & 7, xcd = w2 & 7;
+    const int L = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (w2 >> 3);
+    slice = L / ntail;
+    tile = A.full + L % ntail;
     kt0 = slice * A.per;
     kt1 = min(KT, kt0 + A.per);
   }
@@ -129,41 +143,41 @@ __global__ __launch_bounds__(512) void prefill_gemm_kernel(const Args A) {
   const int nk = kt1 - kt0;
 
   if (A.ss_zero && blockIdx.x == 0)
-    for (int i = threadIdx.x; i < A.M; i += 512) A.ss_zero[i] = 0.f;
+    for (int i = threadIdx.x; i < A.M; i += NTH) A.ss_zero[i] = 0.f;
 
   // ---- per-lane LDS-DMA sources
-  // x piece p (rows lo / hi of each wave row): LDS row lr = (2 wid + q) * 8 + (lane >> 3)
+  // x piece p (rows lo / hi of each wave row): LDS row lr = (LPW wid + q) * 8 + (lane >> 3)
   // holds tile row (lr >> 6) * 128 + 64 p + (lr & 63); its 16-B unit (lane & 7) is the
   // row's logical unit (lane & 7) ^ ((lr >> 1) & 7).
-  const bf16* xs[2][2];
+  const bf16* xs[2][LPW];
 #pragma unroll
   for (int p = 0; p < 2; ++p)
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int lr = (wid * 2 + q) * 8 + (lane >> 3);
+    for (int q = 0; q < LPW; ++q) {
+      const int lr = (wid * LPW + q) * 8 + (lane >> 3);
       const int trow = (lr >> 6) * 128 + p * 64 + (lr & 63);
       const int gr = min(row0 + trow, A.M - 1);
       const int unit = (lane & 7) ^ ((lr >> 1) & 7);
       xs[p][q] = A.x + (size_t)gr * A.ldx + unit * 8;
     }
   const int KS = A.K >> 5;
-  const bf16* wsrc[2];
+  const bf16* wsrc[LPW];
 #pragma unroll
-  for (int q = 0; q < 2; ++q) wsrc[q] = A.wp + ((size_t)(nt * 16 + wid * 2 + q) * KS) * 512 + lane * 8;
+  for (int q = 0; q < LPW; ++q) wsrc[q] = A.wp + ((size_t)(nt * 16 + wid * LPW + q) * KS) * 512 + lane * 8;
 
   auto issue_a = [&](int p, int kt, char* buf) {
 #pragma unroll
-    for (int q = 0; q < 2; ++q) glds16(xs[p][q] + (size_t)kt * 64, buf + p * PIECE + (wid * 2 + q) * 1024);
+    for (int q = 0; q < LPW; ++q) glds16(xs[p][q] + (size_t)kt * 64, buf + p * PIECE + (wid * LPW + q) * 1024);
   };
   auto issue_b = [&](int kh, int kt, char* buf) {
 #pragma unroll
-    for (int q = 0; q < 2; ++q)
-      glds16(wsrc[q] + (size_t)(2 * kt + kh) * 512, buf + OFF_B + kh * PIECE + (wid * 2 + q) * 1024);
+    for (int q = 0; q < LPW; ++q)
+      glds16(wsrc[q] + (size_t)(2 * kt + kh) * 512, buf + OFF_B + kh * PIECE + (wid * LPW + q) * 1024);
   };
-  auto read_b = [&](const char* buf, int kh, bf16x8(&bf)[4]) {
+  auto read_b = [&](const char* buf, int kh, bf16x8(&bf)[CPW]) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
-      bf[j] = *reinterpret_cast<const bf16x8*>(buf + OFF_B + kh * PIECE + (wc * 4 + j) * 1024 + lane * 16);
+    for (int j = 0; j < CPW; ++j)
+      bf[j] = *reinterpret_cast<const bf16x8*>(buf + OFF_B + kh * PIECE + (wc * CPW + j) * 1024 + lane * 16);
   };
   auto read_a = [&](const char* buf, int p, int kh, bf16x8(&af)[4]) {
 #pragma unroll
@@ -174,26 +188,26 @@ __global__ __launch_bounds__(512) void prefill_gemm_kernel(const Args A) {
     }
   };
 
-  f32x4 acc[8][4];
+  f32x4 acc[8][CPW];
 #pragma unroll
   for (int i = 0; i < 8; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < CPW; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  auto mma = [&](auto half, const bf16x8(&af)[4], const bf16x8(&bf)[4]) {
+  auto mma = [&](auto half, const bf16x8(&af)[4], const bf16x8(&bf)[CPW]) {
     constexpr int h = decltype(half)::value;
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
+      for (int j = 0; j < CPW; ++j)
         acc[h * 4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j], af[i], acc[h * 4 + i][j], 0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
   };
 
   char* const b0 = smem;
   char* const b1 = smem + BUF;
-  bf16x8 bk0[4], bk1[4], af[4];
+  bf16x8 bk0[CPW], bk1[CPW], af[4];
 
   // One 64-k tile in four phases. ISS: pieces of the next tiles are issued (main loop:
   // B-k1 and x-hi of tile i + 1 in phases 0/1, B-k0 and x-lo of tile i + 2 in phases 2/3);
@@ -205,14 +219,14 @@ __global__ __launch_bounds__(512) void prefill_gemm_kernel(const Args A) {
     read_b(cur, 0, bk0);
     read_a(cur, 0, 0, af);
     if constexpr (decltype(iss1)::value) issue_b(1, kt0 + i + 1, oth);
-    if constexpr (decltype(w0)::value >= 0) wait_vm<decltype(w0)::value>();
+    if constexpr (decltype(w0)::value >= 0) wait_vm<decltype(w0)::value * LPW / 2>();
     raw_barrier();
     mma(ic<0>{}, af, bk0);
     // phase 1: rows lo, k 32-63
     read_b(cur, 1, bk1);
     read_a(cur, 0, 1, af);
     if constexpr (decltype(iss1)::value) issue_a(1, kt0 + i + 1, oth);
-    if constexpr (decltype(w1)::value >= 0) wait_vm<decltype(w1)::value>();
+    if constexpr (decltype(w1)::value >= 0) wait_vm<decltype(w1)::value * LPW / 2>();
     raw_barrier();
     mma(ic<0>{}, af, bk1);
     // phase 2: rows hi, k 0-31
@@ -223,7 +237,7 @@ __global__ __launch_bounds__(512) void prefill_gemm_kernel(const Args A) {
     // phase 3: rows hi, k 32-63
     read_a(cur, 1, 1, af);
     if constexpr (decltype(iss2)::value) issue_a(0, kt0 + i + 2, cur);
-    if constexpr (decltype(w3)::value >= 0) wait_vm<decltype(w3)::value>();
+    if constexpr (decltype(w3)::value >= 0) wait_vm<decltype(w3)::value * LPW / 2>();
     raw_barrier();
     mma(ic<1>{}, af, bk1);
   };
@@ -250,7 +264,7 @@ __global__ __launch_bounds__(512) void prefill_gemm_kernel(const Args A) {
       if constexpr (decltype(iss)::value) issue_b(0, kt0 + i + 2, cur);
       mma(ic<0>{}, afA, bk0);
       __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this window's LDS reads are done
-      if constexpr (decltype(w0)::value >= 0) wait_vm<decltype(w0)::value>();
+      if constexpr (decltype(w0)::value >= 0) wait_vm<decltype(w0)::value * LPW / 2>();
       raw_barrier();
       // ph1
       read_a(cur, 1, 0, afA);
@@ -263,7 +277,7 @@ __global__ __launch_bounds__(512) void prefill_gemm_kernel(const Args A) {
       if constexpr (decltype(iss)::value) issue_b(1, kt0 + i + 2, cur);
       mma(ic<1>{}, afA, bk0);
       __builtin_amdgcn_s_waitcnt(0xC07F);
-      if constexpr (decltype(w2)::value >= 0) wait_vm<decltype(w2)::value>();
+      if constexpr (decltype(w2)::value >= 0) wait_vm<decltype(w2)::value * LPW / 2>();
       raw_barrier();
       // ph3
       if constexpr (decltype(nxt)::value) {
@@ -273,7 +287,7 @@ __global__ __launch_bounds__(512) void prefill_gemm_kernel(const Args A) {
       if constexpr (decltype(iss)::value) issue_a(1, kt0 + i + 2, cur);
       mma(ic<1>{}, afB, bk1);
       __builtin_amdgcn_s_waitcnt(0xC07F);
-      if constexpr (decltype(w3)::value >= 0) wait_vm<decltype(w3)::value>();
+      if constexpr (decltype(w3)::value >= 0) wait_vm<decltype(w3)::value * LPW / 2>();
       raw_barrier();
     };
     // prologue: the pieces of tiles 0 and 1 in steady-state order, then phase 0's registers
@@ -286,9 +300,9 @@ __global__ __launch_bounds__(512) void prefill_gemm_kernel(const Args A) {
       issue_a(0, kt0 + 1, b1);
       issue_b(1, kt0 + 1, b1);
       issue_a(1, kt0 + 1, b1);
-      wait_vm<10>();  // tile 0's B-k0, x-lo and B-k1 landed
+      wait_vm<10 * LPW / 2>();  // tile 0's B-k0, x-lo and B-k1 landed
     } else {
-      wait_vm<2>();
+      wait_vm<2 * LPW / 2>();
     }
     raw_barrier();
     read_b(b0, 0, bk0);
@@ -310,7 +324,7 @@ __global__ __launch_bounds__(512) void prefill_gemm_kernel(const Args A) {
     issue_a(1, kt0, b0);
     issue_b(0, kt0 + 1, b1);
     issue_a(0, kt0 + 1, b1);
-    wait_vm<8>();
+    wait_vm<8 * LPW / 2>();
     raw_barrier();
     int i = 0;
     for (; i + 2 < nk; ++i) tile_body(i, ic<1>{}, ic<1>{}, ic<8>{}, ic<8>{}, ic<8>{});
@@ -321,7 +335,7 @@ __global__ __launch_bounds__(512) void prefill_gemm_kernel(const Args A) {
     issue_a(0, kt0, b0);
     issue_b(1, kt0, b0);
     issue_a(1, kt0, b0);
-    wait_vm<4>();
+    wait_vm<4 * LPW / 2>();
     raw_barrier();
     tile_body(0, ic<0>{}, ic<0>{}, ic<2>{}, ic<0>{}, ic<-1>{});
   }
@@ -334,9 +348,9 @@ __global__ __launch_bounds__(512) void prefill_gemm_kernel(const Args A) {
 #pragma unroll
       for (int i = 0; i < 8; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+        for (int j = 0; j < CPW; ++j)
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i][j]), rs,
-                                                 (((wid * 8 + i) * 4 + j) * 64 + lane) * 16, 0, 16);
+                                                 (((wid * 8 + i) * CPW + j) * 64 + lane) * 16, 0, 16);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (!handoff_last(A.counters + (tile - A.full), A.S, reinterpret_cast<int*>(smem), A.acq)) return;
@@ -344,18 +358,18 @@ __global__ __launch_bounds__(512) void prefill_gemm_kernel(const Args A) {
       if (p == slice) continue;
       const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(base + (size_t)p * SLAB, 0, SLAB * 4, 0x00020000);
 #pragma unroll
-      for (int i = 0; i < 8; i += 2) {  // 8 loads in flight per lane (the accumulators hold the rest)
-        f32x4 t[2][4];
+      for (int i = 0; i < 8; i += 8 / CPW) {  // 8 loads in flight per lane (the accumulators hold the rest)
+        f32x4 t[8 / CPW][CPW];
 #pragma unroll
-        for (int h = 0; h < 2; ++h)
+        for (int h = 0; h < 8 / CPW; ++h)
 #pragma unroll
-          for (int j = 0; j < 4; ++j)
+          for (int j = 0; j < CPW; ++j)
             t[h][j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                    rp, (((wid * 8 + i + h) * 4 + j) * 64 + lane) * 16, 0, 16));
+                                                    rp, (((wid * 8 + i + h) * CPW + j) * 64 + lane) * 16, 0, 16));
 #pragma unroll
-        for (int h = 0; h < 2; ++h)
+        for (int h = 0; h < 8 / CPW; ++h)
 #pragma unroll
-          for (int j = 0; j < 4; ++j) acc[i + h][j] += t[h][j];
+          for (int j = 0; j < CPW; ++j) acc[i + h][j] += t[h][j];
       }
     }
   }
@@ -373,11 +387,12 @@ __global__ __launch_bounds__(512) void prefill_gemm_kernel(const Args A) {
       if constexpr (NORM) rs = rsqrtf(A.ss_in[m] * inv_k + A.eps);
       if constexpr (pair_epi<EPI>()) {
 #pragma unroll
-        for (int j = 0; j < 4; j += 2)
-          store_quad<EPI>(A, m, nt * 16 + wc * 4 + j, 4 * g, acc[i][j] * rs, acc[i][j + 1] * rs);
+        for (int j = 0; j < CPW; j += 2)
+          store_quad<EPI>(A, m, nt * 16 + wc * CPW + j, 4 * g, acc[i][j] * rs, acc[i][j + 1] * rs);
       } else {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) sq += store_quad<EPI>(A, m, nt * 16 + wc * 4 + j, 4 * g, acc[i][j] * rs, acc[i][j]);
+        for (int j = 0; j < CPW; ++j)
+          sq += store_quad<EPI>(A, m, nt * 16 + wc * CPW + j, 4 * g, acc[i][j] * rs, acc[i][j]);
       }
     }
     if constexpr (EPI == EP_RESID) {
@@ -390,22 +405,240 @@ __global__ __launch_bounds__(512) void prefill_gemm_kernel(const Args A) {
   }
 }
 
-// main-loop schedule: 1 = read-ahead (default), 0 = reads in the phase they feed
+// ---------------------------------------------------------------------------------------
+// 256 x 128 tiles (N = 4,096 / 6,144 projections, and gate_up where 128-wide tiles fill
+// whole rounds: 1,792 tiles = 7 x 256 CUs at M = 2,048). One tile stage is 48 KiB
+// ([x 256 rows x 64 k | W-k0 8 chunks | W-k1 8 chunks]), so THREE stages fit (144 KiB):
+// two tiles are in flight while one is computed, with ONE barrier per 64-k tile (the
+// schedule is at `body` below).
+//
+// 8 waves as 4 (rows) x 2 (columns), 64 x 64 outputs per wave (acc[4][4], 64 VGPRs); the
+// per-wave fragment reads (4 x-rows + 4 W per 32 k) keep the LDS array under half busy.
+// The x image and its (row >> 1) unit swizzle are those of the 256-wide kernel.
+constexpr int BUF128 = 49152;
+constexpr int OFFB128 = 32768;
+constexpr int SLAB128 = 256 * 128;
+
+template <int EPI, bool NORM>
+__global__ __launch_bounds__(512) void prefill_gemm_n128_kernel(const Args A) {
+  __shared__ __attribute__((aligned(1024))) char smem[3 * BUF128];
+
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wid >> 1, wn = wid & 1;
+  const int g = lane >> 4, c = lane & 15;
+
+  const int bid = blockIdx.x;
+  const int KT = A.K >> 6;
+  int tile, kt0, kt1, slice = -1;
+  if (bid < A.full) {
+    const int q8 = A.full >> 3, r8 = A.full & 7, xcd = bid & 7;
+    tile = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+    kt0 = 0;
+    kt1 = KT;
+  } else {
+    // split items, remapped the same way: logical item L = slice * ntail + t runs the
+    // tail tiles row-tile fastest per slice, so the row tiles that share a W panel and a
+    // K-slice sit on one XCD (consecutive blockIdx alternate XCDs; without the remap every
+    // tail item fetched its panel slice from HBM)
+    const int w2 = bid - A.full;
+    const int ntail = A.MT * A.NT - A.full, nitems = ntail * A.S;
+    const int q8 = nitems >> 3, r8 = nitems & 7, xcd = w2 & 7;
+    const int L = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (w2 >> 3);
+    slice = L / ntail;
+    tile = A.full + L % ntail;
+    kt0 = slice * A.per;
+    kt1 = min(KT, kt0 + A.per);
+  }
+  const int mt = tile % A.MT, nt = tile / A.MT;
+  const int row0 = mt * 256;
+  const int nk = kt1 - kt0;
+
+  if (A.ss_zero && blockIdx.x == 0)
+    for (int i = threadIdx.x; i < A.M; i += 512) A.ss_zero[i] = 0.f;
+
+  // wave w stages x rows 32 w .. 32 w + 31 (four 8-row x 128-B pieces) and W chunk w of
+  // both k halves; 6 LDS-DMA loads per lane per tile
+  const bf16* xs[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int lr = (wid * 4 + q) * 8 + (lane >> 3);
+    const int gr = min(row0 + lr, A.M - 1);
+    xs[q] = A.x + (size_t)gr * A.ldx + ((lane & 7) ^ ((lr >> 1) & 7)) * 8;
+  }
+  const int KS = A.K >> 5;
+  const bf16* wsrc = A.wp + ((size_t)(nt * 8 + wid) * KS) * 512 + lane * 8;
+
+  auto stage = [&](int i) { return smem + (i % 3) * BUF128; };
+  auto issue = [&](int kt, char* buf) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) glds16(xs[q] + (size_t)kt * 64, buf + (wid * 4 + q) * 1024);
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh) glds16(wsrc + (size_t)(2 * kt + kh) * 512, buf + OFFB128 + kh * 8192 + wid * 1024);
+  };
+  auto read_frags = [&](const char* buf, int kh, bf16x8(&af)[4], bf16x8(&bf)[4]) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      bf[j] = *reinterpret_cast<const bf16x8*>(buf + OFFB128 + kh * 8192 + (wn * 4 + j) * 1024 + lane * 16);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int lr = wm * 64 + 16 * i + c;
+      af[i] = *reinterpret_cast<const bf16x8*>(buf + lr * 128 + (((4 * kh + g) ^ ((lr >> 1) & 7)) << 4));
+    }
+  };
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto mma = [&](const bf16x8(&af)[4], const bf16x8(&bf)[4]) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j], af[i], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  bf16x8 aA[4], bA[4], aB[4], bB[4];
+  // Tile i in two phases; each phase issues the fragment reads of the NEXT phase into the
+  // other register set, runs its 16 MFMAs on registers read one phase earlier and ends with
+  // lgkmcnt(0) (so no LDS read is in flight at a phase boundary and hipcc never has to wait
+  // for a read issued in the same phase before an MFMA):
+  //   A: k1 of tile i -> set B | MFMAs set A (k0 of i) | lgkmcnt(0), vmcnt retiring tile
+  //      i + 1, s_barrier
+  //   B: k0 of tile i + 1 -> set A | LDS-DMA tile i + 3 into tile i's stage (every read of
+  //      it finished before the barrier) | MFMAs set B (k1 of i) | lgkmcnt(0)
+  // ISS: issue tile i + 3; W: that vmcnt (-1: last tile, no barrier); NXT: tile i + 1 exists
+  auto body = [&](int i, auto iss, auto w, auto nxt) {
+    char* cur = stage(i);
+    read_frags(cur, 1, aB, bB);
+    mma(aA, bA);
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+    if constexpr (decltype(w)::value >= 0) {
+      wait_vm<decltype(w)::value>();
+      raw_barrier();
+    }
+    if constexpr (decltype(nxt)::value) read_frags(stage(i + 1), 0, aA, bA);
+    if constexpr (decltype(iss)::value) issue(kt0 + i + 3, cur);
+    mma(aB, bB);
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+  };
+
+  issue(kt0, stage(0));
+  if (nk > 1) issue(kt0 + 1, stage(1));
+  if (nk > 2) issue(kt0 + 2, stage(2));
+  if (nk > 2) wait_vm<12>();
+  else if (nk == 2) wait_vm<6>();
+  else wait_vm<0>();
+  raw_barrier();
+  read_frags(stage(0), 0, aA, bA);
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  int i = 0;
+  for (; i + 3 < nk; ++i) body(i, ic<1>{}, ic<6>{}, ic<1>{});
+  if (nk >= 3) body(nk - 3, ic<0>{}, ic<6>{}, ic<1>{});
+  if (nk >= 2) body(nk - 2, ic<0>{}, ic<0>{}, ic<1>{});
+  body(nk - 1, ic<0>{}, ic<-1>{}, ic<0>{});
+
+  if (slice >= 0) {
+    float* base = A.ws + (size_t)(tile - A.full) * A.S * SLAB128;
+    {
+      const __amdgpu_buffer_rsrc_t rs =
+          __builtin_amdgcn_make_buffer_rsrc(base + (size_t)slice * SLAB128, 0, SLAB128 * 4, 0x00020000);
+#pragma unroll
+      for (int i2 = 0; i2 < 4; ++i2)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i2][j]), rs,
+                                                 (((wid * 4 + i2) * 4 + j) * 64 + lane) * 16, 0, 16);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (!handoff_last(A.counters + (tile - A.full), A.S, reinterpret_cast<int*>(smem), A.acq)) return;
+    for (int p = 0; p < A.S; ++p) {
+      if (p == slice) continue;
+      const __amdgpu_buffer_rsrc_t rp =
+          __builtin_amdgcn_make_buffer_rsrc(base + (size_t)p * SLAB128, 0, SLAB128 * 4, 0x00020000);
+      f32x4 t[4][4];
+#pragma unroll
+      for (int i2 = 0; i2 < 4; ++i2)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          t[i2][j] = __builtin_bit_cast(
+              f32x4, __builtin_amdgcn_raw_buffer_load_b128(rp, (((wid * 4 + i2) * 4 + j) * 64 + lane) * 16, 0, 16));
+#pragma unroll
+      for (int i2 = 0; i2 < 4; ++i2)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i2][j] += t[i2][j];
+    }
+  }
+
+  const float inv_k = 1.f / (float)A.K;
+#pragma unroll
+  for (int i2 = 0; i2 < 4; ++i2) {
+    const int m = row0 + wm * 64 + 16 * i2 + c;
+    const bool ok = m < A.M;
+    float sq = 0.f;
+    if (ok) {
+      float rs = 1.f;
+      if constexpr (NORM) rs = rsqrtf(A.ss_in[m] * inv_k + A.eps);
+      if constexpr (pair_epi<EPI>()) {
+#pragma unroll
+        for (int j = 0; j < 4; j += 2)
+          store_quad<EPI>(A, m, nt * 8 + wn * 4 + j, 4 * g, acc[i2][j] * rs, acc[i2][j + 1] * rs);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          sq += store_quad<EPI>(A, m, nt * 8 + wn * 4 + j, 4 * g, acc[i2][j] * rs, acc[i2][j]);
+      }
+    }
+    if constexpr (EPI == EP_RESID) {
+      if (A.ss_out) {
+        sq += __shfl_xor(sq, 16, 64);
+        sq += __shfl_xor(sq, 32, 64);
+        if (ok && g == 0) atomicAdd(A.ss_out + m, sq);
+      }
+    }
+  }
+}
+
+// 256-wide main loop: 1 = read-ahead, 8 waves (default); 0 = reads in the phase they feed;
+// 2 = read-ahead, 4 waves of 128 x 128
 static int g_pf_variant = 1;
 
 // Default decomposition: whole tiles while they fill complete rounds of 256 CUs; the
-// remainder is split over K so that the last round is (nearly) full.
-static void plan_default(int M, int N, int K, int& full, int& S) {
-  const int tiles = ((M + 255) / 256) * (N / 256);
+// remaining `rem` tiles run over S K-slices, S chosen to minimise the tail's length in
+// whole-tile times, ceil(rem S / 256) / S, plus a small per-split cost (slab traffic and
+// the last arriver's reduction): e.g. 192 tiles -> 4 slices (3 rounds of quarter tiles),
+// 128 -> 2.
+constexpr long long kWsFloats = 64ll << 20;  // the workspace ops.prefill_workspace allocates
+
+static void plan_default(int M, int N, int K, int bn, int& full, int& S) {
+  const int tiles = ((M + 255) / 256) * (N / bn);
   const int KT = K / 64;
   const int rem = tiles % 256;
   full = tiles - rem;
   S = 1;
   if (rem) {
-    S = std::max(1, std::min(4, 256 / rem));
-    while (S > 1 && KT / S < 8) --S;
+    float best = 1.f;
+    for (int s = 2; s <= 4; ++s) {
+      if (KT / s < 8 || (long long)rem * s * 256 * bn > kWsFloats) break;
+      const float t = (float)((rem * s + 255) / 256) / s + 0.06f * (s - 1);
+      if (t < best - 1e-4f) {
+        best = t;
+        S = s;
+      }
+    }
     if (S == 1) full = tiles;
   }
+}
+
+// Tile width when the caller leaves it open: 128-wide tiles unless the 256-wide grid
+// already fills whole rounds with fewer tiles.
+static int pick_bn(int M, int N) {
+  if (N % 256) return 128;
+  const int t256 = ((M + 255) / 256) * (N / 256);
+  return (t256 % 256 == 0) ? 256 : 128;
 }
 
 }  // namespace pf
@@ -413,35 +646,42 @@ static void plan_default(int M, int N, int K, int& full, int& S) {
 
 extern "C" void pa_prefill_set_variant(int v) { pa::pf::g_pf_variant = v; }
 
-extern "C" void pa_prefill_gemm_plan(int M, int N, int K, int* full, int* S) {
-  pa::pf::plan_default(M, N, K, *full, *S);
+extern "C" int pa_prefill_pick_bn(int M, int N) { return pa::pf::pick_bn(M, N); }
+
+extern "C" void pa_prefill_gemm_plan(int M, int N, int K, int bn, int* full, int* S) {
+  if (bn <= 0) bn = pa::pf::pick_bn(M, N);
+  pa::pf::plan_default(M, N, K, bn, *full, *S);
 }
 
-extern "C" long long pa_prefill_gemm_ws_floats(int M, int N, int full, int S) {
-  const long long tiles = (long long)((M + 255) / 256) * (N / 256);
-  return S > 1 ? (tiles - full) * S * (long long)pa::pf::SLAB : 0;
+extern "C" long long pa_prefill_gemm_ws_floats(int M, int N, int bn, int full, int S) {
+  if (bn <= 0) bn = pa::pf::pick_bn(M, N);
+  const long long tiles = (long long)((M + 255) / 256) * (N / bn);
+  return S > 1 ? (tiles - full) * S * (long long)(256 * bn) : 0;
 }
 
 // Returns 1 if the shape/config is not handled, 0 on success, -2 on a launch error.
-// full < 0 / splits <= 0 pick the defaults. For epi 4 (RoPE + paged KV write) y is unused.
+// full < 0 / splits <= 0 / bn <= 0 pick the defaults. For epi 4 (RoPE + paged KV write) y
+// is unused.
 extern "C" int pa_prefill_gemm(void* y, const void* x, const void* wp, const void* resid, float* ws,
                                long long ws_floats, int* counters, int n_counters, int M, int N, int K, int ldx,
                                int ldy, int ldr, int epi, const float* ss_in, float* ss_out, float* ss_zero,
-                               float eps, int full, int splits, void* q_out, void* k_cache, void* v_cache,
+                               float eps, int full, int splits, int bn, void* q_out, void* k_cache, void* v_cache,
                                const int* positions, const int* slots, const float* cos_sin, int H, int KV,
                                hipStream_t st) {
   using namespace pa::pf;
   if (M <= 0) return 0;
-  if (K % 64 != 0 || N % 256 != 0 || epi < 0 || epi > 4 || ldx % 8 != 0) return 1;
+  if (bn <= 0) bn = pick_bn(M, N);
+  if (bn != 128 && bn != 256) return 1;
+  if (K % 64 != 0 || N % bn != 0 || epi < 0 || epi > 4 || ldx % 8 != 0) return 1;
   const int norm = ss_in != nullptr;
   if (epi == EP_RESID && (!resid || norm)) return 1;
   if (ss_out && epi != EP_RESID) return 1;
   if (epi == EP_ROPEKV && (!q_out || !k_cache || !v_cache || !positions || !slots || !cos_sin ||
                            N != (H + 2 * KV) * 128))
     return 1;
-  const int MT = (M + 255) / 256, NT = N / 256, tiles = MT * NT;
+  const int MT = (M + 255) / 256, NT = N / bn, tiles = MT * NT;
   int dfull, dS;
-  plan_default(M, N, K, dfull, dS);
+  plan_default(M, N, K, bn, dfull, dS);
   if (full < 0) full = dfull;
   int S = splits > 0 ? splits : (full == dfull ? dS : 1);
   full = std::min(std::max(full, 0), tiles);
@@ -451,7 +691,7 @@ extern "C" int pa_prefill_gemm(void* y, const void* x, const void* wp, const voi
   S = (KT + per - 1) / per;  // no empty slices
   if (S == 1) full = tiles;
   if (full < tiles) {
-    const long long need = (long long)(tiles - full) * S * SLAB;
+    const long long need = (long long)(tiles - full) * S * (256 * bn);
     if (!ws || !counters || n_counters < tiles - full || need > ws_floats) return 1;
   }
   Args a{(pa::bf16*)y, (const pa::bf16*)x, (const pa::bf16*)wp, (const pa::bf16*)resid, ws, counters,
@@ -461,8 +701,10 @@ extern "C" int pa_prefill_gemm(void* y, const void* x, const void* wp, const voi
   const int grid = full + (tiles - full) * S;
 #define PA_PF(E, NRM)                                                                                \
   do {                                                                                               \
-    if (g_pf_variant == 1) hipLaunchKernelGGL((prefill_gemm_kernel<E, NRM, true>), dim3(grid), dim3(512), 0, st, a); \
-    else hipLaunchKernelGGL((prefill_gemm_kernel<E, NRM, false>), dim3(grid), dim3(512), 0, st, a);                 \
+    if (bn == 128) hipLaunchKernelGGL((prefill_gemm_n128_kernel<E, NRM>), dim3(grid), dim3(512), 0, st, a);        \
+    else if (g_pf_variant == 2) hipLaunchKernelGGL((prefill_gemm_kernel<E, NRM, true, 4>), dim3(grid), dim3(256), 0, st, a); \
+    else if (g_pf_variant == 1) hipLaunchKernelGGL((prefill_gemm_kernel<E, NRM, true, 8>), dim3(grid), dim3(512), 0, st, a); \
+    else hipLaunchKernelGGL((prefill_gemm_kernel<E, NRM, false, 8>), dim3(grid), dim3(512), 0, st, a);                 \
   } while (0)
   switch (epi) {
     case EP_PLAIN:

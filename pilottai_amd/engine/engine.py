@@ -70,6 +70,7 @@ class EngineConfig:
     num_kv_blocks: Optional[int] = None
     kv_cache_gb: Optional[float] = None
     kv_cache_fraction: float = 0.5
+    kv_reserve_gb: float = 20.0  # HBM always left outside the KV pool (graphs, activations, workspaces)
     prefix_caching: bool = True
     dedup_inflight_prefix: bool = True  # requests wait for an identical prefix another request is prefilling
     split_decode: bool = True
@@ -199,7 +200,9 @@ class LLMEngine:
                 nb = int(cfg.kv_cache_gb * (1 << 30)) // bpb
             elif self.on_gpu:
                 free, _total = torch.cuda.mem_get_info(self.device)
-                nb = int(free * cfg.kv_cache_fraction) // bpb
+                # a fraction of what is free, but never into the reserve: beside a 205 GB
+                # memory index (config 4) 15 % of the rest is too little for the graphs
+                nb = int(max(0.0, min(free * cfg.kv_cache_fraction, free - cfg.kv_reserve_gb * (1 << 30)))) // bpb
             else:
                 nb = 2048
         need_min = (self.max_model_len + cfg.block_size - 1) // cfg.block_size + 1
@@ -270,6 +273,7 @@ class LLMEngine:
         self._wake = threading.Event()
         self._reqs: Dict[int, _Request] = {}
         self._pending_out: list = []  # finished outputs delivered during the next step's GPU time
+        self._embed_ready: dict = {}  # pooling slot -> embedding read at its step's commit
         self._next_id = 1
         self._id_lock = threading.Lock()
         self._thread: Optional[threading.Thread] = None
@@ -277,6 +281,7 @@ class LLMEngine:
         self._err: Optional[BaseException] = None
         self.timings: "deque" = deque(maxlen=1 << 20)  # (ttft_s, tpot_s, output_tokens) per request
         self.stats = {"steps": 0, "tokens": 0, "sampled": 0, "requests": 0, "finished": 0,
+                      "embed_requests": 0, "embed_tokens": 0,
                       "busy_s": 0.0, "prefill_tokens": 0, "decode_steps": 0, "graph_replays": 0,
                       "bucket_tokens": 0, "host_sched_s": 0.0, "host_launch_s": 0.0, "device_wait_s": 0.0,
                       "host_commit_s": 0.0, "host_deliver_s": 0.0}
@@ -647,10 +652,15 @@ class LLMEngine:
     def _deliver(self, o):
         rid, toks, reason, plen, cached, nsamp, nforced, t_first, t_fin, eslot = o
         emb = None
-        if eslot >= 0:  # the request's pooling row: read it (finished) and clear it for reuse
+        if eslot >= 0 and eslot in self._embed_ready:  # read back when its step committed
+            emb = self._embed_ready.pop(eslot)
+        elif eslot >= 0:  # (aborted / not yet read) the request's pooling row: read and clear it
             if reason == 3:
                 emb = (self._embed_pool[eslot] / max(1, plen)).cpu().numpy()
             self._embed_pool[eslot].zero_()
+        if reason == 3:
+            self.stats["embed_requests"] += 1
+            self.stats["embed_tokens"] += plen - cached
         req = self._reqs.pop(rid, None)
         self.stats["finished"] += 1
         if req is None:
@@ -714,6 +724,8 @@ class LLMEngine:
         t_sync = time.perf_counter()
         with trace_range("engine.commit"):
             outs = self.sched.commit(self._sampled_host.data_ptr(), nsamp)
+        if embed:
+            self._read_embeddings(outs)
         st = self.stats
         # host-side phases: schedule, metadata copy + launch, device wait, commit
         st["host_sched_s"] += t_sched - t0
@@ -734,6 +746,19 @@ class LLMEngine:
         if not self.sched.has_work():
             self._flush_deliveries()  # nothing to overlap with: deliver now
         return True
+
+    def _read_embeddings(self, outs):
+        """Pooled rows of the embedding requests this step finished, read while the device
+        is idle (step synchronised): their delivery runs during the NEXT step, where a read
+        would wait for that step to finish."""
+        done = [(o[9], max(1, o[3])) for o in outs if o[9] >= 0 and o[2] == 3]
+        if not done:
+            return
+        idx = torch.tensor([e for e, _ in done], dtype=torch.long, device=self.device)
+        rows = self._embed_pool.index_select(0, idx).cpu().numpy()
+        self._embed_pool.index_fill_(0, idx, 0.0)
+        for (e, plen), r in zip(done, rows):
+            self._embed_ready[e] = r / plen
 
     def _flush_deliveries(self):
         if self._pending_out:

@@ -4,11 +4,14 @@ The reference's agents consult memory inside their work, one query at a time
 (pilott/memory/enhanced_memory.py:93-116 `semantic_search`, called from
 docs/examples/pdf_processing/example_agents.py:328-331). With 64 workers on one
 GPU that is 64 separate scans of the index per agent step. Here every agent step
-`await`s `MemoryLookupBatcher.search(...)`; the requests that arrive within one
-event-loop tick are answered by ONE `EnhancedMemory.search_batch` call, i.e. one
+`await`s `MemoryLookupBatcher.search(...)`; ONE flush task at a time answers every
+request pending when it starts by ONE `EnhancedMemory.search_batch` call, i.e. one
 streaming pass of the HIP cosine top-k kernel over the HBM-resident rows
 (csrc/ops/similarity.hip, up to 64 queries per pass), on the same GPU as the
-engine. Writes (`store`) are coalesced the same way.
+engine; requests that arrive while a pass runs wait for the next pass together.
+(A flush per event-loop tick queued behind the index lock instead: at 100M rows,
+33 ms per pass, that was 190 passes for 384 lookups.) Writes (`store`) are coalesced
+the same way.
 
 `stats` reports lookups, passes and the device time of the passes (HIP events around
 the kernel on the index's own stream; beside a busy engine that span also contains any
@@ -31,6 +34,7 @@ class MemoryLookupBatcher:
         self._pending: List[Tuple[str, Optional[Set[str]], int, int, "asyncio.Future"]] = []
         self._writes: List[Tuple[str, Dict[str, Any], Set[str], int, "asyncio.Future"]] = []
         self._flush_scheduled = False
+        self._active = False  # a flush task is running (it drains everything pending)
         if time_device and getattr(getattr(memory.index, "device", None), "type", "cpu") == "cuda":
             memory.index.pass_events = []  # the index records (start, end) around each pass
         self.stats = {"lookups": 0, "passes": 0, "stores": 0, "store_batches": 0, "host_s": 0.0,
@@ -68,9 +72,18 @@ class MemoryLookupBatcher:
 
     def _start_flush(self):
         self._flush_scheduled = False
-        asyncio.ensure_future(self._flush())
+        if not self._active:
+            asyncio.ensure_future(self._flush())
 
     async def _flush(self):
+        self._active = True
+        try:
+            while self._writes or self._pending:
+                await self._flush_once()
+        finally:
+            self._active = False
+
+    async def _flush_once(self):
         writes, self._writes = self._writes, []
         if writes:
             try:
@@ -85,7 +98,7 @@ class MemoryLookupBatcher:
                         w[4].set_exception(e)
             self.stats["stores"] += len(writes)
             self.stats["store_batches"] += 1
-        while self._pending:
+        if self._pending:
             batch, self._pending = self._pending[: self.max_batch], self._pending[self.max_batch:]
             limit = max(b[3] for b in batch)
             t0 = time.perf_counter()

@@ -1,5 +1,5 @@
-"""Large-M packed-weight projections (csrc/ops/gemm_prefill.hip: 256 x 256 MFMA tiles,
-LDS-DMA pieces, fused epilogues) vs fp32 PyTorch references."""
+"""Large-M packed-weight projections (csrc/ops/gemm_prefill.hip: 256 x 256 and 256 x 128
+MFMA tiles, LDS-DMA stages, fused epilogues) vs fp32 PyTorch references."""
 import pytest
 import torch
 
@@ -23,7 +23,8 @@ def _bf(*shape, dev, scale=1.0):
     (272, 2048, 1024, "plain", False, 3, 2), (64, 1024, 512, "silu", False, -1, 0),
     (1000, 1280, 8192, "rope_perm", True, 0, 2),  # 70B TP=8 QKV shard
     (17, 768, 128, "plain", True, -1, 1), (256, 512, 64, "resid", False, 0, 1)])
-def test_prefill_gemm(gpu, M, N, K, epi, norm, full, splits):
+@pytest.mark.parametrize("bn", [256, 128])
+def test_prefill_gemm(gpu, M, N, K, epi, norm, full, splits, bn):
     """Every epilogue and the folded row norm; run twice so the self-resetting tickets of
     the split tail are exercised."""
     torch.manual_seed(21)
@@ -40,24 +41,26 @@ def test_prefill_gemm(gpu, M, N, K, epi, norm, full, splits):
     elif epi == "resid":
         acc = acc + resid.float()
     for _ in range(2):
-        y = ops.prefill_gemm(x, wp, epi, resid=resid, norm=norm, full=full, splits=splits)
+        y = ops.prefill_gemm(x, wp, epi, resid=resid, norm=norm, full=full, splits=splits, bn=bn)
         torch.testing.assert_close(y.float(), acc, atol=4e-2, rtol=2e-2)
 
 
-def test_prefill_gemm_asymmetric_identity(gpu):
+@pytest.mark.parametrize("bn", [256, 128])
+def test_prefill_gemm_asymmetric_identity(gpu, bn):
     """x = I (rows), W asymmetric: the output must be exactly W^T's rows (catches a
     transposed or permuted C write, guide §3 'A = I-check with asymmetric B')."""
     M, N, K = 512, 1024, 512
     x = torch.zeros(M, K, device=gpu)
     x[torch.arange(M), torch.arange(M) % K] = 1.0
     w = (torch.arange(N * K, device=gpu, dtype=torch.float32).view(N, K) % 251 / 64.0).to(torch.bfloat16)
-    y = ops.prefill_gemm(x.to(torch.bfloat16), ops.pack_decode_weight(w), "plain", full=-1, splits=1)
+    y = ops.prefill_gemm(x.to(torch.bfloat16), ops.pack_decode_weight(w), "plain", full=-1, splits=1, bn=bn)
     want = w.float().T[torch.arange(M) % K]
     assert torch.equal(y.float(), want.to(torch.bfloat16).float())
 
 
 @pytest.mark.parametrize("M,S", [(700, 1), (700, 3), (2048, 2)])
-def test_prefill_gemm_resid_in_place_with_row_stats(gpu, M, S):
+@pytest.mark.parametrize("bn", [256, 128])
+def test_prefill_gemm_resid_in_place_with_row_stats(gpu, M, S, bn):
     """h += x W^T in place, accumulating the next norm's row statistics (ss_out) of the
     written bf16 rows and zeroing another buffer (ss_zero); the following norm-folded
     projection consuming them matches rmsnorm + GEMM."""
@@ -71,21 +74,22 @@ def test_prefill_gemm_resid_in_place_with_row_stats(gpu, M, S):
     ss = torch.zeros(M, dtype=torch.float32, device=gpu)
     junk = torch.full((M,), 7.0, device=gpu)
     ops.prefill_gemm(x, ops.pack_decode_weight(w), "resid", resid=hh, out=hh, full=0 if S > 1 else -1,
-                     splits=S, ss_out=ss, ss_zero=junk)
+                     splits=S, ss_out=ss, ss_zero=junk, bn=bn)
     torch.testing.assert_close(hh.float(), want, atol=4e-2, rtol=2e-2)
     torch.testing.assert_close(ss, hh.float().pow(2).sum(-1), rtol=1e-4, atol=1e-2)
     assert float(junk.abs().max()) == 0.0
     w2 = _bf(2048, N, dev=gpu, scale=0.05)
     g = (torch.rand(N, device=gpu) + 0.5).to(torch.bfloat16)
     wg = w2 * g[None, :]
-    y = ops.prefill_gemm(hh, ops.pack_decode_weight(wg), norm=True, ss_in=ss)
+    y = ops.prefill_gemm(hh, ops.pack_decode_weight(wg), norm=True, ss_in=ss, bn=bn)
     xn = hh.float() * torch.rsqrt(hh.float().pow(2).mean(-1, keepdim=True) + 1e-5)
     torch.testing.assert_close(y.float(), xn @ wg.float().T, atol=4e-2, rtol=2e-2)
 
 
 @pytest.mark.parametrize("M,H,KV,K,full,splits", [
     (1024, 32, 8, 4096, -1, 0), (333, 32, 8, 4096, 0, 4), (600, 8, 2, 1024, -1, 1), (2048, 32, 8, 4096, 0, 2)])
-def test_prefill_qkv_rope(gpu, M, H, KV, K, full, splits):
+@pytest.mark.parametrize("bn", [256, 128])
+def test_prefill_qkv_rope(gpu, M, H, KV, K, full, splits, bn):
     """Norm-folded QKV with RoPE + paged KV write vs fp32 projection + reference rope_cache."""
     torch.manual_seed(23)
     N = (H + 2 * KV) * 128
@@ -102,7 +106,7 @@ def test_prefill_qkv_rope(gpu, M, H, KV, K, full, splits):
     vc = torch.zeros(NB, KV, 128, 16, dtype=torch.bfloat16, device=gpu)
     q = torch.empty(M, H, 128, dtype=torch.bfloat16, device=gpu)
     for _ in range(2):
-        ops.prefill_qkv_rope(x, wp, 1e-5, q, kc, vc, pos, slots, cos_sin, H, KV, full=full, splits=splits)
+        ops.prefill_qkv_rope(x, wp, 1e-5, q, kc, vc, pos, slots, cos_sin, H, KV, full=full, splits=splits, bn=bn)
     xn = x.float() * torch.rsqrt(x.float().pow(2).mean(-1, keepdim=True) + 1e-5) * g.float()
     qkv = (xn @ w.float().T).cpu()
     rq = torch.empty(M, H, 128, dtype=torch.float32)
@@ -112,3 +116,34 @@ def test_prefill_qkv_rope(gpu, M, H, KV, K, full, splits):
     torch.testing.assert_close(q.float().cpu(), rq, atol=4e-2, rtol=2e-2)
     torch.testing.assert_close(kc.float().cpu(), rk, atol=4e-2, rtol=2e-2)
     torch.testing.assert_close(vc.float().cpu(), rv, atol=4e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("M,N,K,epi,norm,full,splits", [
+    (2048, 28672, 4096, "silu", True, -1, 0), (1024, 4096, 14336, "resid", False, -1, 0),
+    (777, 6144, 4096, "rope_perm", True, 0, 3), (300, 4096, 4096, "plain", False, -1, 1)])
+def test_prefill_gemm_four_wave_variant(gpu, M, N, K, epi, norm, full, splits):
+    """The 256-wide kernel's 4-wave schedule (2 x 2 waves of 128 x 128, accumulators in
+    AGPRs; prefill_set_variant(2)) against fp32."""
+    from pilottai_amd.ops import kernels
+
+    C = kernels.require_native()
+    torch.manual_seed(24)
+    x = _bf(M, K, dev=gpu)
+    w = _bf(N, K, dev=gpu, scale=0.05)
+    resid = _bf(M, N, dev=gpu) if epi == "resid" else None
+    pack = {"silu": ops.pack_decode_gate_up, "rope_perm": ops.pack_decode_qkv_rope}.get(epi, ops.pack_decode_weight)
+    wp = pack(w)
+    acc = x.float() @ w.float().T
+    if norm:
+        acc = acc * torch.rsqrt(x.float().pow(2).mean(-1, keepdim=True) + 1e-5)
+    if epi == "silu":
+        acc = torch.nn.functional.silu(acc[:, :N // 2]) * acc[:, N // 2:]
+    elif epi == "resid":
+        acc = acc + resid.float()
+    C.prefill_set_variant(2)
+    try:
+        for _ in range(2):
+            y = ops.prefill_gemm(x, wp, epi, resid=resid, norm=norm, full=full, splits=splits, bn=256)
+            torch.testing.assert_close(y.float(), acc, atol=4e-2, rtol=2e-2)
+    finally:
+        C.prefill_set_variant(1)

@@ -49,8 +49,8 @@ def timeit(fn, ncopies):
 C = kernels.require_native()
 
 
-def v0(fn):  # the round-3 first schedule (reads in the phase they feed), for A/B
-    C.prefill_set_variant(0)
+def v0(fn, v=0):  # 256-wide schedule variant v (0: reads in the phase they feed; 2: 4 waves)
+    C.prefill_set_variant(v)
     try:
         return fn()
     finally:
@@ -74,13 +74,22 @@ for name in a.shapes.split(","):
         yf = torch.empty(M, NO, dtype=torch.bfloat16, device="cuda")
         resid = torch.randn(M, N, device="cuda").to(torch.bfloat16) if epi == "resid" else None
         ss = kernels.row_sumsq(x)
-        full_default, s_default, _ = kernels.require_native().prefill_gemm_plan(M, N, K)
+        full_default, s_default, _, bn_default = kernels.require_native().prefill_gemm_plan(M, N, K)
         variants = {
             "lib": lambda i: torch.nn.functional.linear(x, ws[i]),
             "mid": lambda i: kernels.mid_gemm(x, wps[i], "plain", out=y),
             "pf_default": lambda i: kernels.prefill_gemm(x, wps[i], "plain", out=y),
-            "pf_v0": lambda i: v0(lambda: kernels.prefill_gemm(x, wps[i], "plain", out=y)),
-            "pf_whole": lambda i: kernels.prefill_gemm(x, wps[i], "plain", out=y, full=-1, splits=1),
+            "pf256": lambda i: kernels.prefill_gemm(x, wps[i], "plain", out=y, bn=256),
+            "pf128": lambda i: kernels.prefill_gemm(x, wps[i], "plain", out=y, bn=128),
+            "pf128_s2": lambda i: kernels.prefill_gemm(x, wps[i], "plain", out=y, bn=128, full=0, splits=2),
+            "pf128_fused": lambda i: kernels.prefill_gemm(x, fps[i], epi, out=yf if epi == "silu" else y, resid=resid,
+                                                          norm=nrm, ss_in=ss if nrm else None, bn=128),
+            "pf_v0": lambda i: v0(lambda: kernels.prefill_gemm(x, wps[i], "plain", out=y, bn=256)),
+            "pf_w4": lambda i: v0(lambda: kernels.prefill_gemm(x, wps[i], "plain", out=y, bn=256), 2),
+            "pf_w4_fused": lambda i: v0(lambda: kernels.prefill_gemm(x, fps[i], epi, out=yf if epi == "silu" else y,
+                                                                     resid=resid, norm=nrm, ss_in=ss if nrm else None,
+                                                                     bn=256), 2),
+            "pf_whole": lambda i: kernels.prefill_gemm(x, wps[i], "plain", out=y, full=-1, splits=1, bn=256),
             "pf_s2": lambda i: kernels.prefill_gemm(x, wps[i], "plain", out=y, full=0, splits=2),
             "pf_s3": lambda i: kernels.prefill_gemm(x, wps[i], "plain", out=y, full=0, splits=3),
             "pf_s4": lambda i: kernels.prefill_gemm(x, wps[i], "plain", out=y, full=0, splits=4),
@@ -98,7 +107,7 @@ for name in a.shapes.split(","):
                     times[k].append(timeit(fn, ncopies))
                 except (ValueError, RuntimeError):
                     times[k].append(float("nan"))
-        row = {"M": M, "shape": name, "plan": [full_default, s_default]}
+        row = {"M": M, "shape": name, "plan": [full_default, s_default, bn_default]}
         for k in variants:
             row[k] = round(statistics.median(times[k]), 1)
         flop = 2.0 * M * N * K
@@ -108,9 +117,12 @@ for name in a.shapes.split(","):
         row["tflops_lib"] = round(flop / row["lib"] / 1e6, 1) if "lib" in row else None
         if "pf_default" in row:
             row["tflops_pf"] = round(flop / row["pf_default"] / 1e6, 1)
-            yy = kernels.prefill_gemm(x, wps[0], "plain", out=y)
             ref = x.float() @ ws[0].float().T
-            row["err_pf"] = float(((yy.float() - ref).abs().max() / ref.abs().max()))
+            for bn in (256, 128):
+                yy = kernels.prefill_gemm(x, wps[0], "plain", out=y, bn=bn)
+                row[f"err_pf{bn}"] = float(((yy.float() - ref).abs().max() / ref.abs().max()))
+            yy = v0(lambda: kernels.prefill_gemm(x, wps[0], "plain", out=y, bn=256), 2)
+            row["err_pf_w4"] = float(((yy.float() - ref).abs().max() / ref.abs().max()))
         print(json.dumps(row), flush=True)
         if out_f:
             out_f.write(json.dumps(row) + "\n")
