@@ -125,16 +125,9 @@ __global__ __launch_bounds__(NW * 64) void prefill_gemm_kernel(const Args A) {
     kt0 = 0;
     kt1 = KT;
   } else {
-    // split items, remapped the same way: logical item L = slice * ntail + t runs the
-    // tail tiles row-tile fastest per slice, so the row tiles that share a W panel and a
-    // K-slice sit on one XCD (consecutive blockIdx alternate XCDs; without the remap every
-    // tail item fetched its panel slice from HBM)
     const int w2 = bid - A.full;
-    const int ntail = A.MT * A.NT - A.full, nitems = ntail * A.S;
-    const int q8 = nitems >> 3, r8 = nitems & 7, xcd = w2 & 7;
-    const int L = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (w2 >> 3);
-    slice = L / ntail;
-    tile = A.full + L % ntail;
+    tile = A.full + w2 / A.S;
+    slice = w2 % A.S;
     kt0 = slice * A.per;
     kt1 = min(KT, kt0 + A.per);
   }
@@ -437,16 +430,9 @@ __global__ __launch_bounds__(512) void prefill_gemm_n128_kernel(const Args A) {
     kt0 = 0;
     kt1 = KT;
   } else {
-    // split items, remapped the same way: logical item L = slice * ntail + t runs the
-    // tail tiles row-tile fastest per slice, so the row tiles that share a W panel and a
-    // K-slice sit on one XCD (consecutive blockIdx alternate XCDs; without the remap every
-    // tail item fetched its panel slice from HBM)
     const int w2 = bid - A.full;
-    const int ntail = A.MT * A.NT - A.full, nitems = ntail * A.S;
-    const int q8 = nitems >> 3, r8 = nitems & 7, xcd = w2 & 7;
-    const int L = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (w2 >> 3);
-    slice = L / ntail;
-    tile = A.full + L % ntail;
+    tile = A.full + w2 / A.S;
+    slice = w2 % A.S;
     kt0 = slice * A.per;
     kt1 = min(KT, kt0 + A.per);
   }
@@ -606,11 +592,13 @@ __global__ __launch_bounds__(512) void prefill_gemm_n128_kernel(const Args A) {
 // 2 = read-ahead, 4 waves of 128 x 128
 static int g_pf_variant = 1;
 
-// Default decomposition: whole tiles while they fill complete rounds of 256 CUs; the
-// remaining `rem` tiles run over S K-slices, S chosen to minimise the tail's length in
-// whole-tile times, ceil(rem S / 256) / S, plus a small per-split cost (slab traffic and
-// the last arriver's reduction): e.g. 192 tiles -> 4 slices (3 rounds of quarter tiles),
-// 128 -> 2.
+// Default decomposition: whole tiles while they fill complete rounds of 256 CUs; a
+// remainder of at most half a round is split over K so that the last round is (nearly)
+// full. Measured on MI355X (profiles/r3_prefill_gemm_variants.jsonl): a split slice costs
+// far more than its MFMA share — a 256 KiB fp32 slab written per item and read serially
+// by the tile's last arriver at one CU's bandwidth — so 192 leftover tiles run whole (one
+// 75 %-full round: qkv at M = 2,048 106 us) rather than as 768 quarter items (190 us, and
+// the tail items regrouped per XCD did not recover it).
 constexpr long long kWsFloats = 64ll << 20;  // the workspace ops.prefill_workspace allocates
 
 static void plan_default(int M, int N, int K, int bn, int& full, int& S) {
@@ -620,25 +608,18 @@ static void plan_default(int M, int N, int K, int bn, int& full, int& S) {
   full = tiles - rem;
   S = 1;
   if (rem) {
-    float best = 1.f;
-    for (int s = 2; s <= 4; ++s) {
-      if (KT / s < 8 || (long long)rem * s * 256 * bn > kWsFloats) break;
-      const float t = (float)((rem * s + 255) / 256) / s + 0.06f * (s - 1);
-      if (t < best - 1e-4f) {
-        best = t;
-        S = s;
-      }
-    }
+    S = std::max(1, std::min(4, 256 / rem));
+    while (S > 1 && (KT / S < 8 || (long long)rem * S * 256 * bn > kWsFloats)) --S;
     if (S == 1) full = tiles;
   }
 }
 
-// Tile width when the caller leaves it open: 128-wide tiles unless the 256-wide grid
-// already fills whole rounds with fewer tiles.
+// Tile width when the caller leaves it open: 256 x 128 tiles for the narrow projections
+// (N <= 6,144: qkv / o / down of Llama-3-8B, 0.6-0.85x the 256-wide kernel's time at
+// M <= 1,024), 256 x 256 for wide ones (gate_up: 1.08x faster).
 static int pick_bn(int M, int N) {
-  if (N % 256) return 128;
-  const int t256 = ((M + 255) / 256) * (N / 256);
-  return (t256 % 256 == 0) ? 256 : 128;
+  (void)M;
+  return (N % 256 || N <= 6144) ? 128 : 256;
 }
 
 }  // namespace pf

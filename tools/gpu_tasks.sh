@@ -18,6 +18,7 @@
 #   handoff_cost   tools/handoff_cost.py
 #   pfbench        tools/prefill_gemm_bench.py --M $MLIST
 #   anatomy        tools/step_anatomy.py
+#   danat          tools/decode_anatomy.py under rocprofv3 --kernel-trace --stats (decode-step anatomy)
 #   midsweep       tools/mid_gemm_bench.py $MLIST --fused-sweep (mid-path configs, engine epilogues)
 #   pmc            rocprofv3 --pmc passes over $PMC_SCRIPT, one pass per ';'-separated set in
 #                  $PMC_SETS (each set within the per-block slot limits), summarised per kernel
@@ -60,6 +61,13 @@ for t in "$@"; do
     pfbench) run pfbench 900 python -u tools/prefill_gemm_bench.py --M "$MLIST" --out "$OUT/pfbench.jsonl" $PF_ARGS || exit $? ;;
     midsweep) run midsweep 900 python -u tools/mid_gemm_bench.py "$MLIST" --fused-sweep || exit $? ;;
     anatomy) run anatomy 600 python -u tools/step_anatomy.py $ANATOMY_ARGS || exit $? ;;
+    danat)
+      P=/tmp/pilottai_danat
+      rm -rf "$P" && mkdir -p "$P"
+      run danat 600 rocprofv3 --kernel-trace --stats -d "$P" -o d -- python3 -u tools/decode_anatomy.py --part engine --out "$OUT/danat.jsonl" || exit $?
+      python3 tools/prof_summary.py "$P"/*/*.db "$P"/*.db --after-frac 0.5 --top 40 > "$OUT/danat_kernels.md" 2>&1 || exit $?
+      run danat_proj 600 python3 -u tools/decode_anatomy.py --part proj --out "$OUT/danat.jsonl" || exit $?
+      ;;
     pmc)
       i=0
       IFS=';' read -ra SETS <<< "$PMC_SETS"
