@@ -1,0 +1,306 @@
+// Ping-pong 256 x 256 MFMA GEMM for the large-M projections (included by
+// gemm_prefill.hip, which owns the argument struct, the planner and the launcher).
+//
+//     y[M, N] = epi( rownorm(x)[M, K] · W[N, K]^T )      bf16 in/out, fp32 accumulate
+//
+// Structure (cdna_hip_programming.md §5 "The 256² 8-phase template", re-derived for the
+// operands this engine holds):
+//
+//   * 512 threads = two wave GROUPS of 4 (waves 0-3, 4-7; a SIMD hosts one wave of each).
+//     Group G owns W rows [128 G, 128 G + 128) of the tile, wave wc = wid & 3 owns tokens
+//     [64 wc, 64 wc + 64): 128 x 64 outputs per wave, acc[8 n-frags][4 m-frags] of
+//     v_mfma_f32_16x16x32_bf16 run as C^T = W · x^T, so each lane ends with 4 consecutive
+//     output columns of one token (the packed_epi.h register epilogues).
+//   * the groups run half a phase apart (one extra s_barrier for group 1 up front): while
+//     group 0 runs its MFMA segment, group 1 issues its LDS reads and LDS-DMA pieces, and
+//     vice versa, so every SIMD pairs one matrix-bound wave with one memory-bound wave.
+//   * a 64-k tile lives in one of two 64-KiB LDS buffers as four 16-KiB PARTS:
+//       A0 = W n-frags 0-3 of both groups, A1 = W n-frags 4-7 (packed fragment-major W:
+//            one 1-KiB chunk per LDS-DMA wave instruction, lane-linear, conflict-free reads),
+//       B0 = token frags 0-1 of every wave, B1 = token frags 2-3 (x rows in full 128-B lines,
+//            16-B units XOR-swizzled by (row >> 1) on the SOURCE address).
+//   * one 64-k tile = 4 phases of 16 MFMAs (one output quadrant x K = 64):
+//         phase  reads (this tile)   MFMA quadrant     LDS-DMA issued         vmcnt
+//         0      A0 (8), B0 (4)      n 0-3  x m 0-1    B1 of tile t + 1        8
+//         1      B1 (4)              n 0-3  x m 2-3    A1 of tile t + 1        8
+//         2      A1 (8)              n 4-7  x m 2-3    A0 of tile t + 2        -
+//         3      -                   n 4-7  x m 0-1    B0 of tile t + 2        8
+//     Each part is read in ONE phase, so it can be restaged two phases later (A0 / B0 of
+//     tile t + 2 after phase 0 of tile t) and four parts (64 KiB, ~4 phases) stay in flight
+//     across the raw s_barriers; the counted vmcnt before a phase's first barrier retires
+//     exactly the part(s) the next phase reads (guide: "read a staged buffer one phase after
+//     the wait that retires it"). No vmcnt(0) and no __syncthreads() inside the loop.
+//   * s_setprio(1) around every 16-MFMA cluster (guide §5.5 T5).
+//
+// Work items are those of the prefill launcher: whole tiles (XCD-aware bijective remap, row
+// tiles of one W panel on one XCD) and, for the remainder, K-slices whose fp32 partials
+// are handed to the tile's last arriver through common.h handoff_last.
+#pragma once
+#include "common.h"
+#include "packed_epi.h"
+
+namespace pa {
+namespace pf {
+
+constexpr int PP_PART = 16384;
+constexpr int PP_BUF = 4 * PP_PART;
+
+// STAMP (diagnostic build, whole tiles only): workgroup b's thread 0 writes s_memtime at
+// entry / after the prologue / after the k-loop / after the epilogue and s_memrealtime at
+// entry and exit to A.ws[8 b ..] (as uint64) -- a buffer no output is computed from.
+template <int EPI, bool NORM, bool STAMP = false>
+__global__ __launch_bounds__(512) void pingpong_gemm_kernel(const Args A) {
+  uint64_t st0 = 0, st1 = 0, st2 = 0, rt0 = 0;
+  if constexpr (STAMP) {
+    st0 = __builtin_amdgcn_s_memtime();
+    rt0 = __builtin_amdgcn_s_memrealtime();
+  }
+  __shared__ __attribute__((aligned(1024))) char smem[2 * PP_BUF];
+
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int G = wid >> 2, wc = wid & 3;
+  const int g = lane >> 4, c = lane & 15;
+
+  const int bid = blockIdx.x;
+  const int KT = A.K >> 6;
+  int tile, kt0, kt1, slice = -1;
+  if (bid < A.full) {
+    const int q8 = A.full >> 3, r8 = A.full & 7, xcd = bid & 7;
+    tile = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+    kt0 = 0;
+    kt1 = KT;
+  } else {
+    const int nb = gridDim.x - A.full, w0 = bid - A.full;
+    const int q8 = nb >> 3, r8 = nb & 7, xcd = w0 & 7;
+    const int w2 = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (w0 >> 3);
+    tile = A.full + w2 / A.S;
+    slice = w2 % A.S;
+    kt0 = slice * A.per;
+    kt1 = min(KT, kt0 + A.per);
+  }
+  const int mt = tile % A.MT, nt = tile / A.MT;
+  const int row0 = mt * 256;
+  const int nk = kt1 - kt0;  // >= 2 (launcher)
+
+  if (A.ss_zero && blockIdx.x == 0)
+    for (int i = threadIdx.x; i < A.M; i += 512) A.ss_zero[i] = 0.f;
+
+  // ---- LDS-DMA sources. Every part is 16 wave instructions, two per wave.
+  // W part r: chunk q = 2 wid + h (h = 0, 1) is n-frag (wid & 3) of group (wid >> 2),
+  // k-half h of the 64-k tile: n16 tile nt * 16 + (wid >> 2) * 8 + r * 4 + (wid & 3).
+  const int KS = A.K >> 5;
+  const bf16* wsrc[2];
+#pragma unroll
+  for (int r = 0; r < 2; ++r)
+    wsrc[r] = A.wp + ((size_t)(nt * 16 + G * 8 + r * 4 + wc) * KS) * 512 + lane * 8;
+  // x part c: LDS row lr = (2 wid + h) * 8 + (lane >> 3) holds token (lr >> 5) * 64 + 32 c +
+  // (lr & 31); its 16-B unit (lane & 7) is the row's logical unit (lane & 7) ^ ((lr >> 1) & 7).
+  const bf16* xsrc[2][2];
+#pragma unroll
+  for (int cc = 0; cc < 2; ++cc)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int lr = (2 * wid + h) * 8 + (lane >> 3);
+      const int trow = (lr >> 5) * 64 + cc * 32 + (lr & 31);
+      const int gr = min(row0 + trow, A.M - 1);
+      xsrc[cc][h] = A.x + (size_t)gr * A.ldx + (((lane & 7) ^ ((lr >> 1) & 7)) * 8);
+    }
+
+  char* const sbase = smem;
+  auto buf = [&](int t) -> char* { return sbase + (t & 1) * PP_BUF; };
+  auto issue_w = [&](int r, int t) {
+    char* dst = buf(t) + r * PP_PART + (2 * wid) * 1024;
+    const bf16* s = wsrc[r] + (size_t)(2 * (kt0 + t)) * 512;
+    glds16(s, dst);
+    glds16(s + 512, dst + 1024);
+  };
+  auto issue_x = [&](int cc, int t) {
+    char* dst = buf(t) + (2 + cc) * PP_PART + (2 * wid) * 1024;
+    const size_t ko = (size_t)(kt0 + t) * 64;
+    glds16(xsrc[cc][0] + ko, dst);
+    glds16(xsrc[cc][1] + ko, dst + 1024);
+  };
+  // fragment reads: W frags of part r (4 n-frags x 2 k-halves), x frags of part cc
+  // (2 token frags x 2 k-halves)
+  auto read_w = [&](int r, int t, bf16x8(&af)[4][2]) {
+    const char* p = buf(t) + r * PP_PART + (G * 8) * 1024 + lane * 16;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) af[i][h] = *reinterpret_cast<const bf16x8*>(p + (2 * i + h) * 1024);
+  };
+  auto read_x = [&](int cc, int t, bf16x8(&bfr)[2][2]) {
+    const char* p = buf(t) + (2 + cc) * PP_PART;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int lr = wc * 32 + 16 * j + c;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int u = 4 * h + g;
+        bfr[j][h] = *reinterpret_cast<const bf16x8*>(p + lr * 128 + ((u ^ ((lr >> 1) & 7)) << 4));
+      }
+    }
+  };
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // 16 MFMAs of quadrant (W part r, x part cc)
+  auto mma = [&](auto rr, auto ccc, const bf16x8(&af)[4][2], const bf16x8(&bfr)[2][2]) {
+    constexpr int r = decltype(rr)::value, cc = decltype(ccc)::value;
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[r * 4 + i][cc * 2 + j] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][h], bfr[j][h], acc[r * 4 + i][cc * 2 + j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  auto lgkm0 = [] { __builtin_amdgcn_s_waitcnt(0xC07F); };
+
+  bf16x8 af[4][2], bx0[2][2], bx1[2][2];
+
+  // One 64-k tile. ST: 0 steady (tiles t + 1 and t + 2 exist), 1 = tile nk - 2 (only t + 1
+  // left to issue), 2 = the last tile.
+  auto body = [&](int t, auto st) {
+    constexpr int S = decltype(st)::value;
+    // phase 0
+    read_w(0, t, af);
+    read_x(0, t, bx0);
+    if constexpr (S < 2) issue_x(1, t + 1);
+    if constexpr (S < 2) wait_vm<8>(); else wait_vm<2>();
+    raw_barrier();
+    lgkm0();
+    mma(ic<0>{}, ic<0>{}, af, bx0);
+    raw_barrier();
+    // phase 1
+    read_x(1, t, bx1);
+    if constexpr (S < 2) issue_w(1, t + 1);
+    if constexpr (S < 2) wait_vm<8>(); else wait_vm<0>();
+    raw_barrier();
+    lgkm0();
+    mma(ic<0>{}, ic<1>{}, af, bx1);
+    raw_barrier();
+    // phase 2
+    read_w(1, t, af);
+    if constexpr (S == 0) issue_w(0, t + 2);
+    raw_barrier();
+    lgkm0();
+    mma(ic<1>{}, ic<1>{}, af, bx1);
+    raw_barrier();
+    // phase 3
+    if constexpr (S == 0) {
+      issue_x(0, t + 2);
+      wait_vm<8>();
+    } else if constexpr (S == 1) {
+      wait_vm<4>();
+    }
+    raw_barrier();
+    mma(ic<1>{}, ic<0>{}, af, bx0);
+    raw_barrier();
+  };
+
+  // prologue: parts of tiles 0 and 1 in steady-state issue order
+  issue_w(0, 0);
+  issue_x(0, 0);
+  issue_x(1, 0);
+  issue_w(1, 0);
+  issue_w(0, 1);
+  issue_x(0, 1);
+  wait_vm<8>();  // A0 and B0 of tile 0 landed
+  raw_barrier();
+  if (G == 1) raw_barrier();  // stagger: group 1 runs half a phase behind group 0
+  if constexpr (STAMP) st1 = __builtin_amdgcn_s_memtime();
+
+  int t = 0;
+  for (; t + 2 < nk; ++t) body(t, ic<0>{});
+  body(t, ic<1>{});
+  body(t + 1, ic<2>{});
+  if (G == 0) raw_barrier();  // balance the stagger
+  if constexpr (STAMP) st2 = __builtin_amdgcn_s_memtime();
+
+  // ---- split tiles: publish, the last arriver sums the other slices into its registers
+  if (slice >= 0) {
+    float* base = A.ws + (size_t)(tile - A.full) * A.S * SLAB;
+    {
+      const __amdgpu_buffer_rsrc_t rs =
+          __builtin_amdgcn_make_buffer_rsrc(base + (size_t)slice * SLAB, 0, SLAB * 4, 0x00020000);
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i][j]), rs,
+                                                 (((wid * 8 + i) * 4 + j) * 64 + lane) * 16, 0, 16);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (!handoff_last(A.counters + (tile - A.full), A.S, reinterpret_cast<int*>(smem), A.acq)) return;
+    for (int p = 0; p < A.S; ++p) {
+      if (p == slice) continue;
+      const __amdgpu_buffer_rsrc_t rp =
+          __builtin_amdgcn_make_buffer_rsrc(base + (size_t)p * SLAB, 0, SLAB * 4, 0x00020000);
+#pragma unroll
+      for (int i = 0; i < 8; i += 2) {
+        f32x4 tt[2][4];
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            tt[h][j] = __builtin_bit_cast(
+                f32x4, __builtin_amdgcn_raw_buffer_load_b128(rp, (((wid * 8 + i + h) * 4 + j) * 64 + lane) * 16, 0, 16));
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[i + h][j] += tt[h][j];
+      }
+    }
+  }
+
+  // ---- register epilogue: acc[i][j] holds token row0 + 64 wc + 16 j + c, columns
+  // 4 g .. 4 g + 3 of 16-column tile nt * 16 + 8 G + i
+  const float inv_k = 1.f / (float)A.K;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int m = row0 + wc * 64 + 16 * j + c;
+    const bool ok = m < A.M;
+    float sq = 0.f;
+    if (ok) {
+      float rs = 1.f;
+      if constexpr (NORM) rs = rsqrtf(A.ss_in[m] * inv_k + A.eps);
+      if constexpr (pair_epi<EPI>()) {
+#pragma unroll
+        for (int i = 0; i < 8; i += 2)
+          store_quad<EPI>(A, m, nt * 16 + G * 8 + i, 4 * g, acc[i][j] * rs, acc[i + 1][j] * rs);
+      } else {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) sq += store_quad<EPI>(A, m, nt * 16 + G * 8 + i, 4 * g, acc[i][j] * rs, acc[i][j]);
+      }
+    }
+    if constexpr (EPI == EP_RESID) {
+      if (A.ss_out) {
+        sq += __shfl_xor(sq, 16, 64);
+        sq += __shfl_xor(sq, 32, 64);
+        if (ok && g == 0) atomicAdd(A.ss_out + m, sq);
+      }
+    }
+  }
+  if constexpr (STAMP) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint64_t st3 = __builtin_amdgcn_s_memtime(), rt1 = __builtin_amdgcn_s_memrealtime();
+    if (threadIdx.x == 0) {
+      uint64_t* d = reinterpret_cast<uint64_t*>(A.ws) + (size_t)blockIdx.x * 8;
+      const uint64_t v[8] = {st0, st1, st2, st3, rt0, rt1, (uint64_t)tile, 0};
+#pragma unroll
+      for (int q = 0; q < 8; ++q) __hip_atomic_store(d + q, v[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+}  // namespace pf
+}  // namespace pa

@@ -588,9 +588,19 @@ __global__ __launch_bounds__(512) void prefill_gemm_n128_kernel(const Args A) {
   }
 }
 
-// 256-wide main loop: 1 = read-ahead, 8 waves (default); 0 = reads in the phase they feed;
-// 2 = read-ahead, 4 waves of 128 x 128
-static int g_pf_variant = 1;
+}  // namespace pf
+}  // namespace pa
+
+#include "gemm_pingpong.h"
+
+namespace pa {
+namespace pf {
+
+// 256-wide main loop: 3 = ping-pong wave groups (gemm_pingpong.h, default; items of < 2
+// k-tiles fall back to 1); 1 = read-ahead, 8 waves; 0 = reads in the phase they feed;
+// 2 = read-ahead, 4 waves of 128 x 128; 4 = the ping-pong kernel's cycle-stamp build
+constexpr int kPfDefaultVariant = 3;
+static int g_pf_variant = kPfDefaultVariant;
 
 // Default decomposition: whole tiles while they fill complete rounds of 256 CUs; a
 // remainder of at most half a round is split over K so that the last round is (nearly)
@@ -625,7 +635,7 @@ static int pick_bn(int M, int N) {
 }  // namespace pf
 }  // namespace pa
 
-extern "C" void pa_prefill_set_variant(int v) { pa::pf::g_pf_variant = v; }
+extern "C" void pa_prefill_set_variant(int v) { pa::pf::g_pf_variant = v < 0 ? pa::pf::kPfDefaultVariant : v; }
 
 extern "C" int pa_prefill_pick_bn(int M, int N) { return pa::pf::pick_bn(M, N); }
 
@@ -671,6 +681,9 @@ extern "C" int pa_prefill_gemm(void* y, const void* x, const void* wp, const voi
   int per = (KT + S - 1) / S;
   S = (KT + per - 1) / per;  // no empty slices
   if (S == 1) full = tiles;
+  // the ping-pong kernel's schedule needs >= 2 k-tiles per work item
+  int variant = g_pf_variant;
+  if (variant >= 3 && (KT < 2 || (S > 1 && (per < 2 || KT - (S - 1) * per < 2)))) variant = 1;
   if (full < tiles) {
     const long long need = (long long)(tiles - full) * S * (256 * bn);
     if (!ws || !counters || n_counters < tiles - full || need > ws_floats) return 1;
@@ -683,8 +696,11 @@ extern "C" int pa_prefill_gemm(void* y, const void* x, const void* wp, const voi
 #define PA_PF(E, NRM)                                                                                \
   do {                                                                                               \
     if (bn == 128) hipLaunchKernelGGL((prefill_gemm_n128_kernel<E, NRM>), dim3(grid), dim3(512), 0, st, a);        \
-    else if (g_pf_variant == 2) hipLaunchKernelGGL((prefill_gemm_kernel<E, NRM, true, 4>), dim3(grid), dim3(256), 0, st, a); \
-    else if (g_pf_variant == 1) hipLaunchKernelGGL((prefill_gemm_kernel<E, NRM, true, 8>), dim3(grid), dim3(512), 0, st, a); \
+    else if (variant == 4 && E == EP_PLAIN && !NRM && full == tiles)                                 \
+      hipLaunchKernelGGL((pingpong_gemm_kernel<EP_PLAIN, false, true>), dim3(grid), dim3(512), 0, st, a);      \
+    else if (variant >= 3) hipLaunchKernelGGL((pingpong_gemm_kernel<E, NRM>), dim3(grid), dim3(512), 0, st, a); \
+    else if (variant == 2) hipLaunchKernelGGL((prefill_gemm_kernel<E, NRM, true, 4>), dim3(grid), dim3(256), 0, st, a); \
+    else if (variant == 1) hipLaunchKernelGGL((prefill_gemm_kernel<E, NRM, true, 8>), dim3(grid), dim3(512), 0, st, a); \
     else hipLaunchKernelGGL((prefill_gemm_kernel<E, NRM, false, 8>), dim3(grid), dim3(512), 0, st, a);                 \
   } while (0)
   switch (epi) {

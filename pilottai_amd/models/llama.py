@@ -137,21 +137,20 @@ class LlamaModel:
     # (csrc/ops/gemm_mid.hip) with every norm / SwiGLU / residual / RoPE + KV write fused
     MID_MAX_T = 256
     # steps above MID_MAX_T and up to this many tokens run the same fused packed-weight layer
-    # with the prefill kernels (csrc/ops/gemm_prefill.hip: 256 x 128 tiles for qkv / o / down,
-    # 256 x 256 for gate_up) for the projections PF_CFG assigns to them; larger steps take
-    # the library GEMMs + elementwise kernels. End to end, 64 workers, same box, 2 runs each
-    # (profiles/r3_prefill_path_ab.jsonl): 416-512-token steps 2-4 % faster on the fused
-    # kernels, 640-768-token steps 3-7 % slower, 2,048-token steps 27.0 vs 25.8 ms.
-    # EngineConfig.prefill_max_t / bench.py --prefill-max-t move the boundary (0 = off).
-    PREFILL_MAX_T = 512
+    # with the prefill kernels (csrc/ops/gemm_prefill.hip) for the projections PF_CFG assigns
+    # to them: the ping-pong 256 x 256 kernel (gemm_pingpong.h) for qkv / gate_up / down,
+    # 256 x 128 tiles for o; no library GEMM and no separate norm / SwiGLU / RoPE launch.
+    # EngineConfig.prefill_max_t / bench.py --prefill-max-t move the boundary (0 = off:
+    # library GEMMs + elementwise kernels above MID_MAX_T).
+    PREFILL_MAX_T = 1 << 30
     # per projection: (largest M, path, config); the first row whose M covers the step is used.
-    # "pf": prefill kernel (full = whole tiles, -1 = the kernel's plan; splits of the rest),
-    # "mid": mid kernel (fm, fn, splits as MID_CFG)
+    # "pf": prefill kernel (full = whole tiles, -1 = the kernel's plan; splits of the rest;
+    # bn = tile width), "mid": mid kernel (fm, fn, splits as MID_CFG)
     PF_CFG = {
-        "qkv": [(1 << 30, "pf", {"full": -1, "splits": 0})],
-        "o": [(1 << 30, "pf", {"full": -1, "splits": 0})],
-        "gate_up": [(1 << 30, "pf", {"full": -1, "splits": 0})],
-        "down": [(1 << 30, "pf", {"full": -1, "splits": 0})],
+        "qkv": [(1 << 30, "pf", {"full": -1, "splits": 0, "bn": 256})],
+        "o": [(1 << 30, "pf", {"full": -1, "splits": 0, "bn": 128})],
+        "gate_up": [(1 << 30, "pf", {"full": -1, "splits": 0, "bn": 256})],
+        "down": [(1 << 30, "pf", {"full": -1, "splits": 0, "bn": 256})],
     }
     # decode/small steps: let the attention launch's idle workgroups read the O
     # projection's weights into the Infinity Cache (MALL-resident weights run the 34 MB

@@ -23,10 +23,21 @@ def _bf(*shape, dev, scale=1.0):
     (272, 2048, 1024, "plain", False, 3, 2), (64, 1024, 512, "silu", False, -1, 0),
     (1000, 1280, 8192, "rope_perm", True, 0, 2),  # 70B TP=8 QKV shard
     (17, 768, 128, "plain", True, -1, 1), (256, 512, 64, "resid", False, 0, 1)])
-@pytest.mark.parametrize("bn", [256, 128])
-def test_prefill_gemm(gpu, M, N, K, epi, norm, full, splits, bn):
+@pytest.mark.parametrize("bn,variant", [(256, 3), (256, 1), (128, -1)])
+def test_prefill_gemm(gpu, M, N, K, epi, norm, full, splits, bn, variant):
     """Every epilogue and the folded row norm; run twice so the self-resetting tickets of
-    the split tail are exercised."""
+    the split tail are exercised. 256-wide tiles on the ping-pong kernel (variant 3, the
+    default) and on the read-ahead kernel (variant 1, the fallback for < 2 k-tiles)."""
+    from pilottai_amd.ops import kernels
+
+    kernels.require_native().prefill_set_variant(variant)
+    try:
+        _check_prefill_gemm(gpu, M, N, K, epi, norm, full, splits, bn)
+    finally:
+        kernels.require_native().prefill_set_variant(-1)
+
+
+def _check_prefill_gemm(gpu, M, N, K, epi, norm, full, splits, bn):
     torch.manual_seed(21)
     x = _bf(M, K, dev=gpu)
     w = _bf(N, K, dev=gpu, scale=0.05)
@@ -146,4 +157,4 @@ def test_prefill_gemm_four_wave_variant(gpu, M, N, K, epi, norm, full, splits):
             y = ops.prefill_gemm(x, wp, epi, resid=resid, norm=norm, full=full, splits=splits, bn=256)
             torch.testing.assert_close(y.float(), acc, atol=4e-2, rtol=2e-2)
     finally:
-        C.prefill_set_variant(1)
+        C.prefill_set_variant(-1)

@@ -20,6 +20,7 @@
 #   anatomy        tools/step_anatomy.py
 #   danat          tools/decode_anatomy.py under rocprofv3 --kernel-trace --stats (decode-step anatomy)
 #   midsweep       tools/mid_gemm_bench.py $MLIST --fused-sweep (mid-path configs, engine epilogues)
+#   cmd            bash -c "$CMD" (log: $CMD_NAME.log, limit $CMD_SECS s)
 #   pmc            rocprofv3 --pmc passes over $PMC_SCRIPT, one pass per ';'-separated set in
 #                  $PMC_SETS (each set within the per-block slot limits), summarised per kernel
 set -o pipefail
@@ -60,6 +61,7 @@ for t in "$@"; do
     handoff_cost) run handoff_cost 300 python -u tools/handoff_cost.py --out "$OUT/handoff_cost.jsonl" || exit $? ;;
     pfbench) run pfbench 900 python -u tools/prefill_gemm_bench.py --M "$MLIST" --out "$OUT/pfbench.jsonl" $PF_ARGS || exit $? ;;
     midsweep) run midsweep 900 python -u tools/mid_gemm_bench.py "$MLIST" --fused-sweep || exit $? ;;
+    cmd) run "${CMD_NAME:-cmd}" "${CMD_SECS:-600}" bash -c "$CMD" || exit $? ;;
     anatomy) run anatomy 600 python -u tools/step_anatomy.py $ANATOMY_ARGS || exit $? ;;
     danat)
       P=/tmp/pilottai_danat

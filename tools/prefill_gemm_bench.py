@@ -29,8 +29,8 @@ ap.add_argument("--variants", default="")
 ap.add_argument("--out", default="")
 a = ap.parse_args()
 load_tuned_gemms("llama-3-8b", 1)
-SHAPES = {"qkv": (6144, 4096), "o": (4096, 4096), "gate_up": (28672, 4096), "down": (4096, 14336)}
-FUSED = {"qkv": ("rope_perm", True), "o": ("resid", False), "gate_up": ("silu", True), "down": ("resid", False)}
+SHAPES = {"sq": (4096, 4096), "qkv": (6144, 4096), "o": (4096, 4096), "gate_up": (28672, 4096), "down": (4096, 14336)}
+FUSED = {"sq": ("resid", False), "qkv": ("rope_perm", True), "o": ("resid", False), "gate_up": ("silu", True), "down": ("resid", False)}
 out_f = open(a.out, "a") if a.out else None
 
 
@@ -54,7 +54,7 @@ def v0(fn, v=0):  # 256-wide schedule variant v (0: reads in the phase they feed
     try:
         return fn()
     finally:
-        C.prefill_set_variant(1)
+        C.prefill_set_variant(-1)
 
 
 torch.manual_seed(0)
@@ -89,6 +89,12 @@ for name in a.shapes.split(","):
             "pf_w4_fused": lambda i: v0(lambda: kernels.prefill_gemm(x, fps[i], epi, out=yf if epi == "silu" else y,
                                                                      resid=resid, norm=nrm, ss_in=ss if nrm else None,
                                                                      bn=256), 2),
+            "pp": lambda i: v0(lambda: kernels.prefill_gemm(x, wps[i], "plain", out=y, bn=256), 3),
+            "pp_whole": lambda i: v0(lambda: kernels.prefill_gemm(x, wps[i], "plain", out=y, full=-1, splits=1, bn=256), 3),
+            "pp_s2": lambda i: v0(lambda: kernels.prefill_gemm(x, wps[i], "plain", out=y, full=0, splits=2, bn=256), 3),
+            "pp_fused": lambda i: v0(lambda: kernels.prefill_gemm(x, fps[i], epi, out=yf if epi == "silu" else y,
+                                                                 resid=resid, norm=nrm, ss_in=ss if nrm else None,
+                                                                 bn=256), 3),
             "pf_whole": lambda i: kernels.prefill_gemm(x, wps[i], "plain", out=y, full=-1, splits=1, bn=256),
             "pf_s2": lambda i: kernels.prefill_gemm(x, wps[i], "plain", out=y, full=0, splits=2),
             "pf_s3": lambda i: kernels.prefill_gemm(x, wps[i], "plain", out=y, full=0, splits=3),
@@ -123,6 +129,15 @@ for name in a.shapes.split(","):
                 row[f"err_pf{bn}"] = float(((yy.float() - ref).abs().max() / ref.abs().max()))
             yy = v0(lambda: kernels.prefill_gemm(x, wps[0], "plain", out=y, bn=256), 2)
             row["err_pf_w4"] = float(((yy.float() - ref).abs().max() / ref.abs().max()))
+        if any(k.startswith("pp") for k in variants):
+            ref = x.float() @ ws[0].float().T
+            for nm, kw in (("pp", {}), ("pp_whole", dict(full=-1, splits=1)), ("pp_s2", dict(full=0, splits=2))):
+                try:
+                    y.fill_(float("nan"))
+                    yy = v0(lambda: kernels.prefill_gemm(x, wps[0], "plain", out=y, bn=256, **kw), 3)
+                    row[f"err_{nm}"] = float(((yy.float() - ref).abs().max() / ref.abs().max()))
+                except (ValueError, RuntimeError):
+                    row[f"err_{nm}"] = None
         print(json.dumps(row), flush=True)
         if out_f:
             out_f.write(json.dumps(row) + "\n")
