@@ -60,7 +60,7 @@ int pa_prefill_gemm(void* y, const void* x, const void* wp, const void* resid, f
                     int* counters, int n_counters, int M, int N, int K, int ldx, int ldy, int ldr, int epi,
                     const float* ss_in, float* ss_out, float* ss_zero, float eps, int full, int splits, int bn,
                     void* q_out, void* k_cache, void* v_cache, const int* positions, const int* slots,
-                    const float* cos_sin, int H, int KV, hipStream_t st);
+                    const float* cos_sin, int H, int KV, int kernel_variant, hipStream_t st);
 int pa_prefetch(const void* p, long long bytes, void* sink, int wgs, hipStream_t st);
 long long pa_cosine_topk_workspace_bytes(int Q, int N, int K);
 int pa_cosine_topk(float* out_scores, int* out_rows, void* workspace, const void* queries,
@@ -432,7 +432,8 @@ bool mid_qkv_rope(at::Tensor x, at::Tensor wp, at::Tensor ss_in, double eps, at:
 // weights with the same epilogues as mid_gemm (0 plain, 1 SwiGLU, 2 residual, 3 rope-perm).
 bool prefill_gemm(at::Tensor y, at::Tensor x, at::Tensor wp, c10::optional<at::Tensor> resid, at::Tensor ws,
                   at::Tensor counters, int64_t epi, c10::optional<at::Tensor> ss_in, c10::optional<at::Tensor> ss_out,
-                  c10::optional<at::Tensor> ss_zero, double eps, int64_t full, int64_t splits, int64_t bn) {
+                  c10::optional<at::Tensor> ss_zero, double eps, int64_t full, int64_t splits, int64_t bn,
+                  int64_t variant) {
   check_gpu(wp, "wp"); check_gpu(ws, "ws"); check_gpu(counters, "counters");
   TORCH_CHECK(x.is_cuda() && x.dim() == 2 && x.stride(1) == 1, "x must be a 2-D GPU tensor, unit inner stride");
   TORCH_CHECK(y.is_cuda() && y.dim() == 2 && y.stride(1) == 1, "y must be a 2-D GPU tensor, unit inner stride");
@@ -462,14 +463,15 @@ bool prefill_gemm(at::Tensor y, at::Tensor x, at::Tensor wp, c10::optional<at::T
                                  (int)epi, opt_rows(ss_in, M, "ss_in"), const_cast<float*>(opt_rows(ss_out, M, "ss_out")),
                                  const_cast<float*>(opt_rows(ss_zero, M, "ss_zero")), (float)eps, (int)full,
                                  (int)splits, (int)bn, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0,
-                                 cur_stream());
+                                 (int)variant, cur_stream());
   TORCH_CHECK(rc >= 0, "prefill_gemm launch failed");
   return rc == 0;
 }
 
 bool prefill_qkv_rope(at::Tensor x, at::Tensor wp, at::Tensor ss_in, double eps, at::Tensor q_out, at::Tensor k_cache,
                       at::Tensor v_cache, at::Tensor positions, at::Tensor slots, at::Tensor cos_sin, int64_t H,
-                      int64_t KV, at::Tensor ws, at::Tensor counters, int64_t full, int64_t splits, int64_t bn) {
+                      int64_t KV, at::Tensor ws, at::Tensor counters, int64_t full, int64_t splits, int64_t bn,
+                      int64_t variant) {
   check_gpu(wp, "wp"); check_gpu(q_out, "q_out"); check_gpu(k_cache, "k_cache"); check_gpu(v_cache, "v_cache");
   check_gpu(positions, "positions"); check_gpu(slots, "slots"); check_gpu(cos_sin, "cos_sin");
   check_gpu(ws, "ws"); check_gpu(counters, "counters");
@@ -497,7 +499,8 @@ bool prefill_qkv_rope(at::Tensor x, at::Tensor wp, at::Tensor ss_in, double eps,
                                  counters.data_ptr<int>(), counters.numel(), M, N, K, x.stride(0), 0, 0, 4,
                                  ss_in.data_ptr<float>(), nullptr, nullptr, (float)eps, (int)full, (int)splits,
                                  (int)bn, q_out.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(), positions.data_ptr<int>(),
-                                 slots.data_ptr<int>(), cos_sin.data_ptr<float>(), (int)H, (int)KV, cur_stream());
+                                 slots.data_ptr<int>(), cos_sin.data_ptr<float>(), (int)H, (int)KV, (int)variant,
+                                 cur_stream());
   TORCH_CHECK(rc >= 0, "prefill_qkv_rope launch failed");
   return rc == 0;
 }
@@ -726,11 +729,11 @@ PYBIND11_MODULE(_C, m) {
   m.def("prefill_gemm", &prefill_gemm, py::arg("y"), py::arg("x"), py::arg("wp"), py::arg("resid"), py::arg("ws"),
         py::arg("counters"), py::arg("epi") = 0, py::arg("ss_in") = py::none(), py::arg("ss_out") = py::none(),
         py::arg("ss_zero") = py::none(), py::arg("eps") = 1e-5, py::arg("full") = -1, py::arg("splits") = 0,
-        py::arg("bn") = 0);
+        py::arg("bn") = 0, py::arg("variant") = -1);
   m.def("prefill_qkv_rope", &prefill_qkv_rope, py::arg("x"), py::arg("wp"), py::arg("ss_in"), py::arg("eps"),
         py::arg("q_out"), py::arg("k_cache"), py::arg("v_cache"), py::arg("positions"), py::arg("slots"),
         py::arg("cos_sin"), py::arg("H"), py::arg("KV"), py::arg("ws"), py::arg("counters"), py::arg("full") = -1,
-        py::arg("splits") = 0, py::arg("bn") = 0);
+        py::arg("splits") = 0, py::arg("bn") = 0, py::arg("variant") = -1);
   m.def("prefill_set_variant", [](int v) { pa_prefill_set_variant(v); });
   m.def("prefill_gemm_plan", &prefill_gemm_plan, py::arg("M"), py::arg("N"), py::arg("K"), py::arg("bn") = 0,
         "default (full tiles, splits, workspace floats, tile width) of prefill_gemm");

@@ -48,14 +48,23 @@ constexpr int PP_BUF = 4 * PP_PART;
 // STAMP (diagnostic build, whole tiles only): workgroup b's thread 0 writes s_memtime at
 // entry / after the prologue / after the k-loop / after the epilogue and s_memrealtime at
 // entry and exit to A.ws[8 b ..] (as uint64) -- a buffer no output is computed from.
-template <int EPI, bool NORM, bool STAMP = false>
+// BUFLD: stage through buffer_load ... lds with one per-lane 32-bit voffset per stream and the
+// k advance in the SGPR soffset (no per-issue 64-bit address arithmetic in the load segment).
+// F = W n-frags per wave: 8 -> 256 x 256 tiles (two 64-KiB buffers of parts A0 A1 B0 B1),
+// 4 -> 256 x 128 tiles (three 48-KiB buffers of parts A B0 B1; schedule at `body4`).
+template <int EPI, bool NORM, bool STAMP = false, bool BUFLD = false, int F = 8>
 __global__ __launch_bounds__(512) void pingpong_gemm_kernel(const Args A) {
+  static_assert(F == 8 || F == 4, "256- or 128-wide tiles");
+  constexpr int NA = F / 4;                 // W parts per 64-k tile
+  constexpr int BUFB = (NA + 2) * PP_PART;  // bytes per tile buffer
+  constexpr int NBUF = F == 8 ? 2 : 3;
+  constexpr int SLABF = 256 * 32 * F;       // floats per split slab
   uint64_t st0 = 0, st1 = 0, st2 = 0, rt0 = 0;
   if constexpr (STAMP) {
     st0 = __builtin_amdgcn_s_memtime();
     rt0 = __builtin_amdgcn_s_memrealtime();
   }
-  __shared__ __attribute__((aligned(1024))) char smem[2 * PP_BUF];
+  __shared__ __attribute__((aligned(1024))) char smem[NBUF * BUFB];
 
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -90,36 +99,69 @@ __global__ __launch_bounds__(512) void pingpong_gemm_kernel(const Args A) {
   // W part r: chunk q = 2 wid + h (h = 0, 1) is n-frag (wid & 3) of group (wid >> 2),
   // k-half h of the 64-k tile: n16 tile nt * 16 + (wid >> 2) * 8 + r * 4 + (wid & 3).
   const int KS = A.K >> 5;
-  const bf16* wsrc[2];
-#pragma unroll
-  for (int r = 0; r < 2; ++r)
-    wsrc[r] = A.wp + ((size_t)(nt * 16 + G * 8 + r * 4 + wc) * KS) * 512 + lane * 8;
   // x part c: LDS row lr = (2 wid + h) * 8 + (lane >> 3) holds token (lr >> 5) * 64 + 32 c +
   // (lr & 31); its 16-B unit (lane & 7) is the row's logical unit (lane & 7) ^ ((lr >> 1) & 7).
-  const bf16* xsrc[2][2];
+  int xrow[2][2], xunit[2][2];
 #pragma unroll
   for (int cc = 0; cc < 2; ++cc)
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int lr = (2 * wid + h) * 8 + (lane >> 3);
-      const int trow = (lr >> 5) * 64 + cc * 32 + (lr & 31);
-      const int gr = min(row0 + trow, A.M - 1);
-      xsrc[cc][h] = A.x + (size_t)gr * A.ldx + (((lane & 7) ^ ((lr >> 1) & 7)) * 8);
+      xrow[cc][h] = min(row0 + (lr >> 5) * 64 + cc * 32 + (lr & 31), A.M - 1);
+      xunit[cc][h] = (lane & 7) ^ ((lr >> 1) & 7);
     }
-
   char* const sbase = smem;
-  auto buf = [&](int t) -> char* { return sbase + (t & 1) * PP_BUF; };
+  auto buf = [&](int t) -> char* { return sbase + (NBUF == 2 ? (t & 1) : (t % 3)) * BUFB; };
+
+  // flat sources (BUFLD = false)
+  const bf16* wsrc[2];
+  const bf16* xsrc[2][2];
+  // buffer sources (BUFLD = true): the tile's W panel and x as buffer resources
+  const __amdgpu_buffer_rsrc_t wrs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(A.wp + (size_t)nt * 2 * F * KS * 512), 0, 2 * F * KS * 1024, 0x00020000);
+  const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)A.x, 0, (int)min(((long long)(A.M - 1) * A.ldx + A.K) * 2, 0x7fffffffll), 0x00020000);
+  uint32_t woff[2] = {0, 0}, xoff[2][2] = {{0, 0}, {0, 0}};
+  if constexpr (BUFLD) {
+#pragma unroll
+    for (int r = 0; r < NA; ++r) woff[r] = (uint32_t)(((G * F + r * 4 + wc) * KS * 512 + lane * 8) * 2);
+#pragma unroll
+    for (int cc = 0; cc < 2; ++cc)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) xoff[cc][h] = (uint32_t)(((size_t)xrow[cc][h] * A.ldx + xunit[cc][h] * 8) * 2);
+  } else {
+#pragma unroll
+    for (int r = 0; r < NA; ++r)
+      wsrc[r] = A.wp + ((size_t)(nt * 2 * F + G * F + r * 4 + wc) * KS) * 512 + lane * 8;
+#pragma unroll
+    for (int cc = 0; cc < 2; ++cc)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) xsrc[cc][h] = A.x + (size_t)xrow[cc][h] * A.ldx + xunit[cc][h] * 8;
+  }
   auto issue_w = [&](int r, int t) {
     char* dst = buf(t) + r * PP_PART + (2 * wid) * 1024;
-    const bf16* s = wsrc[r] + (size_t)(2 * (kt0 + t)) * 512;
-    glds16(s, dst);
-    glds16(s + 512, dst + 1024);
+    if constexpr (BUFLD) {
+      const int so = (kt0 + t) * 2048;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, (lds_t*)dst, 16, woff[r], so, 0, 0);
+      // (the instruction offset would move the LDS address too: advance soffset instead)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, (lds_t*)(dst + 1024), 16, woff[r], so + 1024, 0, 0);
+    } else {
+      const bf16* s = wsrc[r] + (size_t)(2 * (kt0 + t)) * 512;
+      glds16(s, dst);
+      glds16(s + 512, dst + 1024);
+    }
   };
   auto issue_x = [&](int cc, int t) {
-    char* dst = buf(t) + (2 + cc) * PP_PART + (2 * wid) * 1024;
-    const size_t ko = (size_t)(kt0 + t) * 64;
-    glds16(xsrc[cc][0] + ko, dst);
-    glds16(xsrc[cc][1] + ko, dst + 1024);
+    char* dst = buf(t) + (NA + cc) * PP_PART + (2 * wid) * 1024;
+    if constexpr (BUFLD) {
+      const int so = (kt0 + t) * 128;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (lds_t*)dst, 16, xoff[cc][0], so, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (lds_t*)(dst + 1024), 16, xoff[cc][1], so, 0, 0);
+    } else {
+      const size_t ko = (size_t)(kt0 + t) * 64;
+      glds16(xsrc[cc][0] + ko, dst);
+      glds16(xsrc[cc][1] + ko, dst + 1024);
+    }
   };
   // fragment reads: W frags of part r (4 n-frags x 2 k-halves), x frags of part cc
   // (2 token frags x 2 k-halves)
@@ -131,7 +173,7 @@ __global__ __launch_bounds__(512) void pingpong_gemm_kernel(const Args A) {
       for (int h = 0; h < 2; ++h) af[i][h] = *reinterpret_cast<const bf16x8*>(p + (2 * i + h) * 1024);
   };
   auto read_x = [&](int cc, int t, bf16x8(&bfr)[2][2]) {
-    const char* p = buf(t) + (2 + cc) * PP_PART;
+    const char* p = buf(t) + (NA + cc) * PP_PART;
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const int lr = wc * 32 + 16 * j + c;
@@ -143,9 +185,9 @@ __global__ __launch_bounds__(512) void pingpong_gemm_kernel(const Args A) {
     }
   };
 
-  f32x4 acc[8][4];
+  f32x4 acc[F][4];
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
+  for (int i = 0; i < F; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
@@ -207,53 +249,104 @@ __global__ __launch_bounds__(512) void pingpong_gemm_kernel(const Args A) {
     raw_barrier();
   };
 
-  // prologue: parts of tiles 0 and 1 in steady-state issue order
-  issue_w(0, 0);
-  issue_x(0, 0);
-  issue_x(1, 0);
-  issue_w(1, 0);
-  issue_w(0, 1);
-  issue_x(0, 1);
-  wait_vm<8>();  // A0 and B0 of tile 0 landed
-  raw_barrier();
-  if (G == 1) raw_barrier();  // stagger: group 1 runs half a phase behind group 0
-  if constexpr (STAMP) st1 = __builtin_amdgcn_s_memtime();
+  // 256 x 128 tiles: one 64-k tile = 2 phases, three buffers
+  //     phase  reads (tile t)   MFMA        LDS-DMA issued            vmcnt
+  //     0      A (8), B0 (4)    A x B0      A, B0 of tile t + 2       10
+  //     1      B1 (4)           A x B1      B1 of tile t + 2           8
+  // (a part is restaged two phases after its last read; the wait before a phase's first
+  // barrier retires exactly what the next phase reads)
+  auto body4 = [&](int t, auto st) {
+    constexpr int S = decltype(st)::value;  // 0 steady, 1 tile nk - 2, 2 the last tile
+    read_w(0, t, af);
+    read_x(0, t, bx0);
+    if constexpr (S == 0) {
+      issue_w(0, t + 2);
+      issue_x(0, t + 2);
+      wait_vm<10>();
+    } else if constexpr (S == 1) {
+      wait_vm<6>();
+    } else {
+      wait_vm<0>();
+    }
+    raw_barrier();
+    lgkm0();
+    mma(ic<0>{}, ic<0>{}, af, bx0);
+    raw_barrier();
+    read_x(1, t, bx1);
+    if constexpr (S == 0) {
+      issue_x(1, t + 2);
+      wait_vm<8>();
+    } else if constexpr (S == 1) {
+      wait_vm<2>();
+    }
+    raw_barrier();
+    lgkm0();
+    mma(ic<0>{}, ic<1>{}, af, bx1);
+    raw_barrier();
+  };
 
   int t = 0;
-  for (; t + 2 < nk; ++t) body(t, ic<0>{});
-  body(t, ic<1>{});
-  body(t + 1, ic<2>{});
+  if constexpr (F == 8) {
+    // prologue: parts of tiles 0 and 1 in steady-state issue order
+    issue_w(0, 0);
+    issue_x(0, 0);
+    issue_x(1, 0);
+    issue_w(1, 0);
+    issue_w(0, 1);
+    issue_x(0, 1);
+    wait_vm<8>();  // A0 and B0 of tile 0 landed
+    raw_barrier();
+    if (G == 1) raw_barrier();  // stagger: group 1 runs half a phase behind group 0
+    if constexpr (STAMP) st1 = __builtin_amdgcn_s_memtime();
+    for (; t + 2 < nk; ++t) body(t, ic<0>{});
+    body(t, ic<1>{});
+    body(t + 1, ic<2>{});
+  } else {
+    issue_w(0, 0);
+    issue_x(0, 0);
+    issue_x(1, 0);
+    issue_w(0, 1);
+    issue_x(0, 1);
+    issue_x(1, 1);
+    wait_vm<8>();  // A and B0 of tile 0 landed
+    raw_barrier();
+    if (G == 1) raw_barrier();
+    if constexpr (STAMP) st1 = __builtin_amdgcn_s_memtime();
+    for (; t + 2 < nk; ++t) body4(t, ic<0>{});
+    body4(t, ic<1>{});
+    body4(t + 1, ic<2>{});
+  }
   if (G == 0) raw_barrier();  // balance the stagger
   if constexpr (STAMP) st2 = __builtin_amdgcn_s_memtime();
 
   // ---- split tiles: publish, the last arriver sums the other slices into its registers
   if (slice >= 0) {
-    float* base = A.ws + (size_t)(tile - A.full) * A.S * SLAB;
+    float* base = A.ws + (size_t)(tile - A.full) * A.S * SLABF;
     {
       const __amdgpu_buffer_rsrc_t rs =
-          __builtin_amdgcn_make_buffer_rsrc(base + (size_t)slice * SLAB, 0, SLAB * 4, 0x00020000);
+          __builtin_amdgcn_make_buffer_rsrc(base + (size_t)slice * SLABF, 0, SLABF * 4, 0x00020000);
 #pragma unroll
-      for (int i = 0; i < 8; ++i)
+      for (int i = 0; i < F; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j)
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i][j]), rs,
-                                                 (((wid * 8 + i) * 4 + j) * 64 + lane) * 16, 0, 16);
+                                                 (((wid * F + i) * 4 + j) * 64 + lane) * 16, 0, 16);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (!handoff_last(A.counters + (tile - A.full), A.S, reinterpret_cast<int*>(smem), A.acq)) return;
     for (int p = 0; p < A.S; ++p) {
       if (p == slice) continue;
       const __amdgpu_buffer_rsrc_t rp =
-          __builtin_amdgcn_make_buffer_rsrc(base + (size_t)p * SLAB, 0, SLAB * 4, 0x00020000);
+          __builtin_amdgcn_make_buffer_rsrc(base + (size_t)p * SLABF, 0, SLABF * 4, 0x00020000);
 #pragma unroll
-      for (int i = 0; i < 8; i += 2) {
+      for (int i = 0; i < F; i += 2) {
         f32x4 tt[2][4];
 #pragma unroll
         for (int h = 0; h < 2; ++h)
 #pragma unroll
           for (int j = 0; j < 4; ++j)
             tt[h][j] = __builtin_bit_cast(
-                f32x4, __builtin_amdgcn_raw_buffer_load_b128(rp, (((wid * 8 + i + h) * 4 + j) * 64 + lane) * 16, 0, 16));
+                f32x4, __builtin_amdgcn_raw_buffer_load_b128(rp, (((wid * F + i + h) * 4 + j) * 64 + lane) * 16, 0, 16));
 #pragma unroll
         for (int h = 0; h < 2; ++h)
 #pragma unroll
@@ -275,11 +368,11 @@ __global__ __launch_bounds__(512) void pingpong_gemm_kernel(const Args A) {
       if constexpr (NORM) rs = rsqrtf(A.ss_in[m] * inv_k + A.eps);
       if constexpr (pair_epi<EPI>()) {
 #pragma unroll
-        for (int i = 0; i < 8; i += 2)
-          store_quad<EPI>(A, m, nt * 16 + G * 8 + i, 4 * g, acc[i][j] * rs, acc[i + 1][j] * rs);
+        for (int i = 0; i < F; i += 2)
+          store_quad<EPI>(A, m, nt * 2 * F + G * F + i, 4 * g, acc[i][j] * rs, acc[i + 1][j] * rs);
       } else {
 #pragma unroll
-        for (int i = 0; i < 8; ++i) sq += store_quad<EPI>(A, m, nt * 16 + G * 8 + i, 4 * g, acc[i][j] * rs, acc[i][j]);
+        for (int i = 0; i < F; ++i) sq += store_quad<EPI>(A, m, nt * 2 * F + G * F + i, 4 * g, acc[i][j] * rs, acc[i][j]);
       }
     }
     if constexpr (EPI == EP_RESID) {

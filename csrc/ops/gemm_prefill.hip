@@ -651,6 +651,8 @@ extern "C" long long pa_prefill_gemm_ws_floats(int M, int N, int bn, int full, i
 }
 
 // Returns 1 if the shape/config is not handled, 0 on success, -2 on a launch error.
+// kernel_variant >= 0 picks the kernel family for this call (3: ping-pong, 1: read-ahead /
+// 3-stage 256 x 128), < 0 the process default (pa_prefill_set_variant).
 // full < 0 / splits <= 0 / bn <= 0 pick the defaults. For epi 4 (RoPE + paged KV write) y
 // is unused.
 extern "C" int pa_prefill_gemm(void* y, const void* x, const void* wp, const void* resid, float* ws,
@@ -658,7 +660,7 @@ extern "C" int pa_prefill_gemm(void* y, const void* x, const void* wp, const voi
                                int ldy, int ldr, int epi, const float* ss_in, float* ss_out, float* ss_zero,
                                float eps, int full, int splits, int bn, void* q_out, void* k_cache, void* v_cache,
                                const int* positions, const int* slots, const float* cos_sin, int H, int KV,
-                               hipStream_t st) {
+                               int kernel_variant, hipStream_t st) {
   using namespace pa::pf;
   if (M <= 0) return 0;
   if (bn <= 0) bn = pick_bn(M, N);
@@ -682,7 +684,7 @@ extern "C" int pa_prefill_gemm(void* y, const void* x, const void* wp, const voi
   S = (KT + per - 1) / per;  // no empty slices
   if (S == 1) full = tiles;
   // the ping-pong kernel's schedule needs >= 2 k-tiles per work item
-  int variant = g_pf_variant;
+  int variant = kernel_variant >= 0 ? kernel_variant : g_pf_variant;
   if (variant >= 3 && (KT < 2 || (S > 1 && (per < 2 || KT - (S - 1) * per < 2)))) variant = 1;
   if (full < tiles) {
     const long long need = (long long)(tiles - full) * S * (256 * bn);
@@ -695,9 +697,13 @@ extern "C" int pa_prefill_gemm(void* y, const void* x, const void* wp, const voi
   const int grid = full + (tiles - full) * S;
 #define PA_PF(E, NRM)                                                                                \
   do {                                                                                               \
-    if (bn == 128) hipLaunchKernelGGL((prefill_gemm_n128_kernel<E, NRM>), dim3(grid), dim3(512), 0, st, a);        \
+    if (bn == 128 && variant == 4 && E == EP_PLAIN && !NRM && full == tiles)                          \
+      hipLaunchKernelGGL((pingpong_gemm_kernel<EP_PLAIN, false, true, false, 4>), dim3(grid), dim3(512), 0, st, a); \
+    else if (bn == 128 && variant >= 3) hipLaunchKernelGGL((pingpong_gemm_kernel<E, NRM, false, false, 4>), dim3(grid), dim3(512), 0, st, a); \
+    else if (bn == 128) hipLaunchKernelGGL((prefill_gemm_n128_kernel<E, NRM>), dim3(grid), dim3(512), 0, st, a); \
     else if (variant == 4 && E == EP_PLAIN && !NRM && full == tiles)                                 \
       hipLaunchKernelGGL((pingpong_gemm_kernel<EP_PLAIN, false, true>), dim3(grid), dim3(512), 0, st, a);      \
+    else if (variant == 5) hipLaunchKernelGGL((pingpong_gemm_kernel<E, NRM, false, true>), dim3(grid), dim3(512), 0, st, a); \
     else if (variant >= 3) hipLaunchKernelGGL((pingpong_gemm_kernel<E, NRM>), dim3(grid), dim3(512), 0, st, a); \
     else if (variant == 2) hipLaunchKernelGGL((prefill_gemm_kernel<E, NRM, true, 4>), dim3(grid), dim3(256), 0, st, a); \
     else if (variant == 1) hipLaunchKernelGGL((prefill_gemm_kernel<E, NRM, true, 8>), dim3(grid), dim3(512), 0, st, a); \

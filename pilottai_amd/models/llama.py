@@ -138,19 +138,22 @@ class LlamaModel:
     MID_MAX_T = 256
     # steps above MID_MAX_T and up to this many tokens run the same fused packed-weight layer
     # with the prefill kernels (csrc/ops/gemm_prefill.hip) for the projections PF_CFG assigns
-    # to them: the ping-pong 256 x 256 kernel (gemm_pingpong.h) for qkv / gate_up / down,
-    # 256 x 128 tiles for o; no library GEMM and no separate norm / SwiGLU / RoPE launch.
+    # to them; no library GEMM and no separate norm / SwiGLU / RoPE launch.
     # EngineConfig.prefill_max_t / bench.py --prefill-max-t move the boundary (0 = off:
     # library GEMMs + elementwise kernels above MID_MAX_T).
     PREFILL_MAX_T = 1 << 30
     # per projection: (largest M, path, config); the first row whose M covers the step is used.
-    # "pf": prefill kernel (full = whole tiles, -1 = the kernel's plan; splits of the rest;
-    # bn = tile width), "mid": mid kernel (fm, fn, splits as MID_CFG)
+    # "pf": prefill kernel — bn = tile width (256 / 128), variant = kernel family (3: the
+    # ping-pong kernels of gemm_pingpong.h, 1: the read-ahead 256 x 256 / 3-stage 256 x 128
+    # kernels), full / splits = the decomposition (-1 / 0: the kernel's plan); "mid": mid
+    # kernel (fm, fn, splits as MID_CFG). Rows from tools/prefill_gemm_bench.py on MI355X
+    # (profiles/r3_pingpong_gemm_bench_n128.jsonl: fastest fused kernel per shape and M).
     PF_CFG = {
-        "qkv": [(1 << 30, "pf", {"full": -1, "splits": 0, "bn": 256})],
-        "o": [(1 << 30, "pf", {"full": -1, "splits": 0, "bn": 128})],
-        "gate_up": [(1 << 30, "pf", {"full": -1, "splits": 0, "bn": 256})],
-        "down": [(1 << 30, "pf", {"full": -1, "splits": 0, "bn": 256})],
+        "qkv": [(640, "pf", {"bn": 128, "variant": 1}), (1280, "pf", {"bn": 128, "variant": 3}),
+                (1 << 30, "pf", {"bn": 256, "variant": 3})],
+        "o": [(1280, "pf", {"bn": 128, "variant": 1}), (1 << 30, "pf", {"bn": 128, "variant": 3})],
+        "gate_up": [(1 << 30, "pf", {"bn": 256, "variant": 3})],
+        "down": [(640, "pf", {"bn": 128, "variant": 1}), (1 << 30, "pf", {"bn": 256, "variant": 3})],
     }
     # decode/small steps: let the attention launch's idle workgroups read the O
     # projection's weights into the Infinity Cache (MALL-resident weights run the 34 MB

@@ -518,11 +518,12 @@ def prefill_workspace(device):
 def prefill_gemm(x: torch.Tensor, wp: torch.Tensor, epi: str = "plain", resid: Optional[torch.Tensor] = None,
                  out: Optional[torch.Tensor] = None, norm: bool = False, eps: float = 1e-5, full: int = -1,
                  splits: int = 0, ss_in: Optional[torch.Tensor] = None, ss_out: Optional[torch.Tensor] = None,
-                 ss_zero: Optional[torch.Tensor] = None, bn: int = 0) -> torch.Tensor:
+                 ss_zero: Optional[torch.Tensor] = None, bn: int = 0, variant: int = -1) -> torch.Tensor:
     """y = epi(rownorm(x) @ W.T) for large M (256 x `bn` MFMA tiles, bn 128 / 256, 0 = the
     kernel's pick) with W packed by pack_decode_weight; same epilogues and row-statistics
     conventions as mid_gemm. `full` tiles run whole, the rest over `splits` K-slices (-1 / 0:
-    the kernel's plan)."""
+    the kernel's plan). `variant`: kernel family (3 ping-pong, 1 read-ahead / 3-stage;
+    -1 = the process default)."""
     M, K = x.shape
     N = wp.shape[0] * 16
     code = MID_EPI[epi]
@@ -534,7 +535,7 @@ def prefill_gemm(x: torch.Tensor, wp: torch.Tensor, epi: str = "plain", resid: O
     if _on_gpu(x):
         ws, cnt = prefill_workspace(x.device)
         if not require_native().prefill_gemm(out, x, wp, resid, ws, cnt, code, ss_in if norm else None, ss_out,
-                                              ss_zero, float(eps), int(full), int(splits), int(bn)):
+                                              ss_zero, float(eps), int(full), int(splits), int(bn), int(variant)):
             raise ValueError(f"prefill_gemm does not handle M={M} N={N} K={K} epi={epi} full={full} S={splits}")
         return out
     return mid_gemm(x, wp, epi, resid=resid, out=out, norm=norm, eps=eps, ss_in=ss_in, ss_out=ss_out,
@@ -543,7 +544,7 @@ def prefill_gemm(x: torch.Tensor, wp: torch.Tensor, epi: str = "plain", resid: O
 
 def prefill_qkv_rope(x: torch.Tensor, wp: torch.Tensor, eps: float, q_out: torch.Tensor, k_cache, v_cache,
                      positions, slots, cos_sin, H: int, KV: int, full: int = -1, splits: int = 0,
-                     ss_in: Optional[torch.Tensor] = None, bn: int = 0) -> torch.Tensor:
+                     ss_in: Optional[torch.Tensor] = None, bn: int = 0, variant: int = -1) -> torch.Tensor:
     """Large-M QKV projection (RMSNorm folded, row statistics ss_in) with RoPE and the paged
     KV write in the epilogue (csrc/ops/gemm_prefill.hip EP_ROPEKV)."""
     if ss_in is None:
@@ -552,7 +553,7 @@ def prefill_qkv_rope(x: torch.Tensor, wp: torch.Tensor, eps: float, q_out: torch
         ws, cnt = prefill_workspace(x.device)
         if not require_native().prefill_qkv_rope(x, wp, ss_in, float(eps), q_out, k_cache, v_cache, positions,
                                                   slots, cos_sin, int(H), int(KV), ws, cnt, int(full),
-                                                  int(splits), int(bn)):
+                                                  int(splits), int(bn), int(variant)):
             raise ValueError(f"prefill_qkv_rope does not handle M={x.shape[0]} K={x.shape[1]}")
         return q_out
     return mid_qkv_rope(x, wp, eps, q_out, k_cache, v_cache, positions, slots, cos_sin, H, KV, ss_in=ss_in)

@@ -80,7 +80,11 @@ for name in a.shapes.split(","):
             "mid": lambda i: kernels.mid_gemm(x, wps[i], "plain", out=y),
             "pf_default": lambda i: kernels.prefill_gemm(x, wps[i], "plain", out=y),
             "pf256": lambda i: kernels.prefill_gemm(x, wps[i], "plain", out=y, bn=256),
-            "pf128": lambda i: kernels.prefill_gemm(x, wps[i], "plain", out=y, bn=128),
+            "pf128": lambda i: v0(lambda: kernels.prefill_gemm(x, wps[i], "plain", out=y, bn=128), 1),
+            "pp128": lambda i: v0(lambda: kernels.prefill_gemm(x, wps[i], "plain", out=y, full=-1, splits=1, bn=128), 3),
+            "pp128_fused": lambda i: v0(lambda: kernels.prefill_gemm(x, fps[i], epi, out=yf if epi == "silu" else y,
+                                                                    resid=resid, norm=nrm, ss_in=ss if nrm else None,
+                                                                    full=-1, splits=1, bn=128), 3),
             "pf128_s2": lambda i: kernels.prefill_gemm(x, wps[i], "plain", out=y, bn=128, full=0, splits=2),
             "pf128_fused": lambda i: kernels.prefill_gemm(x, fps[i], epi, out=yf if epi == "silu" else y, resid=resid,
                                                           norm=nrm, ss_in=ss if nrm else None, bn=128),
@@ -90,6 +94,7 @@ for name in a.shapes.split(","):
                                                                      resid=resid, norm=nrm, ss_in=ss if nrm else None,
                                                                      bn=256), 2),
             "pp": lambda i: v0(lambda: kernels.prefill_gemm(x, wps[i], "plain", out=y, bn=256), 3),
+            "pp_buf": lambda i: v0(lambda: kernels.prefill_gemm(x, wps[i], "plain", out=y, full=-1, splits=1, bn=256), 5),
             "pp_whole": lambda i: v0(lambda: kernels.prefill_gemm(x, wps[i], "plain", out=y, full=-1, splits=1, bn=256), 3),
             "pp_s2": lambda i: v0(lambda: kernels.prefill_gemm(x, wps[i], "plain", out=y, full=0, splits=2, bn=256), 3),
             "pp_fused": lambda i: v0(lambda: kernels.prefill_gemm(x, fps[i], epi, out=yf if epi == "silu" else y,
@@ -129,12 +134,20 @@ for name in a.shapes.split(","):
                 row[f"err_pf{bn}"] = float(((yy.float() - ref).abs().max() / ref.abs().max()))
             yy = v0(lambda: kernels.prefill_gemm(x, wps[0], "plain", out=y, bn=256), 2)
             row["err_pf_w4"] = float(((yy.float() - ref).abs().max() / ref.abs().max()))
+        if "pp128" in variants:
+            ref = x.float() @ ws[0].float().T
+            y.fill_(float("nan"))
+            yy = v0(lambda: kernels.prefill_gemm(x, wps[0], "plain", out=y, full=-1, splits=1, bn=128), 3)
+            row["err_pp128"] = float(((yy.float() - ref).abs().max() / ref.abs().max()))
         if any(k.startswith("pp") for k in variants):
             ref = x.float() @ ws[0].float().T
-            for nm, kw in (("pp", {}), ("pp_whole", dict(full=-1, splits=1)), ("pp_s2", dict(full=0, splits=2))):
+            for nm, kw, vv in (("pp", {}, 3), ("pp_whole", dict(full=-1, splits=1), 3), ("pp_s2", dict(full=0, splits=2), 3),
+                               ("pp_buf", dict(full=-1, splits=1), 5)):
+                if nm not in variants:
+                    continue
                 try:
                     y.fill_(float("nan"))
-                    yy = v0(lambda: kernels.prefill_gemm(x, wps[0], "plain", out=y, bn=256, **kw), 3)
+                    yy = v0(lambda: kernels.prefill_gemm(x, wps[0], "plain", out=y, bn=256, **kw), vv)
                     row[f"err_{nm}"] = float(((yy.float() - ref).abs().max() / ref.abs().max()))
                 except (ValueError, RuntimeError):
                     row[f"err_{nm}"] = None
