@@ -440,12 +440,11 @@ class LlamaModel:
 
     @staticmethod
     def _down_cfg(T: int) -> dict:
-        """down_proj config for 9-16-row decode steps: 2 column tiles x 16 waves x 2 K-slices
-        (sc1 slabs + last-arriver reduce). Measured end to end: 16-token decode steps
-        4.16 -> 4.04 ms (16 workers) and 4.09 -> 3.97 ms (8 workers). 8-row steps: one tile
-        x 8 waves per workgroup (with the non-temporal weight stream 22.9 vs 24.6 us for the
-        default 16 waves; profiles/r2_decode_sweep_nt.jsonl)."""
-        return {"nt": 2, "waves": 16, "splits": 2} if T > 8 else {"nt": 1, "waves": 8}
+        """down_proj config for decode steps: one 16-column tile x 8 waves per workgroup, no
+        K split, at 8 and at 9-16 rows (cache-cold, interleaved: 21.0 us at M = 8, 25.4 us at
+        M = 16 against 27.6 for the 2-tile x 16-wave x 2-slice config that 9-16-row steps
+        used before; profiles/r3_decode_cfg_sweep.jsonl, tools/decode_cfg_sweep.py)."""
+        return {"nt": 1, "waves": 8}
 
     def _forward_wide(self, meta: StepMeta, kv: KVCache, T: int, num_logit_rows: int,
                       part_o: torch.Tensor, part_ml: torch.Tensor, embed=None) -> torch.Tensor:
