@@ -19,7 +19,10 @@
 //            one 1-KiB chunk per LDS-DMA wave instruction, lane-linear, conflict-free reads),
 //       B0 = token frags 0-1 of every wave, B1 = token frags 2-3 (x rows in full 128-B lines,
 //            16-B units XOR-swizzled by (row >> 1) on the SOURCE address).
-//   * one 64-k tile = 4 phases of 16 MFMAs (one output quadrant x K = 64):
+//   * default (PH2) schedule: one 64-k tile = 2 phases of 32 MFMAs, see `body2` (9 % fewer
+//     loop cycles than the four-phase schedule below, which stays as variant 6:
+//     profiles/r3_pingpong_ph2_ab.jsonl); four-phase schedule, one 64-k tile = 4 phases of
+//     16 MFMAs (one output quadrant x K = 64):
 //         phase  reads (this tile)   MFMA quadrant     LDS-DMA issued         vmcnt
 //         0      A0 (8), B0 (4)      n 0-3  x m 0-1    B1 of tile t + 1        8
 //         1      B1 (4)              n 0-3  x m 2-3    A1 of tile t + 1        8
@@ -52,7 +55,10 @@ constexpr int PP_BUF = 4 * PP_PART;
 // k advance in the SGPR soffset (no per-issue 64-bit address arithmetic in the load segment).
 // F = W n-frags per wave: 8 -> 256 x 256 tiles (two 64-KiB buffers of parts A0 A1 B0 B1),
 // 4 -> 256 x 128 tiles (three 48-KiB buffers of parts A B0 B1; schedule at `body4`).
-template <int EPI, bool NORM, bool STAMP = false, bool BUFLD = false, int F = 8>
+// PH2 (F = 8): two 32-MFMA phases per 64-k tile instead of four 16-MFMA phases (schedule at
+// `body2`); each load segment retires its own LDS reads before its barrier, so a part can be
+// restaged one phase after its last read.
+template <int EPI, bool NORM, bool STAMP = false, bool BUFLD = false, int F = 8, bool PH2 = false>
 __global__ __launch_bounds__(512) void pingpong_gemm_kernel(const Args A) {
   static_assert(F == 8 || F == 4, "256- or 128-wide tiles");
   constexpr int NA = F / 4;                 // W parts per 64-k tile
@@ -206,11 +212,33 @@ __global__ __launch_bounds__(512) void pingpong_gemm_kernel(const Args A) {
     __builtin_amdgcn_s_setprio(0);
   };
   auto lgkm0 = [] { __builtin_amdgcn_s_waitcnt(0xC07F); };
+  // 32 MFMAs: W part r (4 n-frags) x all 4 token frags x K = 64
+  auto mma32 = [&](auto rr, const bf16x8(&af)[4][2], const bf16x8(&b0)[2][2], const bf16x8(&b1)[2][2]) {
+    constexpr int r = decltype(rr)::value;
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[r * 4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][h], j < 2 ? b0[j][h] : b1[j - 2][h],
+                                                                      acc[r * 4 + i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
 
   bf16x8 af[4][2], bx0[2][2], bx1[2][2];
 
   // One 64-k tile. ST: 0 steady (tiles t + 1 and t + 2 exist), 1 = tile nk - 2 (only t + 1
   // left to issue), 2 = the last tile.
+  // STAMP: s_memtime on arrival at each of the 8 barriers of k-tile 8 (lane 0 of every wave)
+  uint64_t tb[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  auto pbar = [&](int t, int k) {
+    if constexpr (STAMP) {
+      if (t == 8) tb[k] = __builtin_amdgcn_s_memtime();
+    }
+    raw_barrier();
+  };
   auto body = [&](int t, auto st) {
     constexpr int S = decltype(st)::value;
     // phase 0
@@ -218,25 +246,25 @@ __global__ __launch_bounds__(512) void pingpong_gemm_kernel(const Args A) {
     read_x(0, t, bx0);
     if constexpr (S < 2) issue_x(1, t + 1);
     if constexpr (S < 2) wait_vm<8>(); else wait_vm<2>();
-    raw_barrier();
+    pbar(t, 0);
     lgkm0();
     mma(ic<0>{}, ic<0>{}, af, bx0);
-    raw_barrier();
+    pbar(t, 1);
     // phase 1
     read_x(1, t, bx1);
     if constexpr (S < 2) issue_w(1, t + 1);
     if constexpr (S < 2) wait_vm<8>(); else wait_vm<0>();
-    raw_barrier();
+    pbar(t, 2);
     lgkm0();
     mma(ic<0>{}, ic<1>{}, af, bx1);
-    raw_barrier();
+    pbar(t, 3);
     // phase 2
     read_w(1, t, af);
     if constexpr (S == 0) issue_w(0, t + 2);
-    raw_barrier();
+    pbar(t, 4);
     lgkm0();
     mma(ic<1>{}, ic<1>{}, af, bx1);
-    raw_barrier();
+    pbar(t, 5);
     // phase 3
     if constexpr (S == 0) {
       issue_x(0, t + 2);
@@ -244,9 +272,9 @@ __global__ __launch_bounds__(512) void pingpong_gemm_kernel(const Args A) {
     } else if constexpr (S == 1) {
       wait_vm<4>();
     }
-    raw_barrier();
+    pbar(t, 6);
     mma(ic<1>{}, ic<0>{}, af, bx0);
-    raw_barrier();
+    pbar(t, 7);
   };
 
   // 256 x 128 tiles: one 64-k tile = 2 phases, three buffers
@@ -285,8 +313,58 @@ __global__ __launch_bounds__(512) void pingpong_gemm_kernel(const Args A) {
     raw_barrier();
   };
 
+  // 256 x 256 tiles, two phases per 64-k tile (PH2):
+  //     phase  reads (tile t)          MFMA              LDS-DMA issued          vmcnt
+  //     0      A0 (8), B0 (4), B1 (4)  A0 x (B0, B1)     B1, A1 of tile t + 1      8
+  //     1      A1 (8)                  A1 x (B0, B1)     A0, B0 of tile t + 2      6
+  // lgkmcnt(0) before each load segment's barrier, so a part is restaged one phase after its
+  // last read (the partner group's reads of that phase are retired behind the same barrier).
+  auto body2 = [&](int t, auto st) {
+    constexpr int S = decltype(st)::value;  // 0 steady, 1 tile nk - 2, 2 the last tile
+    read_w(0, t, af);
+    read_x(0, t, bx0);
+    read_x(1, t, bx1);
+    if constexpr (S < 2) {
+      issue_x(1, t + 1);
+      issue_w(1, t + 1);
+      wait_vm<8>();
+    } else {
+      wait_vm<0>();
+    }
+    lgkm0();
+    raw_barrier();
+    mma32(ic<0>{}, af, bx0, bx1);
+    raw_barrier();
+    read_w(1, t, af);
+    if constexpr (S == 0) {
+      issue_w(0, t + 2);
+      issue_x(0, t + 2);
+      wait_vm<6>();
+    } else if constexpr (S == 1) {
+      wait_vm<2>();
+    }
+    lgkm0();
+    raw_barrier();
+    mma32(ic<1>{}, af, bx0, bx1);
+    raw_barrier();
+  };
+
   int t = 0;
-  if constexpr (F == 8) {
+  if constexpr (F == 8 && PH2) {
+    issue_w(0, 0);
+    issue_x(0, 0);
+    issue_x(1, 0);
+    issue_w(1, 0);
+    issue_w(0, 1);
+    issue_x(0, 1);
+    wait_vm<6>();  // A0, B0 and B1 of tile 0 landed
+    raw_barrier();
+    if (G == 1) raw_barrier();
+    if constexpr (STAMP) st1 = __builtin_amdgcn_s_memtime();
+    for (; t + 2 < nk; ++t) body2(t, ic<0>{});
+    body2(t, ic<1>{});
+    body2(t + 1, ic<2>{});
+  } else if constexpr (F == 8) {
     // prologue: parts of tiles 0 and 1 in steady-state issue order
     issue_w(0, 0);
     issue_x(0, 0);
@@ -391,6 +469,11 @@ __global__ __launch_bounds__(512) void pingpong_gemm_kernel(const Args A) {
       const uint64_t v[8] = {st0, st1, st2, st3, rt0, rt1, (uint64_t)tile, 0};
 #pragma unroll
       for (int q = 0; q < 8; ++q) __hip_atomic_store(d + q, v[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (lane == 0) {  // per-wave barrier arrivals of k-tile 8: A.ws[8 * gridDim.x + (b * 8 + wid) * 8 ..]
+      uint64_t* d = reinterpret_cast<uint64_t*>(A.ws) + (size_t)gridDim.x * 8 + ((size_t)blockIdx.x * 8 + wid) * 8;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) __hip_atomic_store(d + q, tb[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
 }

@@ -596,9 +596,11 @@ __global__ __launch_bounds__(512) void prefill_gemm_n128_kernel(const Args A) {
 namespace pa {
 namespace pf {
 
-// 256-wide main loop: 3 = ping-pong wave groups (gemm_pingpong.h, default; items of < 2
-// k-tiles fall back to 1); 1 = read-ahead, 8 waves; 0 = reads in the phase they feed;
-// 2 = read-ahead, 4 waves of 128 x 128; 4 = the ping-pong kernel's cycle-stamp build
+// Kernel family: 3 = ping-pong wave groups (gemm_pingpong.h; default; 256-wide tiles on the
+// two-phase schedule, 128-wide on the three-buffer one; items of < 2 k-tiles fall back to 1);
+// 4 = its cycle-stamp build; 6 = the four-phase 256-wide schedule, 7 = its stamp build;
+// 5 = four-phase with buffer_load staging; 1 = read-ahead 8-wave 256 x 256 / 3-stage
+// 256 x 128; 0 = reads in the phase they feed; 2 = read-ahead, 4 waves of 128 x 128
 constexpr int kPfDefaultVariant = 3;
 static int g_pf_variant = kPfDefaultVariant;
 
@@ -697,14 +699,18 @@ extern "C" int pa_prefill_gemm(void* y, const void* x, const void* wp, const voi
   const int grid = full + (tiles - full) * S;
 #define PA_PF(E, NRM)                                                                                \
   do {                                                                                               \
-    if (bn == 128 && variant == 4 && E == EP_PLAIN && !NRM && full == tiles)                          \
+    const bool stamp = E == EP_PLAIN && !NRM && full == tiles;                                       \
+    if (bn == 128 && variant == 4 && stamp)                                                          \
       hipLaunchKernelGGL((pingpong_gemm_kernel<EP_PLAIN, false, true, false, 4>), dim3(grid), dim3(512), 0, st, a); \
     else if (bn == 128 && variant >= 3) hipLaunchKernelGGL((pingpong_gemm_kernel<E, NRM, false, false, 4>), dim3(grid), dim3(512), 0, st, a); \
     else if (bn == 128) hipLaunchKernelGGL((prefill_gemm_n128_kernel<E, NRM>), dim3(grid), dim3(512), 0, st, a); \
-    else if (variant == 4 && E == EP_PLAIN && !NRM && full == tiles)                                 \
-      hipLaunchKernelGGL((pingpong_gemm_kernel<EP_PLAIN, false, true>), dim3(grid), dim3(512), 0, st, a);      \
+    else if (variant == 4 && stamp)                                                                  \
+      hipLaunchKernelGGL((pingpong_gemm_kernel<EP_PLAIN, false, true, false, 8, true>), dim3(grid), dim3(512), 0, st, a); \
+    else if (variant == 7 && stamp)                                                                  \
+      hipLaunchKernelGGL((pingpong_gemm_kernel<EP_PLAIN, false, true, false, 8, false>), dim3(grid), dim3(512), 0, st, a); \
     else if (variant == 5) hipLaunchKernelGGL((pingpong_gemm_kernel<E, NRM, false, true>), dim3(grid), dim3(512), 0, st, a); \
-    else if (variant >= 3) hipLaunchKernelGGL((pingpong_gemm_kernel<E, NRM>), dim3(grid), dim3(512), 0, st, a); \
+    else if (variant == 6 || variant == 7) hipLaunchKernelGGL((pingpong_gemm_kernel<E, NRM>), dim3(grid), dim3(512), 0, st, a); \
+    else if (variant >= 3) hipLaunchKernelGGL((pingpong_gemm_kernel<E, NRM, false, false, 8, true>), dim3(grid), dim3(512), 0, st, a); \
     else if (variant == 2) hipLaunchKernelGGL((prefill_gemm_kernel<E, NRM, true, 4>), dim3(grid), dim3(256), 0, st, a); \
     else if (variant == 1) hipLaunchKernelGGL((prefill_gemm_kernel<E, NRM, true, 8>), dim3(grid), dim3(512), 0, st, a); \
     else hipLaunchKernelGGL((prefill_gemm_kernel<E, NRM, false, 8>), dim3(grid), dim3(512), 0, st, a);                 \

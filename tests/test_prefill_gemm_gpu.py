@@ -23,11 +23,12 @@ def _bf(*shape, dev, scale=1.0):
     (272, 2048, 1024, "plain", False, 3, 2), (64, 1024, 512, "silu", False, -1, 0),
     (1000, 1280, 8192, "rope_perm", True, 0, 2),  # 70B TP=8 QKV shard
     (17, 768, 128, "plain", True, -1, 1), (256, 512, 64, "resid", False, 0, 1)])
-@pytest.mark.parametrize("bn,variant", [(256, 3), (256, 1), (128, 3), (128, 1)])
+@pytest.mark.parametrize("bn,variant", [(256, 3), (256, 6), (256, 1), (128, 3), (128, 1)])
 def test_prefill_gemm(gpu, M, N, K, epi, norm, full, splits, bn, variant):
     """Every epilogue and the folded row norm; run twice so the self-resetting tickets of
-    the split tail are exercised. 256-wide tiles on the ping-pong kernel (variant 3, the
-    default) and on the read-ahead kernel (variant 1, the fallback for < 2 k-tiles)."""
+    the split tail are exercised. Ping-pong kernels (variant 3, the default: two-phase
+    256-wide / three-buffer 128-wide schedules; variant 6: the four-phase 256-wide schedule)
+    and the read-ahead / 3-stage kernels (variant 1, the fallback for < 2 k-tiles)."""
     from pilottai_amd.ops import kernels
 
     kernels.require_native().prefill_set_variant(variant)
