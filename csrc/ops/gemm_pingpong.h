@@ -46,6 +46,9 @@ namespace pa {
 namespace pf {
 
 constexpr int PP_PART = 16384;
+// non-pair epilogues: 16-B stores of 8 columns per lane (packed_epi.h store_pair_wide)
+// instead of 8-B quads
+constexpr bool kPpWideStores = false;
 constexpr int PP_BUF = 4 * PP_PART;
 
 // STAMP (diagnostic build, whole tiles only): workgroup b's thread 0 writes s_memtime at
@@ -59,7 +62,7 @@ constexpr int PP_BUF = 4 * PP_PART;
 // `body2`); each load segment retires its own LDS reads before its barrier, so a part can be
 // restaged one phase after its last read.
 template <int EPI, bool NORM, bool STAMP = false, bool BUFLD = false, int F = 8, bool PH2 = false>
-__global__ __launch_bounds__(512) void pingpong_gemm_kernel(const Args A) {
+__device__ __forceinline__ void pingpong_tile(const Args& A, const int bid, const int nblocks, char* smem) {
   static_assert(F == 8 || F == 4, "256- or 128-wide tiles");
   constexpr int NA = F / 4;                 // W parts per 64-k tile
   constexpr int BUFB = (NA + 2) * PP_PART;  // bytes per tile buffer
@@ -70,14 +73,12 @@ __global__ __launch_bounds__(512) void pingpong_gemm_kernel(const Args A) {
     st0 = __builtin_amdgcn_s_memtime();
     rt0 = __builtin_amdgcn_s_memrealtime();
   }
-  __shared__ __attribute__((aligned(1024))) char smem[NBUF * BUFB];
 
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int G = wid >> 2, wc = wid & 3;
   const int g = lane >> 4, c = lane & 15;
 
-  const int bid = blockIdx.x;
   const int KT = A.K >> 6;
   int tile, kt0, kt1, slice = -1;
   if (bid < A.full) {
@@ -86,7 +87,7 @@ __global__ __launch_bounds__(512) void pingpong_gemm_kernel(const Args A) {
     kt0 = 0;
     kt1 = KT;
   } else {
-    const int nb = gridDim.x - A.full, w0 = bid - A.full;
+    const int nb = nblocks - A.full, w0 = bid - A.full;
     const int q8 = nb >> 3, r8 = nb & 7, xcd = w0 & 7;
     const int w2 = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (w0 >> 3);
     tile = A.full + w2 / A.S;
@@ -98,7 +99,7 @@ __global__ __launch_bounds__(512) void pingpong_gemm_kernel(const Args A) {
   const int row0 = mt * 256;
   const int nk = kt1 - kt0;  // >= 2 (launcher)
 
-  if (A.ss_zero && blockIdx.x == 0)
+  if (A.ss_zero && bid == 0)
     for (int i = threadIdx.x; i < A.M; i += 512) A.ss_zero[i] = 0.f;
 
   // ---- LDS-DMA sources. Every part is 16 wave instructions, two per wave.
@@ -449,8 +450,15 @@ __global__ __launch_bounds__(512) void pingpong_gemm_kernel(const Args A) {
         for (int i = 0; i < F; i += 2)
           store_quad<EPI>(A, m, nt * 2 * F + G * F + i, 4 * g, acc[i][j] * rs, acc[i + 1][j] * rs);
       } else {
+        if constexpr (kPpWideStores) {
 #pragma unroll
-        for (int i = 0; i < F; ++i) sq += store_quad<EPI>(A, m, nt * 2 * F + G * F + i, 4 * g, acc[i][j] * rs, acc[i][j]);
+          for (int i = 0; i < F; i += 2)
+            sq += store_pair_wide<EPI>(A, m, nt * 2 * F + G * F + i, g, acc[i][j] * rs, acc[i + 1][j] * rs);
+        } else {
+#pragma unroll
+          for (int i = 0; i < F; ++i)
+            sq += store_quad<EPI>(A, m, nt * 2 * F + G * F + i, 4 * g, acc[i][j] * rs, acc[i][j]);
+        }
       }
     }
     if constexpr (EPI == EP_RESID) {
@@ -465,17 +473,38 @@ __global__ __launch_bounds__(512) void pingpong_gemm_kernel(const Args A) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const uint64_t st3 = __builtin_amdgcn_s_memtime(), rt1 = __builtin_amdgcn_s_memrealtime();
     if (threadIdx.x == 0) {
-      uint64_t* d = reinterpret_cast<uint64_t*>(A.ws) + (size_t)blockIdx.x * 8;
+      uint64_t* d = reinterpret_cast<uint64_t*>(A.ws) + (size_t)bid * 8;
       const uint64_t v[8] = {st0, st1, st2, st3, rt0, rt1, (uint64_t)tile, 0};
 #pragma unroll
       for (int q = 0; q < 8; ++q) __hip_atomic_store(d + q, v[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    if (lane == 0) {  // per-wave barrier arrivals of k-tile 8: A.ws[8 * gridDim.x + (b * 8 + wid) * 8 ..]
-      uint64_t* d = reinterpret_cast<uint64_t*>(A.ws) + (size_t)gridDim.x * 8 + ((size_t)blockIdx.x * 8 + wid) * 8;
+    if (lane == 0) {  // per-wave barrier arrivals of k-tile 8: A.ws[8 * nblocks + (b * 8 + wid) * 8 ..]
+      uint64_t* d = reinterpret_cast<uint64_t*>(A.ws) + (size_t)nblocks * 8 + ((size_t)bid * 8 + wid) * 8;
 #pragma unroll
       for (int q = 0; q < 8; ++q) __hip_atomic_store(d + q, tb[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
+}
+
+
+// One tile family per launch: the whole grid runs pingpong_tile.
+template <int EPI, bool NORM, bool STAMP = false, bool BUFLD = false, int F = 8, bool PH2 = false>
+__global__ __launch_bounds__(512) void pingpong_gemm_kernel(const Args A) {
+  __shared__ __attribute__((aligned(1024))) char smem[(F == 8 ? 2 * 4 : 3 * 3) * PP_PART];
+  pingpong_tile<EPI, NORM, STAMP, BUFLD, F, PH2>(A, blockIdx.x, gridDim.x, smem);
+}
+
+// Full rounds of 256 x 256 tiles, then the remaining columns as 256 x 128 tiles in the same
+// launch (workgroups [0, nbig) run A's 256-wide tiles, the rest B's 128-wide tiles of the
+// columns A leaves out): a tail of r <= 128 wide tiles costs one round of half-size tiles
+// (~60 % of a wide-tile round) instead of a whole wide-tile round.
+template <int EPI, bool NORM>
+__global__ __launch_bounds__(512) void pingpong_mixed_kernel(const Args A, const Args B, const int nbig) {
+  __shared__ __attribute__((aligned(1024))) char smem[9 * PP_PART];
+  if ((int)blockIdx.x < nbig)
+    pingpong_tile<EPI, NORM, false, false, 8, true>(A, blockIdx.x, nbig, smem);
+  else
+    pingpong_tile<EPI, NORM, false, false, 4, false>(B, blockIdx.x - nbig, gridDim.x - nbig, smem);
 }
 
 }  // namespace pf

@@ -675,6 +675,7 @@ extern "C" int pa_prefill_gemm(void* y, const void* x, const void* wp, const voi
                            N != (H + 2 * KV) * 128))
     return 1;
   const int MT = (M + 255) / 256, NT = N / bn, tiles = MT * NT;
+  const bool default_plan = full < 0 && splits <= 0;
   int dfull, dS;
   plan_default(M, N, K, bn, dfull, dS);
   if (full < 0) full = dfull;
@@ -697,6 +698,43 @@ extern "C" int pa_prefill_gemm(void* y, const void* x, const void* wp, const voi
          (pa::bf16*)q_out, (pa::bf16*)k_cache, (pa::bf16*)v_cache, positions, slots, cos_sin, H, KV,
          pa::g_handoff_acquire};
   const int grid = full + (tiles - full) * S;
+  // Mixed tail (variant 8): full rounds of 256 x 256 tiles over the first c1 column tiles,
+  // the remaining columns as 256 x 128 tiles in the same launch, when that tail fits one
+  // round of half-size tiles (pingpong_mixed_kernel). Not for the RoPE + KV-write epilogue
+  // (its head index comes from the absolute column tile).
+  if (variant == 8) {
+    const int r = tiles % 256, c1 = (tiles - r) / MT, nsmall = MT * 2 * (NT - c1);
+    if (!(bn == 256 && default_plan && r > 0 && c1 > 0 && nsmall <= 256 && epi != EP_ROPEKV)) {
+      variant = 3;
+    } else {
+      const int nbig = c1 * MT;
+      Args big = a;
+      big.full = nbig;
+      big.S = 1;
+      big.per = KT;
+      Args sm = a;
+      const int co = c1 * 256;  // first column (packed) of the 128-wide tiles
+      sm.wp = a.wp + (size_t)c1 * 16 * (K / 32) * 512;
+      sm.y = a.y ? a.y + (epi == EP_SILU ? co / 2 : co) : nullptr;
+      sm.resid = a.resid ? a.resid + co : nullptr;
+      sm.N = N - co;
+      sm.NT = sm.N / 128;
+      sm.full = nsmall;
+      sm.S = 1;
+      sm.per = KT;
+      sm.ss_zero = nullptr;
+#define PA_MIX(E, NRM) hipLaunchKernelGGL((pingpong_mixed_kernel<E, NRM>), dim3(nbig + nsmall), dim3(512), 0, st, big, sm, nbig)
+      switch (epi) {
+        case EP_PLAIN: if (norm) PA_MIX(EP_PLAIN, true); else PA_MIX(EP_PLAIN, false); break;
+        case EP_RESID: PA_MIX(EP_RESID, false); break;
+        case EP_ROPEPERM: if (norm) PA_MIX(EP_ROPEPERM, true); else PA_MIX(EP_ROPEPERM, false); break;
+        case EP_SILU: if (norm) PA_MIX(EP_SILU, true); else PA_MIX(EP_SILU, false); break;
+        default: return 1;
+      }
+#undef PA_MIX
+      return (int)hipGetLastError() == 0 ? 0 : -2;
+    }
+  }
 #define PA_PF(E, NRM)                                                                                \
   do {                                                                                               \
     const bool stamp = E == EP_PLAIN && !NRM && full == tiles;                                       \

@@ -98,5 +98,40 @@ __device__ __forceinline__ float store_quad(const AT& A, int m, int tile, int cq
   }
 }
 
+// Non-pair epilogues on two adjacent tiles at once, stored 16 B per lane: lanes g and g ^ 1
+// (lane groups of 16) trade halves (lane ^ 16 exchange), so lane (g, c) ends with 8
+// consecutive columns of ONE tile — tile `tile` for even g, tile + 1 for odd g — starting
+// at column 8 (g >> 1). One dwordx4 store per lane instead of two dwordx2 (the guide's T21:
+// a store-issue-bound epilogue tail halves). a = tile's quad, b = tile + 1's quad (columns
+// 4 g .. 4 g + 3 of each). Returns sum(y^2) of the written bf16 values (EP_RESID).
+template <int EPI, class AT>
+__device__ __forceinline__ float store_pair_wide(const AT& A, int m, int tile, int g, f32x4 a, f32x4 b) {
+  static_assert(!pair_epi<EPI>(), "pair epilogues keep store_quad");
+  const bool odd = g & 1;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {  // even g keeps a and receives the partner's a; odd g the reverse
+    const float got = __shfl_xor(odd ? a[r] : b[r], 16, 64);
+    if (odd) a[r] = got; else b[r] = got;
+  }
+  const int t = tile + (g & 1);
+  const int col = (EPI == EP_ROPEPERM ? ropeperm_tile(t) * 16 : t * 16) + 8 * (g >> 1);
+  float v[8] = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+  if constexpr (EPI == EP_RESID) {
+    const bf16x8 rv = *reinterpret_cast<const bf16x8*>(A.resid + (size_t)m * A.ldr + col);
+#pragma unroll
+    for (int r = 0; r < 8; ++r) v[r] += (float)rv[r];
+  }
+  bf16x8 o;
+  float sq = 0.f;
+#pragma unroll
+  for (int r = 0; r < 8; ++r) {
+    o[r] = (bf16)v[r];
+    const float f = (float)o[r];
+    sq = fmaf(f, f, sq);
+  }
+  *reinterpret_cast<bf16x8*>(A.y + (size_t)m * A.ldy + col) = o;
+  return sq;
+}
+
 }  // namespace pk
 }  // namespace pa

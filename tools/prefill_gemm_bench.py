@@ -98,6 +98,10 @@ for name in a.shapes.split(","):
             "pp_ph4_fused": lambda i: v0(lambda: kernels.prefill_gemm(x, fps[i], epi, out=yf if epi == "silu" else y,
                                                                      resid=resid, norm=nrm, ss_in=ss if nrm else None,
                                                                      bn=256), 6),
+            "pp_mix": lambda i: v0(lambda: kernels.prefill_gemm(x, wps[i], "plain", out=y, bn=256), 8),
+            "pp_mix_fused": lambda i: v0(lambda: kernels.prefill_gemm(x, fps[i], epi, out=yf if epi == "silu" else y,
+                                                                     resid=resid, norm=nrm, ss_in=ss if nrm else None,
+                                                                     bn=256), 8),
             "pp_buf": lambda i: v0(lambda: kernels.prefill_gemm(x, wps[i], "plain", out=y, full=-1, splits=1, bn=256), 5),
             "pp_whole": lambda i: v0(lambda: kernels.prefill_gemm(x, wps[i], "plain", out=y, full=-1, splits=1, bn=256), 3),
             "pp_s2": lambda i: v0(lambda: kernels.prefill_gemm(x, wps[i], "plain", out=y, full=0, splits=2, bn=256), 3),
@@ -146,7 +150,7 @@ for name in a.shapes.split(","):
         if any(k.startswith("pp") for k in variants):
             ref = x.float() @ ws[0].float().T
             for nm, kw, vv in (("pp", {}, 3), ("pp_whole", dict(full=-1, splits=1), 3), ("pp_s2", dict(full=0, splits=2), 3),
-                               ("pp_buf", dict(full=-1, splits=1), 5), ("pp_ph4", dict(full=-1, splits=1), 6)):
+                               ("pp_buf", dict(full=-1, splits=1), 5), ("pp_ph4", dict(full=-1, splits=1), 6), ("pp_mix", {}, 8)):
                 if nm not in variants:
                     continue
                 try:
