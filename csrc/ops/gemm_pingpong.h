@@ -48,7 +48,7 @@ namespace pf {
 constexpr int PP_PART = 16384;
 // non-pair epilogues: 16-B stores of 8 columns per lane (packed_epi.h store_pair_wide)
 // instead of 8-B quads
-constexpr bool kPpWideStores = false;
+constexpr bool kPpWideStores = true;
 constexpr int PP_BUF = 4 * PP_PART;
 
 // STAMP (diagnostic build, whole tiles only): workgroup b's thread 0 writes s_memtime at

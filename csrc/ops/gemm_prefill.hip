@@ -597,7 +597,8 @@ namespace pa {
 namespace pf {
 
 // Kernel family: 3 = ping-pong wave groups (gemm_pingpong.h; default; 256-wide tiles on the
-// two-phase schedule, 128-wide on the three-buffer one; items of < 2 k-tiles fall back to 1);
+// two-phase schedule with the mixed 128-wide tail when it applies, 128-wide tiles on the
+// three-buffer schedule; items of < 2 k-tiles fall back to 1); 9 = 3 without the mixed tail;
 // 4 = its cycle-stamp build; 6 = the four-phase 256-wide schedule, 7 = its stamp build;
 // 5 = four-phase with buffer_load staging; 1 = read-ahead 8-wave 256 x 256 / 3-stage
 // 256 x 128; 0 = reads in the phase they feed; 2 = read-ahead, 4 waves of 128 x 128
@@ -698,11 +699,12 @@ extern "C" int pa_prefill_gemm(void* y, const void* x, const void* wp, const voi
          (pa::bf16*)q_out, (pa::bf16*)k_cache, (pa::bf16*)v_cache, positions, slots, cos_sin, H, KV,
          pa::g_handoff_acquire};
   const int grid = full + (tiles - full) * S;
-  // Mixed tail (variant 8): full rounds of 256 x 256 tiles over the first c1 column tiles,
+  // Mixed tail (variant 3, the default, and 8; 9 = without it): full rounds of 256 x 256
+  // tiles over the first c1 column tiles,
   // the remaining columns as 256 x 128 tiles in the same launch, when that tail fits one
   // round of half-size tiles (pingpong_mixed_kernel). Not for the RoPE + KV-write epilogue
   // (its head index comes from the absolute column tile).
-  if (variant == 8) {
+  if (variant == 3 || variant == 8) {
     const int r = tiles % 256, c1 = (tiles - r) / MT, nsmall = MT * 2 * (NT - c1);
     if (!(bn == 256 && default_plan && r > 0 && c1 > 0 && nsmall <= 256 && epi != EP_ROPEKV)) {
       variant = 3;

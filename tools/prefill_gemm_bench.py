@@ -93,7 +93,7 @@ for name in a.shapes.split(","):
             "pf_w4_fused": lambda i: v0(lambda: kernels.prefill_gemm(x, fps[i], epi, out=yf if epi == "silu" else y,
                                                                      resid=resid, norm=nrm, ss_in=ss if nrm else None,
                                                                      bn=256), 2),
-            "pp": lambda i: v0(lambda: kernels.prefill_gemm(x, wps[i], "plain", out=y, bn=256), 3),
+            "pp": lambda i: v0(lambda: kernels.prefill_gemm(x, wps[i], "plain", out=y, bn=256), 9),
             "pp_ph4": lambda i: v0(lambda: kernels.prefill_gemm(x, wps[i], "plain", out=y, full=-1, splits=1, bn=256), 6),
             "pp_ph4_fused": lambda i: v0(lambda: kernels.prefill_gemm(x, fps[i], epi, out=yf if epi == "silu" else y,
                                                                      resid=resid, norm=nrm, ss_in=ss if nrm else None,
