@@ -78,6 +78,8 @@ def parse():
                     help="admit requests whose prefix another request is prefilling right away (no deferral)")
     ap.add_argument("--no-prefetch", action="store_true", help="decode steps without the side-stream weight prefetch")
     ap.add_argument("--token-align", type=int, default=256, help="GEMM-friendly step sizes (0 = off)")
+    ap.add_argument("--async-steps", type=int, default=None, choices=[0, 1],
+                    help="pipelined engine steps (schedule/launch step N+1 while step N runs); default: engine's")
     ap.add_argument("--align-slack", type=int, default=96)
     ap.add_argument("--cpu", action="store_true", help="tiny model on CPU (plumbing smoke only)")
     ap.add_argument("--dp-mode", choices=["node", "independent"], default="node",
@@ -130,6 +132,7 @@ async def run_rank(a, rank: int, world: int, device):
                                  reply_tokens=a.reply_tokens,
                                  prefetch_weights=False if a.no_prefetch else None,
                                  dedup_inflight_prefix=not a.no_prefix_dedup,
+                                 **({"async_steps": bool(a.async_steps)} if a.async_steps is not None else {}),
                                  **({"att_wide_min_tokens": a.att_wide_min_tokens}
                                     if a.att_wide_min_tokens is not None else {})), device=device)
     register_engine(eng.model_cfg.name, eng)
@@ -282,6 +285,9 @@ async def run_rank(a, rank: int, world: int, device):
         "completion_tokens": u1["completion_tokens"] - u0["completion_tokens"],
         "busy_s": st1["busy_s"] - st0["busy_s"], "prefix_hit": em["prefix_cache_hit_tokens"],
         "prefix_defers": em["prefix_defers"],
+        "spec_rows": em.get("spec_rows", 0),
+        "spec_voided": em.get("spec_voided", 0),
+        "async_steps": bool(eng._async),
         "host_phases": {k: st1[k] - st0[k] for k in ("host_sched_s", "host_launch_s", "device_wait_s",
                                                      "host_commit_s", "host_deliver_s")},
         "bucket_tokens": st1["bucket_tokens"] - st0["bucket_tokens"],
@@ -413,6 +419,9 @@ def main():
             "engine_busy_frac": round(tot("busy_s") / (dt * len(gathered)), 3),
             "prefix_cache_hit_frac": round(tot("prefix_hit") / max(1, tot("prompt_total")), 3),
             "prefix_defers": tot("prefix_defers"),
+            "async_steps": bool(gathered[0].get("async_steps")),
+            "spec_rows": tot("spec_rows"),
+            "spec_voided": tot("spec_voided"),
             "graph_pad_frac": round(1 - tot("tokens") / max(1, tot("bucket_tokens")), 3),
             # rank 0's engine thread, ms per step: schedule / copy+launch / wait for the device /
             # commit / deliver (the host phases are the device's idle time between steps)

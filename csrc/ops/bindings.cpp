@@ -21,6 +21,7 @@ int pa_paged_attention(void* out, float* part_o, float* part_ml, const void* q, 
                        int max_blocks, int H, int KV, float scale_log2, const void* pf, long long pf_bytes,
                        void* pf_sink, hipStream_t st);
 int pa_sample_workspace_floats(int rows, int V);
+int pa_patch_pending_ids(int* ids, const int* sampled, int T, int n_sampled, hipStream_t st);
 int pa_sample(int* out_tokens, float* out_keys, float* workspace, const void* logits, int rows,
               int V, int ld, int vocab_offset, const float* temperature, const int* mask_class,
               const uint32_t* class_masks, int mask_words, const int64_t* seeds,
@@ -532,6 +533,15 @@ int64_t sample_workspace_floats(int64_t rows, int64_t V) {
   return pa_sample_workspace_floats(rows, V);
 }
 
+void patch_pending_ids(at::Tensor ids, at::Tensor sampled) {
+  TORCH_CHECK(ids.is_cuda() && ids.scalar_type() == at::kInt && ids.is_contiguous(), "ids: int32 device tensor");
+  TORCH_CHECK(sampled.is_cuda() && sampled.scalar_type() == at::kInt && sampled.is_contiguous(),
+              "sampled: int32 device tensor");
+  check_rc(pa_patch_pending_ids(ids.data_ptr<int>(), sampled.data_ptr<int>(), (int)ids.numel(),
+                                (int)sampled.numel(), cur_stream()),
+           "patch_pending_ids");
+}
+
 void sample(at::Tensor out_tokens, c10::optional<at::Tensor> out_keys, at::Tensor workspace,
             at::Tensor logits, int64_t vocab_offset, at::Tensor temperature, at::Tensor mask_class,
             at::Tensor class_masks, at::Tensor seeds, at::Tensor offsets,
@@ -745,6 +755,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("part_size") = py::none(), py::arg("prefetch") = py::none(), py::arg("prefetch_sink") = py::none(),
         py::arg("split_prefill") = 0);
   m.def("sample_workspace_floats", &sample_workspace_floats);
+  m.def("patch_pending_ids", &patch_pending_ids);
   m.def("sample", &sample, py::arg("out_tokens"), py::arg("out_keys"), py::arg("workspace"),
         py::arg("logits"), py::arg("vocab_offset"), py::arg("temperature"), py::arg("mask_class"),
         py::arg("class_masks"), py::arg("seeds"), py::arg("offsets"), py::arg("forced"),

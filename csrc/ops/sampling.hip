@@ -266,3 +266,28 @@ extern "C" int pa_sample(int* out_tokens, float* out_keys, float* workspace, con
                      pk, pi, forced, nchunk);
   return (int)hipGetLastError();
 }
+
+// Pipelined engine steps (engine.py, async_steps): a row whose previous token is still
+// being sampled by the step in flight enters the next step with input id -(r + 1), r =
+// its sampling row there. This runs first in the next step's graph, after the previous
+// step's sampler (same stream), and replaces each such id by the sampled token.
+namespace pa {
+__global__ __launch_bounds__(256) void patch_pending_ids_kernel(int* __restrict__ ids,
+                                                                const int* __restrict__ sampled, int T,
+                                                                int n_sampled) {
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  if (t >= T) return;
+  const int v = ids[t];
+  if (v < 0) {
+    const int r = -v - 1;
+    ids[t] = r < n_sampled ? sampled[r] : 0;
+  }
+}
+}  // namespace pa
+
+extern "C" int pa_patch_pending_ids(int* ids, const int* sampled, int T, int n_sampled, hipStream_t st) {
+  if (T <= 0) return 0;
+  hipLaunchKernelGGL(pa::patch_pending_ids_kernel, dim3((T + 255) / 256), dim3(256), 0, st, ids, sampled, T,
+                     n_sampled);
+  return (int)hipGetLastError();
+}

@@ -174,6 +174,9 @@ PYBIND11_MODULE(_runtime, m) {
       .def("take_embed_resets", &Scheduler::take_embed_resets)
       .def("num_free_embed_rows", &Scheduler::num_free_embed_rows)
       .def_property_readonly("prefix_defers", &Scheduler::prefix_defers)
+      .def_property_readonly("inflight_steps", &Scheduler::inflight_steps)
+      .def_property_readonly("spec_rows", &Scheduler::spec_rows)
+      .def_property_readonly("spec_voided", &Scheduler::spec_voided)
       .def("debug_state", [](const Scheduler& s) {
         py::list l;
         for (const auto& x : s.debug_state())

@@ -2,65 +2,71 @@
 
 namespace rt {
 
-void Grammar::skip_empty() {
-  while (seg_ < (int32_t)segs_.size() && segs_[seg_].kind == Segment::LIT &&
-         segs_[seg_].tokens.empty())
-    ++seg_;
+void Grammar::skip_empty(Cursor& c) const {
+  while (c.seg < (int32_t)segs_.size() && segs_[c.seg].kind == Segment::LIT &&
+         segs_[c.seg].tokens.empty())
+    ++c.seg;
 }
 
-void Grammar::next(int32_t* cls, int32_t* forced) const {
+void Grammar::next_at(const Cursor& c, int32_t* cls, int32_t* forced) const {
   *cls = -1;
   *forced = -1;
-  if (done()) return;
-  const Segment& s = segs_[seg_];
+  if (done_at(c)) return;
+  const Segment& s = segs_[c.seg];
   switch (s.kind) {
     case Segment::LIT:
-      *forced = s.tokens[pos_];
+      *forced = s.tokens[c.pos];
       return;
     case Segment::CHOICE:
       *cls = s.cls;
       return;
     case Segment::STR:
-      if (pos_ >= s.max_tokens) *forced = s.end_tok;
-      else if (s.cls_last >= 0 && pos_ < s.min_items) *cls = s.cls_last;  // body shorter than its minimum
+      if (c.pos >= s.max_tokens) *forced = s.end_tok;
+      else if (s.cls_last >= 0 && c.pos < s.min_items) *cls = s.cls_last;  // body shorter than its minimum
       else *cls = s.cls;
       return;
     case Segment::LIST:
-      if (pos_ >= s.max_tokens) {
+      if (c.pos >= s.max_tokens) {
         // item budget exhausted: close the item; keep going until min_items
-        *forced = (items_ + 1 < s.min_items && items_ + 1 < s.max_items) ? s.sep_tok : s.end_tok;
+        *forced = (c.items + 1 < s.min_items && c.items + 1 < s.max_items) ? s.sep_tok : s.end_tok;
       } else {
-        *cls = (items_ + 1 >= s.max_items) ? s.cls_last : s.cls;
+        *cls = (c.items + 1 >= s.max_items) ? s.cls_last : s.cls;
       }
       return;
   }
 }
 
-void Grammar::advance(int32_t token) {
-  if (done()) return;
-  const Segment& s = segs_[seg_];
+void Grammar::advance_at(Cursor& c, int32_t token) const {
+  if (done_at(c)) return;
+  const Segment& s = segs_[c.seg];
   switch (s.kind) {
     case Segment::LIT:
-      if (++pos_ >= (int32_t)s.tokens.size()) next_segment();
+      if (++c.pos >= (int32_t)s.tokens.size()) next_segment(c);
       return;
     case Segment::CHOICE:
-      next_segment();
+      next_segment(c);
       return;
     case Segment::STR:
-      if (token == s.end_tok) next_segment();
-      else ++pos_;
+      if (token == s.end_tok) next_segment(c);
+      else ++c.pos;
       return;
     case Segment::LIST:
       if (token == s.end_tok) {
-        next_segment();
+        next_segment(c);
       } else if (token == s.sep_tok) {
-        ++items_;
-        pos_ = 0;
+        ++c.items;
+        c.pos = 0;
       } else {
-        ++pos_;
+        ++c.pos;
       }
       return;
   }
+}
+
+bool Grammar::token_independent(const Cursor& c) const {
+  if (done_at(c)) return true;
+  const Segment& s = segs_[c.seg];
+  return s.kind == Segment::LIT || s.kind == Segment::CHOICE;
 }
 
 int32_t Grammar::take_forced_run(std::vector<int32_t>& out, int32_t max) {

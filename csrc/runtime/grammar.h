@@ -18,6 +18,10 @@
 // Runs of forced tokens are handed to the scheduler in one piece ("jump-forward"):
 // they enter the KV cache as a multi-token chunk in the next forward instead of
 // one decode step per token.
+//
+// The automaton state is a Cursor (segment, position, item count), so the scheduler
+// can run it ahead on a copy: pipelined steps plan a row's next step before its
+// pending token is known (scheduler.cpp, "speculative rows").
 #pragma once
 #include <cstdint>
 #include <vector>
@@ -39,25 +43,42 @@ struct Segment {
 
 class Grammar {
  public:
-  explicit Grammar(std::vector<Segment> segs) : segs_(std::move(segs)) { skip_empty(); }
-  bool done() const { return seg_ >= (int32_t)segs_.size(); }
+  struct Cursor {
+    int32_t seg = 0, pos = 0, items = 0;
+    bool operator==(const Cursor& o) const { return seg == o.seg && pos == o.pos && items == o.items; }
+  };
+  // a token id that is neither a closing nor a separator token of any segment
+  static constexpr int32_t GENERIC = -2;
+
+  explicit Grammar(std::vector<Segment> segs) : segs_(std::move(segs)) { skip_empty(cur_); }
+  bool done() const { return done_at(cur_); }
   // (mask class, forced token); forced >= 0 means the token is determined.
-  void next(int32_t* cls, int32_t* forced) const;
-  void advance(int32_t token);
+  void next(int32_t* cls, int32_t* forced) const { next_at(cur_, cls, forced); }
+  void advance(int32_t token) { advance_at(cur_, token); }
   // Append the run of forced tokens starting at the current state (at most `max`),
   // advancing the automaton over them.
   int32_t take_forced_run(std::vector<int32_t>& out, int32_t max);
 
+  // cursor form (a copy of the state the scheduler can run ahead)
+  const Cursor& cursor() const { return cur_; }
+  bool done_at(const Cursor& c) const { return c.seg >= (int32_t)segs_.size(); }
+  void next_at(const Cursor& c, int32_t* cls, int32_t* forced) const;
+  void advance_at(Cursor& c, int32_t token) const;
+  // true when advance_at(c, t) gives the same state for every token t the mask allows
+  // (forced literals and single-choice fields); false for string / list bodies, where
+  // the closing or separator token changes the state
+  bool token_independent(const Cursor& c) const;
+
  private:
-  void skip_empty();
-  void next_segment() {
-    ++seg_;
-    pos_ = 0;
-    items_ = 0;
-    skip_empty();
+  void skip_empty(Cursor& c) const;
+  void next_segment(Cursor& c) const {
+    ++c.seg;
+    c.pos = 0;
+    c.items = 0;
+    skip_empty(c);
   }
   std::vector<Segment> segs_;
-  int32_t seg_ = 0, pos_ = 0, items_ = 0;
+  Cursor cur_;
 };
 
 }  // namespace rt

@@ -166,19 +166,36 @@ int32_t Scheduler::schedule(int32_t* buf) {
   int32_t tok_budget = cfg_.max_num_batched_tokens;
   int32_t prefill_budget = cfg_.max_prefill_tokens;
 
-  // 1) running sequences: decode tokens, jump-forward runs, unfinished prefill chunks
+  // 1) running sequences: decode tokens, jump-forward runs, unfinished prefill chunks.
+  //    With a step in flight (pipelined use), a row that samples in it is continued
+  //    speculatively (predict()); rows listed by an in-flight step are never preempted.
+  if (plans_.size() > 1) throw std::logic_error("scheduler: at most one uncommitted step may be in flight");
+  const int64_t prev_id = plans_.empty() ? -1 : plans_.back().id;
   for (size_t i = 0; i < running_.size(); ++i) {
     Sequence* s = running_[i];
-    if (!s->running) continue;
+    if (!s->running || s->abort_pending) continue;
+    if (prev_id >= 0 && s->pend_plan == prev_id) {
+      Planned e{s, 0, true};
+      if (tok_budget <= 0 || !predict(s, e)) continue;  // may finish: wait for the commit
+      e.n = 1 + (int32_t)e.run.size();
+      if (e.n > tok_budget || !ensure_blocks(s, s->num_computed + e.n)) continue;
+      e.spec = true;
+      e.src_idx = s->pend_idx;
+      tok_budget -= e.n;
+      ++stat_spec_rows_;
+      last_plan_.push_back(std::move(e));
+      continue;
+    }
     const int32_t pending = (int32_t)s->tokens.size() - s->num_computed;
     if (pending <= 0 || tok_budget <= 0) continue;
     const int32_t n = std::min(pending, tok_budget);
     bool ok = ensure_blocks(s, s->num_computed + n);
     while (!ok) {
       // preempt the most recently arrived running sequence that is not yet planned
+      // (and not listed by an in-flight step)
       Sequence* victim = nullptr;
       for (size_t j = running_.size(); j-- > i + 1;) {
-        if (running_[j]->running) {
+        if (running_[j]->running && running_[j]->inflight == 0 && !running_[j]->abort_pending) {
           victim = running_[j];
           break;
         }
@@ -188,7 +205,7 @@ int32_t Scheduler::schedule(int32_t* buf) {
       ok = ensure_blocks(s, s->num_computed + n);
     }
     if (!ok) {
-      preempt(s);
+      if (s->inflight == 0) preempt(s);
       continue;
     }
     last_plan_.push_back({s, n, !s->embed && s->num_computed + n == (int32_t)s->tokens.size()});
@@ -254,11 +271,12 @@ int32_t Scheduler::schedule(int32_t* buf) {
     const int32_t r = T % cfg_.token_align;
     if (T > cfg_.token_align && r > 0 && r <= cfg_.align_slack) {
       int32_t cap = 0;
-      for (const Planned& p : last_plan_) cap += p.n - 1;
+      for (const Planned& p : last_plan_) cap += p.spec ? 0 : p.n - 1;
       if (cap >= r) {
         int32_t left = r;
         for (size_t i = last_plan_.size(); i-- > 0 && left > 0;) {
           Planned& p = last_plan_[i];
+          if (p.spec) continue;
           const int32_t cut = std::min(left, p.n - 1);
           p.n -= cut;
           left -= cut;
@@ -341,7 +359,9 @@ int32_t Scheduler::schedule(int32_t* buf) {
       it[0] = (int32_t)si; it[1] = qb; it[2] = std::min(qtile, n - qb) | (1 << 20); it[3] = 0;
     }
   }
-  for (const Planned& p : last_plan_) {
+  const int64_t plan_id = next_plan_id_;
+  for (size_t pi = 0; pi < last_plan_.size(); ++pi) {
+    Planned& p = last_plan_[pi];
     Sequence* s = p.s;
     const int32_t n = p.n, c0 = s->num_computed, ctx = c0 + n;
     qs[ns] = T;
@@ -350,7 +370,9 @@ int32_t Scheduler::schedule(int32_t* buf) {
     const int32_t erow = s->embed_slot >= 0 ? s->embed_slot : L.max_seqs;
     for (int32_t j = 0; j < n; ++j) {
       const int32_t ppos = c0 + j;
-      ids[T + j] = s->tokens[ppos];
+      // speculative entry: the pending token comes from the in-flight step's sampled row
+      // src_idx (the device patches -(src_idx + 1) before the embedding lookup)
+      ids[T + j] = !p.spec ? s->tokens[ppos] : (j == 0 ? -(p.src_idx + 1) : p.run[j - 1]);
       pos[T + j] = ppos;
       slots[T + j] = s->blocks[ppos / B] * B + ppos % B;
       er[T + j] = erow;
@@ -361,10 +383,15 @@ int32_t Scheduler::schedule(int32_t* buf) {
     if (p.sample) {
       lr[nsamp] = T + n - 1;
       int32_t cls = -1, forced = -1;
-      if (s->grammar) s->grammar->next(&cls, &forced);
+      if (s->grammar) {
+        if (p.spec) s->grammar->next_at(p.cur, &cls, &forced);
+        else s->grammar->next(&cls, &forced);
+      }
       mc[nsamp] = cls;
       fc[nsamp] = forced;
-      off[nsamp] = (int32_t)s->tokens.size();
+      off[nsamp] = ctx;  // the sampled token's position (= tokens.size() for a known row)
+      s->pend_plan = plan_id;
+      s->pend_idx = nsamp;
       temp[nsamp] = s->temperature;
       tk[nsamp] = s->top_k;
       tp[nsamp] = s->top_p;
@@ -388,6 +415,12 @@ int32_t Scheduler::schedule(int32_t* buf) {
       }
     }
     s->num_computed = ctx;
+    p.end = ctx;
+    ++s->inflight;
+    if (p.spec) {
+      s->spec_plan = plan_id;
+      s->spec_entry = (int32_t)pi;
+    }
     T += n;
     ++ns;
   }
@@ -424,8 +457,41 @@ int32_t Scheduler::schedule(int32_t* buf) {
   if (nit > L.max_items)  // by construction (psz guard above, max_items sizing) this cannot happen
     throw std::logic_error("scheduler: attention item list overflows max_items");
   buf[L.n_items] = nit;
-  if (T > 0) ++stat_steps_;
+  if (T > 0) {
+    ++stat_steps_;
+    plans_.push_back(Plan{next_plan_id_++, std::move(last_plan_)});
+  }
+  last_plan_.clear();
   return T;
+}
+
+bool Scheduler::predict(Sequence* s, Planned& e) const {
+  // Mirrors commit() for the pending token (any token the row's mask allows, and for
+  // string / list bodies one that neither closes nor separates; no EOS for free text):
+  // false when the row could finish there, so it waits for the commit instead.
+  const int32_t ng = s->num_generated + 1;
+  const int32_t ntok = (int32_t)s->tokens.size() + 1;
+  if (ng >= s->max_tokens || ntok >= cfg_.max_model_len) return false;
+  e.run.clear();
+  if (!s->grammar) return true;
+  const Grammar& g = *s->grammar;
+  Grammar::Cursor c = g.cursor();
+  int32_t cls, forced;
+  g.next_at(c, &cls, &forced);
+  g.advance_at(c, forced >= 0 ? forced : Grammar::GENERIC);
+  if (g.done_at(c)) return false;
+  const int32_t room = std::min(s->max_tokens - ng, cfg_.max_model_len - ntok);
+  int32_t k = 0;
+  while (k < room && !g.done_at(c)) {
+    g.next_at(c, &cls, &forced);
+    if (forced < 0) break;
+    e.run.push_back(forced);
+    g.advance_at(c, forced);
+    ++k;
+  }
+  if (g.done_at(c) || ng + k >= s->max_tokens || ntok + k >= cfg_.max_model_len) return false;
+  e.cur = c;
+  return true;
 }
 
 SeqOutput Scheduler::finish(Sequence* s, int32_t reason, double now) {
@@ -447,21 +513,31 @@ SeqOutput Scheduler::finish(Sequence* s, int32_t reason, double now) {
 
 std::vector<SeqOutput> Scheduler::commit(const int32_t* sampled, int32_t n) {
   std::vector<SeqOutput> outs;
+  if (plans_.empty()) return outs;
+  Plan plan = std::move(plans_.front());
+  plans_.pop_front();
+  Plan* next = plans_.empty() ? nullptr : &plans_.front();  // the step still in flight, if any
   const double now = now_seconds();
+  for (const Planned& p : plan.rows) --p.s->inflight;
   int32_t idx = 0;
   std::vector<Sequence*> done;
-  for (const Planned& p : last_plan_) {
+  for (const Planned& p : plan.rows) {
     Sequence* s = p.s;
+    int32_t tok = -1;
+    if (p.sample) {
+      if (idx >= n) break;
+      tok = sampled[idx++];
+    }
+    if (p.voided || s->done || s->abort_pending) continue;
     if (!p.sample) {
       register_full_blocks(s);
-      if (s->embed && s->num_computed == (int32_t)s->tokens.size()) {
+      if (s->embed && p.end == (int32_t)s->tokens.size()) {
         outs.push_back(finish(s, FINISH_EMBED, now));  // frees the row: the caller reads it first
         done.push_back(s);
       }
       continue;
     }
-    if (idx >= n) break;
-    const int32_t tok = sampled[idx++];
+    const int32_t before = (int32_t)s->tokens.size();
     if (s->t_first_token < 0) s->t_first_token = now;
     s->tokens.push_back(tok);
     ++s->num_generated;
@@ -486,19 +562,55 @@ std::vector<SeqOutput> Scheduler::commit(const int32_t* sampled, int32_t n) {
       if (s->grammar->done()) fin = FINISH_STOP;
       else if (s->num_generated >= s->max_tokens) fin = FINISH_LENGTH;
     }
+    // check the speculative continuation the in-flight step holds for this row
+    if (next && s->spec_plan == next->id) {
+      Planned& e = next->rows[s->spec_entry];
+      bool ok = fin == NOT_FINISHED &&
+                (int32_t)s->tokens.size() == before + 1 + (int32_t)e.run.size() &&
+                std::equal(e.run.begin(), e.run.end(), s->tokens.begin() + before + 1);
+      if (ok && s->grammar) ok = s->grammar->cursor() == e.cur;
+      if (!ok) {
+        // drop the entry: its sample is discarded, and the row resumes from the
+        // sampled token (recomputed next step: same KV, written again)
+        e.voided = true;
+        ++stat_spec_voided_;
+        s->num_computed = before;
+        s->pend_plan = -1;
+      }
+      s->spec_plan = -1;
+    }
     register_full_blocks(s);
     if (fin != NOT_FINISHED) {
       outs.push_back(finish(s, fin, now));
       done.push_back(s);
     }
   }
-  last_plan_.clear();
+  // rows aborted while listed by an in-flight step finish once no step lists them
+  for (size_t i = 0; i < abort_wait_.size();) {
+    Sequence* s = abort_wait_[i];
+    if (s->inflight > 0) {
+      ++i;
+      continue;
+    }
+    aborted_.push_back(finish(s, FINISH_ABORT, now));
+    done.push_back(s);
+    abort_wait_.erase(abort_wait_.begin() + i);
+  }
   if (!done.empty()) {
     running_.erase(std::remove_if(running_.begin(), running_.end(),
                                   [](Sequence* s) { return !s->running; }),
                    running_.end());
-    for (Sequence* s : done) seqs_.erase(s->id);
+    for (Sequence* s : done) {
+      s->done = true;
+      auto it = seqs_.find(s->id);
+      if (it == seqs_.end()) continue;
+      if (s->inflight > 0) zombies_.push_back(std::move(it->second));  // a voided entry still lists it
+      seqs_.erase(it);
+    }
   }
+  zombies_.erase(std::remove_if(zombies_.begin(), zombies_.end(),
+                                [](const std::unique_ptr<Sequence>& z) { return z->inflight == 0; }),
+                 zombies_.end());
   return outs;
 }
 
@@ -506,6 +618,13 @@ bool Scheduler::abort(int64_t id) {
   auto it = seqs_.find(id);
   if (it == seqs_.end()) return false;
   Sequence* s = it->second.get();
+  if (s->inflight > 0) {  // listed by an uncommitted step: finished at that step's commit
+    if (!s->abort_pending) {
+      s->abort_pending = true;
+      abort_wait_.push_back(s);
+    }
+    return true;
+  }
   waiting_.erase(std::remove(waiting_.begin(), waiting_.end(), s), waiting_.end());
   aborted_.push_back(finish(s, FINISH_ABORT, now_seconds()));
   running_.erase(std::remove(running_.begin(), running_.end(), s), running_.end());

@@ -106,6 +106,16 @@ struct Sequence {
   bool embed = false;
   int32_t embed_slot = -1;
   int32_t defer_count = 0;  // steps deferred waiting for an in-flight identical prefix
+  // pipelined steps (Scheduler "speculative rows"): plans not yet committed that list this
+  // sequence; the plan (id) and row in which it last sampled; the plan and entry index of
+  // its speculative continuation
+  int32_t inflight = 0;
+  int64_t pend_plan = -1;
+  int32_t pend_idx = -1;
+  int64_t spec_plan = -1;
+  int32_t spec_entry = -1;
+  bool done = false;           // finished while a later in-flight plan still lists it
+  bool abort_pending = false;  // aborted while in flight: finished once no plan lists it
 };
 
 class Scheduler {
@@ -121,9 +131,23 @@ class Scheduler {
   bool abort(int64_t id);
   // Fill `buf` (layout()) for the next step. Returns the number of tokens in the
   // step (0 = nothing to run).
+  //
+  // Pipelined use: schedule() may be called again before the previous step is
+  // committed (at most one uncommitted step). A row that samples in that in-flight step
+  // is then planned speculatively: its unknown token enters the new step as input id
+  // -(r + 1) (r = its sampling row in the in-flight step; the device replaces it from
+  // that step's sampled tokens before the embedding lookup), followed by the grammar's
+  // forced run where that run does not depend on the token. String and list bodies
+  // assume a body token (not the closing / separator token), free-text rows assume no
+  // EOS. commit() of the in-flight step checks the guess; a wrong guess voids the row's
+  // speculative entry (its sample is dropped, its KV beyond the pending token is
+  // recomputed) — only the sampled token's own KV is kept, and it is always right.
   int32_t schedule(int32_t* buf);
-  // Consume the sampled tokens of the last scheduled step (one per sampling row).
+  // Consume the sampled tokens of the oldest uncommitted step (one per sampling row).
   std::vector<SeqOutput> commit(const int32_t* sampled, int32_t n);
+  int32_t inflight_steps() const { return (int32_t)plans_.size(); }
+  int64_t spec_rows() const { return stat_spec_rows_; }
+  int64_t spec_voided() const { return stat_spec_voided_; }
   // Finished-by-abort outputs are returned here as well.
   std::vector<SeqOutput> drain_aborted();
 
@@ -168,8 +192,24 @@ class Scheduler {
     Sequence* s;
     int32_t n;
     bool sample;
+    int32_t end = 0;              // num_computed after this entry (its last token's position + 1)
+    bool spec = false;            // speculative continuation of a row sampling in the previous plan
+    bool voided = false;          // the speculation failed: nothing of this entry is committed
+    int32_t src_idx = -1;         // spec: sampling row of the pending token in the previous plan
+    std::vector<int32_t> run;     // spec: predicted forced tokens after the pending token
+    Grammar::Cursor cur;          // spec: predicted automaton state before this entry's sample
   };
-  std::vector<Planned> last_plan_;
+  struct Plan {
+    int64_t id;
+    std::vector<Planned> rows;
+  };
+  bool predict(Sequence* s, Planned& e) const;
+  std::vector<Planned> last_plan_;   // the plan being built by schedule()
+  std::deque<Plan> plans_;           // scheduled, not yet committed (oldest first)
+  int64_t next_plan_id_ = 0;
+  std::vector<std::unique_ptr<Sequence>> zombies_;
+  std::vector<Sequence*> abort_wait_;               // aborted while listed by an in-flight step  // finished, still listed by an in-flight plan
+  int64_t stat_spec_rows_ = 0, stat_spec_voided_ = 0;
   std::vector<SeqOutput> aborted_;
   std::vector<int32_t> embed_free_;    // free pooling rows (0 .. max_seqs - 1)
   std::vector<int32_t> embed_resets_;  // rows of preempted embedding requests, to be cleared

@@ -97,6 +97,9 @@ class EngineConfig:
     # interpreter thread-switch interval while the engine thread runs (sys.setswitchinterval);
     # None = env PILOTTAI_GIL_SWITCH_S or the interpreter default (5 ms)
     gil_switch_interval: Optional[float] = None
+    # pipelined steps: step N+1 is scheduled and launched while step N runs;
+    # rows sampling in N continue speculatively (runtime/scheduler.h). TP = 1 only.
+    async_steps: bool = False
 
 
 # TP step header: [op, T, ns, nsamp, bucket, masks_changed, n_copy, truncate, embed]
@@ -228,11 +231,16 @@ class LLMEngine:
             "eos_ids": list(self.tok.eos_ids)})
         L = self.L = self.sched.layout()
         pin = self.on_gpu
-        self._host_meta = torch.zeros(L["total"], dtype=torch.int32, pin_memory=pin)
+        # pipelined steps: two host-side step descriptions (one being copied / in flight,
+        # one being scheduled); the device copy is stream-ordered behind the previous step
+        self._async = bool(cfg.async_steps) and self.tp.size == 1
+        nbuf = 2 if self._async else 1
+        self._host_metas = [torch.zeros(L["total"], dtype=torch.int32, pin_memory=pin) for _ in range(nbuf)]
+        self._host_meta = self._host_metas[0]
         self._host_ptr = self._host_meta.data_ptr()
         self._host_np = self._host_meta.numpy()
-        self._dev_meta = torch.zeros(L["total"], dtype=torch.int32, device=self.device) if self.on_gpu \
-            else self._host_meta
+        self._dev_meta = torch.zeros(L["total"], dtype=torch.int32, device=self.device) \
+            if (self.on_gpu or self._async) else self._host_meta
         self._att_counters = torch.zeros(L["max_seqs"] * kv_local, dtype=torch.int32, device=self.device)
         self._init_views()
         V = mc.vocab_size
@@ -242,7 +250,11 @@ class LLMEngine:
         self._sync_masks()
         S = cfg.max_num_seqs
         self._sampled_dev = torch.zeros(S, dtype=torch.int32, device=self.device)
-        self._sampled_host = torch.zeros(S, dtype=torch.int32, pin_memory=pin)
+        self._sampled_hosts = [torch.zeros(S, dtype=torch.int32, pin_memory=pin) for _ in range(nbuf)]
+        self._sampled_host = self._sampled_hosts[0]
+        self._inflight: "deque" = deque()  # launched, not yet committed steps (pipelined mode)
+        self._slot = 0
+        self._last_done = 0.0
         self._keys_dev = torch.zeros(S, dtype=torch.float32, device=self.device)
         # embedding requests: per-request pooling rows (+ one row that collects every other
         # token), summed in the step graph, read and cleared when the request finishes
@@ -349,6 +361,8 @@ class LLMEngine:
 
     def _forward_and_sample(self, bucket: int, s_b: int, ns: int, trunc: bool = False, embed: bool = False):
         meta = self._meta_for(bucket, s_b, ns)
+        if self._async:  # pending tokens of rows that sampled in the previous step
+            ops.patch_pending_ids(meta.input_ids[:bucket], self._sampled_dev)
         logits = self.model.forward(meta, self.kv, bucket, s_b, self._part_o, self._part_ml,
                                     embed=(self._embed_rows, self._embed_pool) if embed else None)
         tau = None
@@ -383,9 +397,11 @@ class LLMEngine:
         if g is None:
             saved = self._dev_meta[:n_copy].clone()
             pool = self._embed_pool.clone()
+            samp = self._sampled_dev.clone()  # the previous step's tokens (pipelined mode)
             self.capture_graphs([bucket], trunc=trunc, embed=embed)  # clobbers the device metadata
             self._dev_meta[:n_copy].copy_(saved)
             self._embed_pool.copy_(pool)
+            self._sampled_dev.copy_(samp)
             g = self._graphs[(bucket, trunc, embed)]
         g.replay()
         self.stats["graph_replays"] += 1
@@ -678,6 +694,8 @@ class LLMEngine:
 
     def step(self) -> bool:
         """Run one engine step. Returns False when there was nothing to run."""
+        if self._async:
+            return self._step_pipelined()
         self._drain_inbox()
         if not self.sched.has_work():
             self._flush_deliveries()
@@ -747,6 +765,92 @@ class LLMEngine:
             self._flush_deliveries()  # nothing to overlap with: deliver now
         return True
 
+    # ------------------------------------------------------------- pipelined steps
+    def _step_pipelined(self) -> bool:
+        """One turn of the pipelined loop: launch the next step if fewer than two are in
+        flight, then (with two in flight, or nothing new to launch) wait for the oldest and
+        commit it. In steady state step N+1 is scheduled, copied and launched while step N
+        runs on the device, so the device never waits for the host's schedule / launch /
+        commit (0.5-0.6 ms per step in the serial loop, BENCH_r02 step_phase_ms)."""
+        self._drain_inbox()
+        launched = False
+        if len(self._inflight) < 2 and self.sched.has_work():
+            launched = self._launch_next()
+        if self._inflight and (len(self._inflight) == 2 or not launched):
+            self._complete(self._inflight.popleft())
+            return True
+        if not launched:
+            self._flush_deliveries()
+        return launched
+
+    def _launch_next(self) -> bool:
+        L = self.L
+        slot = self._slot
+        hm = self._host_metas[slot]
+        t0 = time.perf_counter()
+        with trace_range("engine.schedule"):
+            T = self.sched.schedule(hm.data_ptr())
+        t_sched = time.perf_counter()
+        if T == 0:
+            if not self._inflight and self.sched.num_running == 0 and self.sched.num_waiting > 0:
+                raise RuntimeError("KV cache too small for the head request")
+            return False
+        c = hm.numpy()[L["counts"]:L["counts"] + 8]
+        ns, nsamp, trunc, embed = int(c[1]), int(c[2]), int(c[6]) > 0, int(c[7]) > 0
+        bucket = next(b for b in self.buckets if b >= T)
+        self._sync_masks()
+        n_copy = L["embed_rows"] + bucket if embed else L["block_table"] + ns * L["max_blocks"]
+        resets = self.sched.take_embed_resets()
+        if resets:
+            self._embed_pool[torch.tensor(resets, dtype=torch.long, device=self.device)] = 0.0
+        self._dev_meta[:n_copy].copy_(hm[:n_copy], non_blocking=self.on_gpu)
+        with torch.inference_mode(), trace_range("engine.forward"):
+            self._run(bucket, ns, trunc, n_copy, embed)
+        if nsamp:
+            self._sampled_hosts[slot][:nsamp].copy_(self._sampled_dev[:nsamp], non_blocking=self.on_gpu)
+        ev = None
+        if self.on_gpu:
+            ev = torch.cuda.Event()
+            ev.record()
+        t_launch = time.perf_counter()
+        self._inflight.append((slot, T, bucket, nsamp, embed, ev, t0))
+        self._slot = (slot + 1) % len(self._host_metas)
+        st = self.stats
+        st["host_sched_s"] += t_sched - t0
+        st["host_launch_s"] += t_launch - t_sched
+        self._flush_deliveries()  # the previous step's outputs, while this one is queued
+        st["host_deliver_s"] += time.perf_counter() - t_launch
+        return True
+
+    def _complete(self, rec):
+        slot, T, bucket, nsamp, embed, ev, t0 = rec
+        t_w = time.perf_counter()
+        if ev is not None:
+            ev.synchronize()
+        t_sync = time.perf_counter()
+        with trace_range("engine.commit"):
+            outs = self.sched.commit(self._sampled_hosts[slot].data_ptr(), nsamp)
+        if embed:
+            self._read_embeddings(outs)
+        st = self.stats
+        st["device_wait_s"] += t_sync - t_w
+        st["steps"] += 1
+        st["tokens"] += T
+        st["bucket_tokens"] += bucket
+        st["sampled"] += nsamp
+        # device time attributable to this step: from its launch (or the previous step's
+        # completion, whichever is later) to its completion
+        dt = t_sync - max(t0, self._last_done)
+        self._last_done = t_sync
+        st["busy_s"] += dt
+        bh = self.bucket_hist.setdefault(bucket, [0, 0.0])
+        bh[0] += 1
+        bh[1] += dt
+        st["host_commit_s"] += time.perf_counter() - t_sync
+        self._pending_out.extend(outs)
+        if not self._inflight and not self.sched.has_work():
+            self._flush_deliveries()
+
     def _read_embeddings(self, outs):
         """Pooled rows of the embedding requests this step finished, read while the device
         is idle (step synchronised): their delivery runs during the NEXT step, where a read
@@ -807,6 +911,7 @@ class LLMEngine:
             "prompt_tokens": s.total_prompt_tokens, "prefix_cache_hit_tokens": s.total_cached_tokens,
             "preemptions": s.total_preemptions, "graphs": len(self._graphs), "aligned_steps": s.aligned_steps,
             "prefix_defers": s.prefix_defers,
+            "spec_rows": s.spec_rows, "spec_voided": s.spec_voided,
             "kv_cache_gb": self.kv.k.numel() * 2 * 2 / 2**30,
             "weights_gb": self.model.weight_bytes() / 2**30,
         })

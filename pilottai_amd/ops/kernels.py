@@ -176,6 +176,19 @@ def topkp_threshold(logits, V: int, temperature, top_k, top_p, mask_class, class
     return tau
 
 
+def patch_pending_ids(ids: torch.Tensor, sampled: torch.Tensor) -> None:
+    """In place: ids[t] = sampled[-ids[t] - 1] where ids[t] < 0 (pipelined engine steps:
+    a row's pending token comes from the previous step's sampler, csrc/ops/sampling.hip)."""
+    if _on_gpu(ids):
+        require_native().patch_pending_ids(ids, sampled)
+        return
+    neg = ids < 0
+    if bool(neg.any()):
+        r = (-ids[neg] - 1).long()
+        ids[neg] = torch.where(r < sampled.numel(), sampled[r.clamp(max=sampled.numel() - 1)],
+                               torch.zeros_like(r, dtype=ids.dtype))
+
+
 def sample(logits, temperature, mask_class, class_masks, seeds, offsets, forced=None,
            out: Optional[torch.Tensor] = None, workspace: Optional[torch.Tensor] = None,
            vocab_offset: int = 0, out_keys: Optional[torch.Tensor] = None,

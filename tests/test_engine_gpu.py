@@ -202,3 +202,34 @@ def test_embedding_requests_on_the_gpu_engine(engine):
     assert gen in outs and engine.failed is None
     assert float(((v2 - v).norm(dim=1) / v.norm(dim=1)).max()) < 1e-2
     assert float(engine._embed_pool[:-1].abs().sum()) == 0.0
+
+
+def test_pipelined_steps_on_gpu(gpu):
+    """Pipelined engine steps (EngineConfig.async_steps: step N+1 scheduled, copied and
+    launched while step N runs; pending tokens patched on the device by
+    csrc/ops/sampling.hip patch_pending_ids inside the step graph) at the exact
+    Llama-3-8B layer dims: greedy tokens of a mixed batch match the dense fp32 reference,
+    and schema replies decoded with speculative rows parse."""
+    from pilottai_amd.engine.engine import EngineConfig, LLMEngine
+
+    eng = LLMEngine(EngineConfig(model="llama-3-8b-2l", max_num_seqs=16, max_num_batched_tokens=512,
+                                 max_model_len=1024, num_kv_blocks=512, token_buckets=[16, 48, 128, 256, 512],
+                                 async_steps=True), device=gpu)
+    try:
+        assert eng._async
+        tok = eng.tok
+        words = ("agents plan tasks and tools while the orchestrator checks every result " * 40).split()
+        prompts = [tok.encode(" ".join(words[:k])) for k in (6, 40, 150)]
+        outs = eng.generate(prompts, temperature=0.0, max_tokens=8, ignore_eos=True)
+        for p, o in zip(prompts, outs):
+            assert len(o.token_ids) == 8
+            _check_greedy(eng, p, o.token_ids)
+        segs = eng.grammar.compile("agent.task_analysis")
+        rs = eng.generate([tok.encode(f"Task {i}: summarize the report") for i in range(8)], temperature=0.8,
+                          max_tokens=160, grammar=segs)
+        for r in rs:
+            assert r.finish_reason == "stop"
+            json.loads(r.text)
+        assert eng.sched.spec_rows > 0 and eng.sched.inflight_steps == 0
+    finally:
+        eng.stop()

@@ -478,3 +478,87 @@ def test_prefix_cache_protects_reused_blocks_under_eviction():
     for i in range(10):  # 10 one-off prompts of 5 blocks: more than the pool holds
         _sched_run(s, L, [(10 + i, [3000 + 100 * i + t for t in range(80)])])
     assert _sched_run(s, L, [(99, P + [13] * 16)])[99][4] == 64
+
+
+def _pipeline_workload(tok, async_steps: bool, nkv: int):
+    """Mixed requests on the tiny CPU engine: schema replies, two hand-made grammars whose
+    string / list classes hold the closing and separator tokens at high odds (so the
+    pipelined scheduler's body-token guess fails often), free text with frequent stop
+    tokens, ignore_eos rows, an abort mid-run; a small KV pool forces preemption."""
+    from pilottai_amd.engine.engine import EngineConfig, LLMEngine
+    from pilottai_amd.engine.grammar import LIST, STR
+
+    e = LLMEngine(EngineConfig(model="tiny", max_num_seqs=16, max_num_batched_tokens=128, max_model_len=512,
+                               num_kv_blocks=nkv, async_steps=async_steps, token_align=32, align_slack=8),
+                  device="cpu")
+    reg = e.grammar.reg
+    V = e.model_cfg.vocab_size
+    q_end, sep, a, b = tok.encode('"')[0], 11, 40, 41
+    mask = np.zeros(V, dtype=bool)
+    mask[[a, b, q_end]] = True
+    c_str = reg._add("test:str3", mask)
+    mask2 = mask.copy()
+    mask2[sep] = True
+    c_list = reg._add("test:list4", mask2)
+    lit = e.grammar._finalize(['{"k": "'])
+    g_str = lit + [(STR, [], c_str, -1, q_end, -1, 12, 1, 1)] + e.grammar._finalize(['"}'])
+    g_list = lit + [(LIST, [], c_list, c_str, q_end, sep, 6, 1, 4)] + e.grammar._finalize(['"]}'])
+    names = ["orchestrator.result_evaluation", "agent.task_analysis", "agent.tool_selection",
+             "orchestrator.task_decomposition", "workflow.analyze"]
+    stops = list(range(0, V, 40))
+    p = tok.encode("Task: evaluate the quarterly report. Result: ok " * 4)
+    outs = {}
+
+    def cb(o):
+        outs[o.request_id] = o
+
+    ids = []
+    for i in range(28):
+        q = p + tok.encode(f" item {i} " * (i % 4))
+        kind = i % 6
+        if kind == 0:
+            ids.append(e.submit(q, cb, temperature=1.0, max_tokens=200 if i == 0 else 30, seed=i, ignore_eos=True))
+        elif kind == 1:
+            ids.append(e.submit(q, cb, temperature=1.0, max_tokens=40, seed=i, stop_ids=stops))
+        elif kind == 2:
+            ids.append(e.submit(q, cb, temperature=1.0, max_tokens=60, seed=i, grammar=g_str))
+        elif kind == 3:
+            ids.append(e.submit(q, cb, temperature=1.0, max_tokens=80, seed=i, grammar=g_list))
+        else:
+            ids.append(e.submit(q, cb, temperature=1.0, max_tokens=120, seed=i,
+                                grammar=e.grammar.compile(names[i % len(names)])))
+    n = 0
+    while len(outs) < len(ids):
+        assert e.step() or e.sched.has_work() or not e._inbox.empty()
+        n += 1
+        if n == 10:
+            e.abort(ids[0])
+        assert n < 5000
+    assert e.sched.num_running == 0 and e.sched.inflight_steps == 0
+    return e, [outs[i] for i in ids]
+
+
+@pytest.mark.parametrize("nkv", [256, 30])
+def test_pipelined_steps_match_serial_engine(tok, nkv):
+    """Pipelined steps (engine async_steps, runtime/scheduler.h speculative rows): every
+    request's tokens and finish reason equal the serial loop's, including rows whose
+    speculative continuation was voided (closing / separator tokens, stop tokens) and
+    under preemption; the aborted request ends as an abort either way."""
+    s_eng, s_out = _pipeline_workload(tok, False, nkv)
+    a_eng, a_out = _pipeline_workload(tok, True, nkv)
+    assert s_eng.sched.spec_rows == 0
+    assert a_eng.sched.spec_rows > 300 and a_eng.sched.spec_voided > 10, (a_eng.sched.spec_rows,
+                                                                          a_eng.sched.spec_voided)
+    if nkv == 30:
+        assert s_eng.sched.total_preemptions > 0 and a_eng.sched.total_preemptions > 0
+    for i, (x, y) in enumerate(zip(s_out, a_out)):
+        if i == 0:
+            assert x.finish_reason == y.finish_reason == "abort"
+            continue
+        assert x.finish_reason == y.finish_reason, i
+        assert x.token_ids == y.token_ids, i
+    for i, o in enumerate(a_out):
+        if i % 6 >= 4 and o.finish_reason == "stop":  # schema replies parse
+            json.loads(o.text)
+    # every KV block is back in the pool (nothing leaked by voided / aborted entries)
+    assert a_eng.sched.num_free_blocks == s_eng.sched.num_free_blocks
