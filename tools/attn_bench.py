@@ -77,6 +77,8 @@ def main():
     ap.add_argument("--pad", type=int, default=2228, help="items reserved by the 768-token bucket")
     ap.add_argument("--scan", action="store_true", help="prefill length scan instead of the step cases")
     ap.add_argument("--small", action="store_true", help="small-batch decode (8/16 rows) over partition sizes")
+    ap.add_argument("--cases", default="", help="comma-separated subset of the step cases")
+    ap.add_argument("--qcols", default="32,128", help="prefill item widths to time")
     a = ap.parse_args()
     torch.manual_seed(0)
     cases = {
@@ -87,6 +89,10 @@ def main():
         "mix": ([1] * 64 + [320, 320], [512] * 64 + [480, 480]),
         "prefill8x256": ([256] * 8, [768] * 8),
         "prefill2048": ([2048], [2048]),
+        # the bench's dominant step: 4 prompts x 512 new tokens on a 256-token cached prefix
+        "prefill4x512": ([512] * 4, [768] * 4),
+        # ... as it really runs: beside ~40 decode / forced-run rows
+        "step2048": ([512] * 4 + [1] * 40, [768] * 4 + [600] * 40),
     }
     if a.scan:
         cases = {f"pf{n}": ([n], [n]) for n in (8, 32, 128, 256, 512, 1024, 2048, 4096)}
@@ -100,8 +106,10 @@ def main():
                     print(json.dumps({"case": f"decode{ns}_ctx{ctx}", "part": part, "items": n, "us": round(us, 1),
                                       "kv_TBps": round(kvb / us / 1e6, 2)}), flush=True)
         return
+    if a.cases:
+        cases = {k: v for k, v in cases.items() if k in a.cases.split(",")}
     for name, (ql, cl) in cases.items():
-        for qcols in (32, 128):
+        for qcols in [int(x) for x in a.qcols.split(",")]:
             for pad in ((0,) if a.scan else (0, a.pad)):
                 args, kvb, fl, n = setup(ql, cl, pad_items=pad, qcols=qcols)
                 us = timeit(args, a.iters)
