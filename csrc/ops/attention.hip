@@ -613,6 +613,16 @@ constexpr int ATT_LDS_BYTES = ATT_LDS_BYTES0 > PW_NBUF * PW_TILE ? ATT_LDS_BYTES
 // [0, n_items[1]) -- the scheduler lists them first. Split into two launches, each kernel
 // gets the register budget of its own paths (the mixed kernel carries 254 VGPRs, 2 waves
 // per SIMD, for the wide prefill path's sake).
+// MODE 3 (the engine's default): a persistent 1-D grid of 2 workgroups per CU, work-queue
+// scheduled. Workgroup b serves KV head b % KV -- with KV = 8 that is its XCD under the
+// round-robin dispatch, so every K/V page of a head is read through one XCD's L2 -- and
+// takes item b / KV first, then pulls further items from the head's queue counter
+// (queue[kvh]; queue[KV + kvh] counts the workgroups done, and the last one resets both
+// for the next launch). The scheduler lists the items heaviest first, so the workgroups
+// that finish a short prefill item pick up the decode items: in a mixed step they run
+// beside the long prefill items instead of in a second wave after them (MODE 0 holds the
+// decode items until a prefill item retires, and its padded grid's empty workgroups are
+// dispatched between the real ones).
 template <int G, int MODE>
 __global__ __launch_bounds__(256, 2) void paged_attn_kernel(
     bf16* __restrict__ out, float* __restrict__ part_o, float* __restrict__ part_ml,
@@ -621,9 +631,61 @@ __global__ __launch_bounds__(256, 2) void paged_attn_kernel(
     const int* __restrict__ n_items, const int* __restrict__ part_size, const int* __restrict__ q_start,
     const int* __restrict__ q_len, const int* __restrict__ ctx_len,
     const int* __restrict__ block_table, int max_blocks, int H, int KV, float scale_log2,
-    const u32x4* __restrict__ pf, long long pf_lines, u32x4* __restrict__ pf_sink, int acq) {
+    const u32x4* __restrict__ pf, long long pf_lines, u32x4* __restrict__ pf_sink, int acq,
+    int* __restrict__ queue) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int TPW = 16 / G;
+  const int psz_q = part_size ? part_size[0] : ATT_PART;
+  if (MODE == 3) {
+    __shared__ int s_next;
+    const int kvh = (int)blockIdx.x % KV;
+    const int nslot = (int)gridDim.x / KV;
+    const int slot = (int)blockIdx.x / KV;
+    const int n = n_items[0];
+    int item = slot;
+    if (item >= n && pf_lines > 0) {  // no item at all: prefetch as in the grid modes
+      const long long idle = (long long)(nslot - n) * KV;
+      const long long me = (long long)kvh * (nslot - n) + (slot - n);
+      const long long per = (pf_lines + idle - 1) / idle;
+      const long long l1 = min(pf_lines, (me + 1) * per);
+      u32x4 acc = {0u, 0u, 0u, 0u};
+      for (long long l = me * per + threadIdx.x; l < l1; l += blockDim.x) acc ^= pf[4 * l];
+      if (acc.x == 0x9E3779B9u && acc.y == 0x7F4A7C15u && acc.z == 0xF39CC060u && acc.w == 0x5CEDC834u)
+        pf_sink[threadIdx.x] = acc;
+    }
+    while (item < n) {
+      const int4 it = items[item];
+      // the next item is claimed while this one runs: the claim's return is only consumed
+      // after the item (older than the item's loads, it only makes their counted waits
+      // conservative in wave 0)
+      int claimed = 0;
+      if (threadIdx.x == 0)
+        claimed = nslot + __hip_atomic_fetch_add((gi32*)(queue + kvh), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int nq = it.z & 0xff;
+      if (nq <= TPW)
+        decode_item<G>(it, smem, out, part_o, part_ml, counters, q, k_cache, v_cache, q_start, q_len, ctx_len,
+                       block_table, max_blocks, H, KV, kvh, scale_log2, psz_q, acq);
+      else if (nq <= 32 / G)
+        prefill_item<G>(it, smem, out, q, k_cache, v_cache, q_start, q_len, ctx_len, block_table,
+                        max_blocks, H, KV, kvh, scale_log2);
+      else
+        prefill_item_wg<G>(it, smem, out, q, k_cache, v_cache, q_start, q_len, ctx_len, block_table,
+                           max_blocks, H, KV, kvh, scale_log2);
+      if (threadIdx.x == 0) s_next = claimed;
+      __syncthreads();  // LDS reuse by the next item; s_next visible to every wave
+      item = s_next;
+      __syncthreads();
+    }
+    // every workgroup of this head is past its last claim: the last one resets the queue
+    if (threadIdx.x == 0) {
+      const int d = __hip_atomic_fetch_add((gi32*)(queue + KV + kvh), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (d == nslot - 1) {
+        __hip_atomic_store((gi32*)(queue + kvh), 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store((gi32*)(queue + KV + kvh), 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    return;
+  }
   // The first item is loaded together with the item count, not after it: one dependent
   // memory round trip less before the K/V stream starts (decode steps with few rows are
   // latency-bound). In bounds: the host sizes the grid to gridDim.x <= max_items, the
@@ -649,7 +711,7 @@ __global__ __launch_bounds__(256, 2) void paged_attn_kernel(
     }
     return;
   }
-  const int psz = part_size ? part_size[0] : ATT_PART;  // decode partition (keys), per step
+  const int psz = psz_q;  // decode partition (keys), per step
   const int kvh = blockIdx.y;
   for (int item = blockIdx.x + i0; item < n; item += gridDim.x) {
     const int4 it = it_next;
@@ -680,7 +742,7 @@ extern "C" int pa_paged_attention(void* out, float* part_o, float* part_ml, cons
                                   const int* q_len, const int* ctx_len, const int* block_table,
                                   int max_blocks, int H, int KV, float scale_log2,
                                   const void* pf, long long pf_bytes, void* pf_sink,
-                                  hipStream_t st) {
+                                  int* queue, hipStream_t st) {
   if (H % KV != 0) return -1;
   if (pf_bytes > 0 && (pf == nullptr || pf_sink == nullptr || (reinterpret_cast<uintptr_t>(pf) & 15))) return -1;
   const long long pf_lines = pf_bytes > 0 ? pf_bytes / 64 : 0;
@@ -688,6 +750,9 @@ extern "C" int pa_paged_attention(void* out, float* part_o, float* part_ml, cons
   // items are strided over the grid: ~8 resident workgroups per CU over all KV heads
   const int gx = max_items < 1 ? 1 : (max_items < 2048 / KV ? max_items : (2048 / KV > 0 ? 2048 / KV : 1));
   dim3 grid(gx, KV);
+  // queue mode: 2 workgroups per CU (256 CUs), a multiple of KV, at most one slot per item
+  const int qslots = std::max(1, std::min(max_items, 512 / std::max(1, KV)));
+  dim3 qgrid(qslots * KV);
 #define PA_ATT1(GG, MD, GRID, PFP, PFL)                                                         \
   do {                                                                                          \
     static bool attr_##GG##_##MD = false;                                                       \
@@ -701,12 +766,14 @@ extern "C" int pa_paged_attention(void* out, float* part_o, float* part_ml, cons
                        (const pa::bf16*)k_cache, (const pa::bf16*)v_cache, (const int4*)items, \
                        n_items, part_size, q_start, q_len, ctx_len, block_table, max_blocks, H, \
                        KV, scale_log2, (const pa::u32x4*)PFP, PFL, (pa::u32x4*)pf_sink,        \
-                       pa::g_handoff_attn);                                                  \
+                       pa::g_handoff_attn, queue);                                           \
   } while (0)
 #define PA_ATT(GG)                                                                              \
   do {                                                                                          \
     if (max_items <= 0) break;                                                                  \
-    if (split_prefill > 0) {                                                                    \
+    if (queue != nullptr) {                                                                     \
+      PA_ATT1(GG, 3, qgrid, pf, pf_lines);                                                      \
+    } else if (split_prefill > 0) {                                                             \
       PA_ATT1(GG, 2, dim3(std::min(split_prefill, max_items), KV), nullptr, 0LL);              \
       PA_ATT1(GG, 1, grid, pf, pf_lines);                                                       \
     } else {                                                                                    \

@@ -349,15 +349,27 @@ int32_t Scheduler::schedule(int32_t* buf) {
   }
   buf[L.part_size] = psz;
 
-  // prefill (q-split) tiles go first in the item list, heaviest (last) tile of a
-  // chunk first, so the long-running workgroups start before the decode items
+  // prefill (q-split) tiles go first in the item list, heaviest (most keys) first across
+  // all chunks, then the decode items, longest partition first: the attention kernel's
+  // work queue (attention.hip MODE 3) hands them out in this order, so the long items
+  // start first and the short ones fill in behind them
+  struct ItemCost {
+    int32_t keys, a, b, c, d;
+  };
+  std::vector<ItemCost> pre, dec;
   for (size_t si = 0; si < last_plan_.size(); ++si) {
     const int32_t n = last_plan_[si].n;
     if (n <= tpw) continue;
+    const int32_t c0 = last_plan_[si].s->num_computed;
     for (int32_t qb = ((n - 1) / qtile) * qtile; qb >= 0; qb -= qtile) {
-      int32_t* it = items + 4 * nit++;
-      it[0] = (int32_t)si; it[1] = qb; it[2] = std::min(qtile, n - qb) | (1 << 20); it[3] = 0;
+      const int32_t nq = std::min(qtile, n - qb);
+      pre.push_back({c0 + qb + nq, (int32_t)si, qb, nq | (1 << 20), 0});
     }
+  }
+  std::stable_sort(pre.begin(), pre.end(), [](const ItemCost& x, const ItemCost& y) { return x.keys > y.keys; });
+  for (const ItemCost& c : pre) {
+    int32_t* it = items + 4 * nit++;
+    it[0] = c.a; it[1] = c.b; it[2] = c.c; it[3] = c.d;
   }
   const int64_t plan_id = next_plan_id_;
   for (size_t pi = 0; pi < last_plan_.size(); ++pi) {
@@ -403,15 +415,12 @@ int32_t Scheduler::schedule(int32_t* buf) {
     if (n <= tpw) {
       const int32_t nparts = cfg_.split_decode ? std::max(1, (ctx + psz - 1) / psz) : 1;
       if (nparts > 1) {
-        for (int32_t q = 0; q < nparts; ++q) {
-          int32_t* it = items + 4 * nit++;
-          it[0] = ns; it[1] = 0; it[2] = n | (q << 8) | (nparts << 20); it[3] = pslot + q;
-        }
+        for (int32_t q = 0; q < nparts; ++q)
+          dec.push_back({std::min(psz, ctx - q * psz), ns, 0, n | (q << 8) | (nparts << 20), pslot + q});
         ++nparted;  // merged in-kernel by the last partition (attention.hip)
         pslot += nparts;
       } else {
-        int32_t* it = items + 4 * nit++;
-        it[0] = ns; it[1] = 0; it[2] = n | (1 << 20); it[3] = 0;
+        dec.push_back({ctx, ns, 0, n | (1 << 20), 0});
       }
     }
     s->num_computed = ctx;
@@ -423,6 +432,11 @@ int32_t Scheduler::schedule(int32_t* buf) {
     }
     T += n;
     ++ns;
+  }
+  std::stable_sort(dec.begin(), dec.end(), [](const ItemCost& x, const ItemCost& y) { return x.keys > y.keys; });
+  for (const ItemCost& c : dec) {
+    int32_t* it = items + 4 * nit++;
+    it[0] = c.a; it[1] = c.b; it[2] = c.c; it[3] = c.d;
   }
   // padding: tokens write no KV, sample rows are greedy on row 0
   for (int32_t t = T; t < L.max_tokens; ++t) {

@@ -92,6 +92,10 @@ class EngineConfig:
     # ... used only for steps with at least this many prefill tokens (1,024: 1,024-2,048-token steps
     # 1-2 % faster than with 2,048, which most mixed steps never reached; profiles/r2_att_wide_min_ab.jsonl)
     att_wide_min_tokens: int = 1024
+    # persistent work-queue attention launch (2 workgroups per CU, KV head = XCD, items pulled
+    # heaviest first: decode items run beside a mixed step's prefill items); False = the
+    # grid-strided launch
+    att_queue: bool = True
     prefetch_weights: Optional[bool] = None  # decode-step MALL prefetch on a side stream (None: model default)
     reply_tokens: Optional[int] = None  # fixed length of every reply schema's free-text slot (grammar.py)
     # interpreter thread-switch interval while the engine thread runs (sys.setswitchinterval);
@@ -242,6 +246,8 @@ class LLMEngine:
         self._dev_meta = torch.zeros(L["total"], dtype=torch.int32, device=self.device) \
             if (self.on_gpu or self._async) else self._host_meta
         self._att_counters = torch.zeros(L["max_seqs"] * kv_local, dtype=torch.int32, device=self.device)
+        self._att_queue = torch.zeros(2 * kv_local, dtype=torch.int32, device=self.device) \
+            if (cfg.att_queue and self.on_gpu) else None
         self._init_views()
         V = mc.vocab_size
         self._mask_words = (V + 31) // 32
@@ -330,6 +336,7 @@ class LLMEngine:
             items=sl("items", 4 * L["max_items"]).view(L["max_items"], 4),
             n_items=sl("n_items", 1),
             att_counters=self._att_counters,
+            att_queue=self._att_queue,
             part_size=sl("part_size", 1),
             logit_rows=sl("logit_rows", ms))
         self._temp = sl("temperature", ms).view(torch.float32)
@@ -357,7 +364,7 @@ class LLMEngine:
         n_it = self._items_for_bucket(bucket, s_b)
         return StepMeta(m.input_ids, m.positions, m.slots, m.q_start, m.q_len, m.ctx_len,
                         m.block_table, m.items[:n_it], m.n_items, m.att_counters, m.logit_rows, num_seqs=ns,
-                        part_size=m.part_size)
+                        part_size=m.part_size, att_queue=m.att_queue)
 
     def _forward_and_sample(self, bucket: int, s_b: int, ns: int, trunc: bool = False, embed: bool = False):
         meta = self._meta_for(bucket, s_b, ns)

@@ -105,6 +105,9 @@ class StepMeta:
     logit_rows: torch.Tensor
     num_seqs: int = 0  # host-side count, used only by the CPU reference path
     part_size: Optional[torch.Tensor] = None  # device int[1]: decode partition size of the step
+    # persistent zeroed int[2 * KV]: the attention work queue (csrc/ops/attention.hip MODE 3);
+    # None = the grid-strided launch
+    att_queue: Optional[torch.Tensor] = None
 
 
 class KVCache:
@@ -373,7 +376,8 @@ class LlamaModel:
             attn = torch.empty(T, H, hd, dtype=self.dtype, device=self.device)
             ops.paged_attention(attn, part_o, part_ml, q, kv.k[li], kv.v[li], meta.items, meta.n_items,
                                 meta.att_counters, meta.q_start, meta.q_len, meta.ctx_len,
-                                meta.block_table, self.scale, num_seqs=meta.num_seqs, part_size=meta.part_size)
+                                meta.block_table, self.scale, num_seqs=meta.num_seqs, part_size=meta.part_size,
+                                queue=meta.att_queue)
             o = ops.linear(attn.view(T, H * hd), L["wo"], "o")
             if self.tp.size > 1:
                 self.tp.all_reduce(o)
@@ -416,6 +420,7 @@ class LlamaModel:
             ops.paged_attention(attn, part_o, part_ml, q, kv.k[li], kv.v[li], meta.items, meta.n_items,
                                 meta.att_counters, meta.q_start, meta.q_len, meta.ctx_len,
                                 meta.block_table, self.scale, num_seqs=meta.num_seqs, part_size=meta.part_size,
+                                queue=meta.att_queue,
                                 prefetch=L["wo_p"] if pf else None)
             a2 = attn.view(T, H * hd)
             if tp:
@@ -472,6 +477,7 @@ class LlamaModel:
             ops.paged_attention(attn, part_o, part_ml, q, kv.k[li], kv.v[li], meta.items, meta.n_items,
                                 meta.att_counters, meta.q_start, meta.q_len, meta.ctx_len,
                                 meta.block_table, self.scale, num_seqs=meta.num_seqs, part_size=meta.part_size,
+                                queue=meta.att_queue,
                                 prefetch=L["wo_p"] if self.PREFETCH_WEIGHTS and self.device.type == "cuda" else None)
             a2 = attn.view(T, H * hd)
             if tp:
@@ -562,7 +568,8 @@ class LlamaModel:
             attn = torch.empty(T, H, hd, dtype=self.dtype, device=self.device)
             ops.paged_attention(attn, part_o, part_ml, q, kv.k[li], kv.v[li], meta.items, meta.n_items,
                                 meta.att_counters, meta.q_start, meta.q_len, meta.ctx_len,
-                                meta.block_table, self.scale, num_seqs=meta.num_seqs, part_size=meta.part_size)
+                                meta.block_table, self.scale, num_seqs=meta.num_seqs, part_size=meta.part_size,
+                                queue=meta.att_queue)
             a2 = attn.view(T, H * hd)
             if tp:
                 o = self._gemm("o", T, a2, L["wo_p"], "plain")

@@ -27,12 +27,17 @@ def build_attention_items(q_lens: Sequence[int], ctx_lens: Sequence[int], group:
     if sum(pre) < wide_min_tokens or (wide_min_tokens > 0 and len(pre) < 2):
         qcols = 32
     qtile = max(1, max(32, qcols) // group)
-    items: List[Tuple[int, int, int, int]] = []
-    # prefill tiles first, heaviest tile of each chunk first (as the scheduler)
+    # prefill tiles first, most keys first across all chunks; then the decode items,
+    # longest partition first (as the scheduler: the attention work queue takes them in order)
+    pre: List[Tuple[int, Tuple[int, int, int, int]]] = []
     for s, (ql, ctx) in enumerate(zip(q_lens, ctx_lens)):
         if ql > tpw:
             for qb in range(((ql - 1) // qtile) * qtile, -1, -qtile):
-                items.append((s, qb, min(qtile, ql - qb) | (1 << 20), 0))
+                nq = min(qtile, ql - qb)
+                pre.append((ctx - ql + qb + nq, (s, qb, nq | (1 << 20), 0)))
+    pre.sort(key=lambda kv: -kv[0])  # stable
+    items: List[Tuple[int, int, int, int]] = [it for _, it in pre]
+    dec: List[Tuple[int, Tuple[int, int, int, int]]] = []
     slot = 0
     for s, (ql, ctx) in enumerate(zip(q_lens, ctx_lens)):
         if ql <= 0:
@@ -42,8 +47,10 @@ def build_attention_items(q_lens: Sequence[int], ctx_lens: Sequence[int], group:
             nparts = max(1, nparts)
             if nparts > 1:
                 for p in range(nparts):
-                    items.append((s, 0, ql | (p << 8) | (nparts << 20), slot + p))
+                    dec.append((min(part, ctx - p * part), (s, 0, ql | (p << 8) | (nparts << 20), slot + p)))
                 slot += nparts
             else:
-                items.append((s, 0, ql | (1 << 20), 0))
+                dec.append((ctx, (s, 0, ql | (1 << 20), 0)))
+    dec.sort(key=lambda kv: -kv[0])
+    items += [it for _, it in dec]
     return items, slot

@@ -70,7 +70,7 @@ def test_rope_cache(gpu):
 
 
 def _run_attention(gpu, H, KV, q_lens, ctx_lens, seed=0, split=True, part=512, qcols=128, pad=1,
-                   prefetch=None):
+                   prefetch=None, queue=False, launches=1):
     torch.manual_seed(seed)
     G = H // KV
     blk = 16
@@ -99,11 +99,15 @@ def _run_attention(gpu, H, KV, q_lens, ctx_lens, seed=0, split=True, part=512, q
     out = torch.zeros(T, H, 128, dtype=torch.bfloat16, device=gpu)
     scale = 1.0 / math.sqrt(128)
     dev_i = lambda a: torch.tensor(a, dtype=torch.int32, device=gpu)  # noqa: E731
-    ops.paged_attention(out, part_o, part_ml, q, kc, vc, it, n_it, cnt, dev_i(q_start),
-                        dev_i(q_lens), dev_i(ctx_lens), bt.to(gpu), scale, part_size=dev_i([part]),
-                        prefetch=prefetch)
+    qt = torch.zeros(2 * KV, dtype=torch.int32, device=gpu) if queue else None
+    for _ in range(launches):  # the work queue must reset itself for the next launch
+        ops.paged_attention(out, part_o, part_ml, q, kc, vc, it, n_it, cnt, dev_i(q_start),
+                            dev_i(q_lens), dev_i(ctx_lens), bt.to(gpu), scale, part_size=dev_i([part]),
+                            prefetch=prefetch, queue=qt)
     torch.cuda.synchronize()
     assert int(cnt.abs().sum()) == 0, "partition tickets must be left zeroed"
+    if qt is not None:
+        assert int(qt.abs().sum()) == 0, "the work queue must be left zeroed"
     r = ref.paged_attention(q.cpu(), kc.cpu(), vc.cpu(), q_start, q_lens, ctx_lens, bt, scale)
     return out.cpu().float(), r.float()
 
@@ -156,6 +160,31 @@ def test_attention_small_partitions(gpu, part):
     ctx = [1, 100, 127, 128, 129, 700, 2049, 64]
     o, r = _run_attention(gpu, 32, 8, [1, 1, 2, 1, 4, 1, 1, 3], ctx, seed=13, part=part)
     torch.testing.assert_close(o, r, atol=2e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("case", ["decode", "mixed32", "mixed128", "tiles", "kv1", "kv16", "small_part", "step2048"])
+def test_attention_work_queue_matches_grid_launch(gpu, case):
+    """Persistent work-queue launch (attention.hip MODE 3: 2 workgroups per CU, KV head =
+    blockIdx % KV, items claimed from a per-head counter, last workgroup resets it):
+    bit-identical to the grid-strided launch (same device code per item, the same
+    partition-merge order) and equal to fp32, over three back-to-back launches on one
+    queue tensor, with padded item lists as the engine's graphs have."""
+    cfg = {
+        "decode": dict(H=32, KV=8, q=[1] * 12, c=[1, 15, 16, 17, 33, 100, 511, 512, 513, 1500, 2049, 64]),
+        "mixed32": dict(H=32, KV=8, q=[37, 1, 100, 3, 16, 5, 250, 129, 33], c=[37, 700, 164, 40, 16, 1029, 260, 1000, 2100],
+                        qcols=32),
+        "mixed128": dict(H=32, KV=8, q=[37, 1, 100, 3, 16, 5, 250, 129, 33], c=[37, 700, 164, 40, 16, 1029, 260, 1000, 2100]),
+        "tiles": dict(H=64, KV=8, q=[300, 129, 33, 1, 2, 77], c=[300, 1129, 65, 900, 18, 589]),
+        "kv1": dict(H=8, KV=1, q=[37, 1, 100, 3, 16], c=[37, 700, 164, 40, 16]),
+        "kv16": dict(H=16, KV=16, q=[1, 1, 40, 3], c=[100, 2049, 40, 700]),
+        "small_part": dict(H=32, KV=8, q=[1, 1, 2, 1, 4, 1, 1, 3], c=[1, 100, 127, 128, 129, 700, 2049, 64], part=256),
+        "step2048": dict(H=32, KV=8, q=[512] * 4 + [1] * 40, c=[768] * 4 + [600] * 40),
+    }[case]
+    kw = dict(seed=17, qcols=cfg.get("qcols", 128), part=cfg.get("part", 512), pad=200)
+    og, r = _run_attention(gpu, cfg["H"], cfg["KV"], cfg["q"], cfg["c"], **kw)
+    oq, _ = _run_attention(gpu, cfg["H"], cfg["KV"], cfg["q"], cfg["c"], queue=True, launches=3, **kw)
+    torch.testing.assert_close(oq, r, atol=2e-2, rtol=2e-2)
+    assert torch.equal(oq, og)
 
 
 def test_attention_nosplit_long(gpu):
