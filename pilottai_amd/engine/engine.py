@@ -95,7 +95,7 @@ class EngineConfig:
     # persistent work-queue attention launch (2 workgroups per CU, KV head = XCD, items pulled
     # heaviest first: decode items run beside a mixed step's prefill items); False = the
     # grid-strided launch
-    att_queue: bool = True
+    att_queue: bool = False
     prefetch_weights: Optional[bool] = None  # decode-step MALL prefetch on a side stream (None: model default)
     reply_tokens: Optional[int] = None  # fixed length of every reply schema's free-text slot (grammar.py)
     # interpreter thread-switch interval while the engine thread runs (sys.setswitchinterval);
