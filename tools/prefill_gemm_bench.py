@@ -117,6 +117,11 @@ for name in a.shapes.split(","):
             "mid_fused": lambda i: kernels.mid_gemm(x, fps[i], epi, out=yf if epi == "silu" else y, resid=resid,
                                                     norm=nrm, ss_in=ss if nrm else None),
         }
+        for bn_ in (128, 256):  # fused epilogue on an explicit (whole tiles, K-slices) decomposition
+            for S_ in (1, 2, 3, 4):
+                variants[f"pf{bn_}_s{S_}_fused"] = (lambda bn_, S_: lambda i: kernels.prefill_gemm(
+                    x, fps[i], epi, out=yf if epi == "silu" else y, resid=resid, norm=nrm,
+                    ss_in=ss if nrm else None, bn=bn_, full=0 if S_ > 1 else -1, splits=S_))(bn_, S_)
         if a.variants:
             variants = {k: v for k, v in variants.items() if k in a.variants.split(",")}
         times = {k: [] for k in variants}
