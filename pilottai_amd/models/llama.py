@@ -145,18 +145,29 @@ class LlamaModel:
     # EngineConfig.prefill_max_t / bench.py --prefill-max-t move the boundary (0 = off:
     # library GEMMs + elementwise kernels above MID_MAX_T).
     PREFILL_MAX_T = 1 << 30
-    # per projection: (largest M, path, config); the first row whose M covers the step is used.
+    # PF_CFG's prefill-kernel rows also for steps of <= MID_MAX_T tokens (False: the mid
+    # kernel takes every such step, the round-2 split)
+    PF_MIDRANGE = True
+    # per projection: (largest M, path, config); the first row whose M covers the step is used,
+    # for every step on the fused packed-weight path (T > WIDE_MAX_T).
     # "pf": prefill kernel — bn = tile width (256 / 128), variant = kernel family (3: the
     # ping-pong kernels of gemm_pingpong.h, 1: the read-ahead 256 x 256 / 3-stage 256 x 128
     # kernels), full / splits = the decomposition (-1 / 0: the kernel's plan); "mid": mid
     # kernel (fm, fn, splits as MID_CFG). Rows from tools/prefill_gemm_bench.py on MI355X
-    # (profiles/r3_pingpong_gemm_bench_n128.jsonl: fastest fused kernel per shape and M).
+    # (profiles/r3_pingpong_gemm_bench_n128.jsonl: fastest fused kernel per shape and M above
+    # 256 rows; profiles/r3_midrange_pf_vs_mid.jsonl: from 192 rows the 256 x 128 prefill tiles
+    # beat the mid kernel's 128-256-row tiles, e.g. qkv 50.1 -> 27.5 us and o 40.9 -> 25.8 at
+    # 256 rows, because the mid tiles' x panel leaves LDS room for one 64-k chunk in flight;
+    # crossovers from profiles/r3_midrange_fused_sweep.jsonl: qkv above 80 rows, the others above 128)
     PF_CFG = {
-        "qkv": [(640, "pf", {"bn": 128, "variant": 1}), (1280, "pf", {"bn": 128, "variant": 3}),
+        "qkv": [(80, "mid", {}), (640, "pf", {"bn": 128, "variant": 1}), (1280, "pf", {"bn": 128, "variant": 3}),
                 (1 << 30, "pf", {"bn": 256, "variant": 3})],
-        "o": [(1280, "pf", {"bn": 128, "variant": 1}), (1 << 30, "pf", {"bn": 128, "variant": 3})],
-        "gate_up": [(1 << 30, "pf", {"bn": 256, "variant": 3})],
-        "down": [(640, "pf", {"bn": 128, "variant": 1}), (1 << 30, "pf", {"bn": 256, "variant": 3})],
+        "o": [(128, "mid", {}), (1280, "pf", {"bn": 128, "variant": 1}),
+              (1 << 30, "pf", {"bn": 128, "variant": 3})],
+        "gate_up": [(128, "mid", {}), (256, "pf", {"bn": 128, "variant": 1}),
+                    (1 << 30, "pf", {"bn": 256, "variant": 3})],
+        "down": [(128, "mid", {}), (640, "pf", {"bn": 128, "variant": 1}),
+                 (1 << 30, "pf", {"bn": 256, "variant": 3})],
     }
     # decode/small steps: let the attention launch's idle workgroups read the O
     # projection's weights into the Infinity Cache (MALL-resident weights run the 34 MB
@@ -518,7 +529,7 @@ class LlamaModel:
 
     def _proj_path(self, kind: str, T: int):
         """("mid", cfg) or ("pf", cfg) for projection `kind` on a T-token step."""
-        if T > self.MID_MAX_T and self.device.type == "cuda":
+        if self.device.type == "cuda" and (T > self.MID_MAX_T or self.PF_MIDRANGE):
             for mmax, path, cfg in self.PF_CFG[kind]:
                 if T <= mmax:
                     return path, (dict(cfg) if path == "pf" else self._mid_cfg(kind, T) | dict(cfg))
