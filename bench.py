@@ -78,8 +78,9 @@ def parse():
                     help="admit requests whose prefix another request is prefilling right away (no deferral)")
     ap.add_argument("--no-prefetch", action="store_true", help="decode steps without the side-stream weight prefetch")
     ap.add_argument("--token-align", type=int, default=256, help="GEMM-friendly step sizes (0 = off)")
-    ap.add_argument("--pf-midrange", type=int, default=None, choices=[0, 1],
-                    help="prefill kernels for 129-256-token projections per LlamaModel.PF_CFG (default: model's)")
+    ap.add_argument("--pf-midrange", default=None,
+                    help="comma-separated projections (qkv,o,gate_up,down) on the prefill kernels at <= 256 tokens "
+                         "per LlamaModel.PF_CFG; 'none' = mid kernel only (default: model's)")
     ap.add_argument("--att-queue", type=int, default=None, choices=[0, 1],
                     help="persistent work-queue attention launch (default: engine's)")
     ap.add_argument("--async-steps", type=int, default=None, choices=[0, 1],
@@ -138,7 +139,8 @@ async def run_rank(a, rank: int, world: int, device):
                                  dedup_inflight_prefix=not a.no_prefix_dedup,
                                  **({"async_steps": bool(a.async_steps)} if a.async_steps is not None else {}),
                                  **({"att_queue": bool(a.att_queue)} if a.att_queue is not None else {}),
-                                 **({"pf_midrange": bool(a.pf_midrange)} if a.pf_midrange is not None else {}),
+                                 **({"pf_midrange": [k for k in a.pf_midrange.split(",") if k and k != "none"]}
+                                    if a.pf_midrange is not None else {}),
                                  **({"att_wide_min_tokens": a.att_wide_min_tokens}
                                     if a.att_wide_min_tokens is not None else {})), device=device)
     register_engine(eng.model_cfg.name, eng)

@@ -88,8 +88,9 @@ class EngineConfig:
     # largest step on the fused packed-weight path with the 256 x 256 prefill kernels (above
     # mid_max_t); 0 = such steps take the library (hipBLASLt) path; None = model default
     prefill_max_t: Optional[int] = None
-    # prefill kernels for the PF_CFG rows of <= 256-token steps too (None: model default, on)
-    pf_midrange: Optional[bool] = None
+    # projections ("qkv", "o", "gate_up", "down") whose PF_CFG prefill-kernel rows also apply to
+    # <= 256-token steps (None: model default)
+    pf_midrange: Optional[List[str]] = None
     att_qcols: int = 128  # prefill attention item width in MFMA columns (128: LDS-staged 4-wave items)
     # ... used only for steps with at least this many prefill tokens (1,024: 1,024-2,048-token steps
     # 1-2 % faster than with 2,048, which most mixed steps never reached; profiles/r2_att_wide_min_ab.jsonl)
@@ -197,7 +198,7 @@ class LLMEngine:
         if cfg.prefill_max_t is not None:
             self.model.PREFILL_MAX_T = int(cfg.prefill_max_t)
         if cfg.pf_midrange is not None:
-            self.model.PF_MIDRANGE = bool(cfg.pf_midrange)
+            self.model.PF_MIDRANGE = frozenset(cfg.pf_midrange)
         if cfg.prefetch_weights is not None:
             self.model.PREFETCH_WEIGHTS = bool(cfg.prefetch_weights)
         self.load_time = time.time() - t0

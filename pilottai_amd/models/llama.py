@@ -145,9 +145,14 @@ class LlamaModel:
     # EngineConfig.prefill_max_t / bench.py --prefill-max-t move the boundary (0 = off:
     # library GEMMs + elementwise kernels above MID_MAX_T).
     PREFILL_MAX_T = 1 << 30
-    # PF_CFG's prefill-kernel rows also for steps of <= MID_MAX_T tokens (False: the mid
-    # kernel takes every such step, the round-2 split)
-    PF_MIDRANGE = True
+    # projections whose PF_CFG prefill-kernel rows also apply to steps of <= MID_MAX_T tokens
+    # (empty: the mid kernel takes every such step). In isolation the 256 x 128 prefill tiles
+    # beat the mid kernel for every projection from 96-160 rows even with cold weights
+    # (profiles/r3_midrange_cold_sweep.jsonl), but in the engine only gate_up keeps the gain
+    # (144-256-token steps 0.1-0.2 ms faster in two alternating runs); qkv's paged-KV-write and
+    # o / down's row-statistics epilogues make those slower there
+    # (profiles/r3_midrange_engine_ab.jsonl)
+    PF_MIDRANGE = frozenset({"gate_up"})
     # per projection: (largest M, path, config); the first row whose M covers the step is used,
     # for every step on the fused packed-weight path (T > WIDE_MAX_T).
     # "pf": prefill kernel — bn = tile width (256 / 128), variant = kernel family (3: the
@@ -529,7 +534,7 @@ class LlamaModel:
 
     def _proj_path(self, kind: str, T: int):
         """("mid", cfg) or ("pf", cfg) for projection `kind` on a T-token step."""
-        if self.device.type == "cuda" and (T > self.MID_MAX_T or self.PF_MIDRANGE):
+        if self.device.type == "cuda" and (T > self.MID_MAX_T or kind in self.PF_MIDRANGE):
             for mmax, path, cfg in self.PF_CFG[kind]:
                 if T <= mmax:
                     return path, (dict(cfg) if path == "pf" else self._mid_cfg(kind, T) | dict(cfg))

@@ -27,6 +27,9 @@ ap.add_argument("--iters", type=int, default=10)
 ap.add_argument("--shapes", default="qkv,o,gate_up,down")
 ap.add_argument("--variants", default="")
 ap.add_argument("--out", default="")
+ap.add_argument("--cold-mb", type=int, default=0,
+                help="rotate enough weight copies that their total exceeds this many MB (e.g. 1024: more than the "
+                     "256 MB Infinity Cache, as in the engine, where every step streams 15 GB of weights)")
 a = ap.parse_args()
 load_tuned_gemms("llama-3-8b", 1)
 SHAPES = {"sq": (4096, 4096), "qkv": (6144, 4096), "o": (4096, 4096), "gate_up": (28672, 4096), "down": (4096, 14336)}
@@ -61,7 +64,7 @@ torch.manual_seed(0)
 for name in a.shapes.split(","):
     N, K = SHAPES[name]
     gb = N * K * 2 / 1e9
-    ncopies = 2
+    ncopies = max(2, -(-a.cold_mb * 1_000_000 // (N * K * 2))) if a.cold_mb else 2
     ws = [(torch.randn(N, K, device="cuda") * 0.02).to(torch.bfloat16) for _ in range(ncopies)]
     wps = [kernels.pack_decode_weight(w) for w in ws]
     epi, nrm = FUSED[name]
