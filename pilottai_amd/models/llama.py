@@ -151,7 +151,9 @@ class LlamaModel:
     # (profiles/r3_midrange_cold_sweep.jsonl), but in the engine only gate_up keeps the gain
     # (144-256-token steps 0.1-0.2 ms faster in two alternating runs); qkv's paged-KV-write and
     # o / down's row-statistics epilogues make those slower there
-    # (profiles/r3_midrange_engine_ab.jsonl)
+    # (profiles/r3_midrange_engine_ab.jsonl; tools/midrange_ab.py, one engine per choice, alternating:
+    # profiles/r3_midrange_inengine_ab.jsonl — 160 / 192 / 256-token steps 6.20 / 6.35 / 6.73 ms
+    # with the mid kernel, 5.96 / 6.11 / 6.59 with gate_up here, 6.72 / 6.89 / 7.22 with all four)
     PF_MIDRANGE = frozenset({"gate_up"})
     # per projection: (largest M, path, config); the first row whose M covers the step is used,
     # for every step on the fused packed-weight path (T > WIDE_MAX_T).
