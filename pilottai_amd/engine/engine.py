@@ -36,7 +36,7 @@ from collections import deque
 import threading
 import time
 from dataclasses import dataclass, field
-from typing import Callable, Dict, List, Optional, Sequence
+from typing import Any, Callable, Dict, List, Optional, Sequence
 
 import numpy as np
 import torch
@@ -91,6 +91,9 @@ class EngineConfig:
     # projections ("qkv", "o", "gate_up", "down") whose PF_CFG prefill-kernel rows also apply to
     # <= 256-token steps (None: model default)
     pf_midrange: Optional[List[str]] = None
+    # LlamaModel class-level tunables to override on this engine's model (name -> value),
+    # e.g. {"DEC_QKV_MAX_T": 64}; for A/B tools (tools/engine_ab.py)
+    model_overrides: Optional[Dict[str, Any]] = None
     att_qcols: int = 128  # prefill attention item width in MFMA columns (128: LDS-staged 4-wave items)
     # ... used only for steps with at least this many prefill tokens (1,024: 1,024-2,048-token steps
     # 1-2 % faster than with 2,048, which most mixed steps never reached; profiles/r2_att_wide_min_ab.jsonl)
@@ -197,6 +200,10 @@ class LLMEngine:
             self.model.MID_MAX_T = int(cfg.mid_max_t)
         if cfg.prefill_max_t is not None:
             self.model.PREFILL_MAX_T = int(cfg.prefill_max_t)
+        for k, v in (cfg.model_overrides or {}).items():
+            if not hasattr(self.model, k):
+                raise ValueError(f"unknown model tunable {k!r}")
+            setattr(self.model, k, frozenset(v) if isinstance(v, (list, tuple, set)) else v)
         if cfg.pf_midrange is not None:
             self.model.PF_MIDRANGE = frozenset(cfg.pf_midrange)
         if cfg.prefetch_weights is not None:

@@ -149,12 +149,16 @@ class LlamaModel:
     # (empty: the mid kernel takes every such step). In isolation the 256 x 128 prefill tiles
     # beat the mid kernel for every projection from 96-160 rows even with cold weights
     # (profiles/r3_midrange_cold_sweep.jsonl), but in the engine only gate_up keeps the gain
-    # (144-256-token steps 0.1-0.2 ms faster in two alternating runs); qkv's paged-KV-write and
-    # o / down's row-statistics epilogues make those slower there
-    # (profiles/r3_midrange_engine_ab.jsonl; tools/midrange_ab.py, one engine per choice, alternating:
+    # (144-256-token steps 0.1-0.2 ms faster in two alternating runs); qkv, o and down lose there
+    # for a reason not isolated yet (their engine-exact epilogues cost the prefill kernels only
+    # ~3 us, profiles/r3_epilogue_cost.jsonl) (profiles/r3_midrange_engine_ab.jsonl; tools/midrange_ab.py, one engine per choice, alternating:
     # profiles/r3_midrange_inengine_ab.jsonl — 160 / 192 / 256-token steps 6.20 / 6.35 / 6.73 ms
     # with the mid kernel, 5.96 / 6.11 / 6.59 with gate_up here, 6.72 / 6.89 / 7.22 with all four)
     PF_MIDRANGE = frozenset({"gate_up"})
+    # steps of at most this many tokens (above WIDE_MAX_T) run the QKV projection on the
+    # packed decode kernel (all rows per workgroup, norm from x, RoPE + KV write; csrc/ops/
+    # gemm_decode.hip handles M <= 64) instead of the mid kernel; 0 = off
+    DEC_QKV_MAX_T = 0
     # per projection: (largest M, path, config); the first row whose M covers the step is used,
     # for every step on the fused packed-weight path (T > WIDE_MAX_T).
     # "pf": prefill kernel — bn = tile width (256 / 128), variant = kernel family (3: the
@@ -549,6 +553,9 @@ class LlamaModel:
 
     def _qkv_rope(self, T: int, x, wp, eps, q, k_cache, v_cache, meta, ss_in):
         H, KVh = self.h_local, self.kv_local
+        if T <= min(self.DEC_QKV_MAX_T, 64) and self.device.type == "cuda":
+            return ops.decode_qkv_rope(x, wp, eps, q, k_cache, v_cache, meta.positions, meta.slots, self.cos_sin,
+                                       H, KVh)
         path, cfg = self._proj_path("qkv", T)
         fn = ops.prefill_qkv_rope if path == "pf" else ops.mid_qkv_rope
         return fn(x, wp, eps, q, k_cache, v_cache, meta.positions, meta.slots, self.cos_sin, H, KVh,

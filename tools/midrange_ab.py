@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""In-engine A/B of the kernel choice for 96-256-token steps (LlamaModel.PF_MIDRANGE).
+"""In-engine A/B of per-step kernel choices (LlamaModel tunables, e.g. PF_MIDRANGE).
 
 One Llama-3-8B engine per configuration (random-init weights, 16 GB each, all resident on one
 MI355X); every repetition sends the same fresh T-token prompt (max_tokens = 1: one prefill
@@ -8,6 +8,7 @@ configurations alternate and see the same box state. Reported: median step wall 
 engine's own per-bucket clock, bucket_hist) per configuration and T.
 
     python tools/midrange_ab.py [--T 96,128,160,192,256] [--reps 12] [--configs none;gate_up;all]
+    python tools/midrange_ab.py --T 32,48,64 --overrides '[{}, {"DEC_QKV_MAX_T": 64}]'
 """
 import argparse
 import json
@@ -24,18 +25,28 @@ def main():
     ap.add_argument("--T", default="96,128,160,192,256")
     ap.add_argument("--reps", type=int, default=12)
     ap.add_argument("--configs", default="none;gate_up;qkv,o,gate_up,down")
+    ap.add_argument("--overrides", default="",
+                    help="JSON list of LlamaModel tunable overrides, one engine each (replaces --configs)")
     ap.add_argument("--out", default="")
     a = ap.parse_args()
     from pilottai_amd.engine.engine import EngineConfig, LLMEngine
 
     Ts = [int(t) for t in a.T.split(",")]
-    cfgs = [c for c in a.configs.split(";")]
     engines = {}
-    for c in cfgs:
-        kinds = [k for k in c.split(",") if k and k != "none"]
-        engines[c] = LLMEngine(EngineConfig(model="llama-3-8b", max_num_seqs=64, max_num_batched_tokens=2048,
-                                            kv_cache_gb=8, prefix_caching=False, token_buckets=sorted(set(Ts)),
-                                            pf_midrange=kinds, capture_on_start=True))
+    if a.overrides:
+        ovs = json.loads(a.overrides)
+        cfgs = [json.dumps(o, sort_keys=True) for o in ovs]
+        for c, o in zip(cfgs, ovs):
+            engines[c] = LLMEngine(EngineConfig(model="llama-3-8b", max_num_seqs=64, max_num_batched_tokens=2048,
+                                                kv_cache_gb=8, prefix_caching=False, token_buckets=sorted(set(Ts)),
+                                                model_overrides=o, capture_on_start=True))
+    else:
+        cfgs = [c for c in a.configs.split(";")]
+        for c in cfgs:
+            kinds = [k for k in c.split(",") if k and k != "none"]
+            engines[c] = LLMEngine(EngineConfig(model="llama-3-8b", max_num_seqs=64, max_num_batched_tokens=2048,
+                                                kv_cache_gb=8, prefix_caching=False, token_buckets=sorted(set(Ts)),
+                                                pf_midrange=kinds, capture_on_start=True))
     rng = random.Random(0)
     res = {c: {T: [] for T in Ts} for c in cfgs}
     for r in range(a.reps + 1):
