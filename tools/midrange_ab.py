@@ -34,8 +34,8 @@ def main():
     Ts = [int(t) for t in a.T.split(",")]
     engines = {}
     if a.overrides:
-        ovs = json.loads(a.overrides)
-        cfgs = [json.dumps(o, sort_keys=True) for o in ovs]
+        ovs = json.load(open(a.overrides)) if a.overrides.endswith(".json") else json.loads(a.overrides)
+        cfgs = [f"cfg{i}" for i in range(len(ovs))]
         for c, o in zip(cfgs, ovs):
             engines[c] = LLMEngine(EngineConfig(model="llama-3-8b", max_num_seqs=64, max_num_batched_tokens=2048,
                                                 kv_cache_gb=8, prefix_caching=False, token_buckets=sorted(set(Ts)),
