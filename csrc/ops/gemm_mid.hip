@@ -461,7 +461,9 @@ extern "C" int pa_mid_gemm(void* y, const void* x, const void* wp, const void* r
          slots, cos_sin, H, KV, pa::g_handoff_acquire};
   const int grid = MT * NT * S;
   int rc;
-  if (fm == 1 && fn == 2) rc = launch_f<1, 2>(a, epi, norm != 0, grid, st);
+  if (fm == 1 && fn == 1) rc = launch_f<1, 1>(a, epi, norm != 0, grid, st);
+  else if (fm == 2 && fn == 1) rc = launch_f<2, 1>(a, epi, norm != 0, grid, st);
+  else if (fm == 1 && fn == 2) rc = launch_f<1, 2>(a, epi, norm != 0, grid, st);
   else if (fm == 1 && fn == 4) rc = launch_f<1, 4>(a, epi, norm != 0, grid, st);
   else if (fm == 2 && fn == 2) rc = launch_f<2, 2>(a, epi, norm != 0, grid, st);
   else if (fm == 2 && fn == 4) rc = launch_f<2, 4>(a, epi, norm != 0, grid, st);
