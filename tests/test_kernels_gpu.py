@@ -448,7 +448,10 @@ def test_wide_gemm(gpu, M, N, K, epi, norm, ntw, waves, splits):
     (130, 1024, 1024, "silu", False, 8, 4, 2), (33, 512, 2048, "resid", False, 4, 2, 6),
     # 32-row tiles (17-32-token steps)
     (24, 4096, 4096, "resid", False, 1, 2, 4), (32, 28672, 4096, "silu", True, 1, 4, 1),
-    (20, 6144, 4096, "rope_perm", True, 1, 2, 2), (48, 4096, 14336, "resid", False, 1, 2, 3)])
+    (20, 6144, 4096, "rope_perm", True, 1, 2, 2), (48, 4096, 14336, "resid", False, 1, 2, 3),
+    # 32-column tiles (fn = 1)
+    (64, 4096, 4096, "resid", False, 1, 1, 1), (128, 4096, 14336, "resid", False, 2, 1, 1),
+    (96, 4096, 4096, "plain", True, 2, 1, 2)])
 def test_mid_gemm(gpu, M, N, K, epi, norm, fm, fn, splits):
     _check_mid(gpu, M, N, K, epi, norm, fm, fn, splits)
 
