@@ -46,11 +46,15 @@ constexpr float NEG_BIG = -1.0e30f;
 // ---------------------------------------------------------------------------
 // kv-split path (decode tokens / short runs, nq <= 16/G): 16x16x32 MFMA, the 4
 // waves interleave 32-key tiles and merge through LDS.
-constexpr int ATT_LDS_DECODE_BYTES = (4 * 16 * (ATT_HD + 4) + 2 * 4 * 16) * 4;
+// NW waves per workgroup (4, or 8 for small decode batches: each wave's chain of 32-key
+// tiles halves, which is what a latency-bound 8-row decode step waits on)
+template <int NW>
+constexpr int att_lds_decode_bytes() { return (NW * 16 * (ATT_HD + 4) + 2 * NW * 16) * 4; }
+constexpr int ATT_LDS_DECODE_BYTES = att_lds_decode_bytes<4>();
 typedef __attribute__((address_space(1))) unsigned long long gu64;
 typedef __attribute__((address_space(1))) int gi32;
 
-template <int G>
+template <int G, int NW = 4>
 __device__ __forceinline__ void decode_item(
     const int4 it, char* smem, bf16* __restrict__ out, float* __restrict__ part_o,
     float* __restrict__ part_ml, int* __restrict__ counters, const bf16* __restrict__ q, const bf16* __restrict__ k_cache,
@@ -124,9 +128,9 @@ __device__ __forceinline__ void decode_item(
   };
   bf16x8 kf[2][4], vf[8];
   if (t_first + wid < t_last) load_tile(t_first + wid, kf, vf);
-  for (int t = t_first + wid; t < t_last; t += 4) {
+  for (int t = t_first + wid; t < t_last; t += NW) {
     bf16x8 kn[2][4], vn[8];
-    if (t + 4 < t_last) load_tile(t + 4, kn, vn);
+    if (t + NW < t_last) load_tile(t + NW, kn, vn);
 
     f32x4 sc[2];
 #pragma unroll
@@ -180,10 +184,10 @@ __device__ __forceinline__ void decode_item(
   l_run += __shfl_xor(l_run, 16, 64);
   l_run += __shfl_xor(l_run, 32, 64);
 
-  // merge the four waves through LDS
+  // merge the NW waves through LDS
   float(*lds_o)[16][ATT_HD + 4] = reinterpret_cast<float(*)[16][ATT_HD + 4]>(smem);
-  float(*lds_m)[16] = reinterpret_cast<float(*)[16]>(smem + 4 * 16 * (ATT_HD + 4) * sizeof(float));
-  float(*lds_l)[16] = lds_m + 4;
+  float(*lds_m)[16] = reinterpret_cast<float(*)[16]>(smem + NW * 16 * (ATT_HD + 4) * sizeof(float));
+  float(*lds_l)[16] = lds_m + NW;
 #pragma unroll
   for (int n = 0; n < 8; ++n)
 #pragma unroll
@@ -193,14 +197,17 @@ __device__ __forceinline__ void decode_item(
     lds_l[wid][col] = l_run;
   }
   __syncthreads();
-  const int ccol = threadIdx.x >> 4;
+  // the first 256 threads merge (16 columns x 16 threads x 8 dims); with NW = 8 the others
+  // only join the workgroup-wide steps (the partition hand-off)
+  const bool mthr = NW == 4 || threadIdx.x < 256;
+  const int ccol = (threadIdx.x >> 4) & 15;
   const int d0 = (threadIdx.x & 15) * 8;
   float mt = NEG_BIG;
 #pragma unroll
-  for (int w = 0; w < 4; ++w) mt = fmaxf(mt, lds_m[w][ccol]);
-  float wgt[4], L = 0.f;
+  for (int w = 0; w < NW; ++w) mt = fmaxf(mt, lds_m[w][ccol]);
+  float wgt[NW], L = 0.f;
 #pragma unroll
-  for (int w = 0; w < 4; ++w) {
+  for (int w = 0; w < NW; ++w) {
     wgt[w] = exp2f(lds_m[w][ccol] - mt);
     L += wgt[w] * lds_l[w][ccol];
   }
@@ -209,7 +216,7 @@ __device__ __forceinline__ void decode_item(
   for (int j = 0; j < 8; ++j) {
     float a = 0.f;
 #pragma unroll
-    for (int w = 0; w < 4; ++w) a += wgt[w] * lds_o[w][ccol][d0 + j];
+    for (int w = 0; w < NW; ++w) a += wgt[w] * lds_o[w][ccol][d0 + j];
     acc[j] = a;
   }
   const int ctq = ccol / G, chg = ccol % G;
@@ -222,19 +229,21 @@ __device__ __forceinline__ void decode_item(
     const __amdgpu_buffer_rsrc_t ps = __builtin_amdgcn_make_buffer_rsrc(
         part_o + ((size_t)pidx * KV + kvh) * 16 * ATT_HD, 0, 16 * ATT_HD * 4, 0x00020000);
     const int soff = (ccol * ATT_HD + d0) * 4;
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, f32x4{acc[0], acc[1], acc[2], acc[3]}),
-                                           ps, soff, 0, 16);
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, f32x4{acc[4], acc[5], acc[6], acc[7]}),
-                                           ps, soff + 16, 0, 16);
-    if ((threadIdx.x & 15) == 0) {
+    if (mthr) {
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, f32x4{acc[0], acc[1], acc[2], acc[3]}),
+                                             ps, soff, 0, 16);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, f32x4{acc[4], acc[5], acc[6], acc[7]}),
+                                             ps, soff + 16, 0, 16);
+    }
+    if (mthr && (threadIdx.x & 15) == 0) {
       const unsigned long long mlv =
           ((unsigned long long)__float_as_uint(L) << 32) | (unsigned long long)__float_as_uint(mt);
       __hip_atomic_store((gu64*)(part_ml + (((size_t)pidx * KV + kvh) * 16 + ccol) * 2), mlv,
                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    int* lflag = reinterpret_cast<int*>(smem + ATT_LDS_DECODE_BYTES);
+    int* lflag = reinterpret_cast<int*>(smem + att_lds_decode_bytes<NW>());
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (!handoff_last(counters + (size_t)s * KV + kvh, nparts, lflag, acq) || ctq >= nq) return;
+    if (!handoff_last(counters + (size_t)s * KV + kvh, nparts, lflag, acq) || ctq >= nq || !mthr) return;
     const int p0 = pidx - part;
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
         part_o + (size_t)p0 * KV * 16 * ATT_HD, 0, nparts * KV * 16 * ATT_HD * 4, 0x00020000);
@@ -266,7 +275,7 @@ __device__ __forceinline__ void decode_item(
     *reinterpret_cast<bf16x8*>(out + ((size_t)(q0 + qb + ctq) * H + kvh * G + chg) * ATT_HD + d0) = g8;
     return;
   }
-  if (ctq >= nq) return;
+  if (ctq >= nq || !mthr) return;
   const float inv = 1.f / L;
   bf16x8 w8;
 #pragma unroll
@@ -346,7 +355,7 @@ __device__ __forceinline__ f32x16 qk_tile(const bf16x8 (&kf)[8], const bf16x8 (&
   return s;
 }
 
-template <int G>
+template <int G, int NW = 4>
 __device__ __forceinline__ void prefill_item(
     const int4 it, char* smem, bf16* __restrict__ out, const bf16* __restrict__ q,
     const bf16* __restrict__ k_cache, const bf16* __restrict__ v_cache,
@@ -389,7 +398,7 @@ __device__ __forceinline__ void prefill_item(
     for (int j = 0; j < 16; ++j) o[m][j] = 0.f;
   float m_run = NEG_BIG, l_run = 0.f;
 
-  for (int t = wid; t < ntiles; t += 4) {
+  for (int t = wid; t < ntiles; t += NW) {
     const int pb0 = bt[min(2 * t, nblk - 1)], pb1 = bt[min(2 * t + 1, nblk - 1)];
     // dims 16i + 8h = chunk 2i + h; key krow & 15 of page krow >> 4
     const bf16* kbase = k_cache + (size_t)(krow >= 16 ? pb1 : pb0) * kv_stride_blk +
@@ -410,10 +419,10 @@ __device__ __forceinline__ void prefill_item(
   }
   l_run += __shfl_xor(l_run, 32, 64);
 
-  // merge the four waves: O^T images [wave][col][dim] (fp32) + per-column (m, l)
+  // merge the NW waves: O^T images [wave][col][dim] (fp32) + per-column (m, l)
   float* lo = reinterpret_cast<float*>(smem);
-  float* lm = lo + 4 * 32 * PF_LD;
-  float* ll = lm + 4 * 32;
+  float* lm = lo + NW * 32 * PF_LD;
+  float* ll = lm + NW * 32;
 #pragma unroll
   for (int m = 0; m < 4; ++m)
 #pragma unroll
@@ -428,13 +437,13 @@ __device__ __forceinline__ void prefill_item(
   __syncthreads();
   const int ccol = threadIdx.x >> 3, d0 = (threadIdx.x & 7) * 16;
   const int ctq = ccol / G, chg = ccol % G;
-  if (ctq >= nq) return;
+  if (ctq >= nq || (NW == 8 && threadIdx.x >= 256)) return;
   float mt = NEG_BIG;
 #pragma unroll
-  for (int w = 0; w < 4; ++w) mt = fmaxf(mt, lm[w * 32 + ccol]);
-  float wgt[4], L = 0.f;
+  for (int w = 0; w < NW; ++w) mt = fmaxf(mt, lm[w * 32 + ccol]);
+  float wgt[NW], L = 0.f;
 #pragma unroll
-  for (int w = 0; w < 4; ++w) {
+  for (int w = 0; w < NW; ++w) {
     wgt[w] = exp2f(lm[w * 32 + ccol] - mt);
     L += wgt[w] * ll[w * 32 + ccol];
   }
@@ -444,7 +453,7 @@ __device__ __forceinline__ void prefill_item(
   for (int c8 = 0; c8 < 2; ++c8) {
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int w = 0; w < 4; ++w) {
+    for (int w = 0; w < NW; ++w) {
       const f32x4* src = reinterpret_cast<const f32x4*>(lo + (w * 32 + ccol) * PF_LD + d0 + 8 * c8);
       const f32x4 a = src[0], b = src[1];
 #pragma unroll
@@ -600,7 +609,34 @@ __device__ __forceinline__ void prefill_item_wg(
   }
 }
 
+// A q-split item of either width. 8-wave workgroups run no LDS-staged wide items (their 4-wave
+// image layout): a wide item (128/G tokens) runs there as its 32-column sub-items.
+template <int G, int NW>
+__device__ __forceinline__ void prefill_any(
+    const int4 it, char* smem, bf16* __restrict__ out, const bf16* __restrict__ q,
+    const bf16* __restrict__ k_cache, const bf16* __restrict__ v_cache,
+    const int* __restrict__ q_start, const int* __restrict__ q_len, const int* __restrict__ ctx_len,
+    const int* __restrict__ block_table, int max_blocks, int H, int KV, int kvh, float scale_log2) {
+  const int nq = it.z & 0xff;
+  if (nq <= 32 / G) {
+    prefill_item<G, NW>(it, smem, out, q, k_cache, v_cache, q_start, q_len, ctx_len, block_table, max_blocks, H,
+                        KV, kvh, scale_log2);
+  } else if constexpr (NW == 4) {
+    prefill_item_wg<G>(it, smem, out, q, k_cache, v_cache, q_start, q_len, ctx_len, block_table, max_blocks, H, KV,
+                       kvh, scale_log2);
+  } else {
+    for (int sb = 0; sb < nq; sb += 32 / G) {
+      const int4 sub = {it.x, it.y + sb, min(32 / G, nq - sb) | (it.z & ~0xff), it.w};
+      prefill_item<G, NW>(sub, smem, out, q, k_cache, v_cache, q_start, q_len, ctx_len, block_table, max_blocks,
+                          H, KV, kvh, scale_log2);
+      __syncthreads();  // LDS reuse by the next sub-item
+    }
+  }
+}
+
 constexpr int ATT_LDS_DECODE = ATT_LDS_DECODE_BYTES + 16;  // + last-arriver flag
+// 8-wave workgroups (decode-sized steps: decode and narrow prefill items only)
+constexpr int ATT_LDS_BYTES8 = std::max(att_lds_decode_bytes<8>() + 16, (8 * 32 * PF_LD + 2 * 8 * 32) * 4);
 constexpr int ATT_LDS_PREFILL = (4 * 32 * PF_LD + 2 * 4 * 32) * 4;
 constexpr int ATT_LDS_BYTES0 = ATT_LDS_PREFILL > ATT_LDS_DECODE ? ATT_LDS_PREFILL : ATT_LDS_DECODE;
 constexpr int ATT_LDS_BYTES = ATT_LDS_BYTES0 > PW_NBUF * PW_TILE ? ATT_LDS_BYTES0 : PW_NBUF * PW_TILE;
@@ -623,8 +659,8 @@ constexpr int ATT_LDS_BYTES = ATT_LDS_BYTES0 > PW_NBUF * PW_TILE ? ATT_LDS_BYTES
 // beside the long prefill items instead of in a second wave after them (MODE 0 holds the
 // decode items until a prefill item retires, and its padded grid's empty workgroups are
 // dispatched between the real ones).
-template <int G, int MODE>
-__global__ __launch_bounds__(256, 2) void paged_attn_kernel(
+template <int G, int MODE, int NW = 4>
+__global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void paged_attn_kernel(
     bf16* __restrict__ out, float* __restrict__ part_o, float* __restrict__ part_ml,
     int* __restrict__ counters, const bf16* __restrict__ q, const bf16* __restrict__ k_cache,
     const bf16* __restrict__ v_cache, const int4* __restrict__ items,
@@ -663,14 +699,11 @@ __global__ __launch_bounds__(256, 2) void paged_attn_kernel(
         claimed = nslot + __hip_atomic_fetch_add((gi32*)(queue + kvh), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       const int nq = it.z & 0xff;
       if (nq <= TPW)
-        decode_item<G>(it, smem, out, part_o, part_ml, counters, q, k_cache, v_cache, q_start, q_len, ctx_len,
-                       block_table, max_blocks, H, KV, kvh, scale_log2, psz_q, acq);
-      else if (nq <= 32 / G)
-        prefill_item<G>(it, smem, out, q, k_cache, v_cache, q_start, q_len, ctx_len, block_table,
-                        max_blocks, H, KV, kvh, scale_log2);
+        decode_item<G, NW>(it, smem, out, part_o, part_ml, counters, q, k_cache, v_cache, q_start, q_len, ctx_len,
+                           block_table, max_blocks, H, KV, kvh, scale_log2, psz_q, acq);
       else
-        prefill_item_wg<G>(it, smem, out, q, k_cache, v_cache, q_start, q_len, ctx_len, block_table,
-                           max_blocks, H, KV, kvh, scale_log2);
+        prefill_any<G, NW>(it, smem, out, q, k_cache, v_cache, q_start, q_len, ctx_len, block_table, max_blocks, H,
+                           KV, kvh, scale_log2);
       if (threadIdx.x == 0) s_next = claimed;
       __syncthreads();  // LDS reuse by the next item; s_next visible to every wave
       item = s_next;
@@ -718,14 +751,11 @@ __global__ __launch_bounds__(256, 2) void paged_attn_kernel(
     if (item + (int)gridDim.x < n) it_next = items[item + gridDim.x];
     const int nq = it.z & 0xff;
     if (MODE != 2 && nq <= TPW)
-      decode_item<G>(it, smem, out, part_o, part_ml, counters, q, k_cache, v_cache, q_start, q_len, ctx_len,
-                     block_table, max_blocks, H, KV, kvh, scale_log2, psz, acq);
-    else if (MODE != 1 && nq <= 32 / G)
-      prefill_item<G>(it, smem, out, q, k_cache, v_cache, q_start, q_len, ctx_len, block_table,
-                      max_blocks, H, KV, kvh, scale_log2);
+      decode_item<G, NW>(it, smem, out, part_o, part_ml, counters, q, k_cache, v_cache, q_start, q_len, ctx_len,
+                         block_table, max_blocks, H, KV, kvh, scale_log2, psz, acq);
     else if (MODE != 1)
-      prefill_item_wg<G>(it, smem, out, q, k_cache, v_cache, q_start, q_len, ctx_len, block_table,
-                         max_blocks, H, KV, kvh, scale_log2);
+      prefill_any<G, NW>(it, smem, out, q, k_cache, v_cache, q_start, q_len, ctx_len, block_table, max_blocks, H,
+                         KV, kvh, scale_log2);
     __syncthreads();  // LDS reuse by the next item
   }
 }
@@ -742,8 +772,9 @@ extern "C" int pa_paged_attention(void* out, float* part_o, float* part_ml, cons
                                   const int* q_len, const int* ctx_len, const int* block_table,
                                   int max_blocks, int H, int KV, float scale_log2,
                                   const void* pf, long long pf_bytes, void* pf_sink,
-                                  int* queue, hipStream_t st) {
+                                  int* queue, int waves, hipStream_t st) {
   if (H % KV != 0) return -1;
+  if (waves != 4 && waves != 8) return -1;
   if (pf_bytes > 0 && (pf == nullptr || pf_sink == nullptr || (reinterpret_cast<uintptr_t>(pf) & 15))) return -1;
   const long long pf_lines = pf_bytes > 0 ? pf_bytes / 64 : 0;
   const int G = H / KV;
@@ -755,6 +786,21 @@ extern "C" int pa_paged_attention(void* out, float* part_o, float* part_ml, cons
   dim3 qgrid(qslots * KV);
 #define PA_ATT1(GG, MD, GRID, PFP, PFL)                                                         \
   do {                                                                                          \
+    if (waves == 8) {                                                                           \
+      static bool attr8_##GG##_##MD = false;                                                    \
+      if (!attr8_##GG##_##MD) {                                                                 \
+        (void)hipFuncSetAttribute((const void*)pa::paged_attn_kernel<GG, MD, 8>,                \
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, pa::ATT_LDS_BYTES8); \
+        attr8_##GG##_##MD = true;                                                               \
+      }                                                                                         \
+      hipLaunchKernelGGL((pa::paged_attn_kernel<GG, MD, 8>), GRID, dim3(512), pa::ATT_LDS_BYTES8, st, \
+                         (pa::bf16*)out, part_o, part_ml, counters, (const pa::bf16*)q,         \
+                         (const pa::bf16*)k_cache, (const pa::bf16*)v_cache, (const int4*)items, \
+                         n_items, part_size, q_start, q_len, ctx_len, block_table, max_blocks, H, \
+                         KV, scale_log2, (const pa::u32x4*)PFP, PFL, (pa::u32x4*)pf_sink,      \
+                         pa::g_handoff_attn, queue);                                           \
+      break;                                                                                    \
+    }                                                                                           \
     static bool attr_##GG##_##MD = false;                                                       \
     if (!attr_##GG##_##MD) {                                                                    \
       (void)hipFuncSetAttribute((const void*)pa::paged_attn_kernel<GG, MD>,                     \

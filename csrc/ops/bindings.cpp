@@ -19,7 +19,7 @@ int pa_paged_attention(void* out, float* part_o, float* part_ml, const void* q, 
                        int split_prefill, const int* part_size, int* counters, const int* q_start,
                        const int* q_len, const int* ctx_len, const int* block_table,
                        int max_blocks, int H, int KV, float scale_log2, const void* pf, long long pf_bytes,
-                       void* pf_sink, int* queue, hipStream_t st);
+                       void* pf_sink, int* queue, int waves, hipStream_t st);
 int pa_sample_workspace_floats(int rows, int V);
 int pa_patch_pending_ids(int* ids, const int* sampled, int T, int n_sampled, hipStream_t st);
 int pa_sample(int* out_tokens, float* out_keys, float* workspace, const void* logits, int rows,
@@ -169,7 +169,7 @@ void paged_attention(at::Tensor out, at::Tensor part_o, at::Tensor part_ml, at::
                      at::Tensor ctx_len, at::Tensor block_table, double scale,
                      c10::optional<at::Tensor> part_size, c10::optional<at::Tensor> prefetch,
                      c10::optional<at::Tensor> prefetch_sink, int64_t split_prefill,
-                     c10::optional<at::Tensor> queue) {
+                     c10::optional<at::Tensor> queue, int64_t waves) {
   for (auto* t : {&out, &part_o, &part_ml, &q, &k_cache, &v_cache, &items, &n_items, &counters,
                   &q_start, &q_len, &ctx_len, &block_table})
     check_gpu(*t, "paged_attention arg");
@@ -219,7 +219,8 @@ void paged_attention(at::Tensor out, at::Tensor part_o, at::Tensor part_ml, at::
                               counters.data_ptr<int>(),
                               q_start.data_ptr<int>(), q_len.data_ptr<int>(),
                               ctx_len.data_ptr<int>(), block_table.data_ptr<int>(),
-                              block_table.size(1), H, KV, scale_log2, pf, pf_bytes, pf_sink, qptr, cur_stream()),
+                              block_table.size(1), H, KV, scale_log2, pf, pf_bytes, pf_sink, qptr, (int)waves,
+                              cur_stream()),
            "paged_attention");
 }
 
@@ -761,7 +762,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("k_cache"), py::arg("v_cache"), py::arg("items"), py::arg("n_items"), py::arg("counters"),
         py::arg("q_start"), py::arg("q_len"), py::arg("ctx_len"), py::arg("block_table"), py::arg("scale"),
         py::arg("part_size") = py::none(), py::arg("prefetch") = py::none(), py::arg("prefetch_sink") = py::none(),
-        py::arg("split_prefill") = 0, py::arg("queue") = py::none());
+        py::arg("split_prefill") = 0, py::arg("queue") = py::none(), py::arg("waves") = 4);
   m.def("sample_workspace_floats", &sample_workspace_floats);
   m.def("patch_pending_ids", &patch_pending_ids);
   m.def("sample", &sample, py::arg("out_tokens"), py::arg("out_keys"), py::arg("workspace"),

@@ -135,19 +135,21 @@ def rope_cache(q_out, k_cache, v_cache, qkv, positions, slot_mapping, cos_sin, H
 def paged_attention(out, part_o, part_ml, q, k_cache, v_cache, items, n_items, counters,
                     q_start, q_len, ctx_len, block_table, scale: float, num_seqs: Optional[int] = None,
                     part_size: Optional[torch.Tensor] = None, prefetch: Optional[torch.Tensor] = None,
-                    queue: Optional[torch.Tensor] = None):
+                    queue: Optional[torch.Tensor] = None, waves: int = 4):
     """Attention over the paged cache. On GPU `items` must be a device int32
     [max, 4] tensor with a device count (graph-capturable) and `counters` a
     zero-initialised int32 tensor of >= seqs * KV entries (partition tickets; the
     kernel leaves it zeroed); on CPU the reference path ignores both. `prefetch`: a
     tensor (e.g. the next projection's packed weights) that the grid's idle workgroups
     read into the Infinity Cache. `queue`: a zero-initialised device int32 [>= 2 * KV]
-    (left zeroed) selects the persistent work-queue launch (csrc/ops/attention.hip MODE 3)."""
+    (left zeroed) selects the persistent work-queue launch (csrc/ops/attention.hip MODE 3).
+    `waves` 8: 512-thread workgroups for the decode and 32-column prefill items (small decode
+    batches; wide items run as their 32-column sub-items)."""
     if _on_gpu(q):
         sink = _prefetch_sink(q.device) if prefetch is not None else None
         require_native().paged_attention(out, part_o, part_ml, q, k_cache, v_cache, items, n_items,
                                          counters, q_start, q_len, ctx_len, block_table,
-                                         float(scale), part_size, prefetch, sink, 0, queue)
+                                         float(scale), part_size, prefetch, sink, 0, queue, int(waves))
         return out
     ns = len(q_len) if num_seqs is None else num_seqs
     r = ref.paged_attention(q, k_cache, v_cache, q_start[:ns], q_len[:ns], ctx_len[:ns],

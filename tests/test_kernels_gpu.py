@@ -70,7 +70,7 @@ def test_rope_cache(gpu):
 
 
 def _run_attention(gpu, H, KV, q_lens, ctx_lens, seed=0, split=True, part=512, qcols=128, pad=1,
-                   prefetch=None, queue=False, launches=1):
+                   prefetch=None, queue=False, launches=1, waves=4):
     torch.manual_seed(seed)
     G = H // KV
     blk = 16
@@ -103,7 +103,7 @@ def _run_attention(gpu, H, KV, q_lens, ctx_lens, seed=0, split=True, part=512, q
     for _ in range(launches):  # the work queue must reset itself for the next launch
         ops.paged_attention(out, part_o, part_ml, q, kc, vc, it, n_it, cnt, dev_i(q_start),
                             dev_i(q_lens), dev_i(ctx_lens), bt.to(gpu), scale, part_size=dev_i([part]),
-                            prefetch=prefetch, queue=qt)
+                            prefetch=prefetch, queue=qt, waves=waves)
     torch.cuda.synchronize()
     assert int(cnt.abs().sum()) == 0, "partition tickets must be left zeroed"
     if qt is not None:
@@ -185,6 +185,28 @@ def test_attention_work_queue_matches_grid_launch(gpu, case):
     oq, _ = _run_attention(gpu, cfg["H"], cfg["KV"], cfg["q"], cfg["c"], queue=True, launches=3, **kw)
     torch.testing.assert_close(oq, r, atol=2e-2, rtol=2e-2)
     assert torch.equal(oq, og)
+
+
+@pytest.mark.parametrize("case", ["decode", "small_part", "mixed32", "mixed128_wide", "kv1", "queue"])
+def test_attention_eight_wave_workgroups(gpu, case):
+    """512-thread workgroups (waves=8, the engine's decode-sized steps): decode items split
+    their 32-key tiles over 8 waves, 32-column prefill items too, and wide (128-column)
+    items run as their 32-column sub-items; equal to fp32 and to the 4-wave launch."""
+    cfg = {
+        "decode": dict(H=32, KV=8, q=[1] * 12, c=[1, 15, 16, 17, 33, 100, 511, 512, 513, 1500, 2049, 64]),
+        "small_part": dict(H=32, KV=8, q=[1, 1, 2, 1, 4, 1, 1, 3], c=[1, 100, 127, 128, 129, 700, 2049, 64], part=256),
+        "mixed32": dict(H=32, KV=8, q=[37, 1, 100, 3, 16, 5, 250, 129, 33], c=[37, 700, 164, 40, 16, 1029, 260, 1000, 2100],
+                        qcols=32),
+        "mixed128_wide": dict(H=32, KV=8, q=[37, 1, 100, 3, 16, 5, 250, 129, 33],
+                              c=[37, 700, 164, 40, 16, 1029, 260, 1000, 2100]),
+        "kv1": dict(H=8, KV=1, q=[1, 1, 2, 12, 1], c=[100, 600, 33, 40, 2000]),
+        "queue": dict(H=32, KV=8, q=[1] * 8 + [5], c=[600] * 8 + [300], queue=True),
+    }[case]
+    kw = dict(seed=23, qcols=cfg.get("qcols", 128), part=cfg.get("part", 256), pad=50, queue=cfg.get("queue", False))
+    o4, r = _run_attention(gpu, cfg["H"], cfg["KV"], cfg["q"], cfg["c"], **kw)
+    o8, _ = _run_attention(gpu, cfg["H"], cfg["KV"], cfg["q"], cfg["c"], waves=8, launches=2, **kw)
+    torch.testing.assert_close(o8, r, atol=2e-2, rtol=2e-2)
+    torch.testing.assert_close(o8, o4, atol=1e-2, rtol=1e-2)
 
 
 def test_attention_nosplit_long(gpu):

@@ -58,14 +58,14 @@ def setup(q_lens, ctx_lens, H=32, KV=8, pad_items=0, dev="cuda", part=512, qcols
     return args, kv_bytes, flops, n_items
 
 
-def timeit(args, iters, queue=None):
+def timeit(args, iters, queue=None, waves=4):
     for _ in range(3):
-        ops.paged_attention(*args, queue=queue)
+        ops.paged_attention(*args, queue=queue, waves=waves)
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     for _ in range(iters):
-        ops.paged_attention(*args, queue=queue)
+        ops.paged_attention(*args, queue=queue, waves=waves)
     e1.record()
     torch.cuda.synchronize()
     return e0.elapsed_time(e1) * 1000 / iters
@@ -80,6 +80,7 @@ def main():
     ap.add_argument("--cases", default="", help="comma-separated subset of the step cases")
     ap.add_argument("--qcols", default="32,128", help="prefill item widths to time")
     ap.add_argument("--queue", default="0", help="0 = grid-strided launch, 1 = work-queue launch (attention.hip MODE 3)")
+    ap.add_argument("--waves", default="4", help="waves per workgroup to time (4, 8), comma-separated")
     a = ap.parse_args()
     torch.manual_seed(0)
     cases = {
@@ -101,11 +102,12 @@ def main():
     if a.small:
         for ns in (8, 16):
             for ctx in (600, 1000):
-                for part in (128, 256, 512):
-                    args, kvb, fl, n = setup([1] * ns, [ctx] * ns, part=part)
-                    us = timeit(args, a.iters)
-                    print(json.dumps({"case": f"decode{ns}_ctx{ctx}", "part": part, "items": n, "us": round(us, 1),
-                                      "kv_TBps": round(kvb / us / 1e6, 2)}), flush=True)
+                for part in (128, 256, 512, 4096):
+                    for w in [int(x) for x in a.waves.split(",")]:
+                        args, kvb, fl, n = setup([1] * ns, [ctx] * ns, part=part, pad_items=141)
+                        us = timeit(args, a.iters, waves=w)
+                        print(json.dumps({"case": f"decode{ns}_ctx{ctx}", "part": part, "waves": w, "items": n,
+                                          "us": round(us, 1), "kv_TBps": round(kvb / us / 1e6, 2)}), flush=True)
         return
     if a.cases:
         cases = {k: v for k, v in cases.items() if k in a.cases.split(",")}
