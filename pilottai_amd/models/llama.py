@@ -159,6 +159,9 @@ class LlamaModel:
     # packed decode kernel (all rows per workgroup, norm from x, RoPE + KV write; csrc/ops/
     # gemm_decode.hip handles M <= 64) instead of the mid kernel; 0 = off
     DEC_QKV_MAX_T = 0
+    # waves per attention workgroup on decode-sized steps (T <= DECODE_FUSED_MAX_T): 8 splits
+    # each item's chain of 32-key tiles over twice the waves (csrc/ops/attention.hip NW = 8)
+    ATT_DECODE_WAVES = 4
     # per projection: (largest M, path, config); the first row whose M covers the step is used,
     # for every step on the fused packed-weight path (T > WIDE_MAX_T).
     # "pf": prefill kernel — bn = tile width (256 / 128), variant = kernel family (3: the
@@ -442,7 +445,7 @@ class LlamaModel:
             ops.paged_attention(attn, part_o, part_ml, q, kv.k[li], kv.v[li], meta.items, meta.n_items,
                                 meta.att_counters, meta.q_start, meta.q_len, meta.ctx_len,
                                 meta.block_table, self.scale, num_seqs=meta.num_seqs, part_size=meta.part_size,
-                                queue=meta.att_queue,
+                                queue=meta.att_queue, waves=self.ATT_DECODE_WAVES,
                                 prefetch=L["wo_p"] if pf else None)
             a2 = attn.view(T, H * hd)
             if tp:
