@@ -27,6 +27,9 @@ def main():
     ap.add_argument("--configs", default="none;gate_up;qkv,o,gate_up,down")
     ap.add_argument("--overrides", default="",
                     help="JSON list of LlamaModel tunable overrides, one engine each (replaces --configs)")
+    ap.add_argument("--decode", default="",
+                    help="decode mode: 'R,CTX,N' = R concurrent prompts of CTX tokens, N generated tokens each; "
+                         "the timed steps are the R-row decode steps (bucket T = the --T value, e.g. 8 or 16)")
     ap.add_argument("--out", default="")
     a = ap.parse_args()
     from pilottai_amd.engine.engine import EngineConfig, LLMEngine
@@ -49,7 +52,20 @@ def main():
                                                 pf_midrange=kinds, capture_on_start=True))
     rng = random.Random(0)
     res = {c: {T: [] for T in Ts} for c in cfgs}
-    for r in range(a.reps + 1):
+    if a.decode:
+        R, CTX, N = (int(v) for v in a.decode.split(","))
+        for r in range(a.reps + 1):
+            prompts = [[rng.randrange(1000, 100000) for _ in range(CTX)] for _ in range(R)]
+            order = cfgs if r % 2 == 0 else cfgs[::-1]
+            for c in order:
+                e = engines[c]
+                h0 = {T: list(e.bucket_hist.get(T, [0, 0.0])) for T in Ts}
+                e.generate(prompts, temperature=0.7, max_tokens=N, ignore_eos=True)
+                for T in Ts:
+                    h1 = e.bucket_hist.get(T, [0, 0.0])
+                    if r > 0 and h1[0] > h0[T][0]:
+                        res[c][T].append(1000 * (h1[1] - h0[T][1]) / (h1[0] - h0[T][0]))
+    for r in range(0 if a.decode else a.reps + 1):
         for T in Ts:
             prompt = [rng.randrange(1000, 100000) for _ in range(T - 1)]
             order = cfgs if r % 2 == 0 else cfgs[::-1]
