@@ -562,3 +562,46 @@ def test_pipelined_steps_match_serial_engine(tok, nkv):
             json.loads(o.text)
     # every KV block is back in the pool (nothing leaked by voided / aborted entries)
     assert a_eng.sched.num_free_blocks == s_eng.sched.num_free_blocks
+
+
+def test_scheduler_lists_attention_items_heaviest_first():
+    """The attention work list (csrc/runtime/scheduler.cpp, mirrored by ops.attn_meta):
+    prefill q-tiles first, most keys first across all chunks; then the decode items, the
+    longest partition first. The work-queue launch hands items out in this order, and the
+    grid launch's low block ids (dispatched first) get the long ones."""
+    L_cfg = {"num_blocks": 512, "block_size": 16, "max_num_seqs": 16, "max_num_batched_tokens": 1024,
+             "max_prefill_tokens": 1024, "max_model_len": 4096, "gqa_group": 4, "att_wide_min_tokens": 0,
+             "att_qcols": 128, "eos_ids": [128009]}
+    s = _runtime.Scheduler(L_cfg)
+    L = s.layout()
+    buf = np.zeros(L["total"], dtype=np.int32)
+    rng = np.random.default_rng(0)
+    # two long decode rows first (ctx 1200 / 700 after their prefill), then two prompts
+    for rid, n in ((1, 1199), (2, 699)):
+        s.add_request(rid, list(rng.integers(1000, 9000, n)), 0.0, 50, rid, True, [], None)
+        while True:
+            s.schedule(buf.ctypes.data)
+            outs = s.commit(np.array([7], np.int32).ctypes.data, 1)
+            st = {x[0]: x for x in s.debug_state()}  # (id, running, embed, slot, num_computed, ...)
+            if st[rid][4] >= n:
+                break
+    s.add_request(3, list(rng.integers(1000, 9000, 100)), 0.0, 5, 3, True, [], None)
+    s.add_request(4, list(rng.integers(1000, 9000, 300)), 0.0, 5, 4, True, [], None)
+    T = s.schedule(buf.ctypes.data)
+    c = buf[L["counts"]:L["counts"] + 8]
+    items = buf[L["items"]:L["items"] + 4 * c[3]].reshape(-1, 4)
+    ql, cl = buf[L["q_len"]:L["q_len"] + c[1]], buf[L["ctx_len"]:L["ctx_len"] + c[1]]
+    nq = items[:, 2] & 0xFF
+    pre = [(int(cl[s_] - ql[s_] + qb + n)) for s_, qb, n in zip(items[:, 0], items[:, 1], nq) if ql[s_] > 4]
+    n_pre = len(pre)
+    assert n_pre > 2 and all(ql[items[i, 0]] > 4 for i in range(n_pre))
+    assert pre == sorted(pre, reverse=True)
+    part = int(buf[L["part_size"]])
+    dec = []
+    for s_, _, z, _ in items[n_pre:]:
+        p, np_ = (z >> 8) & 0xFFF, z >> 20
+        dec.append(min(part, int(cl[s_]) - p * part) if np_ > 1 else int(cl[s_]))
+    assert len(dec) >= 2 and dec == sorted(dec, reverse=True)
+    ref_items, _ = build_attention_items(list(ql), list(cl), 4, part=part, qcols=128, wide_min_tokens=0)
+    assert [tuple(int(v) for v in x) for x in items] == ref_items
+    assert T == int(ql.sum())
