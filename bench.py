@@ -81,6 +81,8 @@ def parse():
     ap.add_argument("--pf-midrange", default=None,
                     help="comma-separated projections (qkv,o,gate_up,down) on the prefill kernels at <= 256 tokens "
                          "per LlamaModel.PF_CFG; 'none' = mid kernel only (default: model's)")
+    ap.add_argument("--att-decode-waves", type=int, default=None, choices=[4, 8],
+                    help="attention workgroup width on decode-sized steps (default: model's)")
     ap.add_argument("--att-queue", type=int, default=None, choices=[0, 1],
                     help="persistent work-queue attention launch (default: engine's)")
     ap.add_argument("--async-steps", type=int, default=None, choices=[0, 1],
@@ -139,6 +141,7 @@ async def run_rank(a, rank: int, world: int, device):
                                  dedup_inflight_prefix=not a.no_prefix_dedup,
                                  **({"async_steps": bool(a.async_steps)} if a.async_steps is not None else {}),
                                  **({"att_queue": bool(a.att_queue)} if a.att_queue is not None else {}),
+                                 **({"att_decode_waves": a.att_decode_waves} if a.att_decode_waves is not None else {}),
                                  **({"pf_midrange": [k for k in a.pf_midrange.split(",") if k and k != "none"]}
                                     if a.pf_midrange is not None else {}),
                                  **({"att_wide_min_tokens": a.att_wide_min_tokens}

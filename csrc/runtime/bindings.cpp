@@ -129,6 +129,8 @@ PYBIND11_MODULE(_runtime, m) {
         if (d.contains("token_align")) c.token_align = d["token_align"].cast<int32_t>();
         if (d.contains("kv_heads")) c.kv_heads = d["kv_heads"].cast<int32_t>();
         if (d.contains("align_slack")) c.align_slack = d["align_slack"].cast<int32_t>();
+        if (d.contains("small_step_tokens")) c.small_step_tokens = d["small_step_tokens"].cast<int32_t>();
+        if (d.contains("small_step_part")) c.small_step_part = d["small_step_part"].cast<int32_t>();
         if (d.contains("eos_ids")) c.eos_ids = d["eos_ids"].cast<std::vector<int32_t>>();
         return std::make_unique<Scheduler>(c);
       }))

@@ -346,6 +346,10 @@ int32_t Scheduler::schedule(int32_t* buf) {
     }
     const int64_t kv = std::max(1, cfg_.kv_heads), target = 512;
     if (parts512 * kv < target && nprefill + parts256 <= L.max_items) psz = 256;
+    int32_t t_step = 0;
+    for (const Planned& p : last_plan_) t_step += p.n;
+    if (cfg_.small_step_part > 0 && t_step <= cfg_.small_step_tokens && parts512 * kv < target)
+      psz = std::max(psz, cfg_.small_step_part);
   }
   buf[L.part_size] = psz;
 

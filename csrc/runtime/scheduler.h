@@ -44,6 +44,11 @@ struct SchedulerConfig {
   bool dedup_inflight_prefix = true;
   int32_t max_prefix_defer = 4;
   bool split_decode = true;            // flash-decoding partitions for long contexts
+  // decode-sized steps (<= small_step_tokens tokens) with few decode partitions use
+  // small_step_part-key partitions (0 = the general rule); the engine sets it when those
+  // steps run 8-wave attention workgroups, which stream a whole context without a merge
+  int32_t small_step_tokens = 0;
+  int32_t small_step_part = 0;
   // GEMM-friendly step sizes: when a step has T > token_align tokens and
   // T % token_align <= align_slack, the tail of the multi-token chunks (prefill /
   // jump-forward) is deferred so that T is a multiple of token_align (library

@@ -102,6 +102,10 @@ class EngineConfig:
     # heaviest first: decode items run beside a mixed step's prefill items); False = the
     # grid-strided launch
     att_queue: bool = False
+    # attention workgroup width on decode-sized steps (<= the model's DECODE_FUSED_MAX_T
+    # tokens): 8 waves stream a whole context per workgroup (the scheduler then skips the
+    # flash-decoding split for such steps when they have few rows); None = model default
+    att_decode_waves: Optional[int] = None
     prefetch_weights: Optional[bool] = None  # decode-step MALL prefetch on a side stream (None: model default)
     reply_tokens: Optional[int] = None  # fixed length of every reply schema's free-text slot (grammar.py)
     # interpreter thread-switch interval while the engine thread runs (sys.setswitchinterval);
@@ -204,6 +208,8 @@ class LLMEngine:
             if not hasattr(self.model, k):
                 raise ValueError(f"unknown model tunable {k!r}")
             setattr(self.model, k, frozenset(v) if isinstance(v, (list, tuple, set)) else v)
+        if cfg.att_decode_waves is not None:
+            self.model.ATT_DECODE_WAVES = int(cfg.att_decode_waves)
         if cfg.pf_midrange is not None:
             self.model.PF_MIDRANGE = frozenset(cfg.pf_midrange)
         if cfg.prefetch_weights is not None:
@@ -244,6 +250,8 @@ class LLMEngine:
             "dedup_inflight_prefix": cfg.dedup_inflight_prefix,
             "token_align": cfg.token_align, "align_slack": cfg.align_slack,
             "kv_heads": self.model.kv_local,
+            "small_step_tokens": self.model.DECODE_FUSED_MAX_T if self.model.ATT_DECODE_WAVES == 8 else 0,
+            "small_step_part": 4096 if self.model.ATT_DECODE_WAVES == 8 else 0,
             "eos_ids": list(self.tok.eos_ids)})
         L = self.L = self.sched.layout()
         pin = self.on_gpu

@@ -40,9 +40,12 @@ def main():
         ovs = json.load(open(a.overrides)) if a.overrides.endswith(".json") else json.loads(a.overrides)
         cfgs = [f"cfg{i}" for i in range(len(ovs))]
         for c, o in zip(cfgs, ovs):
+            # UPPER-case keys: LlamaModel tunables; lower-case: EngineConfig fields
+            eng_kw = {k: v for k, v in o.items() if not k.isupper()}
+            mod = {k: v for k, v in o.items() if k.isupper()}
             engines[c] = LLMEngine(EngineConfig(model="llama-3-8b", max_num_seqs=64, max_num_batched_tokens=2048,
                                                 kv_cache_gb=8, prefix_caching=False, token_buckets=sorted(set(Ts)),
-                                                model_overrides=o, capture_on_start=True))
+                                                model_overrides=mod, capture_on_start=True, **eng_kw))
     else:
         cfgs = [c for c in a.configs.split(";")]
         for c in cfgs:
