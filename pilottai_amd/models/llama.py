@@ -161,7 +161,7 @@ class LlamaModel:
     DEC_QKV_MAX_T = 0
     # waves per attention workgroup on decode-sized steps (T <= DECODE_FUSED_MAX_T): 8 splits
     # each item's chain of 32-key tiles over twice the waves (csrc/ops/attention.hip NW = 8)
-    ATT_DECODE_WAVES = 4
+    ATT_DECODE_WAVES = int(os.environ.get("PILOTTAI_ATT_DECODE_WAVES", "4"))
     # per projection: (largest M, path, config); the first row whose M covers the step is used,
     # for every step on the fused packed-weight path (T > WIDE_MAX_T).
     # "pf": prefill kernel — bn = tile width (256 / 128), variant = kernel family (3: the
