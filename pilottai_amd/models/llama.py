@@ -160,8 +160,11 @@ class LlamaModel:
     # gemm_decode.hip handles M <= 64) instead of the mid kernel; 0 = off
     DEC_QKV_MAX_T = 0
     # waves per attention workgroup on decode-sized steps (T <= DECODE_FUSED_MAX_T): 8 splits
-    # each item's chain of 32-key tiles over twice the waves (csrc/ops/attention.hip NW = 8)
-    ATT_DECODE_WAVES = int(os.environ.get("PILOTTAI_ATT_DECODE_WAVES", "4"))
+    # each item's chain of 32-key tiles over twice the waves (csrc/ops/attention.hip NW = 8), and
+    # the scheduler then skips the flash-decoding split for such steps with few rows; 8-worker
+    # bench 14.17 / 14.24 -> 14.41 / 14.47 tasks/s, 8-token steps 3.28 -> 3.19-3.20 ms
+    # (profiles/r3_attention_8wave.jsonl)
+    ATT_DECODE_WAVES = int(os.environ.get("PILOTTAI_ATT_DECODE_WAVES", "8"))
     # per projection: (largest M, path, config); the first row whose M covers the step is used,
     # for every step on the fused packed-weight path (T > WIDE_MAX_T).
     # "pf": prefill kernel — bn = tile width (256 / 128), variant = kernel family (3: the
