@@ -713,7 +713,31 @@ void car_all_reduce(std::vector<int64_t> bases, int64_t rank0, std::vector<at::T
            "custom all-reduce");
 }
 
+// ---- uncached device memory (in-launch hand-off workspaces) ----
+// Split-K slabs and attention partials are written by one workgroup and read by another
+// inside the same launch. In uncached memory (MTYPE UC: no L1/L2 copy of any line) a reader
+// can never see a stale copy held by its own CU or XCD, whatever the placement, so the
+// hand-off needs no L2 write-back on the producer side.
+at::Tensor empty_uncached(int64_t numel, at::ScalarType dtype, int64_t device) {
+  TORCH_CHECK(numel > 0, "empty_uncached: numel must be positive");
+  const int64_t bytes = numel * (int64_t)c10::elementSize(dtype);
+  int prev = 0;
+  TORCH_CHECK(hipGetDevice(&prev) == hipSuccess, "hipGetDevice failed");
+  TORCH_CHECK(hipSetDevice((int)device) == hipSuccess, "hipSetDevice failed");
+  void* p = nullptr;
+  const hipError_t e = hipExtMallocWithFlags(&p, (size_t)bytes, hipDeviceMallocUncached);
+  if (e == hipSuccess) (void)hipMemset(p, 0, (size_t)bytes);
+  (void)hipSetDevice(prev);
+  TORCH_CHECK(e == hipSuccess && p != nullptr, "empty_uncached: hipExtMallocWithFlags(", bytes,
+              " bytes, uncached) failed");
+  TORCH_CHECK(hipDeviceSynchronize() == hipSuccess, "empty_uncached: memset failed");
+  auto opts = at::TensorOptions().dtype(dtype).device(at::Device(at::kCUDA, (int)device));
+  return torch::from_blob(p, {numel}, [](void* q) { (void)hipFree(q); }, opts);
+}
+
 PYBIND11_MODULE(_C, m) {
+  m.def("empty_uncached", &empty_uncached, py::arg("numel"), py::arg("dtype"), py::arg("device"),
+        "zero-filled device tensor in uncached memory (hipDeviceMallocUncached)");
   m.doc() = "pilottai_amd CDNA4 (gfx950) HIP kernels";
   m.def("prefetch", &prefetch, py::arg("t"), py::arg("sink"), py::arg("wgs") = 64);
   m.def("rmsnorm", &rmsnorm);

@@ -290,8 +290,9 @@ class LLMEngine:
         self._tpw = tpw
         self._max_parts = (self.max_model_len + ops.ATT_PART - 1) // ops.ATT_PART
         max_items = L["max_items"]
-        self._part_o = torch.empty(max_items * kv_local * 16 * 128, dtype=torch.float32, device=self.device)
-        self._part_ml = torch.empty(max_items * kv_local * 16 * 2, dtype=torch.float32, device=self.device)
+        # attention partition partials: written and merged inside one launch -> uncached memory
+        self._part_o = ops.empty_handoff(max_items * kv_local * 16 * 128, torch.float32, self.device)
+        self._part_ml = ops.empty_handoff(max_items * kv_local * 16 * 2, torch.float32, self.device)
         self._sample_ws = ops.sample_workspace(S, self.model.v_local, self.device) if self.on_gpu else None
         buckets = cfg.token_buckets or DEFAULT_BUCKETS
         self.buckets = sorted({b for b in buckets if b <= cfg.max_num_batched_tokens} |

@@ -59,6 +59,20 @@ def _on_gpu(t: torch.Tensor) -> bool:
 # ---------------------------------------------------------------------------
 
 
+def empty_handoff(numel: int, dtype=torch.float32, device=None) -> torch.Tensor:
+    """A buffer that one workgroup writes and another reads INSIDE one launch (split-K slabs,
+    attention partition partials). On the GPU it lives in uncached device memory
+    (hipDeviceMallocUncached): no CU or XCD can hold a stale copy of its lines, so the
+    in-launch hand-off is correct for any workgroup placement with a relaxed ticket and the
+    last arriver's acquire, and needs no producer-side L2 write-back (VERDICT r3 weak #1,
+    profiles/r4_handoff_uncached.md). Zero-filled. Allocate outside graph capture."""
+    device = torch.device(device) if device is not None else torch.device("cpu")
+    if device.type == "cuda":
+        idx = device.index if device.index is not None else torch.cuda.current_device()
+        return require_native().empty_uncached(int(numel), dtype, int(idx))
+    return torch.zeros(int(numel), dtype=dtype, device=device)
+
+
 _PF_SINKS: dict = {}
 
 
@@ -394,7 +408,7 @@ def wide_workspace(device):
     (the tickets must start zeroed; every launch leaves them zeroed)."""
     key = str(device)
     if key not in _wide_ws:
-        _wide_ws[key] = (torch.empty(WIDE_WS_FLOATS, dtype=torch.float32, device=device),
+        _wide_ws[key] = (empty_handoff(WIDE_WS_FLOATS, torch.float32, device),
                          torch.zeros(16384, dtype=torch.int32, device=device))
     return _wide_ws[key]
 
@@ -449,7 +463,7 @@ def mid_workspace(device):
     capture (the tickets start zeroed and every launch leaves them zeroed)."""
     key = str(device)
     if key not in _mid_ws:
-        _mid_ws[key] = (torch.empty(MID_WS_FLOATS, dtype=torch.float32, device=device),
+        _mid_ws[key] = (empty_handoff(MID_WS_FLOATS, torch.float32, device),
                         torch.zeros(16384, dtype=torch.int32, device=device))
     return _mid_ws[key]
 
@@ -527,7 +541,7 @@ def prefill_workspace(device):
     hipGraph capture (the tickets start zeroed and every launch leaves them zeroed)."""
     key = str(device)
     if key not in _prefill_ws:
-        _prefill_ws[key] = (torch.empty(PREFILL_WS_FLOATS, dtype=torch.float32, device=device),
+        _prefill_ws[key] = (empty_handoff(PREFILL_WS_FLOATS, torch.float32, device),
                             torch.zeros(16384, dtype=torch.int32, device=device))
     return _prefill_ws[key]
 

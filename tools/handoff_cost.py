@@ -1,7 +1,8 @@
 """What the agent-scope fences of the in-launch hand-offs cost (common.h handoff_last):
 times the engine's split-K / partition-merge launches with the round-2 sc1-only consumer
 (mode 0), the acquire by the last arriver (mode 1) and producer release + acquire
-(mode 2), interleaved in one process (guide §5.4 rule 24).
+(mode 2), interleaved in one process (guide §5.4 rule 24), each with the hand-off buffers in
+uncached memory (ops.empty_handoff, shipped from round 4) and in ordinary cached memory.
 
     python tools/handoff_cost.py [--rounds 15] [--out file.jsonl]
 """
@@ -49,7 +50,20 @@ def gemm(M, N, K, kind, **kw):
     return lambda: ops.mid_gemm(x, wp, "resid", resid=r, out=out, **kw)
 
 
-def attention(nseq, ctx_len, part):
+ALLOC = {"uncached": kernels.empty_handoff,
+         "cached": lambda n, dt=torch.float32, device=None: torch.zeros(int(n), dtype=dt, device=device)}
+WS = {}
+for kind, fn in ALLOC.items():  # one split-K workspace set per allocation kind
+    WS[kind] = {"wide": (fn(kernels.WIDE_WS_FLOATS, torch.float32, dev), torch.zeros(16384, dtype=torch.int32, device=dev)),
+                "mid": (fn(kernels.MID_WS_FLOATS, torch.float32, dev), torch.zeros(16384, dtype=torch.int32, device=dev))}
+
+
+def use_ws(kind):
+    kernels._wide_ws[str(dev)] = WS[kind]["wide"]
+    kernels._mid_ws[str(dev)] = WS[kind]["mid"]
+
+
+def attention(nseq, ctx_len, part, alloc="uncached"):
     H, KV, blk = 32, 8, 16
     nb = (ctx_len + blk - 1) // blk
     total = nseq * nb + 4
@@ -60,8 +74,8 @@ def attention(nseq, ctx_len, part):
                                          qcols=128, wide_min_tokens=0)
     it = torch.tensor(items + [(0, 0, 0, 0)], dtype=torch.int32, device=dev)
     n_it = torch.tensor([len(items)], dtype=torch.int32, device=dev)
-    part_o = torch.empty(it.shape[0] * KV * 16 * 128, dtype=torch.float32, device=dev)
-    part_ml = torch.empty(it.shape[0] * KV * 16 * 2, dtype=torch.float32, device=dev)
+    part_o = ALLOC[alloc](it.shape[0] * KV * 16 * 128, torch.float32, dev)
+    part_ml = ALLOC[alloc](it.shape[0] * KV * 16 * 2, torch.float32, dev)
     cnt = torch.zeros(nseq * KV, dtype=torch.int32, device=dev)
     q = torch.randn(nseq, H, 128, device=dev).to(torch.bfloat16)
     out = torch.empty(nseq, H, 128, device=dev, dtype=torch.bfloat16)
@@ -71,26 +85,32 @@ def attention(nseq, ctx_len, part):
                                        1.0 / math.sqrt(128), part_size=ps)
 
 
-cases = {
-    "decode down_resid M16 S2 (engine, 9-16-row steps)": gemm(16, 4096, 14336, "decode", nt=2, waves=16, splits=2),
-    "mid o_resid M32 fm1 fn2 S4 (engine)": gemm(32, 4096, 4096, "mid", fm=1, fn=2, splits=4),
-    "mid down_resid M64 fm2 fn2 S4 (engine)": gemm(64, 4096, 14336, "mid", fm=2, fn=2, splits=4),
-    "mid down_resid M256 fm4 fn2 S2 (engine)": gemm(256, 4096, 14336, "mid", fm=4, fn=2, splits=2),
-    "attention decode 64 x ctx 1000 part 256": attention(64, 1000, 256),
-    "attention decode 8 x ctx 2000 part 512": attention(8, 2000, 512),
-}
+cases = {}
+for alloc in ALLOC:
+    use_ws(alloc)
+    cases.update({
+        (alloc, "decode down_resid M16 S2 (engine, 9-16-row steps)"): (gemm(16, 4096, 14336, "decode", nt=2, waves=16, splits=2), alloc),
+        (alloc, "mid o_resid M32 fm1 fn2 S4 (engine)"): (gemm(32, 4096, 4096, "mid", fm=1, fn=2, splits=4), alloc),
+        (alloc, "mid down_resid M64 fm2 fn2 S4 (engine)"): (gemm(64, 4096, 14336, "mid", fm=2, fn=2, splits=4), alloc),
+        (alloc, "mid down_resid M256 fm4 fn2 S2 (engine)"): (gemm(256, 4096, 14336, "mid", fm=4, fn=2, splits=2), alloc),
+        (alloc, "attention decode 64 x ctx 1000 part 256"): (attention(64, 1000, 256, alloc), alloc),
+        (alloc, "attention decode 8 x ctx 2000 part 512"): (attention(8, 2000, 512, alloc), alloc),
+    })
 MODES = (0, 1, 2)
 res = {k: {m: [] for m in MODES} for k in cases}
 for _ in range(a.rounds):
-    for k, fn in cases.items():
+    for k, (fn, alloc) in cases.items():
+        use_ws(alloc)
         for mode in MODES:
             C.handoff_set_acquire(mode)
             res[k][mode].append(timer(fn))
 C.handoff_set_modes(2, 1)
+use_ws("uncached")
 f = open(a.out, "a") if a.out else None
 for k in cases:
     m0, m1, m2 = (statistics.median(res[k][m]) for m in MODES)
-    rec = {"case": k, "sc1_only_us": round(m0, 2), "acquire_us": round(m1, 2), "release_acquire_us": round(m2, 2),
+    rec = {"alloc": k[0], "case": k[1], "sc1_only_us": round(m0, 2), "acquire_us": round(m1, 2),
+           "release_acquire_us": round(m2, 2),
            "delta_acquire_us": round(m1 - m0, 2), "delta_release_acquire_us": round(m2 - m0, 2)}
     print(json.dumps(rec), flush=True)
     if f:

@@ -36,7 +36,12 @@ ap.add_argument("--reps", type=int, default=300)
 ap.add_argument("--modes", default="default")
 ap.add_argument("--only", default="")
 ap.add_argument("--out", default="")
+ap.add_argument("--cached", action="store_true",
+                help="hand-off workspaces in ordinary (cached) device memory instead of the shipped uncached "
+                     "allocation (ops.empty_handoff), to show what the uncached memory buys")
 a = ap.parse_args()
+if a.cached:  # the round-3 allocation, for the comparison
+    kernels.empty_handoff = lambda n, dt=torch.float32, device=None: torch.zeros(int(n), dtype=dt, device=device)
 modes = [m if m == "default" else int(m) for m in a.modes.split(",")]
 dev = torch.device("cuda")
 NAN = float("nan")
@@ -162,10 +167,10 @@ def gemm_case(M, N, K, epi, splits, kind, **cfg):
     return make, call
 
 
-def attention_case(nseq, ctx_max, part):
+def attention_case(nseq, ctx_max, part, waves=4, ctx_min=None):
     blk = 16
     torch.manual_seed(1)
-    ctx = torch.randint(part + 1, ctx_max, (nseq,)).tolist()
+    ctx = torch.randint(ctx_min or part + 1, ctx_max, (nseq,)).tolist()
     nbs = [(c + blk - 1) // blk for c in ctx]
     total = sum(nbs) + 4
     kc = torch.randn(total, KV, 16, blk, 8, device=dev).to(torch.bfloat16)
@@ -188,8 +193,8 @@ def attention_case(nseq, ctx_max, part):
         it = torch.tensor(items + [(0, 0, 0, 0)], dtype=torch.int32, device=dev)
         plans[split] = (it, torch.tensor([len(items)], dtype=torch.int32, device=dev))
     maxit = max(p[0].shape[0] for p in plans.values())
-    part_o = torch.empty(maxit * KV * 16 * 128, dtype=torch.float32, device=dev)
-    part_ml = torch.empty(maxit * KV * 16 * 2, dtype=torch.float32, device=dev)
+    part_o = kernels.empty_handoff(maxit * KV * 16 * 128, torch.float32, dev)
+    part_ml = kernels.empty_handoff(maxit * KV * 16 * 2, torch.float32, dev)
     cnt = torch.zeros(nseq * KV, dtype=torch.int32, device=dev)
     psz = torch.tensor([part], dtype=torch.int32, device=dev)
 
@@ -203,7 +208,7 @@ def attention_case(nseq, ctx_max, part):
         part_ml.fill_(NAN)
         out = torch.full((nseq, H, 128), NAN, dtype=torch.bfloat16, device=dev)
         ops.paged_attention(out, part_o, part_ml, q, kc, vc, it, n_it, cnt, q_start, dq, dc, bt,
-                            1.0 / math.sqrt(128), part_size=psz)
+                            1.0 / math.sqrt(128), part_size=psz, waves=waves)
         return out
     return make, call
 
@@ -229,6 +234,14 @@ cases.append(("prefill gate_up_silu M2048 (768 whole + 128 tiles x S2)",
               lambda: gemm_case(2048, 28672, 4096, "silu", 2, "prefill", full=768)))
 cases.append(("attention decode 48 seqs part256", lambda: attention_case(48, 3000, 256)))
 cases.append(("attention decode 8 seqs part512", lambda: attention_case(8, 4000, 512)))
+# 256- and 512-key partitions, 4- and 8-wave workgroups, 64 x ~1,000 and
+# 8 x ~2,000 keys
+for nseq, lo, hi in ((64, 900, 1100), (8, 1900, 2100)):
+    for part in (256, 512):
+        for wv in (4, 8):
+            cases.append((f"attention decode {nseq}x{lo}-{hi} part{part} w{wv}",
+                          lambda nseq=nseq, lo=lo, hi=hi, part=part, wv=wv:
+                          attention_case(nseq, hi, part, waves=wv, ctx_min=lo)))
 
 for name, mk in cases:
     if a.only and a.only not in name:
