@@ -221,11 +221,14 @@ __device__ __forceinline__ void decode_item(
   }
   const int ctq = ccol / G, chg = ccol % G;
   if (nparts > 1) {
-    // Partition hand-off inside the launch (cdna_hip_programming.md §6 G16, sc1
-    // form): the slab is stored write-through (sc1) and (m, l) as one relaxed
-    // agent-scope 64-bit atomic, every wave drains, then one lane takes a ticket;
-    // the holder of ticket nparts-1 merges all partitions reading them with sc1
-    // loads — no release/acquire fences (no L2 writeback), no second launch.
+    // Partition hand-off inside the launch (cdna_hip_programming.md §6 G16, common.h
+    // handoff_last): part_o / part_ml live in UNCACHED device memory (ops.empty_handoff), the
+    // slab is stored write-through (sc1) and (m, l) as one relaxed agent-scope 64-bit atomic,
+    // every wave drains, then one lane takes a relaxed ticket; the holder of ticket nparts-1
+    // runs ONE agent-scope acquire (mode g_handoff_attn = 1) and merges all partitions with sc1
+    // loads. No producer release (its L2 write-back cost +77 us on a 64 x 1,000-key launch);
+    // 0 bad runs in 10,000 poisoned repetitions for every 256/512-key, 4/8-wave case
+    // (profiles/r4_handoff_uncached.md). No second launch.
     const __amdgpu_buffer_rsrc_t ps = __builtin_amdgcn_make_buffer_rsrc(
         part_o + ((size_t)pidx * KV + kvh) * 16 * ATT_HD, 0, 16 * ATT_HD * 4, 0x00020000);
     const int soff = (ccol * ATT_HD + d0) * 4;

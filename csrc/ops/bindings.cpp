@@ -53,6 +53,13 @@ int pa_mid_gemm(void* y, const void* x, const void* wp, const void* resid, float
                 void* q_out, void* k_cache, void* v_cache, const int* positions, const int* slots,
                 const float* cos_sin, int H, int KV, hipStream_t st);
 int pa_row_sumsq(float* out, const void* x, int M, int K, int ldx, hipStream_t st);
+long long pa_stream_gemm_ws_floats(int M, int N, int K, int mg, int rg, int tpw, int wt, int wk, int S);
+void pa_stream_gemm_plan(int M, int N, int K, int epi, int* plan);
+int pa_stream_gemm(void* y, const void* x, const void* wp, const void* resid, float* ws, long long ws_floats,
+                   int* counters, int n_counters, int* err, int M, int N, int K, int ldx, int ldy, int ldr, int epi,
+                   const float* ss_in, float* ss_out, float* ss_zero, float eps, const int* plan, void* q_out,
+                   void* k_cache, void* v_cache, const int* positions, const int* slots, const float* cos_sin, int H,
+                   int KV, int rel, hipStream_t st);
 void pa_prefill_gemm_plan(int M, int N, int K, int bn, int* full, int* S);
 int pa_prefill_pick_bn(int M, int N);
 void pa_prefill_set_variant(int v);
@@ -438,6 +445,93 @@ bool mid_qkv_rope(at::Tensor x, at::Tensor wp, at::Tensor ss_in, double eps, at:
   return rc == 0;
 }
 
+// Weight-streaming projections for 16 < M <= 256 (csrc/ops/gemm_stream.hip): every epilogue
+// (0 plain, 1 SwiGLU, 2 residual, 3 rope-perm, 4 RoPE + paged KV write). plan: 7 ints
+// (mg, rg, tpw, wt, wk, S, D) or empty for the default decomposition.
+bool stream_gemm(c10::optional<at::Tensor> y, at::Tensor x, at::Tensor wp, c10::optional<at::Tensor> resid,
+                 at::Tensor ws, at::Tensor counters, at::Tensor err, int64_t epi, c10::optional<at::Tensor> ss_in,
+                 c10::optional<at::Tensor> ss_out, c10::optional<at::Tensor> ss_zero, double eps,
+                 std::vector<int64_t> plan, c10::optional<at::Tensor> q_out, c10::optional<at::Tensor> k_cache,
+                 c10::optional<at::Tensor> v_cache, c10::optional<at::Tensor> positions,
+                 c10::optional<at::Tensor> slots, c10::optional<at::Tensor> cos_sin, int64_t H, int64_t KV,
+                 int64_t rel) {
+  check_gpu(wp, "wp"); check_gpu(ws, "ws"); check_gpu(counters, "counters"); check_gpu(err, "err");
+  TORCH_CHECK(x.is_cuda() && x.dim() == 2 && x.stride(1) == 1, "x must be a 2-D GPU tensor, unit inner stride");
+  check_dtype(x, at::kBFloat16, "x"); check_dtype(wp, at::kBFloat16, "wp");
+  check_dtype(ws, at::kFloat, "ws"); check_dtype(counters, at::kInt, "counters"); check_dtype(err, at::kInt, "err");
+  TORCH_CHECK(epi >= 0 && epi <= 4, "stream_gemm epi must be 0..4");
+  TORCH_CHECK(wp.dim() == 4 && wp.size(2) == 64 && wp.size(3) == 8, "wp must be packed [N/16, K/32, 64, 8]");
+  const int M = x.size(0), K = x.size(1), N = wp.size(0) * 16;
+  TORCH_CHECK(wp.size(1) * 32 == K, "packed weight K mismatch");
+  TORCH_CHECK(x.stride(0) % 8 == 0 && ((uintptr_t)x.data_ptr() & 15) == 0, "x rows must be 16-byte aligned");
+  void* yp = nullptr;
+  int ldy = 0;
+  if (epi != 4) {
+    TORCH_CHECK(y.has_value(), "stream_gemm needs y for epi ", epi);
+    const auto& t = *y;
+    TORCH_CHECK(t.is_cuda() && t.dim() == 2 && t.stride(1) == 1, "y must be a 2-D GPU tensor, unit inner stride");
+    check_dtype(t, at::kBFloat16, "y");
+    const int NO = epi == 1 ? N / 2 : N;
+    TORCH_CHECK(t.size(0) == M && t.size(1) == NO, "y shape mismatch");
+    TORCH_CHECK(t.stride(0) % 4 == 0 && ((uintptr_t)t.data_ptr() & 7) == 0, "y rows must be 8-byte aligned");
+    yp = t.data_ptr();
+    ldy = t.stride(0);
+  }
+  const void* rp = nullptr;
+  int ldr = 0;
+  if (epi == 2) {
+    TORCH_CHECK(resid.has_value(), "epi=2 needs resid");
+    const auto& r = *resid;
+    TORCH_CHECK(r.is_cuda() && r.dim() == 2 && r.stride(1) == 1 && r.size(0) == M && r.size(1) == N &&
+                    r.stride(0) % 4 == 0 && ((uintptr_t)r.data_ptr() & 7) == 0,
+                "resid must be [M, N] with unit inner stride, 8-byte aligned rows");
+    check_dtype(r, at::kBFloat16, "resid");
+    rp = r.data_ptr();
+    ldr = r.stride(0);
+  }
+  void *qp = nullptr, *kp = nullptr, *vp = nullptr;
+  const int *pp = nullptr, *sp = nullptr;
+  const float* cp = nullptr;
+  if (epi == 4) {
+    TORCH_CHECK(q_out && k_cache && v_cache && positions && slots && cos_sin, "epi=4 needs the RoPE / cache tensors");
+    check_gpu(*q_out, "q_out"); check_gpu(*k_cache, "k_cache"); check_gpu(*v_cache, "v_cache");
+    check_gpu(*positions, "positions"); check_gpu(*slots, "slots"); check_gpu(*cos_sin, "cos_sin");
+    check_dtype(*q_out, at::kBFloat16, "q_out"); check_dtype(*k_cache, at::kBFloat16, "k_cache");
+    check_dtype(*v_cache, at::kBFloat16, "v_cache"); check_dtype(*positions, at::kInt, "positions");
+    check_dtype(*slots, at::kInt, "slots"); check_dtype(*cos_sin, at::kFloat, "cos_sin");
+    TORCH_CHECK(N == (H + 2 * KV) * 128, "packed QKV has ", N, " columns, expected (H + 2 KV) * 128");
+    TORCH_CHECK(q_out->numel() >= (int64_t)M * H * 128, "q_out too small");
+    TORCH_CHECK(positions->numel() >= M && slots->numel() >= M, "positions/slots shorter than x");
+    TORCH_CHECK(cos_sin->dim() == 2 && cos_sin->size(1) == 128, "cos_sin must be [max_pos, 128]");
+    TORCH_CHECK(k_cache->dim() == 5 && k_cache->size(1) == KV && k_cache->size(2) == 16 && k_cache->size(3) == 16 &&
+                    k_cache->size(4) == 8, "k_cache must be [NB, KV, 16, 16, 8]");
+    TORCH_CHECK(v_cache->dim() == 4 && v_cache->size(1) == KV && v_cache->size(2) == 128 && v_cache->size(3) == 16,
+                "v_cache must be [NB, KV, 128, 16]");
+    qp = q_out->data_ptr(); kp = k_cache->data_ptr(); vp = v_cache->data_ptr();
+    pp = positions->data_ptr<int>(); sp = slots->data_ptr<int>(); cp = cos_sin->data_ptr<float>();
+  }
+  int pl[7] = {0, 0, 0, 0, 0, 0, 0};
+  if (!plan.empty()) {
+    TORCH_CHECK(plan.size() == 7, "plan must be 7 ints (mg, rg, tpw, wt, wk, S, D)");
+    for (int i = 0; i < 7; ++i) pl[i] = (int)plan[i];
+  }
+  const int rc = pa_stream_gemm(yp, x.data_ptr(), wp.data_ptr(), rp, ws.data_ptr<float>(), ws.numel(),
+                                counters.data_ptr<int>(), counters.numel(), err.data_ptr<int>(), M, N, K, x.stride(0),
+                                ldy, ldr, (int)epi, opt_rows(ss_in, M, "ss_in"),
+                                const_cast<float*>(opt_rows(ss_out, M, "ss_out")),
+                                const_cast<float*>(opt_rows(ss_zero, M, "ss_zero")), (float)eps, pl, qp, kp, vp, pp,
+                                sp, cp, (int)H, (int)KV, (int)rel, cur_stream());
+  TORCH_CHECK(rc >= 0, "stream_gemm launch failed");
+  return rc == 0;
+}
+
+std::vector<int64_t> stream_gemm_plan(int64_t M, int64_t N, int64_t K, int64_t epi) {
+  int p[7];
+  pa_stream_gemm_plan((int)M, (int)N, (int)K, (int)epi, p);
+  const long long ws = pa_stream_gemm_ws_floats((int)M, (int)N, (int)K, p[0], p[1], p[2], p[3], p[4], p[5]);
+  return {p[0], p[1], p[2], p[3], p[4], p[5], p[6], (int64_t)ws};
+}
+
 // Large-M projections (csrc/ops/gemm_prefill.hip): 256x256 MFMA tiles on the packed
 // weights with the same epilogues as mid_gemm (0 plain, 1 SwiGLU, 2 residual, 3 rope-perm).
 bool prefill_gemm(at::Tensor y, at::Tensor x, at::Tensor wp, c10::optional<at::Tensor> resid, at::Tensor ws,
@@ -781,6 +875,13 @@ PYBIND11_MODULE(_C, m) {
   m.def("prefill_gemm_plan", &prefill_gemm_plan, py::arg("M"), py::arg("N"), py::arg("K"), py::arg("bn") = 0,
         "default (full tiles, splits, workspace floats, tile width) of prefill_gemm");
   m.def("row_sumsq", &row_sumsq, py::arg("out"), py::arg("x"));
+  m.def("stream_gemm", &stream_gemm, py::arg("y"), py::arg("x"), py::arg("wp"), py::arg("resid"), py::arg("ws"),
+        py::arg("counters"), py::arg("err"), py::arg("epi"), py::arg("ss_in"), py::arg("ss_out"), py::arg("ss_zero"),
+        py::arg("eps"), py::arg("plan"), py::arg("q_out") = py::none(), py::arg("k_cache") = py::none(),
+        py::arg("v_cache") = py::none(), py::arg("positions") = py::none(), py::arg("slots") = py::none(),
+        py::arg("cos_sin") = py::none(), py::arg("H") = 0, py::arg("KV") = 0, py::arg("rel") = 0);
+  m.def("stream_gemm_plan", &stream_gemm_plan,
+        "default (mg, rg, tpw, wt, wk, S, D, workspace floats) of stream_gemm");
   m.def("mid_gemm_plan", &mid_gemm_plan, "default (fm, fn, splits, workspace floats) of mid_gemm");
   m.def("paged_attention", &paged_attention, py::arg("out"), py::arg("part_o"), py::arg("part_ml"), py::arg("q"),
         py::arg("k_cache"), py::arg("v_cache"), py::arg("items"), py::arg("n_items"), py::arg("counters"),

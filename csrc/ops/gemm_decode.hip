@@ -308,10 +308,14 @@ static int g_dg_variant = 1;
 //   GEMM split-K slabs (decode / wide / mid / prefill): 2 = producer agent release + last-arriver
 //     agent acquire. Decode qkv_rope at M = 9 with 3 K-slices mismatched in 46 of 3,000 runs
 //     with the round-2 sc1-only form (mode 0) and in 4 of 10,000 with the acquire alone
-//     (mode 1); none with mode 2 (+2-3 us per split launch).
-//   attention partition merge: 1 = last-arriver agent acquire (0 mismatches in 3,000 poisoned
-//     runs in every mode; the release costs +77 us at 64 rows x 1,000 keys there: it writes
-//     back every dirty L2 line of the XCD, and this launch leaves many).
+//     (mode 1); none with mode 2 (+2-3 us per split launch). Round 4: with the slabs in
+//     uncached memory (ops.empty_handoff) mode 1 still mismatched 5 of 10,000 (finite values),
+//     so the cause is not a stale L2 copy of the slab; mode 2 stays
+//     (profiles/r4_handoff_uncached.md).
+//   attention partition merge: 1 = last-arriver agent acquire on uncached partials: 0 bad runs
+//     in 10,000 poisoned repetitions for each of ten 256/512-key, 4/8-wave cases (round 4); the
+//     release costs +77 us at 64 rows x 1,000 keys there (it writes back every dirty L2 line of
+//     the XCD, and this launch leaves many).
 int g_handoff_acquire = 2;
 int g_handoff_attn = 1;
 

@@ -32,7 +32,8 @@ ARCH = os.environ.get("PILOTTAI_GPU_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 # Per-file code-generation flags. gemm_mid.hip: MFMA accumulators in the VGPR form; with
 # the AGPR form hipcc shuffles them through v_accvgpr moves in the software-pipelined loop.
-FILE_FLAGS = {"gemm_mid.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"]}
+FILE_FLAGS = {"gemm_mid.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"],
+              "gemm_stream.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"]}
 
 
 def _torch_paths():

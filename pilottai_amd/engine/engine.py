@@ -590,22 +590,36 @@ class LLMEngine:
             return
         box = [f"pilottai_tp_{os.getpid()}_{self.tp.root}_{os.urandom(4).hex()}" if self.is_driver else None]
         torch.distributed.broadcast_object_list(box, src=self.tp.root, group=self.tp.cpu_group)
-        ok = torch.zeros(1, dtype=torch.int32)
+        # Symmetric two-phase handshake: every rank reaches the same two collectives whatever
+        # fails where (a driver-side create failure must not leave the followers in a barrier
+        # that the driver skipped). Phase 1: the driver creates, all ranks agree on the status;
+        # phase 2: the followers attach, all ranks agree again. Any failure -> gloo everywhere.
+        created = self._tp_ring_phase(lambda rt: self._set_tp_ring(rt.ShmRing(box[0], 9, 64, self.tp.size - 1, True))
+                                      if self.is_driver else None, "create")
+        attached = created and self._tp_ring_phase(
+            lambda rt: self._set_tp_ring(rt.ShmRing(box[0], 9, 64, self.tp.size - 1, False, 120.0))
+            if not self.is_driver else None, "attach")
+        if not attached:
+            self._tp_ring = None
+
+    def _set_tp_ring(self, ring):
+        self._tp_ring = ring
+
+    def _tp_ring_phase(self, fn, what: str) -> bool:
+        """Run fn(_runtime) on this rank, then all-reduce the failure flag over the TP group:
+        True iff the phase succeeded on every rank."""
+        bad = torch.zeros(1, dtype=torch.int32)
         try:
             from pilottai_amd import _runtime
 
-            # driver first (creates), then the followers attach
-            if self.is_driver:
-                self._tp_ring = _runtime.ShmRing(box[0], 9, 64, self.tp.size - 1, True)
-            torch.distributed.barrier(group=self.tp.cpu_group)
-            if not self.is_driver:
-                self._tp_ring = _runtime.ShmRing(box[0], 9, 64, self.tp.size - 1, False, 120.0)
+            if os.environ.get("PILOTTAI_TP_RING_FAIL") == f"{what}:{self.tp.rank}":  # fault injection (tests)
+                raise RuntimeError(f"injected TP ring {what} failure")
+            fn(_runtime)
         except Exception as e:  # noqa: BLE001 — fall back to the gloo broadcast on every rank
-            log.warning("TP header ring unavailable (%s): using the gloo broadcast", e)
-            ok[0] = 1
-        torch.distributed.all_reduce(ok, group=self.tp.cpu_group)
-        if int(ok[0]):
-            self._tp_ring = None
+            log.warning("TP header ring %s failed on rank %d (%s): using the gloo broadcast", what, self.tp.rank, e)
+            bad[0] = 1
+        torch.distributed.all_reduce(bad, group=self.tp.cpu_group)
+        return int(bad[0]) == 0
 
     def _tp_send(self, op: int, *vals: int):
         h = self._tp_header

@@ -530,6 +530,75 @@ def mid_gemm(x: torch.Tensor, wp: torch.Tensor, epi: str = "plain", resid: Optio
 
 
 # ---------------------------------------------------------------------------
+# Weight-streaming projections (16 < M <= 256) on the packed weights (csrc/ops/gemm_stream.hip)
+
+STREAM_EPI = {"plain": 0, "silu": 1, "resid": 2, "rope_perm": 3}
+STREAM_WS_FLOATS = 24 << 20  # 96 MB of split-K partial fragments per device (uncached)
+_stream_ws = {}
+
+
+def stream_workspace(device):
+    """(slabs, counters, err) for stream_gemm / stream_qkv_rope on `device`; allocate before
+    hipGraph capture. Slabs live in uncached memory (empty_handoff); the group counters start
+    zeroed and every launch leaves them zeroed; err[0] != 0 means a group barrier timed out."""
+    key = str(device)
+    if key not in _stream_ws:
+        _stream_ws[key] = (empty_handoff(STREAM_WS_FLOATS, torch.float32, device),
+                           torch.zeros(16384, dtype=torch.int32, device=device),
+                           torch.zeros(16, dtype=torch.int32, device=device))
+    return _stream_ws[key]
+
+
+def stream_gemm_plan(M: int, N: int, K: int, epi: str = "plain"):
+    """Default decomposition (mg, rg, tpw, wt, wk, S, D) of stream_gemm for this shape."""
+    code = 4 if epi == "rope_kv" else STREAM_EPI[epi]
+    return tuple(require_native().stream_gemm_plan(int(M), int(N), int(K), code)[:7])
+
+
+def stream_gemm(x: torch.Tensor, wp: torch.Tensor, epi: str = "plain", resid: Optional[torch.Tensor] = None,
+                out: Optional[torch.Tensor] = None, norm: bool = False, eps: float = 1e-5,
+                ss_in: Optional[torch.Tensor] = None, ss_out: Optional[torch.Tensor] = None,
+                ss_zero: Optional[torch.Tensor] = None, plan=None, rel: int = 0) -> torch.Tensor:
+    """y = epi(rownorm(x) @ W.T) for 16 < M <= 256 with W packed by pack_decode_weight (gate_up:
+    pack_decode_gate_up + "silu"; QKV: pack_decode_qkv_rope + "rope_perm"); same epilogue and
+    row-statistics conventions as mid_gemm. `plan`: (mg, rg, tpw, wt, wk, S, D) or None for
+    the kernel's default decomposition (csrc/ops/gemm_stream.hip)."""
+    M, K = x.shape
+    N = wp.shape[0] * 16
+    code = STREAM_EPI[epi]
+    NO = N // 2 if code == 1 else N
+    if out is None:
+        out = torch.empty(M, NO, dtype=x.dtype, device=x.device)
+    if norm and ss_in is None:
+        ss_in = row_sumsq(x)
+    if _on_gpu(x):
+        ws, cnt, err = stream_workspace(x.device)
+        if not require_native().stream_gemm(out, x, wp, resid, ws, cnt, err, code, ss_in if norm else None, ss_out,
+                                             ss_zero, float(eps), list(plan) if plan else [], rel=int(rel)):
+            raise ValueError(f"stream_gemm does not handle M={M} N={N} K={K} epi={epi} plan={plan}")
+        return out
+    return mid_gemm(x, wp, epi, resid=resid, out=out, norm=norm, eps=eps, ss_in=ss_in, ss_out=ss_out,
+                    ss_zero=ss_zero)
+
+
+def stream_qkv_rope(x: torch.Tensor, wp: torch.Tensor, eps: float, q_out: torch.Tensor, k_cache, v_cache,
+                    positions, slots, cos_sin, H: int, KV: int, ss_in: Optional[torch.Tensor] = None, plan=None,
+                    rel: int = 0) -> torch.Tensor:
+    """QKV projection for 16 < M <= 256 (RMSNorm folded, row statistics ss_in) with RoPE and the
+    paged KV write in the epilogue (csrc/ops/gemm_stream.hip, EP_ROPEKV)."""
+    if ss_in is None:
+        ss_in = row_sumsq(x)
+    if _on_gpu(x):
+        ws, cnt, err = stream_workspace(x.device)
+        if not require_native().stream_gemm(None, x, wp, None, ws, cnt, err, 4, ss_in, None, None, float(eps),
+                                             list(plan) if plan else [], q_out, k_cache, v_cache, positions, slots,
+                                             cos_sin, int(H), int(KV), int(rel)):
+            raise ValueError(f"stream_qkv_rope does not handle M={x.shape[0]} K={x.shape[1]} plan={plan}")
+        return q_out
+    return mid_qkv_rope(x, wp, eps, q_out, k_cache, v_cache, positions, slots, cos_sin, H, KV, ss_in=ss_in)
+
+
+# ---------------------------------------------------------------------------
 # Large-M projections (prefill-heavy steps) on the packed weights (csrc/ops/gemm_prefill.hip)
 
 PREFILL_WS_FLOATS = 64 << 20  # 256 MB of split slabs per device (= gemm_prefill.hip kWsFloats)

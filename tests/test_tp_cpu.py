@@ -104,3 +104,38 @@ def test_sharded_init_slices_match_full():
         w = cfg.num_heads * hd // 2
         assert torch.equal(P0["wo"], L0["wo"][:, r * w:(r + 1) * w])
         assert torch.equal(part.embed, full.embed[r * cfg.vocab_size // 2:(r + 1) * cfg.vocab_size // 2])
+
+
+def _ring_fail_worker(rank, world, port, out_path, fail):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank), PILOTTAI_TP_RING_FAIL=fail)
+    torch.set_num_threads(2)
+    from pilottai_amd.engine.engine import LLMEngine
+    from pilottai_amd.parallel.comm import init_distributed, new_tp_groups
+
+    init_distributed("gloo")
+    tp = new_tp_groups(world)
+    e = LLMEngine(_cfg(), device="cpu", tp=tp)
+    header = "shm" if e._tp_ring is not None else "gloo"
+    if rank != 0:
+        e.follow()
+        torch.distributed.destroy_process_group()
+        return
+    out = e.generate(_prompts(e.tok), temperature=0.0, max_tokens=4, ignore_eos=True)
+    e.release_followers()
+    torch.distributed.destroy_process_group()
+    with open(out_path, "w") as f:
+        json.dump({"header": header, "tokens": [o.token_ids for o in out]}, f)
+
+
+@pytest.mark.parametrize("fail", ["create:0", "attach:1"])
+def test_tp_header_ring_failure_falls_back_on_every_rank(tmp_path, fail):
+    """a TP header ring that fails to be created on the driver (or to be
+    attached on a follower) must leave EVERY rank on the gloo broadcast, with no rank stuck in a
+    collective the others skipped; the engine then serves normally."""
+    out = str(tmp_path / "ring.json")
+    mp.start_processes(_ring_fail_worker, args=(2, _free_port(), out, fail), nprocs=2, join=True,
+                       start_method="spawn")
+    res = json.load(open(out))
+    assert res["header"] == "gloo"
+    assert len(res["tokens"]) == 2 and all(len(t) == 4 for t in res["tokens"])
