@@ -251,18 +251,33 @@ class EnhancedMemory:
 
     # ---------------------------------------------------------------- checkpoint (App. D MemoryItem format)
     def to_dict(self) -> Dict[str, Any]:
-        return {"semantic": [self._items[r].model_dump(mode="json") for r in sorted(self._items)],
+        # each semantic item records its index row: with the index saved beside the JSON
+        # (SemanticIndex.save, utils/checkpoint.py) the restore re-attaches it without re-embedding
+        return {"semantic": [dict(self._items[r].model_dump(mode="json"), row=r) for r in sorted(self._items)],
                 "tasks": {k: [dict(e, timestamp=e["timestamp"].isoformat()) for e in v]
                           for k, v in self._task_history.items()},
                 "patterns": {k: {"data": v["data"], "timestamp": v["timestamp"].isoformat(),
                                  "expires_at": v["expires_at"].isoformat() if v["expires_at"] else None}
                              for k, v in self._pattern_store.items()}}
 
-    async def load_dict(self, d: Dict[str, Any]):
-        items = [MemoryItem(**x) for x in d.get("semantic", [])]
+    async def load_dict(self, d: Dict[str, Any], index_restored: bool = False):
+        """Restore from to_dict() form. `index_restored`: self.index was loaded from the same
+        checkpoint (SemanticIndex.load), so an item that recorded its row is re-attached to that
+        row as is; only items without a stored row are embedded again."""
+        items, rows = [], []
+        for x in d.get("semantic", []):
+            x = dict(x)
+            r = x.pop("row", None)
+            items.append(MemoryItem(**x))
+            rows.append(r if index_restored and r is not None and 0 <= int(r) < self.index.count else None)
         if items:
             async with self._semantic_lock:
-                self._store_items(items)
+                for r, it in zip(rows, items):
+                    if r is not None:
+                        self._items[int(r)] = it
+                fresh = [it for r, it in zip(rows, items) if r is None]
+                if fresh:
+                    self._store_items(fresh)
         for k, v in d.get("tasks", {}).items():
             h = self._task_history.setdefault(k, deque(maxlen=self.max_task_history))
             for e in v:

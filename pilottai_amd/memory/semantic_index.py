@@ -293,6 +293,119 @@ class SemanticIndex:
     def memory_bytes(self) -> int:
         return self.packed.numel() * 2 + self.capacity * (4 + 8 + 4)
 
+    # -- checkpoint / resume (the embedding matrix as per-GPU binary shards
+    # next to the JSON metadata; reference item form pilott/memory/enhanced_memory.py:9-21) --
+    CKPT_VERSION = 1
+
+    def save(self, path, chunk_bytes: int = 256 << 20) -> Dict[str, float]:
+        """Write the index to directory `path`: packed.npy (the fragment-major bf16 tiles as
+        uint16, exactly the device layout), priority.npy / tagbits.npy / expiry.npy (per-row
+        filter metadata) and meta.json (dims, ring position, clock epoch, tag registry, the
+        overflow-tag rows). Rows leave the device in `chunk_bytes` pieces through one pinned
+        staging buffer straight into the .npy files (np.lib.format.open_memmap): no
+        whole-index host copy, so a 200 GB store needs only the staging buffer of host RAM.
+        Files go to a temp directory renamed into place. Returns timings (s) and bytes."""
+        import json
+        import os
+        import shutil
+        import tempfile
+        from pathlib import Path
+
+        t0 = time.perf_counter()
+        path = Path(path)
+        path.parent.mkdir(parents=True, exist_ok=True)
+        tmp = Path(tempfile.mkdtemp(prefix=".idx-", dir=str(path.parent)))
+        with self._lock:
+            n = self.count
+            tiles = (n + 15) // 16
+            tile_bytes = self.dim // 32 * 64 * 8 * 2
+            per = max(1, chunk_bytes // tile_bytes)
+            out = np.lib.format.open_memmap(tmp / "packed.npy", mode="w+", dtype=np.uint16,
+                                            shape=(tiles, self.dim // 32, 64, 8))
+            stage = None
+            for t in range(0, tiles, per):
+                m = min(per, tiles - t)
+                src = self.packed[t:t + m].view(torch.int16)
+                if self.device.type == "cuda":
+                    if stage is None:
+                        stage = torch.empty((per,) + tuple(src.shape[1:]), dtype=torch.int16, pin_memory=True)
+                    stage[:m].copy_(src)  # synchronous D2H into pinned memory
+                    out[t:t + m] = stage[:m].numpy().view(np.uint16)
+                else:
+                    out[t:t + m] = src.numpy().view(np.uint16)
+            out.flush()
+            del out
+            for name, ten in (("priority", self.priority), ("tagbits", self.tagbits), ("expiry", self.expiry)):
+                arr = np.lib.format.open_memmap(tmp / f"{name}.npy", mode="w+",
+                                                dtype={"priority": np.int32, "tagbits": np.int64,
+                                                       "expiry": np.float32}[name], shape=(n,))
+                rows = max(1, chunk_bytes // 8)
+                for r in range(0, n, rows):
+                    arr[r:r + rows] = ten[r:min(n, r + rows)].cpu().numpy()
+                arr.flush()
+                del arr
+            meta = {"version": self.CKPT_VERSION, "dim": self.dim, "count": n, "size": self.size,
+                    "capacity": self.capacity, "epoch": self.epoch, "tags": self.tags.bits,
+                    "row_tags": {str(k): sorted(v) for k, v in self.row_tags_py.items()}}
+        (tmp / "meta.json").write_text(json.dumps(meta))
+        if path.exists():
+            shutil.rmtree(path)
+        os.replace(tmp, path)
+        secs = time.perf_counter() - t0
+        nbytes = tiles * tile_bytes + n * 16
+        return {"rows": n, "bytes": nbytes, "seconds": secs, "GBps": nbytes / max(secs, 1e-9) / 1e9}
+
+    @classmethod
+    def load(cls, path, device=None, capacity: Optional[int] = None, growable: bool = True,
+             max_capacity: Optional[int] = None, chunk_bytes: int = 256 << 20) -> "SemanticIndex":
+        """Restore an index written by save(): the packed tiles go from the memory-mapped .npy to
+        the device in `chunk_bytes` pieces through a pinned staging buffer (no whole-index host
+        copy, no re-embedding); row ids, ring position, clock epoch and tags are preserved, so
+        MemoryItems that recorded their row (EnhancedMemory.to_dict) re-attach directly.
+        Only .npy (allow_pickle=False) and JSON are read."""
+        import json
+        from pathlib import Path
+
+        path = Path(path)
+        meta = json.loads((path / "meta.json").read_text())
+        if meta.get("version") != cls.CKPT_VERSION:
+            raise ValueError(f"unsupported index checkpoint version {meta.get('version')}")
+        n, dim = int(meta["count"]), int(meta["dim"])
+        cap = max(int(capacity or meta["capacity"]), n, 1)
+        idx = cls(dim=dim, capacity=cap, device=device, growable=growable,
+                  max_capacity=max_capacity or max(cap, int(meta["capacity"])))
+        packed = np.load(path / "packed.npy", mmap_mode="r", allow_pickle=False)
+        tiles = packed.shape[0]
+        if tiles != (n + 15) // 16 or packed.shape[1:] != (dim // 32, 64, 8):
+            raise ValueError("index checkpoint packed.npy does not match meta.json")
+        tile_bytes = dim // 32 * 64 * 8 * 2
+        per = max(1, chunk_bytes // tile_bytes)
+        stage = None
+        for t in range(0, tiles, per):
+            m = min(per, tiles - t)
+            host = torch.from_numpy(np.array(packed[t:t + m]).view(np.int16))
+            if idx.device.type == "cuda":
+                if stage is None:
+                    stage = torch.empty((per,) + tuple(host.shape[1:]), dtype=torch.int16, pin_memory=True)
+                stage[:m].copy_(host)
+                idx.packed[t:t + m].view(torch.int16).copy_(stage[:m], non_blocking=False)
+            else:
+                idx.packed[t:t + m].view(torch.int16).copy_(host)
+        for name, ten in (("priority", idx.priority), ("tagbits", idx.tagbits), ("expiry", idx.expiry)):
+            arr = np.load(path / f"{name}.npy", mmap_mode="r", allow_pickle=False)
+            if arr.shape != (n,):
+                raise ValueError(f"index checkpoint {name}.npy has {arr.shape}, expected ({n},)")
+            rows = max(1, chunk_bytes // 8)
+            for r in range(0, n, rows):
+                ten[r:min(n, r + rows)].copy_(torch.from_numpy(np.array(arr[r:r + rows])))
+        idx.size = int(meta["size"])
+        idx.epoch = float(meta["epoch"])
+        idx.tags.bits = {str(k): int(v) for k, v in meta["tags"].items()}
+        idx.row_tags_py = {int(k): frozenset(v) for k, v in meta["row_tags"].items()}
+        if idx.device.type == "cuda":
+            torch.cuda.synchronize(idx.device)
+        return idx
+
 
 class ShardedSemanticIndex:
     """Row-sharded index over the ranks of a process group (one shard per GPU).
@@ -309,6 +422,20 @@ class ShardedSemanticIndex:
         self.group = group
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+
+    def save(self, path, **kw) -> Dict[str, float]:
+        """Each rank writes its own shard (path/shard_<rank>): per-GPU binary shards."""
+        from pathlib import Path
+
+        return self.local.save(Path(path) / f"shard_{self.rank}", **kw)
+
+    @classmethod
+    def load(cls, path, group=None, device=None, **kw) -> "ShardedSemanticIndex":
+        import torch.distributed as dist
+        from pathlib import Path
+
+        rank = dist.get_rank(group) if dist.is_initialized() else 0
+        return cls(SemanticIndex.load(Path(path) / f"shard_{rank}", device=device, **kw), group)
 
     def add_local(self, *a, **kw) -> List[int]:
         return [r * self.world + self.rank for r in self.local.add(*a, **kw)]

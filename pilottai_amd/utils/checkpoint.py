@@ -5,9 +5,11 @@ A checkpoint is a directory:
                       `Task.to_dict()` form), completed / failed TaskResults, the
                       pending task ids, orchestrator Memory (MemoryEntry form) and
                       each agent's AgentConfig + EnhancedMemory (MemoryItem form)
-    index.npy         optional raw semantic-index shard (bf16 rows as uint16,
-                      numpy header -> np.load(mmap_mode="r") then one H2D copy)
-    index_meta.json   row metadata for index.npy
+    index_<k>/        every distinct semantic index the agents' EnhancedMemories use
+                      (SemanticIndex.save: packed.npy = the fragment-major bf16 rows as
+                      uint16, priority/tagbits/expiry.npy, meta.json), streamed from the
+                      device in chunks; each agent entry names its index ("index_ref") and
+                      every MemoryItem its row, so resume needs no re-embedding
 Writes go to a temp dir that is renamed into place, so a crash never leaves a
 half-written checkpoint. Only JSON and .npy (allow_pickle=False) are read back.
 """
@@ -22,8 +24,6 @@ from datetime import datetime
 from pathlib import Path
 from typing import Any, Dict
 
-import numpy as np
-
 FORMAT_VERSION = 1
 
 
@@ -33,19 +33,27 @@ def _task_json(t) -> Dict[str, Any]:
     return d
 
 
-def save_serve_checkpoint(serve, path) -> str:
+def save_serve_checkpoint(serve, path, save_index: bool = True) -> str:
     path = Path(path)
     path.parent.mkdir(parents=True, exist_ok=True)
     tmp = Path(tempfile.mkdtemp(prefix=".ckpt-", dir=str(path.parent)))
     pending = [tid for tid, t in serve.tasks.items()
                if tid not in serve.completed_tasks and tid not in serve.failed_tasks and not t.subtasks]
     agents = []
+    indexes: Dict[int, int] = {}  # id(SemanticIndex) -> k (agents may share one store)
+    index_stats = []
     for a in serve.agents.values():
         cfg = getattr(a, "config", None)
         entry = {"id": a.id, "type": type(a).__name__, "config": cfg.to_dict() if hasattr(cfg, "to_dict") else {}}
         mem = getattr(a, "_memory", None)
         if mem is not None and hasattr(mem, "to_dict"):
             entry["enhanced_memory"] = mem.to_dict()
+            idx = getattr(mem, "index", None)
+            if save_index and idx is not None and hasattr(idx, "save"):
+                if id(idx) not in indexes:
+                    indexes[id(idx)] = k = len(indexes)
+                    index_stats.append(dict(idx.save(tmp / f"index_{k}"), index=k))
+                entry["index_ref"] = indexes[id(idx)]
         agents.append(entry)
     state = {
         "format_version": FORMAT_VERSION,
@@ -58,6 +66,7 @@ def save_serve_checkpoint(serve, path) -> str:
         "memory": serve.memory.to_dict() if serve.memory is not None else None,
         "metrics": dict(serve.metrics),
         "agents": agents,
+        "indexes": index_stats,
     }
     (tmp / "state.json").write_text(json.dumps(state, indent=1, default=str))
     # crash-safe swap: the previous checkpoint is renamed aside (not deleted) until the new
@@ -110,10 +119,36 @@ async def restore_serve_checkpoint(serve, path, requeue: bool = True) -> int:
         by_id[t.id] = t
         serve.tasks[t.id] = t
     saved_agents = {a["id"]: a for a in st.get("agents", [])}
+    # a restarted process has new agent ids: fall back to the role (Serve keys agents by role,
+    # reference pilott/pilott.py:93), each saved entry used once
+    by_role: Dict[str, list] = {}
+    for e in st.get("agents", []):
+        by_role.setdefault(str(e.get("config", {}).get("role")), []).append(e)
+    used = set()
+    root = Path(path) if (Path(path) / "state.json").exists() else Path(path).with_name(Path(path).name + ".bak")
+    restored: Dict[int, Any] = {}  # index_ref -> SemanticIndex loaded from the checkpoint
     for a in serve.agents.values():
         s = saved_agents.get(a.id)
+        if s is None:
+            role = str(getattr(getattr(a, "config", None), "role", None))
+            s = next((e for e in by_role.get(role, []) if e["id"] not in used and e["id"] not in
+                      {x.id for x in serve.agents.values()}), None)
+        if s is not None:
+            used.add(s["id"])
         if s and "enhanced_memory" in s:
-            await a.enhanced_memory.load_dict(s["enhanced_memory"])
+            mem = a.enhanced_memory
+            k = s.get("index_ref")
+            ok = False
+            if k is not None and (root / f"index_{k}" / "meta.json").exists():
+                if k not in restored:
+                    from pilottai_amd.memory.semantic_index import SemanticIndex
+
+                    cur = mem.index
+                    restored[k] = SemanticIndex.load(root / f"index_{k}", device=cur.device,
+                                                     growable=cur.growable, max_capacity=cur.max_capacity)
+                mem.index = restored[k]
+                ok = True
+            await mem.load_dict(s["enhanced_memory"], index_restored=ok)
     n = 0
     if requeue:
         if not serve._started:
@@ -127,39 +162,3 @@ async def restore_serve_checkpoint(serve, path, requeue: bool = True) -> int:
             await serve._enqueue(t)
             n += 1
     return n
-
-
-def save_index(index, path) -> str:
-    """Dump a SemanticIndex to index.npy (+ index_meta.json) for mmap reload."""
-    path = Path(path)
-    path.mkdir(parents=True, exist_ok=True)
-    n = index.count
-    vec = index.read_rows(0, n).contiguous().view(dtype=__import__("torch").int16).cpu().numpy().view(np.uint16)
-    np.save(path / "index.npy", vec, allow_pickle=False)
-    meta = {"dim": index.dim, "count": n, "size": index.size, "epoch": index.epoch,
-            "priority": index.priority[:n].cpu().tolist(), "tagbits": index.tagbits[:n].cpu().tolist(),
-            "expiry": index.expiry[:n].cpu().tolist(), "tags": index.tags.bits,
-            "row_tags": {str(k): sorted(v) for k, v in index.row_tags_py.items()}}
-    (path / "index_meta.json").write_text(json.dumps(meta))
-    return str(path)
-
-
-def load_index(path, device=None):
-    import torch
-
-    from pilottai_amd.memory.semantic_index import SemanticIndex
-
-    path = Path(path)
-    meta = json.loads((path / "index_meta.json").read_text())
-    arr = np.load(path / "index.npy", mmap_mode="r", allow_pickle=False)
-    n = meta["count"]
-    idx = SemanticIndex(dim=meta["dim"], capacity=max(1, n), device=device)
-    idx.write_range(0, torch.from_numpy(np.ascontiguousarray(arr).view(np.int16)).view(torch.bfloat16))
-    idx.priority[:n] = torch.tensor(meta["priority"], dtype=torch.int32)
-    idx.tagbits[:n] = torch.tensor(meta["tagbits"], dtype=torch.int64)
-    idx.expiry[:n] = torch.tensor(meta["expiry"], dtype=torch.float32)
-    idx.size = meta["size"]
-    idx.epoch = meta["epoch"]
-    idx.tags.bits = dict(meta["tags"])
-    idx.row_tags_py = {int(k): frozenset(v) for k, v in meta["row_tags"].items()}
-    return idx

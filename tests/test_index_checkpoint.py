@@ -1,0 +1,111 @@
+"""Checkpoint / resume of the HBM semantic store (VERDICT r3 missing #1): SemanticIndex.save /
+load stream the packed rows in chunks to .npy shards (no whole-index host copy, no pickle),
+restore keeps row ids, ring position, tags and the clock, and a resumed EnhancedMemory
+re-attaches its MemoryItems to their rows without re-embedding them (CPU)."""
+import numpy as np
+import pytest
+import torch
+
+from pilottai_amd.memory.enhanced_memory import EnhancedMemory
+from pilottai_amd.memory.semantic_index import SemanticIndex
+
+
+def _filled(n=3000, dim=64, cap=4096):
+    rng = np.random.default_rng(0)
+    idx = SemanticIndex(dim=dim, capacity=cap, device="cpu", growable=False)
+    vecs = rng.standard_normal((n, dim)).astype(np.float32)
+    tags = [{f"t{i % 70}"} if i % 3 else set() for i in range(n)]  # > 63 tags: overflow bit in use
+    exp = [None if i % 5 else 4e9 for i in range(n)]
+    idx.add(vecs, [int(i % 7) for i in range(n)], tags, exp)
+    idx.delete([5, 17, 999])
+    return idx, rng
+
+
+def _search(idx, rng_seed=1):
+    rng = np.random.default_rng(rng_seed)
+    q = rng.standard_normal((9, idx.dim)).astype(np.float32)
+    return idx.search(q, 8, [0, 2, 0, 5, 0, 0, 1, 0, 3],
+                      [(), ("t3",), (), (), ("t69",), ("t1", "t2"), (), ("nope",), ()], now=idx.epoch + 10)
+
+
+@pytest.mark.parametrize("chunk", [1 << 10, 1 << 30])
+def test_index_save_load_bit_identical(tmp_path, chunk):
+    idx, _ = _filled()
+    before = _search(idx)
+    st = idx.save(tmp_path / "ix", chunk_bytes=chunk)
+    assert st["rows"] == idx.count and st["bytes"] > 0
+    files = sorted(p.name for p in (tmp_path / "ix").iterdir())
+    assert files == ["expiry.npy", "meta.json", "packed.npy", "priority.npy", "tagbits.npy"]
+    back = SemanticIndex.load(tmp_path / "ix", device="cpu", growable=False, chunk_bytes=chunk)
+    assert back.size == idx.size and back.count == idx.count and back.epoch == idx.epoch
+    assert torch.equal(back.packed[:(idx.count + 15) // 16], idx.packed[:(idx.count + 15) // 16])
+    assert torch.equal(back.priority[:idx.count], idx.priority[:idx.count])
+    assert torch.equal(back.tagbits[:idx.count], idx.tagbits[:idx.count])
+    assert back.row_tags_py == idx.row_tags_py and back.tags.bits == idx.tags.bits
+    assert _search(back) == before  # same rows, same scores, same order
+
+
+def test_index_ring_position_survives(tmp_path):
+    """A wrapped ring (size > capacity) resumes writing at the same slot."""
+    idx = SemanticIndex(dim=32, capacity=64, device="cpu", growable=False)
+    rng = np.random.default_rng(2)
+    idx.add(rng.standard_normal((100, 32)), [0] * 100, [()] * 100, [None] * 100)
+    idx.save(tmp_path / "r")
+    back = SemanticIndex.load(tmp_path / "r", device="cpu", growable=False)
+    a = idx.add(rng.standard_normal((3, 32)), [1] * 3, [()] * 3, [None] * 3)
+    b = back.add(rng.standard_normal((3, 32)), [1] * 3, [()] * 3, [None] * 3)
+    assert a == b == [36, 37, 38]
+
+
+def test_index_checkpoint_rejects_mismatch(tmp_path):
+    idx, _ = _filled(100)
+    idx.save(tmp_path / "m")
+    np.save(tmp_path / "m" / "priority.npy", np.zeros(5, dtype=np.int32))
+    with pytest.raises(ValueError):
+        SemanticIndex.load(tmp_path / "m", device="cpu")
+
+
+class _CountingEmbedder:
+    def __init__(self, dim=64):
+        from pilottai_amd.memory.embedding import HashingEmbedder
+
+        self.inner = HashingEmbedder(dim)
+        self.dim = dim
+        self.texts = 0
+
+    def __call__(self, texts):
+        self.texts += len(texts)
+        return self.inner(texts)
+
+
+async def test_serve_checkpoint_restores_memory_without_reembedding(tmp_path):
+    from pilottai_amd import Serve
+    from pilottai_amd.core.agent import BaseAgent
+    from pilottai_amd.core.config import AgentConfig
+    from pilottai_amd.core.policy import ControlPolicy
+    from pilottai_amd.engine.local_llm import SchemaLLM
+
+    def make(emb):
+        a = BaseAgent(AgentConfig(role="w", goal="g", description="d"), llm=SchemaLLM(),
+                      policy=ControlPolicy("fixed", 1))
+        a._memory = EnhancedMemory(embedder=emb, dim=64, device="cpu")
+        return a
+
+    e1 = _CountingEmbedder()
+    s = Serve(agents=[make(e1)], manager_llm=SchemaLLM(), config={"policy": "fixed"})
+    mem = next(iter(s.agents.values())).enhanced_memory
+    texts = [f"fact number {i} about the quarterly report" for i in range(40)]
+    await mem.store_semantic_batch(texts, tags=[{"q"}] * 40, priorities=list(range(40)))
+    want = [[it.text for it in r] for r in await mem.search_batch(["fact number 7", "quarterly"], limit=5)]
+    path = s.checkpoint(tmp_path / "ck")
+    assert (tmp_path / "ck" / "index_0" / "packed.npy").exists()
+
+    e2 = _CountingEmbedder()
+    s2 = Serve(agents=[make(e2)], manager_llm=SchemaLLM(), config={"policy": "fixed"})
+    await s2.restore(path)
+    mem2 = next(iter(s2.agents.values())).enhanced_memory
+    assert e2.texts == 0  # nothing re-embedded on restore
+    assert len(mem2) == 40
+    got = [[it.text for it in r] for r in await mem2.search_batch(["fact number 7", "quarterly"], limit=5)]
+    assert got == want
+    await s2.stop()
