@@ -133,7 +133,7 @@ __global__ __launch_bounds__(WT * WK * 64) void stream_gemm_kernel(const Args A)
   constexpr int XCH = WK * MT * 128;   // x bytes per chunk (LDS slot)
   constexpr int XU = WK * MT * 8;      // 16-B units per chunk
   constexpr int LX = (XU + NTH - 1) / NTH;  // x loads per thread per chunk (duplicates wrap)
-  static_assert(D == 2 || D == 4 || D == 6 || D == 8, "even ring depth (LDS slot = chunk & 1)");
+  static_assert(D == 2 || D == 4 || D == 8 || D == 16, "even ring depth (LDS slot = chunk & 1)");
   // one LDS object only (guide §5 trap 4a): [2 x-slots][row sums of squares][flag]
   __shared__ __attribute__((aligned(1024))) char smem[2 * XCH + MT * 4 + 16];
   float* rsq = reinterpret_cast<float*>(smem + 2 * XCH);
@@ -359,6 +359,8 @@ static bool launch_d(const Args& a, int D, int grid, hipStream_t st) {
   switch (D) {
     case 2: hipLaunchKernelGGL((stream_gemm_kernel<MG, TPW, WT, WK, 2>), dim3(grid), dim3(WT * WK * 64), 0, st, a); return true;
     case 4: hipLaunchKernelGGL((stream_gemm_kernel<MG, TPW, WT, WK, 4>), dim3(grid), dim3(WT * WK * 64), 0, st, a); return true;
+    case 8: hipLaunchKernelGGL((stream_gemm_kernel<MG, TPW, WT, WK, 8>), dim3(grid), dim3(WT * WK * 64), 0, st, a); return true;
+    case 16: hipLaunchKernelGGL((stream_gemm_kernel<MG, TPW, WT, WK, 16>), dim3(grid), dim3(WT * WK * 64), 0, st, a); return true;
     default: return false;
   }
 }

@@ -6,14 +6,21 @@ KV cache, and is hipGraph-capturable: every device-side shape is fixed by the
 token bucket, all per-step metadata lives in one device buffer that the host
 refreshes with a single H2D copy.
 
-Per layer:  fused_add_rmsnorm -> QKV GEMM (hipBLASLt) -> RoPE + paged KV write
-(HIP) -> paged GQA attention (HIP, MFMA) -> O GEMM [TP all-reduce] ->
-fused_add_rmsnorm -> gate_up GEMM -> SwiGLU (HIP) -> down GEMM [TP all-reduce].
+Per layer on the packed-weight paths (every step of a Llama-3 model that fits two weight
+copies; decode / mid / prefill by step size, see forward()):
+  QKV projection (RMSNorm folded into the weights, RoPE + paged KV write in the epilogue)
+  -> paged GQA attention (csrc/ops/attention.hip, MFMA) -> O projection (+ residual, next
+  norm's row statistics) [TP: all-reduce] -> gate_up (norm folded, SwiGLU epilogue)
+  -> down (+ residual, statistics) [TP: all-reduce]
+all on hand-written gfx950 kernels (gemm_decode / gemm_stream / gemm_mid / gemm_prefill .hip).
+The unpacked fallback (models too large for a second weight copy, e.g. 70B at TP=1) runs
+rmsnorm -> library GEMM -> rope_cache -> attention -> GEMM -> add-norm -> GEMM -> SwiGLU -> GEMM.
 
 Tensor parallelism: QKV and gate_up are column-parallel,
 O and down are row-parallel followed by an all-reduce over RCCL/xGMI, the
 embedding and LM head are vocab-parallel; sampling picks the global winner from
-per-shard Gumbel keys (engine/sampler.py), so TP=8 emits exactly the TP=1 token.
+per-shard Gumbel keys (csrc/ops/sampling.hip via engine/engine.py), so TP=8 emits
+exactly the TP=1 token.
 """
 from __future__ import annotations
 

@@ -747,7 +747,14 @@ class NodeManager:
         return p
 
     def executions_by_rank(self) -> Dict[int, int]:
-        out: Dict[int, int] = {}
-        for aid, r in self.rank_of.items():
-            out.setdefault(r, 0)
+        """Finished tasks (completed or failed) per rank, from the agent each task last ran on
+        (Serve records it in task.metadata["_agent_id"]); every rank with agents appears."""
+        out: Dict[int, int] = {r: 0 for r in self.rank_of.values()}
+        done = set(self.serve.completed_tasks) | set(self.serve.failed_tasks)
+        for tid in done:
+            t = self.serve.tasks.get(tid)
+            aid = t.metadata.get("_agent_id") if t is not None else None
+            if aid is not None and aid in self.rank_of:
+                r = self.rank_of[aid]
+                out[r] = out.get(r, 0) + 1
         return out

@@ -94,6 +94,7 @@ async def _rank0(world: int, port: int, scenario: str, per_rank: int, n_tasks: i
                                         for a in agents)
             out["llm_calls_by_rank"] = {str(k): v for k, v in serve._manager_llm.calls_by_rank.items()}
             out["agents_after"] = len(serve.agents)
+            out["executions_by_rank"] = {str(k): v for k, v in node.executions_by_rank().items()}
         elif scenario == "lb_move":
             p1 = next(p for p in node.proxies.values() if p.rank == 1)
             p2 = next(p for p in node.proxies.values() if p.rank == 2)

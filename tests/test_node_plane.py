@@ -23,6 +23,9 @@ def test_skewed_submission_is_balanced_over_ranks(world):
     assert len(per_rank) == world
     assert max(per_rank) - min(per_rank) <= 1, per_rank
     assert r["ranks"][-1]["forwarded_ok"] == world  # the forwarded half all came back
+    # the manager's per-rank execution count (NodeManager.executions_by_rank) agrees with what
+    # every rank itself executed
+    assert [r["executions_by_rank"][str(k)] for k in range(world)] == per_rank, r["executions_by_rank"]
     assert len(r["llm_calls_by_rank"]) >= world // 2, r["llm_calls_by_rank"]
 
 

@@ -71,7 +71,7 @@ def plans_for(M, N, K, epi):
     rgs = [(mg, (M + 16 * mg - 1) // (16 * mg))]
     out = []
     tiles, KS = N // 16, K // 32
-    for (mg_, rg), (tpw, wt, wk), S, D in itertools.product(rgs, WAVE_SHAPES, (1, 2, 4, 7, 8, 14, 16), (2, 4)):
+    for (mg_, rg), (tpw, wt, wk), S, D in itertools.product(rgs, WAVE_SHAPES, (1, 2, 4, 7, 8, 14, 16), (2, 4, 8, 16)):
         CT = tpw * wt
         if tiles % CT or (epi == "silu" and CT % 2) or KS % S or (KS // S) % (2 * wk):
             continue
