@@ -83,7 +83,8 @@ int pa_car_close(void* p);
 int pa_car_free(void* p);
 int pa_car_all_reduce(void* const* bases, int W, int rank0, int nranks_local, const void* const* ins,
                       void* const* outs, long long nelem, long long cap_bytes, uint32_t* epochs, int* err,
-                      int two_shot, hipStream_t st);
+                      int two_shot, const void* const* resids, float* const* ss, float* const* ss_zero,
+                      int row_len, hipStream_t st);
 }
 
 namespace {
@@ -781,7 +782,8 @@ int64_t car_open(py::bytes handle) {
 
 void car_all_reduce(std::vector<int64_t> bases, int64_t rank0, std::vector<at::Tensor> ins,
                     std::vector<at::Tensor> outs, int64_t cap_bytes, at::Tensor epochs, at::Tensor err,
-                    bool two_shot) {
+                    bool two_shot, std::vector<at::Tensor> resids, std::vector<at::Tensor> ss,
+                    std::vector<at::Tensor> ss_zero, int64_t row_len) {
   const int W = (int)bases.size();
   const int nl = (int)ins.size();
   TORCH_CHECK(W >= 2 && W <= 8, "custom all-reduce supports 2..8 ranks");
@@ -801,9 +803,38 @@ void car_all_reduce(std::vector<int64_t> bases, int64_t rank0, std::vector<at::T
   check_gpu(epochs, "epochs"); check_dtype(epochs, at::kInt, "epochs");
   TORCH_CHECK(epochs.numel() >= (int64_t)nl * pa_car_group(), "epochs too short");
   check_gpu(err, "err"); check_dtype(err, at::kInt, "err");
+  // fused residual epilogue: out = resid + sum, ss[row] += sum(out^2), ss_zero <- 0
+  std::vector<const void*> rp;
+  std::vector<float*> sp, zp;
+  const bool fused = !resids.empty();
+  if (fused) {
+    TORCH_CHECK((int)resids.size() == nl, "one resid per local rank");
+    TORCH_CHECK(row_len > 0 && n % row_len == 0 && (row_len / 8) % 256 == 0 && row_len % 8 == 0,
+                "fused all-reduce needs whole rows of a multiple of 2048 elements");
+    const int64_t rows = n / row_len;
+    for (int i = 0; i < nl; ++i) {
+      check_gpu(resids[i], "resid"); check_dtype(resids[i], at::kBFloat16, "resid");
+      TORCH_CHECK(resids[i].numel() == n && resids[i].is_contiguous() && ((uintptr_t)resids[i].data_ptr() & 15) == 0,
+                  "resid must match the message, contiguous and 16-byte aligned");
+      rp.push_back(resids[i].data_ptr());
+    }
+    TORCH_CHECK(ss.empty() || (int)ss.size() == nl, "one ss per local rank");
+    TORCH_CHECK(ss_zero.empty() || (int)ss_zero.size() == nl, "one ss_zero per local rank");
+    for (auto& t : ss) {
+      check_gpu(t, "ss"); check_dtype(t, at::kFloat, "ss");
+      TORCH_CHECK(t.numel() >= rows, "ss shorter than the message's rows");
+      sp.push_back(t.data_ptr<float>());
+    }
+    for (auto& t : ss_zero) {
+      check_gpu(t, "ss_zero"); check_dtype(t, at::kFloat, "ss_zero");
+      TORCH_CHECK(t.numel() >= rows, "ss_zero shorter than the message's rows");
+      zp.push_back(t.data_ptr<float>());
+    }
+  }
   check_rc(pa_car_all_reduce(b.data(), W, (int)rank0, nl, ip.data(), op.data(), n, cap_bytes,
                              reinterpret_cast<uint32_t*>(epochs.data_ptr<int>()), err.data_ptr<int>(),
-                             two_shot ? 1 : 0, cur_stream()),
+                             two_shot ? 1 : 0, fused ? rp.data() : nullptr, sp.empty() ? nullptr : sp.data(),
+                             zp.empty() ? nullptr : zp.data(), (int)row_len, cur_stream()),
            "custom all-reduce");
 }
 
@@ -901,7 +932,10 @@ PYBIND11_MODULE(_C, m) {
   m.def("car_open", &car_open);
   m.def("car_close", [](int64_t p) { return pa_car_close((void*)(uintptr_t)p); });
   m.def("car_free", [](int64_t p) { return pa_car_free((void*)(uintptr_t)p); });
-  m.def("car_all_reduce", &car_all_reduce);
+  m.def("car_all_reduce", &car_all_reduce, py::arg("bases"), py::arg("rank0"), py::arg("ins"), py::arg("outs"),
+        py::arg("cap_bytes"), py::arg("epochs"), py::arg("err"), py::arg("two_shot"),
+        py::arg("resids") = std::vector<at::Tensor>(), py::arg("ss") = std::vector<at::Tensor>(),
+        py::arg("ss_zero") = std::vector<at::Tensor>(), py::arg("row_len") = 0);
   m.def("car_group", &pa_car_group);
   m.def("car_flag_bytes", &pa_car_flag_bytes);
   m.attr("ATT_PART") = 512;

@@ -49,6 +49,14 @@ struct ArPeers {
 struct ArIO {            // input/output per rank handled by this launch (blockIdx.y)
   const u32x4* in[AR_MAXW];
   u32x4* out[AR_MAXW];
+  // fused residual epilogue (RES): out = resid + sum(in); ss[row] += sum(out^2) over the
+  // written bf16 values (the next RMSNorm's row statistics); ss_zero[0 .. nrows) <- 0 (the
+  // buffer the NEXT fused all-reduce fills, consumed before this launch). resid may alias out.
+  const u32x4* resid[AR_MAXW];
+  float* ss[AR_MAXW];
+  float* ss_zero[AR_MAXW];
+  int row_vec;  // 16-byte vectors per row (hidden / 8); a 4-KiB chunk never straddles rows
+  int nrows;
 };
 
 __device__ __forceinline__ uint32_t* ar_flags(char* base, int which) {
@@ -96,15 +104,49 @@ __device__ __forceinline__ u32x4 pack8(const float* a) {
   return __builtin_bit_cast(u32x4, r);
 }
 
+// sum of squares of the 8 bf16 values of v
+__device__ __forceinline__ float sq8(const u32x4 v) {
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float lo = __uint_as_float(v[i] << 16), hi = __uint_as_float(v[i] & 0xffff0000u);
+    s = fmaf(lo, lo, fmaf(hi, hi, s));
+  }
+  return s;
+}
+
+// one chunk's row statistic: the workgroup's 256 vectors lie in one row (host: row_vec % 256
+// == 0); every thread of the workgroup calls it (sq = 0 past the message end)
+__device__ __forceinline__ void chunk_row_stat(float* ss, long long c, int row_vec, float sq, float* red) {
+  sq = wave_sum(sq);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) red[w] = sq;
+  __syncthreads();
+  if (threadIdx.x == 0) atomicAdd(ss + (c * AR_VPB) / row_vec, red[0] + red[1] + red[2] + red[3]);
+  __syncthreads();
+}
+
 // blockIdx.y selects the rank when several "ranks" share one launch (single-process
 // test mode: rank = rank0 + blockIdx.y, ins/outs indexed by blockIdx.y).
-template <int W, bool TWO>
+// RES: the fused residual epilogue (ArIO.resid / ss / ss_zero): replaces the all-reduce ->
+// h.add_ -> row_sumsq chain of a row-parallel projection under TP with one launch.
+template <int W, bool TWO, bool RES>
 __global__ __launch_bounds__(AR_THREADS) void ar_kernel(ArPeers P, ArIO io, int rank0, long long nvec,
                                                          long long cap_vec, uint32_t* epochs, int* err) {
   const int b = blockIdx.x, t = threadIdx.x;
   const int rank = rank0 + blockIdx.y;
   const u32x4* in = io.in[blockIdx.y];
   u32x4* out = io.out[blockIdx.y];
+  const u32x4* resid = io.resid[blockIdx.y];
+  float* ss = io.ss[blockIdx.y];
+  __shared__ float red[4];
+  if (RES && b == 0 && io.ss_zero[blockIdx.y])
+    for (int i = t; i < io.nrows; i += AR_THREADS) io.ss_zero[blockIdx.y][i] = 0.f;
+  // out = (resid +) sum, rounded to bf16 once; returns the written vector
+  auto finish = [&](float* a, long long v) -> u32x4 {
+    if constexpr (RES) acc8(a, resid[v]);
+    return pack8(a);
+  };
   uint32_t* ep_slot = epochs + blockIdx.y * AR_G + b;
   const uint32_t ep = *ep_slot + 1;
   const long long par_off = (long long)(ep & 1) * cap_vec;
@@ -127,31 +169,46 @@ __global__ __launch_bounds__(AR_THREADS) void ar_kernel(ArPeers P, ArIO io, int 
     // 2) one-shot: every rank sums all W buffers for the chunks this workgroup owns
     for (long long c = b; c < nchunk; c += AR_G) {
       const long long v = c * AR_VPB + t;
-      if (v >= nvec) continue;
-      u32x4 x[W];
+      float sq = 0.f;
+      if (v < nvec) {
+        u32x4 x[W];
 #pragma unroll
-      for (int r = 0; r < W; ++r) x[r] = __builtin_nontemporal_load(data(r) + v);
-      float a[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        for (int r = 0; r < W; ++r) x[r] = __builtin_nontemporal_load(data(r) + v);
+        float a[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
-      for (int r = 0; r < W; ++r) acc8(a, x[r]);  // rank order on every rank: bit-identical results
-      out[v] = pack8(a);
+        for (int r = 0; r < W; ++r) acc8(a, x[r]);  // rank order on every rank: bit-identical results
+        const u32x4 o = finish(a, v);
+        out[v] = o;
+        if constexpr (RES) sq = sq8(o);
+      }
+      if constexpr (RES) {
+        if (ss) chunk_row_stat(ss, c, io.row_vec, sq, red);
+      }
     }
   } else {
     // 2a) reduce-scatter: reduce the chunks this rank owns, write the sum back in place
+    // (with RES the owner adds the residual: h is replicated, so h + sum is the same on every
+    // rank and the gathered chunks are final)
     long long j = 0;
     for (long long c = b; c < nchunk; c += AR_G, ++j) {
       if ((int)(j % W) != rank) continue;
       const long long v = c * AR_VPB + t;
-      if (v >= nvec) continue;
-      u32x4 x[W];
+      float sq = 0.f;
+      if (v < nvec) {
+        u32x4 x[W];
 #pragma unroll
-      for (int r = 0; r < W; ++r) x[r] = __builtin_nontemporal_load(data(r) + v);
-      float a[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        for (int r = 0; r < W; ++r) x[r] = __builtin_nontemporal_load(data(r) + v);
+        float a[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
-      for (int r = 0; r < W; ++r) acc8(a, x[r]);
-      const u32x4 s = pack8(a);
-      __builtin_nontemporal_store(s, mine + v);
-      out[v] = s;
+        for (int r = 0; r < W; ++r) acc8(a, x[r]);
+        const u32x4 s = finish(a, v);
+        __builtin_nontemporal_store(s, mine + v);
+        out[v] = s;
+        if constexpr (RES) sq = sq8(s);
+      }
+      if constexpr (RES) {
+        if (ss) chunk_row_stat(ss, c, io.row_vec, sq, red);
+      }
     }
     ar_stores_done();
     __syncthreads();
@@ -162,7 +219,15 @@ __global__ __launch_bounds__(AR_THREADS) void ar_kernel(ArPeers P, ArIO io, int 
       const int owner = (int)(j % W);
       if (owner == rank) continue;
       const long long v = c * AR_VPB + t;
-      if (v < nvec) out[v] = __builtin_nontemporal_load(data(owner) + v);
+      float sq = 0.f;
+      if (v < nvec) {
+        const u32x4 o = __builtin_nontemporal_load(data(owner) + v);
+        out[v] = o;
+        if constexpr (RES) sq = sq8(o);
+      }
+      if constexpr (RES) {
+        if (ss) chunk_row_stat(ss, c, io.row_vec, sq, red);
+      }
     }
   }
   if (t == 0) *ep_slot = ep;
@@ -210,29 +275,42 @@ int pa_car_free(void* p) { return hipFree(p) == hipSuccess ? 0 : -1; }
 // nranks_local: ranks handled by this launch — 1 in real use; up to W in the
 // single-process test, where ranks rank0.. share one launch (ins/outs per rank,
 // epochs holds nranks_local x AR_G counters).
+// resids / ss / ss_zero (nullable): the fused residual epilogue (ArIO); row_len = hidden size.
 int pa_car_all_reduce(void* const* bases, int W, int rank0, int nranks_local, const void* const* ins,
                       void* const* outs, long long nelem, long long cap_bytes, uint32_t* epochs, int* err,
-                      int two_shot, hipStream_t st) {
+                      int two_shot, const void* const* resids, float* const* ss, float* const* ss_zero,
+                      int row_len, hipStream_t st) {
   if (W < 2 || W > AR_MAXW || nelem % 8 || nelem * 2 > cap_bytes || nranks_local < 1 ||
       rank0 + nranks_local > W)
     return -1;
+  const bool res = resids != nullptr;
+  if (res && (row_len <= 0 || (row_len / 8) % AR_VPB || row_len % 8 || nelem % row_len)) return -1;
   ArPeers P;
   for (int i = 0; i < AR_MAXW; ++i) P.base[i] = i < W ? (char*)bases[i] : nullptr;
   const long long nvec = nelem / 8, cap_vec = cap_bytes / 16;
   dim3 grid(AR_G, nranks_local);
   ArIO io;
   for (int i = 0; i < AR_MAXW; ++i) {
-    io.in[i] = i < nranks_local ? (const u32x4*)ins[i] : nullptr;
-    io.out[i] = i < nranks_local ? (u32x4*)outs[i] : nullptr;
+    const bool on = i < nranks_local;
+    io.in[i] = on ? (const u32x4*)ins[i] : nullptr;
+    io.out[i] = on ? (u32x4*)outs[i] : nullptr;
+    io.resid[i] = on && res ? (const u32x4*)resids[i] : nullptr;
+    io.ss[i] = on && res && ss ? ss[i] : nullptr;
+    io.ss_zero[i] = on && res && ss_zero ? ss_zero[i] : nullptr;
   }
-#define AR_LAUNCH(WW)                                                                                      \
-  case WW:                                                                                                 \
-    if (two_shot)                                                                                          \
-      hipLaunchKernelGGL((ar_kernel<WW, true>), grid, dim3(AR_THREADS), 0, st, P, io, rank0, nvec,  \
-                         cap_vec, epochs, err);                                                            \
-    else                                                                                                   \
-      hipLaunchKernelGGL((ar_kernel<WW, false>), grid, dim3(AR_THREADS), 0, st, P, io, rank0, nvec, \
-                         cap_vec, epochs, err);                                                            \
+  io.row_vec = res ? row_len / 8 : 0;
+  io.nrows = res ? (int)(nelem / row_len) : 0;
+#define AR_KERN(WW, TT, RR) \
+  hipLaunchKernelGGL((ar_kernel<WW, TT, RR>), grid, dim3(AR_THREADS), 0, st, P, io, rank0, nvec, cap_vec, epochs, err)
+#define AR_LAUNCH(WW)                        \
+  case WW:                                   \
+    if (two_shot) {                          \
+      if (res) AR_KERN(WW, true, true);      \
+      else AR_KERN(WW, true, false);         \
+    } else {                                 \
+      if (res) AR_KERN(WW, false, true);     \
+      else AR_KERN(WW, false, false);        \
+    }                                        \
     break;
   switch (W) {
     AR_LAUNCH(2)
@@ -246,6 +324,7 @@ int pa_car_all_reduce(void* const* bases, int W, int rank0, int nranks_local, co
       return -1;
   }
 #undef AR_LAUNCH
+#undef AR_KERN
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

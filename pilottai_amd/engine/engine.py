@@ -23,7 +23,8 @@ owns requests, the scheduler, grammars and the tokenizer. Each step it sends a
 7-int header over a gloo group, then broadcasts the step metadata it already
 holds on the device (one RCCL broadcast); the other ranks sit in `follow()`,
 replay the same hipGraph, and take part in the row-parallel all-reduces and
-the vocab-parallel sampling all-gather inside it. Their schedulers stay idle, so
+the vocab-parallel sampling collectives inside it (all-gather of per-shard winners; top-k /
+top-p thresholds from all-reduced radix histograms, engine/tp_sampling.py). Their schedulers stay idle, so
 nothing on the host has to be kept consistent between ranks.
 """
 from __future__ import annotations
@@ -42,6 +43,7 @@ import numpy as np
 import torch
 
 from pilottai_amd import ops
+from pilottai_amd.engine.tp_sampling import tp_topkp_threshold
 from pilottai_amd.models.llama import KVCache, LlamaModel, StepMeta, get_config
 from pilottai_amd.parallel.comm import TPGroup
 from pilottai_amd.utils.tracing import trace_range
@@ -395,11 +397,16 @@ class LLMEngine:
                                     embed=(self._embed_rows, self._embed_pool) if embed else None)
         tau = None
         if trunc:
-            # exact top-k / top-p threshold on the full vocabulary (TP: all-gathered)
-            full = logits if self.tp.size == 1 else self.tp.all_gather(logits)
-            tau = ops.topkp_threshold(full, self.model_cfg.vocab_size, self._temp[:s_b], self._top_k[:s_b],
-                                      self._top_p[:s_b], self._mask_cls[:s_b], self._class_masks,
-                                      out=self._tau[:s_b])
+            # exact top-k / top-p threshold on the full vocabulary; under TP from all-reduced
+            # per-shard radix histograms (engine/tp_sampling.py), not an all-gather of the logits
+            if self.tp.size == 1:
+                tau = ops.topkp_threshold(logits, self.model_cfg.vocab_size, self._temp[:s_b], self._top_k[:s_b],
+                                          self._top_p[:s_b], self._mask_cls[:s_b], self._class_masks,
+                                          out=self._tau[:s_b])
+            else:
+                tau = tp_topkp_threshold(logits, self.model.vocab_offset, self.model_cfg.vocab_size,
+                                         self._temp[:s_b], self._top_k[:s_b], self._top_p[:s_b],
+                                         self._mask_cls[:s_b], self._class_masks, self.tp, out=self._tau[:s_b])
         if self.tp.size == 1:
             ops.sample(logits, self._temp[:s_b], self._mask_cls[:s_b], self._class_masks,
                        self._seeds[:s_b], self._offsets[:s_b], self._forced[:s_b],

@@ -458,17 +458,13 @@ class LlamaModel:
                                 queue=meta.att_queue, waves=self.ATT_DECODE_WAVES,
                                 prefetch=L["wo_p"] if pf else None)
             a2 = attn.view(T, H * hd)
-            if tp:
-                o = ops.decode_gemm(a2, L["wo_p"], "plain")
-                self.tp.all_reduce(o)
-                h.add_(o)
+            if tp:  # all-reduce + residual add in one launch (custom_ar.hip RES epilogue)
+                self.tp.all_reduce_add(ops.decode_gemm(a2, L["wo_p"], "plain"), h)
             else:
                 ops.decode_gemm(a2, L["wo_p"], "resid", resid=h, out=h)
             a = ops.decode_gemm(h, L["w13_p"], "silu", norm=True, eps=eps)
             if tp:
-                d = ops.decode_gemm(a, L["w2_p"], "plain")
-                self.tp.all_reduce(d)
-                h.add_(d)
+                self.tp.all_reduce_add(ops.decode_gemm(a, L["w2_p"], "plain"), h)
             else:
                 ops.decode_gemm(a, L["w2_p"], "resid", resid=h, out=h, **self._down_cfg(T))
         if embed is not None:
@@ -516,16 +512,12 @@ class LlamaModel:
                                 prefetch=L["wo_p"] if self.PREFETCH_WEIGHTS and self.device.type == "cuda" else None)
             a2 = attn.view(T, H * hd)
             if tp:
-                o = ops.wide_gemm(a2, L["wo_p"], "plain")
-                self.tp.all_reduce(o)
-                h.add_(o)
+                self.tp.all_reduce_add(ops.wide_gemm(a2, L["wo_p"], "plain"), h)
             else:
                 ops.wide_gemm(a2, L["wo_p"], "resid", resid=h, out=h)
             a = ops.wide_gemm(h, L["w13_p"], "silu", norm=True, eps=eps)
             if tp:
-                d = ops.wide_gemm(a, L["w2_p"], "plain")
-                self.tp.all_reduce(d)
-                h.add_(d)
+                self.tp.all_reduce_add(ops.wide_gemm(a, L["w2_p"], "plain"), h)
             else:
                 ops.wide_gemm(a, L["w2_p"], "resid", resid=h, out=h)
         if embed is not None:
@@ -588,7 +580,8 @@ class LlamaModel:
         The RMSNorm statistics sum(h^2) of each row are produced by the residual epilogue
         that writes h (buffers ss_a / ss_b alternate; each residual launch zeroes the
         buffer the next one fills), so no norm kernel runs. Under TP the row-parallel
-        outputs are all-reduced first and the statistics recomputed (row_sumsq)."""
+        outputs go through TPGroup.all_reduce_add: all-reduce, residual add and the row
+        statistics in one custom all-reduce launch (RCCL + add + row_sumsq as the fallback)."""
         cfg = self.cfg
         H, KVh, hd = self.h_local, self.kv_local, cfg.head_dim
         eps = cfg.rms_eps
@@ -609,19 +602,14 @@ class LlamaModel:
                                 meta.block_table, self.scale, num_seqs=meta.num_seqs, part_size=meta.part_size,
                                 queue=meta.att_queue)
             a2 = attn.view(T, H * hd)
-            if tp:
-                o = self._gemm("o", T, a2, L["wo_p"], "plain")
-                self.tp.all_reduce(o)
-                h.add_(o)
-                ops.row_sumsq(h, out=ss_b)
+            if tp:  # all-reduce + residual + the next norm's row statistics in one launch;
+                # ss_b was zeroed by the previous down all-reduce (or above), ss_a is zeroed here
+                self.tp.all_reduce_add(self._gemm("o", T, a2, L["wo_p"], "plain"), h, ss=ss_b, ss_zero=ss_a)
             else:  # ss_b was zeroed by the previous down launch (or above)
                 self._gemm("o", T, a2, L["wo_p"], "resid", resid=h, out=h, ss_out=ss_b, ss_zero=ss_a)
             a = self._gemm("gate_up", T, h, L["w13_p"], "silu", norm=True, eps=eps, ss_in=ss_b)
             if tp:
-                d = self._gemm("down", T, a, L["w2_p"], "plain")
-                self.tp.all_reduce(d)
-                h.add_(d)
-                ops.row_sumsq(h, out=ss_a)
+                self.tp.all_reduce_add(self._gemm("down", T, a, L["w2_p"], "plain"), h, ss=ss_a, ss_zero=ss_b)
             else:
                 self._gemm("down", T, a, L["w2_p"], "resid", resid=h, out=h, ss_out=ss_a, ss_zero=ss_b)
         if embed is not None:

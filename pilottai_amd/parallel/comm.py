@@ -44,6 +44,37 @@ class TPGroup:
             dist.all_reduce(t, group=self.group)
         return t
 
+    def all_reduce_add(self, t: torch.Tensor, resid: torch.Tensor, ss: Optional[torch.Tensor] = None,
+                       ss_zero: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """resid += all_reduce(t) (in place); ss[:rows] <- row sums of squares of the new resid
+        (ss must hold zeros on entry), ss_zero[:rows] <- 0. One fused launch on the custom
+        all-reduce (csrc/ops/custom_ar.hip, RES epilogue); otherwise RCCL / gloo + add + stats."""
+        rows = resid.shape[0]
+        if self.size > 1 and self.custom is not None and self.custom.fusable(t, resid):
+            return self.custom.all_reduce_add(t, resid, ss, ss_zero)
+        self.all_reduce(t)
+        resid.add_(t)
+        if ss is not None:
+            from pilottai_amd import ops
+
+            ops.row_sumsq(resid, out=ss)
+        if ss_zero is not None:
+            ss_zero[:rows].zero_()
+        return resid
+
+    def all_reduce_max(self, t: torch.Tensor) -> torch.Tensor:
+        """In-place elementwise max over the group (any dtype; RCCL / gloo)."""
+        if self.size > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+        return t
+
+    def all_reduce_sum(self, t: torch.Tensor) -> torch.Tensor:
+        """In-place sum over the group through the process group (fp32 histograms etc.; the
+        custom all-reduce is for bf16 activations)."""
+        if self.size > 1:
+            dist.all_reduce(t, group=self.group)
+        return t
+
     def all_gather(self, t: torch.Tensor) -> torch.Tensor:
         """Concatenate `t` from every rank along a new leading dim: [size, *t.shape]."""
         if self.size == 1:

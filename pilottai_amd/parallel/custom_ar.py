@@ -126,6 +126,25 @@ class CustomAllReduce:
         self.calls += 1
         return t
 
+    def all_reduce_add(self, t: torch.Tensor, resid: torch.Tensor, ss: Optional[torch.Tensor] = None,
+                       ss_zero: Optional[torch.Tensor] = None, two_shot: Optional[bool] = None) -> torch.Tensor:
+        """resid += sum over the group of `t` in ONE launch (the row-parallel o / down epilogue
+        under TP): ss[row] += sum of squares of the written bf16 rows (the next RMSNorm's row
+        statistics), ss_zero[:rows] <- 0. Replaces all-reduce -> resid.add_ -> row_sumsq."""
+        if two_shot is None:
+            two_shot = self.world > 2 and t.numel() * 2 > self.two_shot_bytes
+        self.C.car_all_reduce(self.bases, self.rank, [t.reshape(-1)], [resid.reshape(-1)], self.cap_bytes,
+                              self.epochs, self.err, bool(two_shot), resids=[resid.reshape(-1)],
+                              ss=[ss] if ss is not None else [], ss_zero=[ss_zero] if ss_zero is not None else [],
+                              row_len=int(resid.shape[-1]))
+        self.calls += 1
+        return resid
+
+    def fusable(self, t: torch.Tensor, resid: torch.Tensor) -> bool:
+        return (self.eligible(t) and resid.is_contiguous() and resid.numel() == t.numel()
+                and resid.dtype == torch.bfloat16 and resid.data_ptr() % 16 == 0
+                and resid.shape[-1] % 2048 == 0)
+
     def healthy(self) -> bool:
         """False once any barrier timed out (a peer died or stalled); syncs the stream."""
         return int(self.err.item()) == 0
@@ -141,7 +160,9 @@ class CustomAllReduce:
 
 
 def local_group_all_reduce(C, tensors: List[torch.Tensor], cap_bytes: int, two_shot: bool,
-                           state: dict) -> None:
+                           state: dict, resids: Optional[List[torch.Tensor]] = None,
+                           ss: Optional[List[torch.Tensor]] = None, ss_zero: Optional[List[torch.Tensor]] = None,
+                           row_len: int = 0) -> None:
     """Single-process form used by tests: W 'ranks' share one launch on one GPU.
 
     `state` caches the W buffers and epoch counters between calls (keyed by W and cap).
@@ -154,4 +175,8 @@ def local_group_all_reduce(C, tensors: List[torch.Tensor], cap_bytes: int, two_s
         err = torch.zeros(1, dtype=torch.int32, device=tensors[0].device)
         state[key] = (bufs, epochs, err)
     bufs, epochs, err = state[key]
-    C.car_all_reduce(bufs, 0, tensors, tensors, cap_bytes, epochs, err, two_shot)
+    if resids is None:
+        C.car_all_reduce(bufs, 0, tensors, tensors, cap_bytes, epochs, err, two_shot)
+    else:  # fused residual epilogue: resids[r] += sum, row statistics into ss[r]
+        C.car_all_reduce(bufs, 0, tensors, resids, cap_bytes, epochs, err, two_shot, resids=resids,
+                         ss=ss or [], ss_zero=ss_zero or [], row_len=row_len)
