@@ -101,6 +101,11 @@ def parse():
                          "requests in the engine's continuous batch, SURVEY N11)")
     ap.add_argument("--share-gpu", action="store_true",
                     help="rehearsal: every rank on GPU 0 (use with PILOTTAI_DIST_BACKEND=gloo)")
+    ap.add_argument("--hybrid-latency", type=float, default=0.0,
+                    help="hybrid node rehearsal on ONE GPU (VERDICT r3 item 5): rank 0 runs the real engine, "
+                         "the manager Serve, the control plane and all clients; ranks > 0 are CPU processes whose "
+                         "agents answer with model-free schema LLMs after this many seconds per call (the measured "
+                         "per-call latency of an 8-worker GPU rank). Use with PILOTTAI_DIST_BACKEND=gloo.")
     return ap.parse_args()
 
 
@@ -123,6 +128,8 @@ async def run_rank(a, rank: int, world: int, device):
 
     n_local = len(shard_workers(a.workers, world, rank))
     t_init = time.time()
+    if a.hybrid_latency > 0 and rank > 0:
+        return await run_cpu_rank(a, rank, world, n_local)
     memory = lookup = None
     if a.memory_rows > 0:
         # before the engine sizes its KV pool: the index is resident beside the model
@@ -231,6 +238,17 @@ async def run_rank(a, rank: int, world: int, device):
         if serve is not None and not (node and rank > 0):
             await asyncio.gather(*(client(i, n, rec) for i in range(n_clients)))
 
+    lags = []
+
+    async def lag_probe(stop):
+        """Event-loop lag of this rank: how late a 10 ms sleep wakes up (the manager, the plane
+        server, the clients and the engine's delivery callbacks share this loop)."""
+        loop = asyncio.get_running_loop()
+        while not stop.is_set():
+            t = loop.time()
+            await asyncio.sleep(0.01)
+            lags.append(loop.time() - t - 0.01)
+
     if a.warmup > 0:
         await round_(a.warmup, False)
     await coll(comm.barrier)  # worker ranks keep serving the plane meanwhile
@@ -242,7 +260,11 @@ async def run_rank(a, rank: int, world: int, device):
     if device.type == "cuda":
         torch.cuda.synchronize()
     t0 = time.perf_counter()
+    stop_probe = asyncio.Event()
+    probe = asyncio.ensure_future(lag_probe(stop_probe))
     await round_(a.steps, True)
+    stop_probe.set()
+    await probe
     if device.type == "cuda":
         torch.cuda.synchronize()
     await coll(comm.barrier)
@@ -276,8 +298,10 @@ async def run_rank(a, rank: int, world: int, device):
 
         node_load = (await coll(GlobalLoadView().update, local_load(serve)))
     requeued = 0
+    by_rank = None
     if plane is not None:
         requeued = int(serve.metrics.get("requeued_tasks", 0))
+        by_rank = {str(k): v for k, v in mgr.executions_by_rank().items()}
         await serve.stop()
         await plane.stop()
     elif worker is not None:
@@ -289,6 +313,7 @@ async def run_rank(a, rank: int, world: int, device):
     eng.stop()
     local = {
         "dt": dt, "tasks": len(latencies), "lat": latencies, "init_s": init_s, "requeued": requeued,
+        "loop_lag": sorted(lags), "executions_by_rank": by_rank,
         "managers": 1 if serve is not None else 0, "dp_mode": a.dp_mode if world > 1 else "single",
         "tokens": st1["tokens"] - st0["tokens"], "steps": st1["steps"] - st0["steps"],
         "sampled": st1["sampled"] - st0["sampled"], "calls": u1["calls"] - u0["calls"],
@@ -308,6 +333,52 @@ async def run_rank(a, rank: int, world: int, device):
                     for b, v in eng.bucket_hist.items()},
     }
     return local
+
+
+async def run_cpu_rank(a, rank: int, world: int, n_local: int):
+    """--hybrid-latency: a worker rank without a GPU or engine (agents on schema LLMs that
+    answer after a fixed latency), joining rank 0's control plane like a GPU rank does."""
+    from pilottai_amd.core.agent import BaseAgent
+    from pilottai_amd.core.config import AgentConfig
+    from pilottai_amd.core.policy import ControlPolicy
+    from pilottai_amd.engine.local_llm import SchemaLLM
+    from pilottai_amd.parallel import comm
+    from pilottai_amd.parallel.node_plane import PlaneWorker
+    from pilottai_amd.tools.tool import Tool, echo_tool
+
+    t_init = time.time()
+    llm = SchemaLLM(seed=rank, latency_s=a.hybrid_latency)
+    policy = ControlPolicy("fixed", a.steps_per_task)
+    agents = [BaseAgent(AgentConfig(role=f"analyst-{rank}-{i}", goal="Summarize documents and extract key findings",
+                                    max_iterations=a.steps_per_task + 1, task_timeout=900), llm=llm,
+                        tools=[Tool(name="echo", description="identity tool", function=echo_tool, max_retries=1)],
+                        policy=policy)
+              for i in range(n_local)]
+
+    async def coll(fn, *args):
+        return await asyncio.to_thread(fn, *args)
+
+    os.environ["PILOTTAI_PLANE_SECRET"] = await coll(comm.broadcast_object, None)
+    for ag in agents:
+        await ag.start()
+    worker = PlaneWorker(rank, agents, llm=llm)
+    await worker.connect()
+    serving = asyncio.ensure_future(worker.serve_forever())
+    await coll(comm.broadcast_object, None)  # the workload seed
+    init_s = time.time() - t_init
+    await coll(comm.barrier)
+    t0 = time.perf_counter()
+    await coll(comm.barrier)
+    dt = time.perf_counter() - t0
+    await serving
+    for ag in agents:
+        await ag.stop()
+    zero = {k: 0 for k in ("tokens", "steps", "sampled", "busy_s", "prefix_hit", "prefix_defers", "spec_rows",
+                           "spec_voided", "bucket_tokens", "prompt_total", "hbm_used_gb")}
+    return dict(zero, dt=dt, tasks=0, lat=[], init_s=init_s, requeued=0, loop_lag=[], executions_by_rank=None,
+                managers=0, dp_mode="node", calls=len(llm.calls) if hasattr(llm, "calls") else 0, prompt_tokens=0,
+                completion_tokens=0, async_steps=False, host_phases={}, req_lat={}, memory=None, node_load=None,
+                buckets={}, cpu_rank=True)
 
 
 def build_memory(a, device):
@@ -368,7 +439,9 @@ def main():
     rank, world, local_rank = comm.init_distributed()
     if world != a.gpus:
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}: launch one rank per GPU")
-    if a.cpu or not torch.cuda.is_available():
+    if a.hybrid_latency > 0 and rank > 0:
+        device = torch.device("cpu")  # hybrid rehearsal: worker ranks never touch the GPU
+    elif a.cpu or not torch.cuda.is_available():
         device = torch.device("cpu")
         a.cpu = True
     else:
@@ -436,7 +509,7 @@ def main():
             "graph_pad_frac": round(1 - tot("tokens") / max(1, tot("bucket_tokens")), 3),
             # rank 0's engine thread, ms per step: schedule / copy+launch / wait for the device /
             # commit / deliver (the host phases are the device's idle time between steps)
-            "step_phase_ms": {k.replace("_s", ""): round(1000 * v / max(1, gathered[0]["steps"]), 3)
+            "step_phase_ms": {(k[:-2] if k.endswith("_s") else k): round(1000 * v / max(1, gathered[0]["steps"]), 3)
                               for k, v in gathered[0]["host_phases"].items()},
             "ttft_p50_ms": round(lat0.get("ttft_p50_ms") or 0.0, 1),
             "tpot_p50_ms": round(lat0.get("tpot_p50_ms") or 0.0, 2),
@@ -446,6 +519,13 @@ def main():
             "step_buckets": {str(b): [v[0], round(1000 * v[1] / max(1, v[0]), 2)]
                              for b, v in sorted(gathered[0]["buckets"].items()) if v[0] > 0},
             "reply_tokens": a.reply_tokens,
+            # rank 0's event loop (manager, plane server, clients, engine deliveries): lag of a
+            # 10 ms sleep over the timed region
+            "loop_lag_ms": {q: round(1000 * lag[min(len(lag) - 1, int(f * len(lag)))], 2) if lag else None
+                            for q, f, lag in (("p50", 0.5, gathered[0]["loop_lag"]),
+                                              ("p99", 0.99, gathered[0]["loop_lag"]))},
+            "executions_by_rank": gathered[0]["executions_by_rank"],
+            "hybrid_latency_s": a.hybrid_latency or None,
             "memory": gathered[0]["memory"],
             "node_load": gathered[0]["node_load"],
             "notes": "BASELINE.md publishes no number for this config (vs_baseline null); the reference's "
