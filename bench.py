@@ -96,6 +96,9 @@ def parse():
     ap.add_argument("--memory-rows", type=int, default=0,
                     help="semantic memory on the engine's GPU with this many rows; every agent step looks it up")
     ap.add_argument("--memory-top-k", type=int, default=3)
+    ap.add_argument("--memory-min-batch", type=int, default=1,
+                    help="lookups a pass waits for (up to --memory-wait-ms) before it starts")
+    ap.add_argument("--memory-wait-ms", type=float, default=0.0)
     ap.add_argument("--embedder", default="hashing", choices=["hashing", "engine"],
                     help="memory text encoder: feature hashing, or the serving model itself (embedding "
                          "requests in the engine's continuous batch, SURVEY N11)")
@@ -409,7 +412,7 @@ def build_memory(a, device):
         done += m
     if device.type == "cuda":
         torch.cuda.synchronize(device)
-    return mem, MemoryLookupBatcher(mem)
+    return mem, MemoryLookupBatcher(mem, min_batch=a.memory_min_batch, max_wait_s=a.memory_wait_ms / 1000.0)
 
 
 def _launch_ranks(n: int) -> int:

@@ -27,11 +27,18 @@ from .enhanced_memory import EnhancedMemory, MemoryItem
 
 
 class MemoryLookupBatcher:
-    def __init__(self, memory: EnhancedMemory, max_batch: int = 256, time_device: bool = True):
+    def __init__(self, memory: EnhancedMemory, max_batch: int = 256, time_device: bool = True,
+                 min_batch: int = 1, max_wait_s: float = 0.0):
+        """min_batch / max_wait_s: before a pass, wait (in 1 ms sleeps) until `min_batch`
+        queries are pending or the oldest has waited `max_wait_s` — more queries share each
+        streaming pass over the index (whose cost does not depend on the query count up to
+        64), at a bounded latency cost."""
         self.memory = memory
         self.max_batch = max_batch
+        self.min_batch = max(1, int(min_batch))
+        self.max_wait_s = float(max_wait_s)
         self.time_device = time_device
-        self._pending: List[Tuple[str, Optional[Set[str]], int, int, "asyncio.Future"]] = []
+        self._pending: List[Tuple[str, Optional[Set[str]], int, int, "asyncio.Future", float]] = []
         self._writes: List[Tuple[str, Dict[str, Any], Set[str], int, "asyncio.Future"]] = []
         self._flush_scheduled = False
         self._active = False  # a flush task is running (it drains everything pending)
@@ -44,7 +51,7 @@ class MemoryLookupBatcher:
     async def search(self, query: str, limit: int = 5, tags: Optional[Set[str]] = None,
                      min_priority: int = 0) -> List[MemoryItem]:
         fut = asyncio.get_running_loop().create_future()
-        self._pending.append((query, tags, int(min_priority), int(limit), fut))
+        self._pending.append((query, tags, int(min_priority), int(limit), fut, time.perf_counter()))
         self._schedule()
         return await fut
 
@@ -98,6 +105,11 @@ class MemoryLookupBatcher:
                         w[4].set_exception(e)
             self.stats["stores"] += len(writes)
             self.stats["store_batches"] += 1
+        if self._pending and self.min_batch > 1 and self.max_wait_s > 0:
+            while len(self._pending) < self.min_batch and not self._writes and \
+                    time.perf_counter() - self._pending[0][5] < self.max_wait_s:
+                await asyncio.sleep(0.001)
+            self.stats["coalesce_waits"] = self.stats.get("coalesce_waits", 0) + 1
         if self._pending:
             batch, self._pending = self._pending[: self.max_batch], self._pending[self.max_batch:]
             limit = max(b[3] for b in batch)
