@@ -262,6 +262,10 @@ async def run_rank(a, rank: int, world: int, device):
     n_timed0 = len(eng.timings)
     if device.type == "cuda":
         torch.cuda.synchronize()
+    if device.type == "cuda":  # marker kernels: tools/prof_summary.py --between-markers cuts profiles here
+        from pilottai_amd.ops import kernels as _k
+
+        _k.require_native().timeline_marker(0)
     t0 = time.perf_counter()
     stop_probe = asyncio.Event()
     probe = asyncio.ensure_future(lag_probe(stop_probe))
@@ -269,6 +273,7 @@ async def run_rank(a, rank: int, world: int, device):
     stop_probe.set()
     await probe
     if device.type == "cuda":
+        _k.require_native().timeline_marker(1)
         torch.cuda.synchronize()
     await coll(comm.barrier)
     dt = time.perf_counter() - t0

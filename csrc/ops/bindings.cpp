@@ -53,6 +53,7 @@ int pa_mid_gemm(void* y, const void* x, const void* wp, const void* resid, float
                 void* q_out, void* k_cache, void* v_cache, const int* positions, const int* slots,
                 const float* cos_sin, int H, int KV, hipStream_t st);
 int pa_row_sumsq(float* out, const void* x, int M, int K, int ldx, hipStream_t st);
+int pa_timeline_marker(int id, hipStream_t st);
 long long pa_stream_gemm_ws_floats(int M, int N, int K, int mg, int rg, int tpw, int wt, int wk, int S);
 void pa_stream_gemm_plan(int M, int N, int K, int epi, int* plan);
 int pa_stream_gemm(void* y, const void* x, const void* wp, const void* resid, float* ws, long long ws_floats,
@@ -861,6 +862,8 @@ at::Tensor empty_uncached(int64_t numel, at::ScalarType dtype, int64_t device) {
 }
 
 PYBIND11_MODULE(_C, m) {
+  m.def("timeline_marker", [](int64_t id) { check_rc(pa_timeline_marker((int)id, cur_stream()), "timeline_marker"); },
+        "empty marker kernel (0 = begin, 1 = end of a timed region) for profile cutting");
   m.def("empty_uncached", &empty_uncached, py::arg("numel"), py::arg("dtype"), py::arg("device"),
         "zero-filled device tensor in uncached memory (hipDeviceMallocUncached)");
   m.doc() = "pilottai_amd CDNA4 (gfx950) HIP kernels";

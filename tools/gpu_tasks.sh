@@ -55,7 +55,7 @@ for t in "$@"; do
       P=/tmp/pilottai_prof_$WORKERS
       rm -rf "$P" && mkdir -p "$P"
       run "prof_w$WORKERS" 600 rocprofv3 --kernel-trace --stats -d "$P" -o w -- python3 bench.py --steps "$STEPS" --warmup "$WARMUP" --workers "$WORKERS" $BENCH_ARGS || exit $?
-      python3 tools/prof_summary.py "$P"/*/*.db "$P"/*.db --after-frac 0.3 --top 40 > "$OUT/w${WORKERS}_kernels.md" 2>&1 || exit $?
+      python3 tools/prof_summary.py "$P"/*/*.db "$P"/*.db --between-markers --top 40 > "$OUT/w${WORKERS}_kernels.md" 2>&1 || exit $?
       ;;
     splitk) run splitk 900 python -u tools/splitk_check.py --reps "$REPS" --out "$OUT/splitk.jsonl" $SPLITK_ARGS || exit $? ;;
     handoff_cost) run handoff_cost 300 python -u tools/handoff_cost.py --out "$OUT/handoff_cost.jsonl" || exit $? ;;
