@@ -60,7 +60,7 @@ int pa_stream_gemm(void* y, const void* x, const void* wp, const void* resid, fl
                    int* counters, int n_counters, int* err, int M, int N, int K, int ldx, int ldy, int ldr, int epi,
                    const float* ss_in, float* ss_out, float* ss_zero, float eps, const int* plan, void* q_out,
                    void* k_cache, void* v_cache, const int* positions, const int* slots, const float* cos_sin, int H,
-                   int KV, int rel, hipStream_t st);
+                   int KV, int rel, unsigned long long* stamps, hipStream_t st);
 void pa_prefill_gemm_plan(int M, int N, int K, int bn, int* full, int* S);
 int pa_prefill_pick_bn(int M, int N);
 void pa_prefill_set_variant(int v);
@@ -456,7 +456,7 @@ bool stream_gemm(c10::optional<at::Tensor> y, at::Tensor x, at::Tensor wp, c10::
                  std::vector<int64_t> plan, c10::optional<at::Tensor> q_out, c10::optional<at::Tensor> k_cache,
                  c10::optional<at::Tensor> v_cache, c10::optional<at::Tensor> positions,
                  c10::optional<at::Tensor> slots, c10::optional<at::Tensor> cos_sin, int64_t H, int64_t KV,
-                 int64_t rel) {
+                 int64_t rel, c10::optional<at::Tensor> stamps) {
   check_gpu(wp, "wp"); check_gpu(ws, "ws"); check_gpu(counters, "counters"); check_gpu(err, "err");
   TORCH_CHECK(x.is_cuda() && x.dim() == 2 && x.stride(1) == 1, "x must be a 2-D GPU tensor, unit inner stride");
   check_dtype(x, at::kBFloat16, "x"); check_dtype(wp, at::kBFloat16, "wp");
@@ -522,7 +522,9 @@ bool stream_gemm(c10::optional<at::Tensor> y, at::Tensor x, at::Tensor wp, c10::
                                 ldy, ldr, (int)epi, opt_rows(ss_in, M, "ss_in"),
                                 const_cast<float*>(opt_rows(ss_out, M, "ss_out")),
                                 const_cast<float*>(opt_rows(ss_zero, M, "ss_zero")), (float)eps, pl, qp, kp, vp, pp,
-                                sp, cp, (int)H, (int)KV, (int)rel, cur_stream());
+                                sp, cp, (int)H, (int)KV, (int)rel,
+                                stamps ? reinterpret_cast<unsigned long long*>(stamps->data_ptr<int64_t>()) : nullptr,
+                                cur_stream());
   TORCH_CHECK(rc >= 0, "stream_gemm launch failed");
   return rc == 0;
 }
@@ -913,7 +915,8 @@ PYBIND11_MODULE(_C, m) {
         py::arg("counters"), py::arg("err"), py::arg("epi"), py::arg("ss_in"), py::arg("ss_out"), py::arg("ss_zero"),
         py::arg("eps"), py::arg("plan"), py::arg("q_out") = py::none(), py::arg("k_cache") = py::none(),
         py::arg("v_cache") = py::none(), py::arg("positions") = py::none(), py::arg("slots") = py::none(),
-        py::arg("cos_sin") = py::none(), py::arg("H") = 0, py::arg("KV") = 0, py::arg("rel") = 0);
+        py::arg("cos_sin") = py::none(), py::arg("H") = 0, py::arg("KV") = 0, py::arg("rel") = 0,
+        py::arg("stamps") = py::none());
   m.def("stream_gemm_plan", &stream_gemm_plan,
         "default (mg, rg, tpw, wt, wk, S, D, workspace floats) of stream_gemm");
   m.def("mid_gemm_plan", &mid_gemm_plan, "default (fm, fn, splits, workspace floats) of mid_gemm");

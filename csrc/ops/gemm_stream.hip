@@ -71,6 +71,9 @@ struct Args {
   const float* cos_sin;
   int H, KV;
   int rel;  // 1: agent-scope release (L2 write-back) before arriving (diagnostics)
+  // diagnostics (null in the engine): per workgroup 8 wall-clock stamps (s_memrealtime, 100 MHz):
+  // [0] start, [1] first chunk in LDS, [2] main loop done, [3] group barrier passed, [4] end
+  unsigned long long* stamps;
 };
 
 typedef __attribute__((address_space(1))) int gi32;
@@ -156,6 +159,10 @@ __global__ __launch_bounds__(WT * WK * 64) void stream_gemm_kernel(const Args A)
   const int kb0 = s * A.KSW;
   const int nch = A.KSW / KC;  // host: nch % D == 0, nch >= D
 
+  auto stamp = [&](int i) {
+    if (A.stamps && threadIdx.x == 0) A.stamps[(size_t)bid * 8 + i] = __builtin_amdgcn_s_memrealtime();
+  };
+  stamp(0);
   if (A.ss_zero && bid == 0)
     for (int i = threadIdx.x; i < A.M; i += NTH) A.ss_zero[i] = 0.f;
   for (int i = threadIdx.x; i < MT; i += NTH) rsq[i] = 0.f;
@@ -230,11 +237,16 @@ __global__ __launch_bounds__(WT * WK * 64) void stream_gemm_kernel(const Args A)
 #pragma unroll
     for (int d = 0; d < D; ++d) {
       consume(d, d & 1);
+      if (c == 0 && d == 0) stamp(1);
       issue(c + d + D, d);
     }
   }
 #pragma unroll
-  for (int d = 0; d < D; ++d) consume(d, d & 1);
+  for (int d = 0; d < D; ++d) {
+    consume(d, d & 1);
+    if (c == 0 && d == 0) stamp(1);
+  }
+  stamp(2);
 
   const bool pair = A.epi == EP_SILU || A.epi == EP_ROPEKV;
   const float inv_k = 1.f / (float)A.K;
@@ -282,6 +294,8 @@ __global__ __launch_bounds__(WT * WK * 64) void stream_gemm_kernel(const Args A)
       if (A.ss_out) row_stat(mg, m, sq);
     }
     flush_row_stats();
+    stamp(3);
+    stamp(4);
     return;
   }
 
@@ -305,6 +319,7 @@ __global__ __launch_bounds__(WT * WK * 64) void stream_gemm_kernel(const Args A)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   int* ctr = A.counters + 2 * gid;
   group_barrier(ctr, A.S, A.err, A.rel);
+  stamp(3);
 
   // ---- reduce 1/S of the group's fragments and run the epilogue on them
   const int TU = pair ? CT / 2 : CT;  // tile units
@@ -335,6 +350,7 @@ __global__ __launch_bounds__(WT * WK * 64) void stream_gemm_kernel(const Args A)
     if (A.ss_out) row_stat(mg, m, sq);
   }
   flush_row_stats();  // also: every slab read of this workgroup is done
+  stamp(4);
   if (threadIdx.x == 0) {  // the last to leave resets the group's counters for the next launch
     const int left = __hip_atomic_fetch_add((gi32*)(ctr + 1), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (left == A.S - 1) {
@@ -466,7 +482,7 @@ extern "C" int pa_stream_gemm(void* y, const void* x, const void* wp, const void
                               int ldx, int ldy, int ldr, int epi, const float* ss_in, float* ss_out, float* ss_zero,
                               float eps, const int* plan, void* q_out, void* k_cache, void* v_cache,
                               const int* positions, const int* slots, const float* cos_sin, int H, int KV, int rel,
-                              hipStream_t st) {
+                              unsigned long long* stamps, hipStream_t st) {
   using namespace pa::sg;
   if (M <= 0) return 0;
   if (M > 256 || K % 64 != 0 || N % 16 != 0 || epi < 0 || epi > 4) return 1;
@@ -487,7 +503,8 @@ extern "C" int pa_stream_gemm(void* y, const void* x, const void* wp, const void
   const int grid = groups * p.S;
   Args a{(pa::bf16*)y, (const pa::bf16*)x, (const pa::bf16*)wp, (const pa::bf16*)resid, ws, counters, err,
          M, N, K, ldx, ldy, ldr, p.S, p.rg, G, K / 32 / p.S, epi, eps, ss_in, ss_out, ss_zero,
-         (pa::bf16*)q_out, (pa::bf16*)k_cache, (pa::bf16*)v_cache, positions, slots, cos_sin, H, KV, rel};
+         (pa::bf16*)q_out, (pa::bf16*)k_cache, (pa::bf16*)v_cache, positions, slots, cos_sin, H, KV, rel,
+         stamps};
   bool ok = false;
   switch (p.mg) {
     case 2: ok = launch_mg<2>(a, p.tpw, p.wt, p.wk, p.D, grid, st); break;

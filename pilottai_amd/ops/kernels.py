@@ -558,7 +558,8 @@ def stream_gemm_plan(M: int, N: int, K: int, epi: str = "plain"):
 def stream_gemm(x: torch.Tensor, wp: torch.Tensor, epi: str = "plain", resid: Optional[torch.Tensor] = None,
                 out: Optional[torch.Tensor] = None, norm: bool = False, eps: float = 1e-5,
                 ss_in: Optional[torch.Tensor] = None, ss_out: Optional[torch.Tensor] = None,
-                ss_zero: Optional[torch.Tensor] = None, plan=None, rel: int = 0) -> torch.Tensor:
+                ss_zero: Optional[torch.Tensor] = None, plan=None, rel: int = 0,
+                stamps: Optional[torch.Tensor] = None) -> torch.Tensor:
     """y = epi(rownorm(x) @ W.T) for 16 < M <= 256 with W packed by pack_decode_weight (gate_up:
     pack_decode_gate_up + "silu"; QKV: pack_decode_qkv_rope + "rope_perm"); same epilogue and
     row-statistics conventions as mid_gemm. `plan`: (mg, rg, tpw, wt, wk, S, D) or None for
@@ -574,7 +575,8 @@ def stream_gemm(x: torch.Tensor, wp: torch.Tensor, epi: str = "plain", resid: Op
     if _on_gpu(x):
         ws, cnt, err = stream_workspace(x.device)
         if not require_native().stream_gemm(out, x, wp, resid, ws, cnt, err, code, ss_in if norm else None, ss_out,
-                                             ss_zero, float(eps), list(plan) if plan else [], rel=int(rel)):
+                                             ss_zero, float(eps), list(plan) if plan else [], rel=int(rel),
+                                             stamps=stamps):
             raise ValueError(f"stream_gemm does not handle M={M} N={N} K={K} epi={epi} plan={plan}")
         return out
     return mid_gemm(x, wp, epi, resid=resid, out=out, norm=norm, eps=eps, ss_in=ss_in, ss_out=ss_out,
