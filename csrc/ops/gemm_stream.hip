@@ -36,6 +36,7 @@
 #include "packed_epi.h"
 
 #include <algorithm>
+#include <type_traits>
 
 namespace pa {
 namespace sg {
@@ -330,17 +331,32 @@ __global__ __launch_bounds__(WT * WK * 64) void stream_gemm_kernel(const Args A)
     const int tl = pair ? 2 * tu : tu;
     const int f = tl * MG + mg;
     f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f}, v2 = f32x4{0.f, 0.f, 0.f, 0.f};
-    // separate loops per form: a load under a runtime condition makes hipcc wait per load
-    if (pair) {
-      for (int p = 0; p < SV; ++p) {
-        v += __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(ra, ((p * CT * MG + f) * 64 + lane) * 16, 0, 16));
-        v2 += __builtin_bit_cast(f32x4,
-                                 __builtin_amdgcn_raw_buffer_load_b128(ra, ((p * CT * MG + f + MG) * 64 + lane) * 16, 0, 16));
+    // every slab's fragment is loaded before the first add (up to 8 at a time, unconditional
+    // loads of a clamped index; the surplus is masked out): the uncached round trips overlap
+    // instead of running one after the other (a load under a runtime condition, or a loop
+    // hipcc does not unroll, made it wait per slab: 2-5 us per launch, tools/stream_stamps.py)
+    auto gather = [&](auto two) {
+      constexpr bool TWO = decltype(two)::value;
+      for (int p0 = 0; p0 < SV; p0 += 8) {
+        f32x4 ta[8], tb[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const int p = min(p0 + q, SV - 1);
+          ta[q] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(ra, ((p * CT * MG + f) * 64 + lane) * 16, 0, 16));
+          if constexpr (TWO)
+            tb[q] = __builtin_bit_cast(
+                f32x4, __builtin_amdgcn_raw_buffer_load_b128(ra, ((p * CT * MG + f + MG) * 64 + lane) * 16, 0, 16));
+        }
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const float keep = p0 + q < SV ? 1.f : 0.f;
+          v += ta[q] * keep;
+          if constexpr (TWO) v2 += tb[q] * keep;
+        }
       }
-    } else {
-      for (int p = 0; p < SV; ++p)
-        v += __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(ra, ((p * CT * MG + f) * 64 + lane) * 16, 0, 16));
-    }
+    };
+    if (pair) gather(std::true_type{});
+    else gather(std::false_type{});
     const int m = row0 + mg * 16 + cl;
     float sq = 0.f;
     if (m < A.M) {

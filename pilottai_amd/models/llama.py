@@ -193,6 +193,15 @@ class LlamaModel:
         "down": [(128, "mid", {}), (640, "pf", {"bn": 128, "variant": 1}),
                  (1 << 30, "pf", {"bn": 256, "variant": 3})],
     }
+    # per projection: (largest M, plan) rows for the weight-streaming kernel
+    # (csrc/ops/gemm_stream.hip; plan = (mg, rg, tpw, wt, wk, S, D)); the first row whose M
+    # covers a mid-size step (WIDE_MAX_T < T <= MID_MAX_T) replaces PF_CFG / MID_CFG there.
+    # Rows only where tools/stream_gemm_bench.py (graph-replayed, cold weights, engine
+    # epilogues) measured it ahead of the round-3 choice (profiles/r4_stream_gemm_*.jsonl).
+    STREAM_CFG: Dict[str, list] = {}
+    # LM head of steps with more than 32 logit rows (<= 32: the packed decode kernel):
+    # (largest rows, plan) on the weight-streaming kernel; empty = hipBLASLt
+    LM_HEAD_STREAM: list = []
     # decode/small steps: let the attention launch's idle workgroups read the O
     # projection's weights into the Infinity Cache (MALL-resident weights run the 34 MB
     # O projection at M=8 in 8.7 us vs 12.8 us cold, profiles/r2_mall_warm.jsonl). Off by
@@ -263,6 +272,7 @@ class LlamaModel:
             ops.wide_workspace(self.device)  # split-K slabs + tickets, before any graph capture
             ops.mid_workspace(self.device)
             ops.prefill_workspace(self.device)
+            ops.stream_workspace(self.device)
         # RMSNorm row statistics handed from each residual epilogue to the next projection
         self._ss = torch.zeros(2, 1 << 15, dtype=torch.float32, device=self.device)
         if self.device.type == "cuda":
@@ -525,10 +535,9 @@ class LlamaModel:
         rows = meta.logit_rows[:num_logit_rows]
         rows = rows.long() if self.device.type == "cpu" else rows
         xs = ops.rmsnorm(h.index_select(0, rows), self.norm, eps)
-        if num_logit_rows <= 32:  # decode_gemm beats hipBLASLt on the LM head up to 32 rows (24: 180 vs
-            # 191 us, 32: 184.5 vs 196; 48: 221 vs 204; profiles/r2_decode_sweep_nt*.jsonl)
-            return ops.decode_gemm(xs, self.lm_head_p, "plain")
-        return ops.linear(xs, self.lm_head, "lm_head")
+        # decode_gemm beats hipBLASLt on the LM head up to 32 rows (24: 180 vs 191 us, 32: 184.5
+        # vs 196; 48: 221 vs 204; profiles/r2_decode_sweep_nt*.jsonl)
+        return self._lm_head(xs, num_logit_rows)
 
     @staticmethod
     def _pool_embed(hn: torch.Tensor, T: int, embed):
@@ -544,7 +553,11 @@ class LlamaModel:
         return {}
 
     def _proj_path(self, kind: str, T: int):
-        """("mid", cfg) or ("pf", cfg) for projection `kind` on a T-token step."""
+        """("stream" | "mid" | "pf", cfg) for projection `kind` on a T-token step."""
+        if T <= self.MID_MAX_T:
+            for mmax, plan in self.STREAM_CFG.get(kind, ()):
+                if T <= mmax:
+                    return "stream", {"plan": tuple(plan)}
         if self.device.type == "cuda" and (T > self.MID_MAX_T or kind in self.PF_MIDRANGE):
             for mmax, path, cfg in self.PF_CFG[kind]:
                 if T <= mmax:
@@ -553,7 +566,7 @@ class LlamaModel:
 
     def _gemm(self, kind: str, T: int, x, wp, epi: str, **kw):
         path, cfg = self._proj_path(kind, T)
-        fn = ops.prefill_gemm if path == "pf" else ops.mid_gemm
+        fn = {"pf": ops.prefill_gemm, "stream": ops.stream_gemm}.get(path, ops.mid_gemm)
         return fn(x, wp, epi, **cfg, **kw)
 
     def _qkv_rope(self, T: int, x, wp, eps, q, k_cache, v_cache, meta, ss_in):
@@ -562,7 +575,7 @@ class LlamaModel:
             return ops.decode_qkv_rope(x, wp, eps, q, k_cache, v_cache, meta.positions, meta.slots, self.cos_sin,
                                        H, KVh)
         path, cfg = self._proj_path("qkv", T)
-        fn = ops.prefill_qkv_rope if path == "pf" else ops.mid_qkv_rope
+        fn = {"pf": ops.prefill_qkv_rope, "stream": ops.stream_qkv_rope}.get(path, ops.mid_qkv_rope)
         return fn(x, wp, eps, q, k_cache, v_cache, meta.positions, meta.slots, self.cos_sin, H, KVh,
                   ss_in=ss_in, **cfg)
 
@@ -617,8 +630,16 @@ class LlamaModel:
         rows = meta.logit_rows[:num_logit_rows]
         rows = rows.long() if self.device.type == "cpu" else rows
         xs = ops.rmsnorm(h.index_select(0, rows), self.norm, eps)
-        if num_logit_rows <= 32:
+        return self._lm_head(xs, num_logit_rows)
+
+    def _lm_head(self, xs, n: int):
+        """Logits of the step's sampling rows on the packed weights: the decode kernel up to 32
+        rows, the weight-streaming kernel where LM_HEAD_STREAM covers n, else hipBLASLt."""
+        if n <= 32:
             return ops.decode_gemm(xs, self.lm_head_p, "plain")
+        for mmax, plan in self.LM_HEAD_STREAM:
+            if n <= mmax:
+                return ops.stream_gemm(xs, self.lm_head_p, "plain", plan=tuple(plan) if plan else None)
         return ops.linear(xs, self.lm_head, "lm_head")
 
     # -- reference (dense, no cache) forward used by numerics tests ----------------

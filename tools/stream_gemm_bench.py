@@ -68,6 +68,8 @@ def timeit(fn, ncopies):
 
 def plans_for(M, N, K, epi):
     mg = 2 if M <= 32 else (4 if M <= 64 else 8)
+    if M <= 16:
+        mg = 2
     rgs = [(mg, (M + 16 * mg - 1) // (16 * mg))]
     out = []
     tiles, KS = N // 16, K // 32
@@ -109,7 +111,8 @@ for name in a.shapes.split(","):
     pack = {"silu": kernels.pack_decode_gate_up, "rope_perm": kernels.pack_decode_qkv_rope}.get(epi,
                                                                                                kernels.pack_decode_weight)
     wps = [pack(w) for w in ws]
-    del ws
+    if name != "lm_head":
+        del ws
     for M in [int(v) for v in a.M.split(",")]:
         x = torch.randn(M, K, device="cuda").to(torch.bfloat16)
         NO = N // 2 if epi == "silu" else N
@@ -118,7 +121,16 @@ for name in a.shapes.split(","):
         ss = kernels.row_sumsq(x)
         kw = dict(out=y, resid=resid, norm=nrm, ss_in=ss if nrm else None)
         variants = {}
-        if name != "lm_head":
+        if name == "lm_head":  # round 3: packed decode kernel up to 32 logit rows, hipBLASLt above
+            if M <= 32:
+                variants["r3"] = lambda i: kernels.decode_gemm(x, wps[i], "plain", out=y)
+            else:
+                variants["r3"] = lambda i: torch.nn.functional.linear(x, ws[i], out=y)
+        elif M <= 16:  # decode-sized steps: the packed decode kernel
+            dep = {"rope_perm": "plain", "silu": "silu", "resid": "resid", "plain": "plain"}[epi]
+            variants["r3"] = lambda i: kernels.decode_gemm(x, wps[i], dep, out=y if epi != "rope_perm" else y,
+                                                           resid=resid, norm=nrm)
+        else:
             model = LlamaModel.__new__(LlamaModel)  # only the per-shape tables are used
             model.device = torch.device("cuda")
             path, cfg = LlamaModel._proj_path(model, name, M)
