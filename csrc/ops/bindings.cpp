@@ -388,6 +388,12 @@ bool mid_gemm(at::Tensor y, at::Tensor x, at::Tensor wp, c10::optional<at::Tenso
   const int M = x.size(0), K = x.size(1), N = wp.size(0) * 16;
   TORCH_CHECK(wp.size(1) * 32 == K, "packed weight K mismatch");
   TORCH_CHECK(x.stride(0) % 8 == 0 && y.stride(0) % 4 == 0, "x rows must be 16-byte, y rows 8-byte aligned");
+  // the non-pair epilogues (plain, residual) of the ping-pong kernels store -- and read the
+  // residual -- 16 B per lane (packed_epi.h store_pair_wide): y and resid rows 16-byte aligned
+  const bool wide = epi == 0 || epi == 2;
+  auto rows16 = [](const at::Tensor& t) { return t.stride(0) % 8 == 0 && ((uintptr_t)t.data_ptr() & 15) == 0; };
+  TORCH_CHECK(!wide || rows16(y), "y rows must be 16-byte aligned for the plain / residual epilogue");
+  TORCH_CHECK(((uintptr_t)y.data_ptr() & 7) == 0, "y must be 8-byte aligned");
   const int NO = epi == 1 ? N / 2 : N;
   TORCH_CHECK(y.size(0) == M && y.size(1) == NO, "y shape mismatch");
   const void* rp = nullptr;
@@ -395,9 +401,8 @@ bool mid_gemm(at::Tensor y, at::Tensor x, at::Tensor wp, c10::optional<at::Tenso
   if (epi == 2) {
     TORCH_CHECK(resid.has_value(), "epi=2 needs resid");
     const auto& r = *resid;
-    TORCH_CHECK(r.is_cuda() && r.dim() == 2 && r.stride(1) == 1 && r.size(0) == M && r.size(1) == N &&
-                    r.stride(0) % 4 == 0,
-                "resid must be [M, N] with unit inner stride");
+    TORCH_CHECK(r.is_cuda() && r.dim() == 2 && r.stride(1) == 1 && r.size(0) == M && r.size(1) == N && rows16(r),
+                "resid must be [M, N] with unit inner stride and 16-byte aligned rows");
     check_dtype(r, at::kBFloat16, "resid");
     rp = r.data_ptr();
     ldr = r.stride(0);
@@ -552,6 +557,12 @@ bool prefill_gemm(at::Tensor y, at::Tensor x, at::Tensor wp, c10::optional<at::T
   const int M = x.size(0), K = x.size(1), N = wp.size(0) * 16;
   TORCH_CHECK(wp.size(1) * 32 == K, "packed weight K mismatch");
   TORCH_CHECK(x.stride(0) % 8 == 0 && y.stride(0) % 4 == 0, "x rows must be 16-byte, y rows 8-byte aligned");
+  // the non-pair epilogues (plain, residual) of the ping-pong kernels store -- and read the
+  // residual -- 16 B per lane (packed_epi.h store_pair_wide): y and resid rows 16-byte aligned
+  const bool wide = epi == 0 || epi == 2;
+  auto rows16 = [](const at::Tensor& t) { return t.stride(0) % 8 == 0 && ((uintptr_t)t.data_ptr() & 15) == 0; };
+  TORCH_CHECK(!wide || rows16(y), "y rows must be 16-byte aligned for the plain / residual epilogue");
+  TORCH_CHECK(((uintptr_t)y.data_ptr() & 7) == 0, "y must be 8-byte aligned");
   const int NO = epi == 1 ? N / 2 : N;
   TORCH_CHECK(y.size(0) == M && y.size(1) == NO, "y shape mismatch");
   const void* rp = nullptr;
@@ -559,9 +570,8 @@ bool prefill_gemm(at::Tensor y, at::Tensor x, at::Tensor wp, c10::optional<at::T
   if (epi == 2) {
     TORCH_CHECK(resid.has_value(), "epi=2 needs resid");
     const auto& r = *resid;
-    TORCH_CHECK(r.is_cuda() && r.dim() == 2 && r.stride(1) == 1 && r.size(0) == M && r.size(1) == N &&
-                    r.stride(0) % 4 == 0,
-                "resid must be [M, N] with unit inner stride");
+    TORCH_CHECK(r.is_cuda() && r.dim() == 2 && r.stride(1) == 1 && r.size(0) == M && r.size(1) == N && rows16(r),
+                "resid must be [M, N] with unit inner stride and 16-byte aligned rows");
     check_dtype(r, at::kBFloat16, "resid");
     rp = r.data_ptr();
     ldr = r.stride(0);

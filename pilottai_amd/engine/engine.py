@@ -209,7 +209,7 @@ class LLMEngine:
         for k, v in (cfg.model_overrides or {}).items():
             if not hasattr(self.model, k):
                 raise ValueError(f"unknown model tunable {k!r}")
-            setattr(self.model, k, frozenset(v) if isinstance(v, (list, tuple, set)) else v)
+            setattr(self.model, k, frozenset(v) if isinstance(getattr(self.model, k), frozenset) else v)
         if cfg.att_decode_waves is not None:
             self.model.ATT_DECODE_WAVES = int(cfg.att_decode_waves)
         if cfg.pf_midrange is not None:
@@ -241,6 +241,14 @@ class LLMEngine:
         self.kv = KVCache(mc.num_layers, nb, kv_local, self.device, block_size=cfg.block_size)
         self.num_kv_blocks = nb
         # ---- native scheduler + step buffers
+        # the model runs 8-wave decode attention on the fused decode path only, keyed on the
+        # graph bucket: the scheduler's whole-context (unsplit) items for small steps must
+        # follow the same rule, keyed on the step size -> the largest bucket on that path
+        buckets = cfg.token_buckets or DEFAULT_BUCKETS
+        self.buckets = sorted({b for b in buckets if b <= cfg.max_num_batched_tokens} |
+                              {cfg.max_num_batched_tokens})
+        small = [b for b in self.buckets if b <= self.model.DECODE_FUSED_MAX_T]
+        small_step = max(small) if (small and self.model.ATT_DECODE_WAVES == 8 and self.model.decode_packed) else 0
         self.sched = _runtime.Scheduler({
             "num_blocks": nb, "block_size": cfg.block_size, "max_num_seqs": cfg.max_num_seqs,
             "max_num_batched_tokens": cfg.max_num_batched_tokens,
@@ -252,8 +260,8 @@ class LLMEngine:
             "dedup_inflight_prefix": cfg.dedup_inflight_prefix,
             "token_align": cfg.token_align, "align_slack": cfg.align_slack,
             "kv_heads": self.model.kv_local,
-            "small_step_tokens": self.model.DECODE_FUSED_MAX_T if self.model.ATT_DECODE_WAVES == 8 else 0,
-            "small_step_part": 4096 if self.model.ATT_DECODE_WAVES == 8 else 0,
+            "small_step_tokens": small_step,
+            "small_step_part": 4096 if small_step else 0,
             "eos_ids": list(self.tok.eos_ids)})
         L = self.L = self.sched.layout()
         pin = self.on_gpu
@@ -288,6 +296,11 @@ class LLMEngine:
         # token), summed in the step graph, read and cleared when the request finishes
         self._embed_pool = torch.zeros(L["max_seqs"] + 1, mc.hidden_size, dtype=torch.float32, device=self.device)
         self._embed_rows = self._dev_meta[L["embed_rows"]:L["embed_rows"] + L["max_tokens"]]
+        # pipelined steps: a stream-ordered snapshot of the pool per step slot, taken right
+        # behind the step that pools into it, so the commit reads host memory instead of
+        # waiting (.cpu()) for the step queued after it
+        self._embed_hosts = [torch.zeros_like(self._embed_pool, device="cpu", pin_memory=self.on_gpu)
+                             for _ in range(2)] if self._async else None
         tpw = 16 // (self.model.h_local // self.model.kv_local)
         self._tpw = tpw
         self._max_parts = (self.max_model_len + ops.ATT_PART - 1) // ops.ATT_PART
@@ -296,9 +309,6 @@ class LLMEngine:
         self._part_o = ops.empty_handoff(max_items * kv_local * 16 * 128, torch.float32, self.device)
         self._part_ml = ops.empty_handoff(max_items * kv_local * 16 * 2, torch.float32, self.device)
         self._sample_ws = ops.sample_workspace(S, self.model.v_local, self.device) if self.on_gpu else None
-        buckets = cfg.token_buckets or DEFAULT_BUCKETS
-        self.buckets = sorted({b for b in buckets if b <= cfg.max_num_batched_tokens} |
-                              {cfg.max_num_batched_tokens})
         # one graph per (token bucket, top-k/top-p pass); truncating variants are
         # captured on first use, so steps without truncation pay nothing for it
         self._graphs: Dict[tuple, "torch.cuda.CUDAGraph"] = {}
@@ -857,6 +867,8 @@ class LLMEngine:
             self._run(bucket, ns, trunc, n_copy, embed)
         if nsamp:
             self._sampled_hosts[slot][:nsamp].copy_(self._sampled_dev[:nsamp], non_blocking=self.on_gpu)
+        if embed:
+            self._embed_hosts[slot].copy_(self._embed_pool, non_blocking=self.on_gpu)
         ev = None
         if self.on_gpu:
             ev = torch.cuda.Event()
@@ -880,7 +892,7 @@ class LLMEngine:
         with trace_range("engine.commit"):
             outs = self.sched.commit(self._sampled_hosts[slot].data_ptr(), nsamp)
         if embed:
-            self._read_embeddings(outs)
+            self._read_embeddings(outs, self._embed_hosts[slot])
         st = self.stats
         st["device_wait_s"] += t_sync - t_w
         st["steps"] += 1
@@ -900,15 +912,18 @@ class LLMEngine:
         if not self._inflight and not self.sched.has_work():
             self._flush_deliveries()
 
-    def _read_embeddings(self, outs):
-        """Pooled rows of the embedding requests this step finished, read while the device
-        is idle (step synchronised): their delivery runs during the NEXT step, where a read
-        would wait for that step to finish."""
+    def _read_embeddings(self, outs, host: Optional[torch.Tensor] = None):
+        """Pooled rows of the embedding requests this step finished. Serial loop: read from
+        the device while it is idle (step synchronised). Pipelined loop: from `host`, the
+        pinned snapshot taken behind this step (the next step is already queued, so a device
+        read would wait for it too). Delivery runs during the NEXT step either way."""
         done = [(o[9], max(1, o[3])) for o in outs if o[9] >= 0 and o[2] == 3]
         if not done:
             return
-        idx = torch.tensor([e for e, _ in done], dtype=torch.long, device=self.device)
-        rows = self._embed_pool.index_select(0, idx).cpu().numpy()
+        slots = [e for e, _ in done]
+        idx = torch.tensor(slots, dtype=torch.long, device=self.device)
+        rows = host.numpy()[slots] if host is not None else self._embed_pool.index_select(0, idx).cpu().numpy()
+        # stream-ordered: a finished request's row takes no more tokens in the queued step
         self._embed_pool.index_fill_(0, idx, 0.0)
         for (e, plen), r in zip(done, rows):
             self._embed_ready[e] = r / plen
@@ -930,7 +945,12 @@ class LLMEngine:
         except BaseException as e:  # noqa: BLE001
             self._err = e
             log.exception("engine loop crashed")
-            # fail every pending request loudly
+            # requests that already finished (held for overlapped delivery) get their outputs
+            try:
+                self._flush_deliveries()
+            except Exception:  # noqa: BLE001
+                log.exception("delivery after the crash failed")
+            # fail every other pending request loudly
             for rid in list(self._reqs):
                 req = self._reqs.pop(rid)
                 try:

@@ -163,3 +163,28 @@ def test_prefill_gemm_four_wave_variant(gpu, M, N, K, epi, norm, full, splits):
             torch.testing.assert_close(y.float(), acc, atol=4e-2, rtol=2e-2)
     finally:
         C.prefill_set_variant(-1)
+
+
+@pytest.mark.parametrize("epi", ["plain", "resid"])
+def test_prefill_gemm_strided_views(gpu, epi):
+    """The plain / residual epilogues store (and read the residual) 16 B per lane: a padded
+    output view with 16-byte rows is written correctly, a view whose rows are only 8-byte
+    aligned is refused at the binding instead of issuing misaligned wide accesses."""
+    torch.manual_seed(5)
+    M, N, K = 300, 1024, 512
+    x = _bf(M, K, dev=gpu)
+    w = _bf(N, K, dev=gpu, scale=0.05)
+    wp = ops.pack_decode_weight(w)
+    want = x.float() @ w.float().T
+    big = torch.zeros(M, N + 8, dtype=torch.bfloat16, device=gpu)  # padded rows, 16-B aligned
+    resid = None
+    if epi == "resid":
+        rbig = _bf(M, N + 16, dev=gpu)
+        resid = rbig[:, 8:8 + N]
+        want = want + resid.float()
+    y = ops.prefill_gemm(x, wp, epi, resid=resid, out=big[:, :N])
+    torch.testing.assert_close(y.float(), want, atol=4e-2, rtol=2e-2)
+    assert torch.equal(big[:, N:], torch.zeros_like(big[:, N:]))  # the padding is untouched
+    odd = torch.zeros(M, N + 4, dtype=torch.bfloat16, device=gpu)[:, 4:]  # 8-byte aligned only
+    with pytest.raises(RuntimeError, match="16-byte"):
+        ops.prefill_gemm(x, wp, epi, resid=resid, out=odd)

@@ -171,16 +171,18 @@ def test_engine_cpu_tiny_end_to_end(tok):
         assert row[t] >= row.max() - 0.05
 
 
-def test_engine_embedding_requests_match_dense_forward(tok):
+@pytest.mark.parametrize("async_steps", [False, True])
+def test_engine_embedding_requests_match_dense_forward(tok, async_steps):
     """Embedding requests inside the continuous batch (engine.embed): the pooled final
     hidden state equals the dense reference forward's, for prompts that span several
     prefill chunks, share a cached prefix with a generation request (embeddings never
-    reuse the prefix cache), and run beside that request."""
+    reuse the prefix cache), and run beside that request. Pipelined loop: the pooled rows
+    are read from the per-slot snapshot taken behind their step."""
     from pilottai_amd.engine.engine import EngineConfig, LLMEngine
     from pilottai_amd.memory.embedding import EngineEmbedder
 
     e = LLMEngine(EngineConfig(model="tiny", max_num_seqs=8, max_num_batched_tokens=64, max_model_len=512,
-                               num_kv_blocks=128), device="cpu")
+                               num_kv_blocks=128, async_steps=async_steps), device="cpu")
     p_long = tok.encode("Task: summarize the quarterly report. " * 12)[:150]  # 3 chunks of <= 64
     p_short = tok.encode("alpha beta gamma")
     e.generate([p_long], temperature=0.0, max_tokens=2, ignore_eos=True)  # p_long now in the prefix cache
