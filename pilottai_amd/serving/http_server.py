@@ -5,6 +5,7 @@ SURVEY C14); here the model runs on the MI355X in the same process, and this mod
 publishes it to other processes and hosts with the wire format those clients already
 speak:
 
+    GET  /                     landing page with live engine metrics (serving/site.py)
     GET  /health               liveness + engine metrics (steps, tokens/s, KV use, HBM)
     GET  /v1/models            the served model
     POST /v1/chat/completions  messages -> one completion (stream=true: SSE, one delta + [DONE])
@@ -35,7 +36,7 @@ import uuid
 from typing import Any, Dict, List, Optional
 
 from fastapi import FastAPI, HTTPException
-from fastapi.responses import JSONResponse, StreamingResponse
+from fastapi.responses import HTMLResponse, JSONResponse, StreamingResponse
 
 DEFAULT_STR_TOKENS = 32
 
@@ -124,6 +125,12 @@ def create_app(llm, model_name: Optional[str] = None, engine=None) -> FastAPI:
     app = FastAPI(title="pilottai_amd", version="0.1.0")
     name = model_name or getattr(llm, "model_name", "local")
     started = time.time()
+
+    @app.get("/", response_class=HTMLResponse)
+    async def index():
+        from pilottai_amd.serving.site import render
+
+        return render(name)
 
     @app.get("/health")
     async def health():

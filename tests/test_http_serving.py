@@ -148,3 +148,16 @@ def test_engine_backed_server_concurrent_constrained_requests():
         assert h["status"] == "ok" and isinstance(h["engine"], dict) and h["engine"]
     finally:
         eng.stop()
+
+
+def test_landing_page_sections_and_live_metrics(schema_server):
+    """GET / serves the framework's page (the reference's Hero / Features /
+    Agents / Performance / Footer site) with a Performance section fed by /health."""
+    base = schema_server[: -len("/v1")]
+    r = httpx.get(base + "/", timeout=10)
+    assert r.status_code == 200 and r.headers["content-type"].startswith("text/html")
+    for sid in ("navigation", "hero", "features", "agents", "performance", "footer"):
+        assert f'id="{sid}"' in r.text
+    assert "schema-test" in r.text and "fetch('/health')" in r.text
+    h = httpx.get(base + "/health", timeout=10).json()
+    assert h["status"] == "ok" and h["model"] == "schema-test"
