@@ -193,14 +193,16 @@ class LlamaModel:
         "down": [(128, "mid", {}), (640, "pf", {"bn": 128, "variant": 1}),
                  (1 << 30, "pf", {"bn": 256, "variant": 3})],
     }
-    # per projection: (largest M, plan) rows for the weight-streaming kernel
-    # (csrc/ops/gemm_stream.hip; plan = (mg, rg, tpw, wt, wk, S, D)); the first row whose M
-    # covers a mid-size step (WIDE_MAX_T < T <= MID_MAX_T) replaces PF_CFG / MID_CFG there.
+    # per projection: (largest M, shape) rows for the weight-streaming kernel
+    # (csrc/ops/gemm_stream.hip; shape = (rg, tpw, wt, wk, S, D): row groups, 16-column tiles
+    # per wave, waves along N, waves along K, K-split, ring depth; the rows per group follow
+    # from the step, _stream_plan); the first row whose M covers a mid-size step
+    # (WIDE_MAX_T < T <= MID_MAX_T) replaces PF_CFG / MID_CFG there.
     # Rows only where tools/stream_gemm_bench.py (graph-replayed, cold weights, engine
     # epilogues) measured it ahead of the round-3 choice (profiles/r4_stream_gemm_*.jsonl).
     STREAM_CFG: Dict[str, list] = {}
     # LM head of steps with more than 32 logit rows (<= 32: the packed decode kernel):
-    # (largest rows, plan) on the weight-streaming kernel; empty = hipBLASLt
+    # (largest rows, shape as STREAM_CFG) on the weight-streaming kernel; empty = hipBLASLt
     LM_HEAD_STREAM: list = []
     # decode/small steps: let the attention launch's idle workgroups read the O
     # projection's weights into the Infinity Cache (MALL-resident weights run the 34 MB
@@ -552,12 +554,26 @@ class LlamaModel:
                 return {"fm": fm, "fn": fn, "splits": S}
         return {}
 
+    @staticmethod
+    def _stream_plan(M: int, shape) -> tuple:
+        """Full stream-kernel plan (mg, rg, tpw, wt, wk, S, D) for M rows from a table shape
+        (rg, tpw, wt, wk, S, D): mg = the smallest instantiated row-fragment count (2, 4, 8)
+        whose rg row groups cover M, with the row-group count closest to the table's for
+        which every group holds rows (gemm_stream.hip plan_ok)."""
+        rg0, tpw, wt, wk, S, D = (int(v) for v in shape)
+        for rg in sorted(range(1, 17), key=lambda r: (abs(r - rg0), r)):
+            need = -(-M // (16 * rg))
+            mg = next((m for m in (2, 4, 8) if m >= need), 0)
+            if mg and 16 * mg * (rg - 1) < M:
+                return (mg, rg, tpw, wt, wk, S, D)
+        raise ValueError(f"no stream plan for M={M} with shape {shape}")
+
     def _proj_path(self, kind: str, T: int):
         """("stream" | "mid" | "pf", cfg) for projection `kind` on a T-token step."""
         if T <= self.MID_MAX_T:
-            for mmax, plan in self.STREAM_CFG.get(kind, ()):
+            for mmax, shape in self.STREAM_CFG.get(kind, ()):
                 if T <= mmax:
-                    return "stream", {"plan": tuple(plan)}
+                    return "stream", {"plan": self._stream_plan(T, shape)}
         if self.device.type == "cuda" and (T > self.MID_MAX_T or kind in self.PF_MIDRANGE):
             for mmax, path, cfg in self.PF_CFG[kind]:
                 if T <= mmax:
@@ -637,9 +653,9 @@ class LlamaModel:
         rows, the weight-streaming kernel where LM_HEAD_STREAM covers n, else hipBLASLt."""
         if n <= 32:
             return ops.decode_gemm(xs, self.lm_head_p, "plain")
-        for mmax, plan in self.LM_HEAD_STREAM:
+        for mmax, shape in self.LM_HEAD_STREAM:
             if n <= mmax:
-                return ops.stream_gemm(xs, self.lm_head_p, "plain", plan=tuple(plan) if plan else None)
+                return ops.stream_gemm(xs, self.lm_head_p, "plain", plan=self._stream_plan(n, shape))
         return ops.linear(xs, self.lm_head, "lm_head")
 
     # -- reference (dense, no cache) forward used by numerics tests ----------------

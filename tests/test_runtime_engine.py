@@ -413,6 +413,54 @@ def test_mid_path_matches_library_path_logits():
     torch.testing.assert_close(a, b, atol=0.05 * float(b.abs().max()), rtol=0.05)
 
 
+def test_stream_routing_tables_route_mid_steps(monkeypatch):
+    """STREAM_CFG rows (set through EngineConfig.model_overrides) send every projection of a
+    mid-size step to the weight-streaming kernel with a plan derived for that step's rows;
+    on CPU the kernel's reference path is the mid one, so the logits must not change."""
+    import torch
+
+    from pilottai_amd import ops
+    from pilottai_amd.engine.engine import EngineConfig, LLMEngine
+    from pilottai_amd.models.llama import LlamaModel
+
+    calls = []
+    for name in ("stream_gemm", "stream_qkv_rope"):
+        orig = getattr(ops, name)
+
+        def wrap(*a, _o=orig, _n=name, **k):
+            calls.append((_n, k.get("plan")))
+            return _o(*a, **k)
+        monkeypatch.setattr(ops, name, wrap)
+    table = {k: [[64, [1, 2, 4, 1, 4, 4]], [256, [2, 2, 4, 1, 2, 4]]] for k in ("qkv", "o", "gate_up", "down")}
+    logits = {}
+    for routed in (True, False):
+        calls.clear()
+        eng = LLMEngine(EngineConfig(model="tiny", max_num_seqs=8, use_graphs=False, decode_fused=True,
+                                     num_kv_blocks=256, max_model_len=512, token_align=0,
+                                     model_overrides={"STREAM_CFG": table} if routed else None))
+        seen = []
+        fwd = eng.model.forward
+
+        def rec(*a, _f=fwd, _s=seen, **k):
+            out = _f(*a, **k)
+            _s.append((a[2], out.float().clone()))
+            return out
+
+        eng.model.forward = rec
+        eng.generate([list(range(1, 101))], max_tokens=2, temperature=0.0, ignore_eos=True)
+        T = seen[0][0]
+        assert 48 < T <= 256
+        logits[routed] = seen[0][1]
+        if routed:
+            layers = eng.model.cfg.num_layers
+            assert len([c for c in calls if c[0] == "stream_qkv_rope"]) >= layers
+            assert len([c for c in calls if c[0] == "stream_gemm"]) >= 3 * layers
+            assert all(p == LlamaModel._stream_plan(T, [2, 2, 4, 1, 2, 4]) for _, p in calls[:4])
+        else:
+            assert not calls
+    torch.testing.assert_close(logits[True], logits[False])
+
+
 def test_engine_fails_on_custom_allreduce_timeout():
     """A TP peer that stalls past the custom all-reduce's spin budget sets its error word;
     the engine must stop with an error instead of stepping on with partial sums."""
