@@ -125,6 +125,92 @@ __device__ __forceinline__ float epi_quad(const Args& A, int m, int tile, int cq
   return store_quad<EPI>(A, m, tile, cq, v, v2);
 }
 
+// Epilogue inputs that do not depend on the GEMM result (the row's norm scale, the residual
+// quad, the RoPE angle and the KV slot), loaded BEFORE the group barrier so that the split-K
+// epilogue after it waits on one memory round trip (the slab gather) instead of two or three.
+struct Pre {
+  float rs;
+  bf16x4 rv;
+  f32x4 c, sn;
+  int slot;
+};
+
+__device__ __forceinline__ Pre preload(const Args& A, int m, int tile, int cq) {
+  Pre p;
+  p.rs = 1.f;
+  p.slot = -1;
+  p.c = f32x4{1.f, 1.f, 1.f, 1.f};
+  p.sn = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (m >= A.M) return p;
+  if (A.ss_in) p.rs = rsqrtf(A.ss_in[m] * (1.f / (float)A.K) + A.eps);
+  if (A.epi == EP_RESID) {
+    p.rv = *reinterpret_cast<const bf16x4*>(A.resid + (size_t)m * A.ldr + tile * 16 + cq);
+  } else if (A.epi == EP_ROPEKV) {
+    const int hh = tile >> 3;
+    const int d = 16 * ((tile & 7) >> 1) + cq;
+    if (hh < A.H + A.KV) {
+      const float* cs = A.cos_sin + (size_t)A.positions[m] * 128;
+      p.c = *reinterpret_cast<const f32x4*>(cs + d);
+      p.sn = *reinterpret_cast<const f32x4*>(cs + 64 + d);
+    }
+    if (hh >= A.H) p.slot = A.slots[m];
+  }
+  return p;
+}
+
+// store_quad (packed_epi.h) on preloaded inputs: v / v2 already scaled by p.rs
+__device__ __forceinline__ float epi_pre(const Args& A, int m, int tile, int cq, f32x4 v, f32x4 v2, const Pre& p) {
+  if (A.epi == EP_SILU) return store_quad<EP_SILU>(A, m, tile, cq, v, v2);
+  if (A.epi == EP_PLAIN) return store_quad<EP_PLAIN>(A, m, tile, cq, v, v2);
+  if (A.epi == EP_ROPEPERM) return store_quad<EP_ROPEPERM>(A, m, tile, cq, v, v2);
+  if (A.epi == EP_RESID) {
+    bf16x4 o;
+    float sq = 0.f;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      o[r] = (bf16)(v[r] + (float)p.rv[r]);
+      const float f = (float)o[r];
+      sq = fmaf(f, f, sq);
+    }
+    *reinterpret_cast<bf16x4*>(A.y + (size_t)m * A.ldy + tile * 16 + cq) = o;
+    return sq;
+  }
+  // EP_ROPEKV: tile even = original head tile i (dims 16 i + cq ..), v2 = tile i + 4 (dims + 64)
+  const int hh = tile >> 3;
+  const int d = 16 * ((tile & 7) >> 1) + cq;
+  f32x4 o1 = v, o2 = v2;
+  if (hh < A.H + A.KV) {
+    o1 = v * p.c - v2 * p.sn;
+    o2 = v2 * p.c + v * p.sn;
+  }
+  bf16x4 b1, b2;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    b1[r] = (bf16)o1[r];
+    b2[r] = (bf16)o2[r];
+  }
+  if (hh < A.H) {
+    bf16* dst = A.q_out + ((size_t)m * A.H + hh) * 128;
+    *reinterpret_cast<bf16x4*>(dst + d) = b1;
+    *reinterpret_cast<bf16x4*>(dst + d + 64) = b2;
+  } else if (p.slot >= 0) {
+    const int blk = p.slot >> 4, off = p.slot & 15;
+    if (hh < A.H + A.KV) {
+      bf16* page = A.k_cache + ((size_t)blk * A.KV + (hh - A.H)) * 128 * 16;
+      *reinterpret_cast<bf16x4*>(page + ((size_t)(d >> 3) * 16 + off) * 8 + (d & 7)) = b1;
+      *reinterpret_cast<bf16x4*>(page + ((size_t)((d + 64) >> 3) * 16 + off) * 8 + (d & 7)) = b2;
+    } else {
+      bf16* page = A.v_cache + ((size_t)blk * A.KV + (hh - A.H - A.KV)) * 128 * 16 + off;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        page[(size_t)(d + r) * 16] = b1[r];
+        page[(size_t)(d + 64 + r) * 16] = b2[r];
+      }
+    }
+  }
+  return 0.f;
+}
+
 // MG: 16-row groups per workgroup (m_t = 16 MG rows); TPW: 16-column tiles per wave;
 // WT x WK waves (tile groups x k-step groups); D: register-ring depth in chunks.
 // A chunk is KC = 2 WK k-steps (64 WK k); each wave runs KW = 2 k-steps of every chunk.
@@ -300,6 +386,17 @@ __global__ __launch_bounds__(WT * WK * 64) void stream_gemm_kernel(const Args A)
     return;
   }
 
+  // ---- this wave's first reduction unit (most waves have exactly one): its epilogue inputs
+  // are loaded now, behind the slab stores and the barrier, not after the gather
+  const int TU = pair ? CT / 2 : CT;  // tile units
+  const int U = TU * MG;
+  const int u0 = s + A.S * wid;
+  Pre pre0{};
+  if (u0 < U) {
+    const int tl = pair ? 2 * (u0 / MG) : u0 / MG;
+    pre0 = preload(A, row0 + (u0 % MG) * 16 + cl, t0 + tl, 4 * g);
+  }
+
   // ---- publish this wave's partial fragments: slab (gid, s * WK + wk), fragment
   // f = tile_local * MG + mg, 1 KiB each (16 B per lane), write-through into uncached memory
   const int SV = A.S * WK;
@@ -323,8 +420,6 @@ __global__ __launch_bounds__(WT * WK * 64) void stream_gemm_kernel(const Args A)
   stamp(3);
 
   // ---- reduce 1/S of the group's fragments and run the epilogue on them
-  const int TU = pair ? CT / 2 : CT;  // tile units
-  const int U = TU * MG;
   const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(gslab, 0, SV * CT * MG * 1024, 0x00020000);
   for (int u = s + A.S * wid; u < U; u += A.S * W) {
     const int tu = u / MG, mg = u % MG;
@@ -360,8 +455,12 @@ __global__ __launch_bounds__(WT * WK * 64) void stream_gemm_kernel(const Args A)
     const int m = row0 + mg * 16 + cl;
     float sq = 0.f;
     if (m < A.M) {
-      const float rs = A.ss_in ? rsqrtf(A.ss_in[m] * inv_k + A.eps) : 1.f;
-      sq = epi_any(m, t0 + tl, v * rs, v2 * rs);
+      if (u == u0) {
+        sq = epi_pre(A, m, t0 + tl, 4 * g, v * pre0.rs, v2 * pre0.rs, pre0);
+      } else {
+        const float rs = A.ss_in ? rsqrtf(A.ss_in[m] * inv_k + A.eps) : 1.f;
+        sq = epi_any(m, t0 + tl, v * rs, v2 * rs);
+      }
     }
     if (A.ss_out) row_stat(mg, m, sq);
   }

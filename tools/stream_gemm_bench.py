@@ -33,6 +33,7 @@ ap.add_argument("--slabs", default="uncached", help="comma list of slab memories
                 "cached_rel (cached memory + producer release), cached (cached, no release: timing only)")
 ap.add_argument("--cold-mb", type=int, default=1024)
 ap.add_argument("--sweep", action="store_true", help="time every valid stream decomposition too")
+ap.add_argument("--row-groups", action="store_true", help="sweep also splits the rows into 2-4 groups")
 ap.add_argument("--out", default="")
 a = ap.parse_args()
 SHAPES = {"qkv": (6144, 4096, "rope_perm", True), "o": (4096, 4096, "resid", False),
@@ -67,10 +68,13 @@ def timeit(fn, ncopies):
 
 
 def plans_for(M, N, K, epi):
-    mg = 2 if M <= 32 else (4 if M <= 64 else 8)
-    if M <= 16:
-        mg = 2
-    rgs = [(mg, (M + 16 * mg - 1) // (16 * mg))]
+    rgs = []
+    for mg in (2, 4, 8):  # every row split into <= 4 groups whose last group holds rows
+        rg = (M + 16 * mg - 1) // (16 * mg)
+        if rg <= (4 if a.row_groups else 1 if mg < 8 or M <= 128 else 2) and 16 * mg * (rg - 1) < M:
+            rgs.append((mg, rg))
+    if not a.row_groups:  # the single-group plan of the smallest sufficient mg (round-4 sweeps)
+        rgs = rgs[:1] if rgs else [(8, (M + 127) // 128)]
     out = []
     tiles, KS = N // 16, K // 32
     for (mg_, rg), (tpw, wt, wk), S, D in itertools.product(rgs, WAVE_SHAPES, (1, 2, 4, 7, 8, 14, 16), (2, 4, 8, 16)):
@@ -133,6 +137,7 @@ for name in a.shapes.split(","):
         else:
             model = LlamaModel.__new__(LlamaModel)  # only the per-shape tables are used
             model.device = torch.device("cuda")
+            model.STREAM_CFG = {}  # the round-3 choice, whatever the current tables route
             path, cfg = LlamaModel._proj_path(model, name, M)
             f = kernels.prefill_gemm if path == "pf" else kernels.mid_gemm
             variants["r3"] = lambda i, f=f, cfg=cfg: f(x, wps[i], epi, **kw, **cfg)
