@@ -71,7 +71,9 @@ struct Args {
   const int* slots;
   const float* cos_sin;
   int H, KV;
-  int rel;  // 1: agent-scope release (L2 write-back) before arriving (diagnostics)
+  // bit 0: agent-scope release (L2 write-back) before arriving (diagnostics); bit 1: each
+  // workgroup starts its K slice at a different chunk (rotated order; HBM channel spread)
+  int rel;
   // diagnostics (null in the engine): per workgroup 8 wall-clock stamps (s_memrealtime, 100 MHz):
   // [0] start, [1] first chunk in LDS, [2] main loop done, [3] group barrier passed, [4] end
   unsigned long long* stamps;
@@ -245,6 +247,8 @@ __global__ __launch_bounds__(WT * WK * 64) void stream_gemm_kernel(const Args A)
   const int KS = A.K >> 5;
   const int kb0 = s * A.KSW;
   const int nch = A.KSW / KC;  // host: nch % D == 0, nch >= D
+  // rotated chunk order (rel bit 1): chunk c of this workgroup is K chunk (c + rot) % nch
+  const int rot = (A.rel & 2) ? (work * 5) % nch : 0;
 
   auto stamp = [&](int i) {
     if (A.stamps && threadIdx.x == 0) A.stamps[(size_t)bid * 8 + i] = __builtin_amdgcn_s_memrealtime();
@@ -282,7 +286,8 @@ __global__ __launch_bounds__(WT * WK * 64) void stream_gemm_kernel(const Args A)
   // barriers keep every chunk's loads in issue order, so the prologue and the loop body leave
   // the same per-register vmcnt distances and hipcc's counted waits stay at (D - 1) chunks
   // (without them it reordered the prologue and fell back to vmcnt(0) inside the loop).
-  auto issue = [&](int c, int d) {
+  auto issue = [&](int c0, int d) {
+    const int c = rot ? (c0 + rot) % nch : c0;
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int i = 0; i < LX; ++i) xr[d][i] = *reinterpret_cast<const bf16x8*>(xsrc[i] + (size_t)c * KC * 32);
@@ -416,7 +421,7 @@ __global__ __launch_bounds__(WT * WK * 64) void stream_gemm_kernel(const Args A)
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   int* ctr = A.counters + 2 * gid;
-  group_barrier(ctr, A.S, A.err, A.rel);
+  group_barrier(ctr, A.S, A.err, A.rel & 1);
   stamp(3);
 
   // ---- reduce 1/S of the group's fragments and run the epilogue on them

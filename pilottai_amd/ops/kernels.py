@@ -563,7 +563,9 @@ def stream_gemm(x: torch.Tensor, wp: torch.Tensor, epi: str = "plain", resid: Op
     """y = epi(rownorm(x) @ W.T) for 16 < M <= 256 with W packed by pack_decode_weight (gate_up:
     pack_decode_gate_up + "silu"; QKV: pack_decode_qkv_rope + "rope_perm"); same epilogue and
     row-statistics conventions as mid_gemm. `plan`: (mg, rg, tpw, wt, wk, S, D) or None for
-    the kernel's default decomposition (csrc/ops/gemm_stream.hip)."""
+    the kernel's default decomposition (csrc/ops/gemm_stream.hip).
+    rel: bit 0 = producer-side L2 release before the group barrier (diagnostics), bit 1 =
+    each workgroup streams its K slice from a rotated starting chunk."""
     M, K = x.shape
     N = wp.shape[0] * 16
     code = STREAM_EPI[epi]

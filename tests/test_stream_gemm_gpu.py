@@ -26,7 +26,7 @@ def _ref(x, w, epi, norm, resid):
     return acc
 
 
-def _check(gpu, M, N, K, epi, norm, plan, reps=3):
+def _check(gpu, M, N, K, epi, norm, plan, reps=3, rel=0):
     torch.manual_seed(31 + M)
     x = _bf(M, K, dev=gpu)
     w = _bf(N, K, dev=gpu, scale=0.05)
@@ -36,7 +36,7 @@ def _check(gpu, M, N, K, epi, norm, plan, reps=3):
     want = _ref(x, w, epi, norm, resid)
     _, _, err = ops.stream_workspace(gpu)
     for _ in range(reps):  # the group counters must reset themselves between launches
-        y = ops.stream_gemm(x, wp, epi, resid=resid, norm=norm, plan=plan)
+        y = ops.stream_gemm(x, wp, epi, resid=resid, norm=norm, plan=plan, rel=rel)
         torch.testing.assert_close(y.float(), want, atol=4e-2, rtol=2e-2)
     assert int(err[0]) == 0
 
@@ -70,6 +70,15 @@ def test_stream_gemm_llama8b_default_plans(gpu, M, N, K, epi, norm):
 ])
 def test_stream_gemm_plans(gpu, M, N, K, epi, norm, plan):
     _check(gpu, M, N, K, epi, norm, plan)
+
+
+@pytest.mark.parametrize("M,N,K,epi,norm,plan", [
+    (64, 6144, 4096, "rope_perm", True, None), (128, 4096, 14336, "resid", False, None),
+    (48, 28672, 4096, "silu", True, None), (64, 4096, 4096, "plain", False, (4, 1, 2, 4, 1, 1, 4))])
+def test_stream_gemm_rotated_chunk_order(gpu, M, N, K, epi, norm, plan):
+    """rel bit 1: every workgroup streams its K slice from a different starting chunk (the
+    accumulation order changes, the result must not beyond rounding)."""
+    _check(gpu, M, N, K, epi, norm, plan, rel=2)
 
 
 def test_stream_gemm_asymmetric_identity(gpu):

@@ -31,6 +31,7 @@ def main():
     ap.add_argument("--cases", default=DEFAULT)
     ap.add_argument("--cold-mb", type=int, default=1024)
     ap.add_argument("--out", default="")
+    ap.add_argument("--rel", type=int, default=0, help="stream_gemm rel bits (2: rotated K-chunk order)")
     a = ap.parse_args()
     out_f = open(a.out, "a") if a.out else None
     stamps = torch.zeros(8 * 8192, dtype=torch.int64, device="cuda")
@@ -53,7 +54,7 @@ def main():
         kw = dict(out=y, resid=resid, norm=nrm, ss_in=ss if nrm else None, plan=plan)
 
         def call(i, st=None):
-            kernels.stream_gemm(x, wps[i], epi, stamps=st, **kw)
+            kernels.stream_gemm(x, wps[i], epi, stamps=st, rel=a.rel, **kw)
 
         for i in range(len(wps)):
             call(i)
@@ -92,6 +93,11 @@ def main():
                "barrier_wait_us": [med(bar), round(float(bar.max()), 2)],
                "epilogue_us": [med(epi_t), round(float(epi_t.max()), 2)],
                "loop_end_spread_us": round(float(rel[:, 2].max() - rel[:, 2].min()), 2),
+               "rel": a.rel,
+               # per XCD (workgroup id % 8, the dispatcher's round robin): median loop time and
+               # median loop end, to tell a slow XCD from slow CUs spread over all of them
+               "loop_by_xcd_us": [med(loop[x::8]) for x in range(8)],
+               "loop_end_by_xcd_us": [med(rel[x::8, 2]) for x in range(8)],
                "weights_TBps_in_loop": round(N * K * 2 / 1e6 / max(1e-3, float(rel[:, 2].max() - rel[:, 1].min())), 2)}
         print(json.dumps(rec), flush=True)
         if out_f:
