@@ -157,6 +157,14 @@ def gemm_case(M, N, K, epi, splits, kind, **cfg):
         elif kind == "prefill":
             ops.prefill_gemm(x, wp, epi, resid=r if epi == "resid" else None, out=out, norm=(epi == "silu"),
                              splits=s, full=kw.get("full", -1) if s != 1 else -1)
+        elif kind == "stream":  # the hand-off-free baseline: the mid kernel without a K split
+            if sp == 1:
+                ops.mid_gemm(x, wp, epi, resid=r if epi == "resid" else None, out=out, norm=(epi == "silu"),
+                             splits=1)
+            else:
+                kernels.stream_workspace(dev)[0].fill_(NAN)
+                ops.stream_gemm(x, wp, epi, resid=r if epi == "resid" else None, out=out, norm=(epi == "silu"),
+                                plan=kw["plan"], rel=kw.get("rel", 0))
         elif kind == "wide":
             ops.wide_gemm(x, wp, epi, resid=r if epi == "resid" else None, out=out, norm=(epi == "silu"),
                           splits=s, **kw)
@@ -232,6 +240,17 @@ cases.append(("prefill o_resid M2048 S2 (256x256 tiles, every tile split)",
               lambda: gemm_case(2048, 4096, 4096, "resid", 2, "prefill", full=0)))
 cases.append(("prefill gate_up_silu M2048 (768 whole + 128 tiles x S2)",
               lambda: gemm_case(2048, 28672, 4096, "silu", 2, "prefill", full=768)))
+# weight-streaming kernel (gemm_stream.hip): cooperative split-K over uncached slabs; rel 0 =
+# sc1 slab stores + vmcnt(0) + relaxed arrive + acquire (shipped), rel 1 = plus the producer's
+# agent-scope release before arriving
+for rel in (0, 1):
+    for nm, M, N, K, epi, plan in (("qkv_plain M64", 64, 6144, 4096, "plain", (4, 1, 3, 2, 2, 4, 4)),
+                                   ("down_resid M64", 64, 4096, 14336, "resid", (4, 1, 2, 4, 1, 8, 4)),
+                                   ("o_resid M32 wk2", 32, 4096, 4096, "resid", (2, 1, 1, 4, 2, 4, 4)),
+                                   ("gate_up_silu M128", 128, 28672, 4096, "silu", (8, 1, 2, 7, 1, 2, 4))):
+        cases.append((f"stream {nm} S{plan[5]} rel{rel}",
+                      lambda M=M, N=N, K=K, epi=epi, plan=plan, rel=rel:
+                      gemm_case(M, N, K, epi, plan[5], "stream", plan=plan, rel=rel)))
 cases.append(("attention decode 48 seqs part256", lambda: attention_case(48, 3000, 256)))
 cases.append(("attention decode 8 seqs part512", lambda: attention_case(8, 4000, 512)))
 # 256- and 512-key partitions, 4- and 8-wave workgroups, 64 x ~1,000 and
