@@ -200,10 +200,20 @@ class LlamaModel:
     # (WIDE_MAX_T < T <= MID_MAX_T) replaces PF_CFG / MID_CFG there.
     # Rows only where tools/stream_gemm_bench.py (graph-replayed, cold weights, engine
     # epilogues) measured it ahead of the round-3 choice (profiles/r4_stream_gemm_*.jsonl).
-    STREAM_CFG: Dict[str, list] = {}
+    # (profiles/r4_stream_gemm_sweep_final.jsonl, interleaved, cold weights, us stream vs round 3:
+    #  o 32 / 64 / 128 rows: 13.4 / 14.6 / 18.9 vs 15.0 / 16.4 / 20.6 (256: 23.1 vs 22.3, not taken);
+    #  down 32 / 64 / 128 / 256: 27.1 / 29.8 / 35.7 / 49.6 vs 29.0 / 34.0 / 46.3 / 62.5;
+    #  qkv 32: 15.1 vs 16.0 (64 / 128 tie, 256 slower); gate_up: ties at 32, slower above)
+    STREAM_CFG: Dict[str, list] = {
+        "qkv": [(32, (1, 1, 4, 1, 2, 4))],
+        "o": [(64, (1, 1, 4, 1, 4, 4)), (128, (1, 1, 4, 1, 4, 2))],
+        "down": [(32, (1, 1, 4, 1, 4, 4)), (128, (1, 2, 4, 1, 8, 2)), (256, (2, 2, 8, 1, 7, 2))],
+    }
     # LM head of steps with more than 32 logit rows (<= 32: the packed decode kernel):
     # (largest rows, shape as STREAM_CFG) on the weight-streaming kernel; empty = hipBLASLt
-    LM_HEAD_STREAM: list = []
+    # (profiles/r4_stream_lm_head_sweep.jsonl: 24 / 48 / 64 / 128 rows 166 / 172 / 175 / 197 us
+    # vs 176 (packed decode kernel) / 210 / 210 / 235 (hipBLASLt); 17-32 rows included)
+    LM_HEAD_STREAM: list = [(32, (1, 3, 4, 1, 1, 2)), (64, (1, 4, 4, 1, 1, 2)), (128, (1, 2, 8, 1, 1, 2))]
     # decode/small steps: let the attention launch's idle workgroups read the O
     # projection's weights into the Infinity Cache (MALL-resident weights run the 34 MB
     # O projection at M=8 in 8.7 us vs 12.8 us cold, profiles/r2_mall_warm.jsonl). Off by
@@ -649,13 +659,15 @@ class LlamaModel:
         return self._lm_head(xs, num_logit_rows)
 
     def _lm_head(self, xs, n: int):
-        """Logits of the step's sampling rows on the packed weights: the decode kernel up to 32
-        rows, the weight-streaming kernel where LM_HEAD_STREAM covers n, else hipBLASLt."""
+        """Logits of the step's sampling rows on the packed weights: the weight-streaming kernel
+        where LM_HEAD_STREAM covers n (> 16 rows), else the packed decode kernel up to 32 rows,
+        else hipBLASLt."""
+        if n > self.DECODE_FUSED_MAX_T:
+            for mmax, shape in self.LM_HEAD_STREAM:
+                if n <= mmax:
+                    return ops.stream_gemm(xs, self.lm_head_p, "plain", plan=self._stream_plan(n, shape))
         if n <= 32:
             return ops.decode_gemm(xs, self.lm_head_p, "plain")
-        for mmax, shape in self.LM_HEAD_STREAM:
-            if n <= mmax:
-                return ops.stream_gemm(xs, self.lm_head_p, "plain", plan=self._stream_plan(n, shape))
         return ops.linear(xs, self.lm_head, "lm_head")
 
     # -- reference (dense, no cache) forward used by numerics tests ----------------
