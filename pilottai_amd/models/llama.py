@@ -211,6 +211,10 @@ class LlamaModel:
     }
     # LM head of steps with more than 32 logit rows (<= 32: the packed decode kernel):
     # (largest rows, shape as STREAM_CFG) on the weight-streaming kernel; empty = hipBLASLt
+    # the (N, K) each projection's STREAM_CFG rows were measured on (Llama-3-8B at TP = 1); other
+    # shapes (TP shards, other models) keep the round-3 choice. {} = rows apply to any shape.
+    STREAM_NK: Dict[str, tuple] = {"qkv": (6144, 4096), "o": (4096, 4096), "gate_up": (28672, 4096),
+                                   "down": (4096, 14336), "lm_head": (128256, 4096)}
     # (profiles/r4_stream_lm_head_sweep.jsonl: 24 / 48 / 64 / 128 rows 166 / 172 / 175 / 197 us
     # vs 176 (packed decode kernel) / 210 / 210 / 235 (hipBLASLt); 17-32 rows included)
     LM_HEAD_STREAM: list = [(32, (1, 3, 4, 1, 1, 2)), (64, (1, 4, 4, 1, 1, 2)), (128, (1, 2, 8, 1, 1, 2))]
@@ -578,12 +582,44 @@ class LlamaModel:
                 return (mg, rg, tpw, wt, wk, S, D)
         raise ValueError(f"no stream plan for M={M} with shape {shape}")
 
-    def _proj_path(self, kind: str, T: int):
-        """("stream" | "mid" | "pf", cfg) for projection `kind` on a T-token step."""
-        if T <= self.MID_MAX_T:
-            for mmax, shape in self.STREAM_CFG.get(kind, ()):
-                if T <= mmax:
-                    return "stream", {"plan": self._stream_plan(T, shape)}
+    @staticmethod
+    def _stream_plan_ok(plan, M: int, N: int, K: int, pair: bool) -> bool:
+        """Host mirror of gemm_stream.hip plan_ok (+ the workspace bound), so a table row that
+        does not fit a shape falls back instead of failing at launch."""
+        mg, rg, tpw, wt, wk, S, D = plan
+        tiles, KS, CT = N // 16, K // 32, tpw * wt
+        if N % 16 or K % 64 or tiles % CT or (pair and CT % 2) or KS % S or (KS // S) % (2 * wk):
+            return False
+        nch = KS // S // (2 * wk)
+        if nch < D or nch % D or 16 * mg * rg < M or 16 * mg * (rg - 1) >= M:
+            return False
+        grid = tiles // CT * rg * S
+        if S > 1 and grid > 256:
+            return False
+        from pilottai_amd.ops import kernels
+
+        return (tiles // CT) * rg * S * wk * CT * mg * 256 <= kernels.STREAM_WS_FLOATS
+
+    def _stream_for(self, kind: str, T: int, N: int, K: int, rows, pair: bool = False):
+        nk = self.STREAM_NK.get(kind)
+        if nk is not None and tuple(nk) != (N, K):
+            return None
+        for mmax, shape in rows:
+            if T <= mmax:
+                try:
+                    plan = self._stream_plan(T, shape)
+                except ValueError:
+                    return None
+                return plan if self._stream_plan_ok(plan, T, N, K, pair) else None
+        return None
+
+    def _proj_path(self, kind: str, T: int, N: int = 0, K: int = 0):
+        """("stream" | "mid" | "pf", cfg) for projection `kind` (N x K weights) on a T-token step."""
+        if T <= self.MID_MAX_T and N:
+            plan = self._stream_for(kind, T, N, K, self.STREAM_CFG.get(kind, ()),
+                                    pair=kind in ("qkv", "gate_up"))
+            if plan is not None:
+                return "stream", {"plan": plan}
         if self.device.type == "cuda" and (T > self.MID_MAX_T or kind in self.PF_MIDRANGE):
             for mmax, path, cfg in self.PF_CFG[kind]:
                 if T <= mmax:
@@ -591,7 +627,7 @@ class LlamaModel:
         return "mid", self._mid_cfg(kind, T)
 
     def _gemm(self, kind: str, T: int, x, wp, epi: str, **kw):
-        path, cfg = self._proj_path(kind, T)
+        path, cfg = self._proj_path(kind, T, wp.shape[0] * 16, wp.shape[1] * 32)
         fn = {"pf": ops.prefill_gemm, "stream": ops.stream_gemm}.get(path, ops.mid_gemm)
         return fn(x, wp, epi, **cfg, **kw)
 
@@ -600,7 +636,7 @@ class LlamaModel:
         if T <= min(self.DEC_QKV_MAX_T, 64) and self.device.type == "cuda":
             return ops.decode_qkv_rope(x, wp, eps, q, k_cache, v_cache, meta.positions, meta.slots, self.cos_sin,
                                        H, KVh)
-        path, cfg = self._proj_path("qkv", T)
+        path, cfg = self._proj_path("qkv", T, wp.shape[0] * 16, wp.shape[1] * 32)
         fn = {"pf": ops.prefill_qkv_rope, "stream": ops.stream_qkv_rope}.get(path, ops.mid_qkv_rope)
         return fn(x, wp, eps, q, k_cache, v_cache, meta.positions, meta.slots, self.cos_sin, H, KVh,
                   ss_in=ss_in, **cfg)
@@ -663,9 +699,10 @@ class LlamaModel:
         where LM_HEAD_STREAM covers n (> 16 rows), else the packed decode kernel up to 32 rows,
         else hipBLASLt."""
         if n > self.DECODE_FUSED_MAX_T:
-            for mmax, shape in self.LM_HEAD_STREAM:
-                if n <= mmax:
-                    return ops.stream_gemm(xs, self.lm_head_p, "plain", plan=self._stream_plan(n, shape))
+            wp = self.lm_head_p
+            plan = self._stream_for("lm_head", n, wp.shape[0] * 16, wp.shape[1] * 32, self.LM_HEAD_STREAM)
+            if plan is not None:
+                return ops.stream_gemm(xs, wp, "plain", plan=plan)
         if n <= 32:
             return ops.decode_gemm(xs, self.lm_head_p, "plain")
         return ops.linear(xs, self.lm_head, "lm_head")

@@ -437,7 +437,7 @@ def test_stream_routing_tables_route_mid_steps(monkeypatch):
         calls.clear()
         eng = LLMEngine(EngineConfig(model="tiny", max_num_seqs=8, use_graphs=False, decode_fused=True,
                                      num_kv_blocks=256, max_model_len=512, token_align=0,
-                                     model_overrides={"STREAM_CFG": table} if routed else None))
+                                     model_overrides={"STREAM_CFG": table, "STREAM_NK": {}} if routed else None))
         seen = []
         fwd = eng.model.forward
 
@@ -459,6 +459,28 @@ def test_stream_routing_tables_route_mid_steps(monkeypatch):
         else:
             assert not calls
     torch.testing.assert_close(logits[True], logits[False])
+
+
+def test_stream_routing_is_shape_checked():
+    """Table rows apply only to the (N, K) they were measured on, and a row whose plan does
+    not fit the shape (K split not dividing K, too many workgroups) falls back."""
+    from pilottai_amd.models.llama import LlamaModel
+
+    m = LlamaModel.__new__(LlamaModel)
+    m.STREAM_CFG = {"down": [(256, (2, 2, 8, 1, 7, 2))], "o": [(64, (1, 1, 4, 1, 4, 4))]}
+    m.STREAM_NK = {"down": (4096, 14336)}
+    m.MID_MAX_T = 256
+    m.PF_MIDRANGE = frozenset()
+    m.PF_CFG = LlamaModel.PF_CFG
+    m.MID_CFG = LlamaModel.MID_CFG
+    import torch
+
+    m.device = torch.device("cpu")
+    assert m._proj_path("down", 200, 4096, 14336)[0] == "stream"
+    assert m._proj_path("down", 200, 512, 1792)[0] == "mid"  # a TP shard: not the measured shape
+    assert m._proj_path("o", 64, 1024, 1024)[0] == "stream"  # no shape key: any shape that fits
+    assert m._proj_path("o", 64, 1024, 192)[0] == "mid"  # K = 192: 6 k-steps do not split 4 ways
+    assert m._proj_path("o", 100, 1024, 1024)[0] == "mid"  # beyond the table
 
 
 def test_engine_fails_on_custom_allreduce_timeout():
