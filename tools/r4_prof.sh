@@ -1,0 +1,4 @@
+# round-4 GPU job: marker-bounded kernel profiles of the final tree at 64 and 8 workers
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+WORKERS=64 bash tools/gpu_tasks.sh r4_prof64 prof && WORKERS=8 bash tools/gpu_tasks.sh r4_prof8 prof
