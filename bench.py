@@ -328,6 +328,7 @@ async def run_rank(a, rank: int, world: int, device):
         "prompt_tokens": u1["prompt_tokens"] - u0["prompt_tokens"],
         "completion_tokens": u1["completion_tokens"] - u0["completion_tokens"],
         "busy_s": st1["busy_s"] - st0["busy_s"], "prefix_hit": em["prefix_cache_hit_tokens"],
+        "graph_captures": st1.get("graph_captures", 0) - st0.get("graph_captures", 0),
         "prefix_defers": em["prefix_defers"],
         "spec_rows": em.get("spec_rows", 0),
         "spec_voided": em.get("spec_voided", 0),
@@ -382,7 +383,7 @@ async def run_cpu_rank(a, rank: int, world: int, n_local: int):
     for ag in agents:
         await ag.stop()
     zero = {k: 0 for k in ("tokens", "steps", "sampled", "busy_s", "prefix_hit", "prefix_defers", "spec_rows",
-                           "spec_voided", "bucket_tokens", "prompt_total", "hbm_used_gb")}
+                           "spec_voided", "bucket_tokens", "prompt_total", "hbm_used_gb", "graph_captures")}
     return dict(zero, dt=dt, tasks=0, lat=[], init_s=init_s, requeued=0, loop_lag=[], executions_by_rank=None,
                 managers=0, dp_mode="node", calls=len(llm.calls) if hasattr(llm, "calls") else 0, prompt_tokens=0,
                 completion_tokens=0, async_steps=False, host_phases={}, req_lat={}, memory=None, node_load=None,
@@ -515,6 +516,9 @@ def main():
             "spec_rows": tot("spec_rows"),
             "spec_voided": tot("spec_voided"),
             "graph_pad_frac": round(1 - tot("tokens") / max(1, tot("bucket_tokens")), 3),
+            # hipGraphs captured on first use inside the timed region (top-k/top-p or
+            # embedding variants of a bucket; each one stalls the engine for tens of ms)
+            "graph_captures_timed": tot("graph_captures"),
             # rank 0's engine thread, ms per step: schedule / copy+launch / wait for the device /
             # commit / deliver (the host phases are the device's idle time between steps)
             "step_phase_ms": {(k[:-2] if k.endswith("_s") else k): round(1000 * v / max(1, gathered[0]["steps"]), 3)

@@ -333,7 +333,7 @@ class LLMEngine:
         self.timings: "deque" = deque(maxlen=1 << 20)  # (ttft_s, tpot_s, output_tokens) per request
         self.stats = {"steps": 0, "tokens": 0, "sampled": 0, "requests": 0, "finished": 0,
                       "embed_requests": 0, "embed_tokens": 0,
-                      "busy_s": 0.0, "prefill_tokens": 0, "decode_steps": 0, "graph_replays": 0,
+                      "busy_s": 0.0, "prefill_tokens": 0, "decode_steps": 0, "graph_replays": 0, "graph_captures": 0,
                       "bucket_tokens": 0, "host_sched_s": 0.0, "host_launch_s": 0.0, "device_wait_s": 0.0,
                       "host_commit_s": 0.0, "host_deliver_s": 0.0}
         self.bucket_hist: Dict[int, list] = {}  # bucket -> [steps, seconds]
@@ -444,6 +444,7 @@ class LLMEngine:
             pool = self._embed_pool.clone()
             samp = self._sampled_dev.clone()  # the previous step's tokens (pipelined mode)
             self.capture_graphs([bucket], trunc=trunc, embed=embed)  # clobbers the device metadata
+            self.stats["graph_captures"] += 1  # a first-use capture inside serving (tens of ms)
             self._dev_meta[:n_copy].copy_(saved)
             self._embed_pool.copy_(pool)
             self._sampled_dev.copy_(samp)
