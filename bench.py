@@ -139,6 +139,7 @@ async def run_rank(a, rank: int, world: int, device):
         memory, lookup = build_memory(a, device)
     eng = LLMEngine(EngineConfig(model=a.model if not a.cpu else "tiny", max_num_seqs=max(64, 2 * n_local),
                                  max_num_batched_tokens=a.max_batched_tokens,
+                                 max_prefill_tokens=a.max_batched_tokens,
                                  kv_cache_gb=None if a.cpu else (a.kv_gb if a.kv_gb is not None else
                                                                  (48.0 / max(1, world) if a.share_gpu else None)),
                                  kv_cache_fraction=0.85,
