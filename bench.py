@@ -99,6 +99,9 @@ def parse():
     ap.add_argument("--memory-min-batch", type=int, default=1,
                     help="lookups a pass waits for (up to --memory-wait-ms) before it starts")
     ap.add_argument("--memory-wait-ms", type=float, default=0.0)
+    ap.add_argument("--embed-pooling", default="last", choices=["mean", "last"],
+                    help="--embedder engine: last-token states (embedding requests reuse the prefix cache: an "
+                         "agent's successive lookups share the task text) or mean pooling (no reuse)")
     ap.add_argument("--embedder", default="hashing", choices=["hashing", "engine"],
                     help="memory text encoder: feature hashing, or the serving model itself (embedding "
                          "requests in the engine's continuous batch, SURVEY N11)")
@@ -163,7 +166,8 @@ async def run_rank(a, rank: int, world: int, device):
         # states of embedding requests inside the engine's continuous batch
         from pilottai_amd.memory.embedding import EngineEmbedder
 
-        memory.embedder = EngineEmbedder(eng, dim=memory.index.dim, pool="engine", max_tokens=256)
+        memory.embedder = EngineEmbedder(eng, dim=memory.index.dim, pool="engine", max_tokens=256,
+                                         pooling=a.embed_pooling)
     eng.start()
     llm = LocalLLM(LLMConfig(model_name=eng.model_cfg.name, temperature=a.temperature, max_tokens=1024,
                              retry_attempts=1), engine=eng)
@@ -289,6 +293,8 @@ async def run_rank(a, rank: int, world: int, device):
                # the encoder's work when the serving model embeds (--embedder engine):
                # embedding requests and their prefilled tokens inside the continuous batch
                "embedder": a.embedder,
+               "embed_pooling": a.embed_pooling if a.embedder == "engine" else None,
+               "embed_cached_tokens": st1.get("embed_cached_tokens", 0) - st0.get("embed_cached_tokens", 0),
                "embed_requests": st1["embed_requests"] - st0["embed_requests"],
                "embed_tokens": st1["embed_tokens"] - st0["embed_tokens"],
                "embed_token_share": round((st1["embed_tokens"] - st0["embed_tokens"]) /

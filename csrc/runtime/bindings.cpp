@@ -153,13 +153,14 @@ PYBIND11_MODULE(_runtime, m) {
            [](Scheduler& s, int64_t id, const std::vector<int32_t>& prompt, float temperature,
               int32_t max_tokens, int64_t seed, bool ignore_eos,
               const std::vector<int32_t>& stop_ids, const py::object& grammar, int32_t top_k,
-              float top_p, bool embed) {
+              float top_p, bool embed, bool embed_last) {
              s.add_request(id, prompt, temperature, max_tokens, seed, ignore_eos, stop_ids,
-                           make_grammar(grammar), top_k, top_p, embed);
+                           make_grammar(grammar), top_k, top_p, embed, embed_last);
            },
            py::arg("id"), py::arg("prompt"), py::arg("temperature"), py::arg("max_tokens"),
            py::arg("seed"), py::arg("ignore_eos"), py::arg("stop_ids"), py::arg("grammar"),
-           py::arg("top_k") = 0, py::arg("top_p") = 1.0f, py::arg("embed") = false)
+           py::arg("top_k") = 0, py::arg("top_p") = 1.0f, py::arg("embed") = false,
+           py::arg("embed_last") = false)
       .def("schedule", [](Scheduler& s, uintptr_t buf) {
         py::gil_scoped_release nogil;
         return s.schedule(reinterpret_cast<int32_t*>(buf));

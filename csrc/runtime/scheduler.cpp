@@ -57,7 +57,7 @@ Scheduler::Scheduler(const SchedulerConfig& cfg)
 void Scheduler::add_request(int64_t id, std::vector<int32_t> prompt, float temperature,
                             int32_t max_tokens, int64_t seed, bool ignore_eos,
                             std::vector<int32_t> stop_ids, std::unique_ptr<Grammar> grammar,
-                            int32_t top_k, float top_p, bool embed) {
+                            int32_t top_k, float top_p, bool embed, bool embed_last) {
   auto s = std::make_unique<Sequence>();
   s->id = id;
   if ((int32_t)prompt.size() >= cfg_.max_model_len)
@@ -74,6 +74,7 @@ void Scheduler::add_request(int64_t id, std::vector<int32_t> prompt, float tempe
   s->stop_ids = std::move(stop_ids);
   s->grammar = embed ? nullptr : std::move(grammar);
   s->embed = embed;
+  s->embed_last = embed && embed_last;
   s->arrival = arrival_counter_++;
   // a grammar that starts with forced text (e.g. '{"key": ') is jump-forwarded into the prompt
   if (s->grammar) {
@@ -125,7 +126,7 @@ bool Scheduler::ensure_blocks(Sequence* s, int32_t upto_tokens) {
 
 void Scheduler::match_prefix(Sequence* s) {
   const int32_t B = cfg_.block_size;
-  if (cfg_.prefix_caching && !s->embed) {
+  if (cfg_.prefix_caching && (!s->embed || s->embed_last)) {
     const int32_t n_full = ((int32_t)s->tokens.size() - 1) / B;  // never reuse the last token
     uint64_t parent = 0;
     for (int32_t b = 0; b < n_full; ++b) {
@@ -391,7 +392,8 @@ int32_t Scheduler::schedule(int32_t* buf) {
       ids[T + j] = !p.spec ? s->tokens[ppos] : (j == 0 ? -(p.src_idx + 1) : p.run[j - 1]);
       pos[T + j] = ppos;
       slots[T + j] = s->blocks[ppos / B] * B + ppos % B;
-      er[T + j] = erow;
+      // last-token pooling: only the prompt's final token feeds the request's pooling row
+      er[T + j] = (s->embed_last && ppos + 1 != (int32_t)s->tokens.size()) ? L.max_seqs : erow;
     }
     if (s->embed_slot >= 0) nembed += n;
     const int32_t nb = (ctx + B - 1) / B;

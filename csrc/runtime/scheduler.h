@@ -86,6 +86,9 @@ struct SeqOutput {
 
 struct Sequence {
   int64_t id;
+  // embedding request pooled from its LAST token's final hidden state: the prompt may then
+  // reuse cached prefix blocks (a token's hidden state depends only on its prefix)
+  bool embed_last = false;
   std::vector<int32_t> tokens;
   int32_t prompt_len = 0;
   int32_t num_computed = 0;
@@ -132,7 +135,7 @@ class Scheduler {
   void add_request(int64_t id, std::vector<int32_t> prompt, float temperature, int32_t max_tokens,
                    int64_t seed, bool ignore_eos, std::vector<int32_t> stop_ids,
                    std::unique_ptr<Grammar> grammar, int32_t top_k = 0, float top_p = 1.0f,
-                   bool embed = false);
+                   bool embed = false, bool embed_last = false);
   bool abort(int64_t id);
   // Fill `buf` (layout()) for the next step. Returns the number of tokens in the
   // step (0 = nothing to run).

@@ -37,7 +37,7 @@ from collections import deque
 import threading
 import time
 from dataclasses import dataclass, field
-from typing import Any, Callable, Dict, List, Optional, Sequence
+from typing import Any, Callable, Dict, List, Optional, Sequence, Union
 
 import numpy as np
 import torch
@@ -169,6 +169,7 @@ class _Request:
     top_k: int = 0
     top_p: float = 1.0
     embed: bool = False
+    embed_last: bool = False  # last-token pooling (prefix-cache reuse allowed)
 
 
 class LLMEngine:
@@ -501,13 +502,17 @@ class LLMEngine:
     def submit(self, prompt_ids: Sequence[int], callback: Callable[[GenerationOutput], None], *,
                temperature: float = 0.7, max_tokens: int = 256, seed: Optional[int] = None,
                ignore_eos: bool = False, stop_ids: Sequence[int] = (), grammar: Optional[list] = None,
-               request_id: Optional[int] = None, top_k: int = 0, top_p: float = 1.0, embed: bool = False) -> int:
+               request_id: Optional[int] = None, top_k: int = 0, top_p: float = 1.0,
+               embed: Union[bool, str] = False) -> int:
         """Thread-safe; `callback` runs on the engine thread when the request finishes.
 
         top_k > 0 / top_p < 1 truncate the (grammar-masked) distribution before
-        sampling (exact threshold kernel, csrc/ops/sampling.hip). embed=True: an embedding
-        request — the prompt is prefilled in the continuous batch (no prefix-cache reuse),
-        nothing is sampled, and the output carries the mean final-norm hidden state."""
+        sampling (exact threshold kernel, csrc/ops/sampling.hip). embed=True (or "mean"): an
+        embedding request — the prompt is prefilled in the continuous batch (no prefix-cache
+        reuse), nothing is sampled, and the output carries the mean final-norm hidden state.
+        embed="last": the final-norm hidden state of the prompt's last token; since a token's
+        state depends only on its prefix, such requests reuse cached prefix blocks (shared
+        task text across an agent's lookups is computed once)."""
         if self._err is not None:
             raise RuntimeError(f"engine failed: {self._err!r}")
         rid = request_id if request_id is not None else self.new_request_id()
@@ -515,7 +520,7 @@ class LLMEngine:
             seed = (self.cfg.seed * 0x9E3779B1 + rid * 0x85EBCA77) & 0x7FFFFFFFFFFFFFFF
         req = _Request(rid, list(prompt_ids), float(temperature), int(max_tokens), int(seed),
                        bool(ignore_eos), list(stop_ids), grammar, callback, self._rt.now(),
-                       int(top_k or 0), float(1.0 if top_p is None else top_p), bool(embed))
+                       int(top_k or 0), float(1.0 if top_p is None else top_p), bool(embed), embed == "last")
         self._inbox.put(req)
         self._wake.set()
         return rid
@@ -550,11 +555,15 @@ class LLMEngine:
             raise RuntimeError(f"engine failed: {self._err!r}")
         return [results[i] for i in ids]
 
-    def embed(self, prompts: Sequence[Sequence[int]]) -> np.ndarray:
-        """Mean final-norm hidden state of each prompt, [B, hidden] fp32, computed as
-        embedding requests inside the continuous batch (the engine's own kernels and
-        graphs, batched with whatever else is running). Blocking; thread-safe."""
-        outs = self.generate([list(p) or [0] for p in prompts], embed=True, temperature=0.0, max_tokens=1)
+    def embed(self, prompts: Sequence[Sequence[int]], pooling: str = "mean") -> np.ndarray:
+        """Final-norm hidden state of each prompt, mean-pooled (pooling="mean") or of its last
+        token ("last": reuses cached prefix blocks), [B, hidden] fp32, computed as embedding
+        requests inside the continuous batch (the engine's own kernels and graphs, batched
+        with whatever else is running). Blocking; thread-safe."""
+        if pooling not in ("mean", "last"):
+            raise ValueError(f"pooling must be 'mean' or 'last', not {pooling!r}")
+        outs = self.generate([list(p) or [0] for p in prompts], embed="last" if pooling == "last" else True,
+                             temperature=0.0, max_tokens=1)
         bad = [o.finish_reason for o in outs if o.embedding is None]
         if bad:
             raise RuntimeError(f"embedding requests did not complete: {bad}")
@@ -714,7 +723,8 @@ class LLMEngine:
                 break
             self._reqs[req.rid] = req
             self.sched.add_request(req.rid, req.prompt_ids, req.temperature, req.max_tokens, req.seed,
-                                   req.ignore_eos, req.stop_ids, req.grammar, req.top_k, req.top_p, req.embed)
+                                   req.ignore_eos, req.stop_ids, req.grammar, req.top_k, req.top_p, req.embed,
+                                   req.embed_last)
             self.stats["requests"] += 1
         while True:
             try:
@@ -732,11 +742,12 @@ class LLMEngine:
             emb = self._embed_ready.pop(eslot)
         elif eslot >= 0:  # (aborted / not yet read) the request's pooling row: read and clear it
             if reason == 3:
-                emb = (self._embed_pool[eslot] / max(1, plen)).cpu().numpy()
+                emb = (self._embed_pool[eslot] / self._pool_div(rid, plen)).cpu().numpy()
             self._embed_pool[eslot].zero_()
         if reason == 3:
             self.stats["embed_requests"] += 1
             self.stats["embed_tokens"] += plen - cached
+            self.stats["embed_cached_tokens"] = self.stats.get("embed_cached_tokens", 0) + cached
         req = self._reqs.pop(rid, None)
         self.stats["finished"] += 1
         if req is None:
@@ -918,7 +929,7 @@ class LLMEngine:
         the device while it is idle (step synchronised). Pipelined loop: from `host`, the
         pinned snapshot taken behind this step (the next step is already queued, so a device
         read would wait for it too). Delivery runs during the NEXT step either way."""
-        done = [(o[9], max(1, o[3])) for o in outs if o[9] >= 0 and o[2] == 3]
+        done = [(o[9], self._pool_div(o[0], o[3])) for o in outs if o[9] >= 0 and o[2] == 3]
         if not done:
             return
         slots = [e for e, _ in done]
@@ -928,6 +939,11 @@ class LLMEngine:
         self._embed_pool.index_fill_(0, idx, 0.0)
         for (e, plen), r in zip(done, rows):
             self._embed_ready[e] = r / plen
+
+    def _pool_div(self, rid: int, plen: int) -> int:
+        """Tokens pooled into an embedding request's row: its prompt (mean), or 1 (last)."""
+        req = self._reqs.get(rid)
+        return 1 if (req is not None and req.embed_last) else max(1, plen)
 
     def _flush_deliveries(self):
         if self._pending_out:

@@ -58,8 +58,9 @@ class HashingEmbedder:
 
 class EngineEmbedder:
     """Embeddings from the serving model itself: final-norm hidden states
-    mean-pooled over the text's tokens, projected to `dim` by a fixed orthonormal matrix
-    and L2-normalised; texts truncated to `max_tokens`.
+    mean-pooled over the text's tokens (pooling="last": the last token's state, which lets
+    the engine reuse cached prefixes), projected to `dim` by a fixed orthonormal matrix and
+    L2-normalised; texts truncated to `max_tokens`.
 
     pool="engine" (default): embedding requests through `LLMEngine.embed` — prefilled by
     the engine's kernels inside its continuous batch, pooled in the step graph.
@@ -68,7 +69,7 @@ class EngineEmbedder:
     of the input token embeddings."""
 
     def __init__(self, engine, dim: int = 1024, seed: int = 0, pool: str = "engine", batch_size: int = 16,
-                 max_tokens: int = 512):
+                 max_tokens: int = 512, pooling: str = "mean"):
         import torch
 
         self.engine = engine
@@ -83,6 +84,11 @@ class EngineEmbedder:
         self.pool = pool if (pool == "engine" or getattr(engine.model.tp, "size", 1) == 1) else "tokens"
         self.batch_size = batch_size
         self.max_tokens = max_tokens
+        if pooling not in ("mean", "last"):
+            raise ValueError(f"pooling must be 'mean' or 'last', not {pooling!r}")
+        # "last": the last token's state — embedding requests then reuse the engine's prefix
+        # cache (texts that share a prefix, like an agent's successive lookups, share its work)
+        self.pooling = pooling
 
     def embed(self, texts: Sequence[str]) -> np.ndarray:
         import torch
@@ -94,13 +100,13 @@ class EngineEmbedder:
             ids = [self.engine.tok.encode(t)[: self.max_tokens] or [0] for t in texts]
             if not ids:
                 return np.zeros((0, self.dim), np.float32)
-            h = torch.from_numpy(self.engine.embed(ids)).to(self.proj.device)
+            h = torch.from_numpy(self.engine.embed(ids, pooling=self.pooling)).to(self.proj.device)
             return F.normalize(h @ self.proj, dim=1).cpu().numpy()
         with torch.inference_mode():
             if self.pool == "hidden":
                 for i in range(0, len(texts), self.batch_size):
                     ids = [self.engine.tok.encode(t)[: self.max_tokens] or [0] for t in texts[i:i + self.batch_size]]
-                    v = F.normalize(m.hidden_states(ids) @ self.proj, dim=1)
+                    v = F.normalize(m.hidden_states(ids, pooling=self.pooling) @ self.proj, dim=1)
                     rows.extend(v.cpu().numpy())
             else:
                 for t in texts:

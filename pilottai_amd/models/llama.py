@@ -740,8 +740,9 @@ class LlamaModel:
 
     # -- dense batched encoder forward (semantic-memory embeddings) ----
     @torch.no_grad()
-    def hidden_states(self, batch: List[List[int]]) -> torch.Tensor:
-        """Final-norm hidden states mean-pooled over each sequence's tokens: [B, d].
+    def hidden_states(self, batch: List[List[int]], pooling: str = "mean") -> torch.Tensor:
+        """Final-norm hidden states mean-pooled over each sequence's tokens (pooling="last":
+        the state of each sequence's last token): [B, d].
 
         A dense bf16 causal forward (library GEMMs + SDPA attention, no KV cache),
         right-padded to the longest sequence; used by EngineEmbedder to embed
@@ -781,5 +782,8 @@ class LlamaModel:
             g, u = gu.chunk(2, dim=-1)
             h = h + F.linear(F.silu(g) * u, L["w2"])
         x = F.rms_norm(h, (cfg.hidden_size,), self.norm, cfg.rms_eps).float()
+        if pooling == "last":
+            last = torch.tensor([max(1, len(s)) - 1 for s in batch], device=dev)
+            return x[torch.arange(B, device=dev), last]
         w = valid.unsqueeze(-1).float()
         return (x * w).sum(1) / w.sum(1).clamp_min(1.0)

@@ -205,6 +205,34 @@ def test_engine_embedding_requests_match_dense_forward(tok, async_steps):
     assert w.shape == (2, 64) and abs(float((w[0] * w[1]).sum()) - 1.0) < 1e-4
 
 
+def test_engine_last_token_embeddings_reuse_prefix_cache(tok):
+    """embed(pooling="last"): the last token's final-norm hidden state, equal to the dense
+    reference forward's; such requests reuse cached prefix blocks (a second text sharing a
+    long prefix computes only its new tokens) and still give the reference's vector."""
+    import torch
+
+    from pilottai_amd.engine.engine import EngineConfig, LLMEngine
+
+    e = LLMEngine(EngineConfig(model="tiny", max_num_seqs=8, max_num_batched_tokens=64, max_model_len=512,
+                               num_kv_blocks=128), device="cpu")
+    base = tok.encode("Task: summarize the quarterly report and list the key findings. " * 6)[:120]
+    a, b = base + [11, 12, 13], base + [21, 22]
+    va = e.embed([a], pooling="last")
+    t0 = e.stats["embed_tokens"]
+    vb = e.embed([b], pooling="last")
+    new_b = e.stats["embed_tokens"] - t0
+    ref = e.model.hidden_states([a, b], pooling="last").float()
+    got = torch.from_numpy(__import__("numpy").concatenate([va, vb]))
+    rel = (got - ref).norm(dim=1) / ref.norm(dim=1)
+    assert float(rel.max()) < 2e-2, rel
+    assert len(base) >= 64
+    assert new_b <= len(b) - 16 * (len(base) // 16), new_b  # the shared prefix's blocks came from the cache
+    vm = e.embed([b])  # mean pooling: no prefix reuse, the dense mean
+    refm = e.model.hidden_states([b]).float()
+    assert float(((torch.from_numpy(vm) - refm).norm() / refm.norm())) < 2e-2
+    assert float(e._embed_pool[:-1].abs().sum()) == 0.0
+
+
 def test_reference_sampler_masks_and_forced():
     V = 256
     logits = torch.randn(3, V).to(torch.bfloat16)
