@@ -54,6 +54,7 @@ int pa_mid_gemm(void* y, const void* x, const void* wp, const void* resid, float
                 const float* cos_sin, int H, int KV, hipStream_t st);
 int pa_row_sumsq(float* out, const void* x, int M, int K, int ldx, hipStream_t st);
 int pa_timeline_marker(int id, hipStream_t st);
+int pa_store_test(void* dst, long long n16, int mode, int grid, hipStream_t st);
 long long pa_stream_gemm_ws_floats(int M, int N, int K, int mg, int rg, int tpw, int wt, int wk, int S);
 void pa_stream_gemm_plan(int M, int N, int K, int epi, int* plan);
 int pa_stream_gemm(void* y, const void* x, const void* wp, const void* resid, float* ws, long long ws_floats,
@@ -874,6 +875,12 @@ at::Tensor empty_uncached(int64_t numel, at::ScalarType dtype, int64_t device) {
 }
 
 PYBIND11_MODULE(_C, m) {
+  m.def("store_test", [](at::Tensor dst, int64_t mode, int64_t grid) {
+    check_gpu(dst, "dst");
+    TORCH_CHECK(dst.is_contiguous() && dst.nbytes() % 16 == 0, "dst: contiguous, a multiple of 16 bytes");
+    check_rc(pa_store_test(dst.data_ptr(), (long long)(dst.nbytes() / 16), (int)mode, (int)grid, cur_stream()),
+             "store_test");
+  }, py::arg("dst"), py::arg("mode"), py::arg("grid") = 256, "diagnostics: fill dst with one store form");
   m.def("timeline_marker", [](int64_t id) { check_rc(pa_timeline_marker((int)id, cur_stream()), "timeline_marker"); },
         "empty marker kernel (0 = begin, 1 = end of a timed region) for profile cutting");
   m.def("empty_uncached", &empty_uncached, py::arg("numel"), py::arg("dtype"), py::arg("device"),
