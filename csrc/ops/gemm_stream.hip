@@ -619,7 +619,9 @@ extern "C" int pa_stream_gemm(void* y, const void* x, const void* wp, const void
   const int G = N / 16 / CT;
   const int groups = G * p.rg;
   if (!ws || !counters || !err || n_counters < 2 * groups) return 1;
-  if (pa_stream_gemm_ws_floats(M, N, K, p.mg, p.rg, p.tpw, p.wt, p.wk, p.S) > ws_floats) return 1;
+  // slabs only off the direct epilogue (a K split, or pair epilogues split over waves)
+  const bool direct = p.S * p.wk == 1 && (!(epi == EP_SILU || epi == EP_ROPEKV) || p.tpw % 2 == 0);
+  if (!direct && pa_stream_gemm_ws_floats(M, N, K, p.mg, p.rg, p.tpw, p.wt, p.wk, p.S) > ws_floats) return 1;
   const int grid = groups * p.S;
   Args a{(pa::bf16*)y, (const pa::bf16*)x, (const pa::bf16*)wp, (const pa::bf16*)resid, ws, counters, err,
          M, N, K, ldx, ldy, ldr, p.S, p.rg, G, K / 32 / p.S, epi, eps, ss_in, ss_out, ss_zero,

@@ -598,7 +598,8 @@ class LlamaModel:
             return False
         from pilottai_amd.ops import kernels
 
-        return (tiles // CT) * rg * S * wk * CT * mg * 256 <= kernels.STREAM_WS_FLOATS
+        direct = S * wk == 1 and (not pair or tpw % 2 == 0)  # no slabs (gemm_stream.hip)
+        return direct or (tiles // CT) * rg * S * wk * CT * mg * 256 <= kernels.STREAM_WS_FLOATS
 
     def _stream_for(self, kind: str, T: int, N: int, K: int, rows, pair: bool = False):
         nk = self.STREAM_NK.get(kind)

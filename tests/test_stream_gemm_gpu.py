@@ -67,6 +67,7 @@ def test_stream_gemm_llama8b_default_plans(gpu, M, N, K, epi, norm):
     (256, 4096, 14336, "resid", False, (8, 2, 2, 4, 1, 4, 4)),
     (96, 1280, 8192, "rope_perm", True, (8, 1, 2, 4, 1, 8, 2)),  # 70B TP=8 QKV shard
     (48, 128256, 4096, "plain", False, None),  # LM head
+    (200, 128256, 4096, "plain", False, None),  # LM head, two row groups, no K split
 ])
 def test_stream_gemm_plans(gpu, M, N, K, epi, norm, plan):
     _check(gpu, M, N, K, epi, norm, plan)
