@@ -763,7 +763,182 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void paged_attn_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------
+// Decode-sized steps (<= 16 tokens): attention and the O projection (+ residual) in ONE
+// launch (a persistent per-layer structure for the decode regime).
+//
+// Separate launches cost the O projection its whole weight stream (33.5 MB, ~8 us at
+// M = 8, 4.1 TB/s) after the attention launch (~12 us, latency-bound on 64 workgroups for
+// 8 rows) and a kernel boundary. Here the grid is one workgroup per CU (N / 16 = 256 O
+// tiles of 16 output columns for Llama-3-8B):
+//   * workgroups [0, units) run the attention units (item, KV head) exactly as the 8-wave
+//     paged_attn_kernel does; every other workgroup meanwhile loads its O tile's packed
+//     weights (K / 32 KiB, 128 KiB) into LDS by LDS-DMA;
+//   * each attention workgroup publishes its finished unit: stores drained, workgroup
+//     barrier, one agent-scope release, one relaxed ticket on sync[0]; then it loads its own
+//     O tile (its LDS is free again);
+//   * every workgroup waits (one lane, bounded spin, err flag on timeout) until sync[0]
+//     counts every unit, runs one agent-scope acquire, and computes its 16 columns for the
+//     <= 16 rows: 8 waves split K, partial tiles summed through LDS, residual added in place;
+//   * the last workgroup to leave resets sync[] (graph replay safe).
+// All workgroups must be resident at once: the launcher requires grid <= CU count and the
+// LDS (137 KiB) allows one workgroup per CU.
+struct AttnOArgs {
+  bf16* out;
+  float* part_o;
+  float* part_ml;
+  int* counters;
+  const bf16* q;
+  const bf16* k_cache;
+  const bf16* v_cache;
+  const int4* items;
+  const int* n_items;
+  const int* part_size;
+  const int* q_start;
+  const int* q_len;
+  const int* ctx_len;
+  const int* block_table;
+  int max_blocks, H, KV;
+  float scale_log2;
+  int acq;
+  const bf16* wo;  // packed [N / 16][K / 32][64][8]
+  bf16* h;         // [T, ldh], += out . Wo^T in place
+  int T, N, K, ldh;
+  int* sync;  // [2]: published units, departed workgroups (zero between launches)
+  int* err;   // 1 if a wait timed out (never in a healthy run)
+};
+
+template <int G>
+__global__ __launch_bounds__(512, 1) void attn_o_kernel(const AttnOArgs A) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int TPW = 16 / G;
+  const int bid = blockIdx.x, nwg = gridDim.x;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int units = A.n_items[0] * A.KV;
+  const int KS = A.K >> 5;
+  const int psz = A.part_size ? A.part_size[0] : ATT_PART;
+  const bf16* wt = A.wo + (size_t)bid * KS * 512;
+  auto load_w = [&]() {  // k-step ks of the tile -> smem + ks KiB (lane-linear, as packed)
+    for (int ks = wid; ks < KS; ks += 8)
+      __builtin_amdgcn_global_load_lds((att_gbl_t*)(wt + (size_t)ks * 512 + lane * 8),
+                                       (att_lds_t*)(smem + ks * 1024), 16, 0, 0);
+  };
+  const bool att = bid < units;
+  if (!att) load_w();
+  for (int u = bid; u < units; u += nwg) {
+    const int kvh = u % A.KV;
+    const int4 it = A.items[u / A.KV];
+    if ((it.z & 0xff) <= TPW)
+      decode_item<G, 8>(it, smem, A.out, A.part_o, A.part_ml, A.counters, A.q, A.k_cache, A.v_cache, A.q_start,
+                        A.q_len, A.ctx_len, A.block_table, A.max_blocks, A.H, A.KV, kvh, A.scale_log2, psz, A.acq);
+    else
+      prefill_any<G, 8>(it, smem, A.out, A.q, A.k_cache, A.v_cache, A.q_start, A.q_len, A.ctx_len, A.block_table,
+                        A.max_blocks, A.H, A.KV, kvh, A.scale_log2);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's output stores
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_fetch_add((gi32*)A.sync, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  if (att) {
+    __syncthreads();  // every wave is done with the attention LDS
+    load_w();
+  }
+  if (threadIdx.x == 0) {
+    unsigned spins = 0;
+    while (__hip_atomic_load((gi32*)A.sync, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < units) {
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins > (1u << 24)) {
+        __hip_atomic_store((gi32*)A.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's O-tile LDS-DMA landed
+  __syncthreads();
+
+  // O tile: 16 columns x <= 16 rows; wave w sums its K / 8 slice
+  const int c = lane & 15, g = lane >> 4;
+  const int per = KS >> 3;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  const bf16* xrow = A.out + (size_t)min(c, A.T - 1) * A.K + 8 * g;
+  const bool rowok = c < A.T;
+  for (int ks = wid * per; ks < (wid + 1) * per; ++ks) {
+    const bf16x8 wf = *reinterpret_cast<const bf16x8*>(smem + ks * 1024 + lane * 16);
+    bf16x8 xf = *reinterpret_cast<const bf16x8*>(xrow + ks * 32);
+    if (!rowok) xf = bf16x8{};
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf, xf, acc, 0, 0, 0);
+  }
+  f32x4* red = reinterpret_cast<f32x4*>(smem + KS * 1024);
+  red[wid * 64 + lane] = acc;
+  __syncthreads();
+  if (wid == 0 && rowok) {
+    f32x4 v = red[lane];
+#pragma unroll
+    for (int w = 1; w < 8; ++w) v += red[w * 64 + lane];
+    // lane (g, c): columns 16 bid + 4 g .. + 3 of row c
+    bf16* dst = A.h + (size_t)c * A.ldh + bid * 16 + 4 * g;
+    const bf16x4 r = *reinterpret_cast<const bf16x4*>(dst);
+    bf16x4 o;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o[j] = (bf16)(v[j] + (float)r[j]);
+    *reinterpret_cast<bf16x4*>(dst) = o;
+  }
+  if (threadIdx.x == 0) {  // the last workgroup out resets the counters for the next launch
+    const int d = __hip_atomic_fetch_add((gi32*)(A.sync + 1), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (d == nwg - 1) {
+      __hip_atomic_store((gi32*)A.sync, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store((gi32*)(A.sync + 1), 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
 }  // namespace pa
+
+// Fused attention + O projection (+ residual) for decode-sized steps; returns 1 if the shape
+// or the device does not allow it (the caller then runs the two launches), 0 on success.
+extern "C" int pa_attn_o(void* out, float* part_o, float* part_ml, const void* q, const void* k_cache,
+                         const void* v_cache, const int* items, const int* n_items, const int* part_size,
+                         int* counters, const int* q_start, const int* q_len, const int* ctx_len,
+                         const int* block_table, int max_blocks, int H, int KV, float scale_log2, const void* wo,
+                         void* h, int T, int N, int K, int ldh, int* sync, int* err, hipStream_t st) {
+  if (H % KV != 0 || T <= 0 || T > 16 || N % 16 != 0 || K != H * 128 || (K / 32) % 8 != 0) return 1;
+  const int grid = N / 16;
+  static int ncu = 0;
+  if (ncu == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      ncu = -1;
+  }
+  const int lds = std::max(pa::ATT_LDS_BYTES8, (K / 32) * 1024 + 8 * 1024);
+  if (ncu <= 0 || grid > ncu || lds > 160 * 1024) return 1;
+  const pa::AttnOArgs a{(pa::bf16*)out, part_o, part_ml, counters, (const pa::bf16*)q, (const pa::bf16*)k_cache,
+                        (const pa::bf16*)v_cache, (const int4*)items, n_items, part_size, q_start, q_len, ctx_len,
+                        block_table, max_blocks, H, KV, scale_log2, pa::g_handoff_attn, (const pa::bf16*)wo,
+                        (pa::bf16*)h, T, N, K, ldh, sync, err};
+#define PA_AO(GG)                                                                                          \
+  do {                                                                                                     \
+    static bool attr = false;  /* the whole 160 KiB once: any launch's size fits */                       \
+    if (!attr) {                                                                                           \
+      (void)hipFuncSetAttribute((const void*)pa::attn_o_kernel<GG>, hipFuncAttributeMaxDynamicSharedMemorySize, \
+                                160 * 1024);                                                               \
+      attr = true;                                                                                         \
+    }                                                                                                      \
+    hipLaunchKernelGGL((pa::attn_o_kernel<GG>), dim3(grid), dim3(512), lds, st, a);                        \
+  } while (0)
+  switch (H / KV) {
+    case 1: PA_AO(1); break;
+    case 2: PA_AO(2); break;
+    case 4: PA_AO(4); break;
+    case 8: PA_AO(8); break;
+    default: return 1;
+  }
+#undef PA_AO
+  return (int)hipGetLastError() == 0 ? 0 : -2;
+}
 
 // split_prefill > 0: two launches -- the prefill items [0, n_items[1]) on their own kernel
 // with a grid of split_prefill workgroups per KV head, then the decode items.

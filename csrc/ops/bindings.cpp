@@ -54,6 +54,11 @@ int pa_mid_gemm(void* y, const void* x, const void* wp, const void* resid, float
                 const float* cos_sin, int H, int KV, hipStream_t st);
 int pa_row_sumsq(float* out, const void* x, int M, int K, int ldx, hipStream_t st);
 int pa_timeline_marker(int id, hipStream_t st);
+int pa_attn_o(void* out, float* part_o, float* part_ml, const void* q, const void* k_cache, const void* v_cache,
+              const int* items, const int* n_items, const int* part_size, int* counters, const int* q_start,
+              const int* q_len, const int* ctx_len, const int* block_table, int max_blocks, int H, int KV,
+              float scale_log2, const void* wo, void* h, int T, int N, int K, int ldh, int* sync, int* err,
+              hipStream_t st);
 int pa_store_test(void* dst, long long n16, int mode, int grid, hipStream_t st);
 long long pa_stream_gemm_ws_floats(int M, int N, int K, int mg, int rg, int tpw, int wt, int wk, int S);
 void pa_stream_gemm_plan(int M, int N, int K, int epi, int* plan);
@@ -232,6 +237,42 @@ void paged_attention(at::Tensor out, at::Tensor part_o, at::Tensor part_ml, at::
                               block_table.size(1), H, KV, scale_log2, pf, pf_bytes, pf_sink, qptr, (int)waves,
                               cur_stream()),
            "paged_attention");
+}
+
+// Decode-sized steps: paged attention and h += out . Wo^T (packed) in one launch; false if
+// the shape / device does not allow it (attention.hip attn_o_kernel).
+bool attn_o(at::Tensor out, at::Tensor part_o, at::Tensor part_ml, at::Tensor q, at::Tensor k_cache,
+            at::Tensor v_cache, at::Tensor items, at::Tensor n_items, at::Tensor counters, at::Tensor q_start,
+            at::Tensor q_len, at::Tensor ctx_len, at::Tensor block_table, double scale,
+            c10::optional<at::Tensor> part_size, at::Tensor wo, at::Tensor h, at::Tensor sync, at::Tensor err) {
+  for (auto* t : {&out, &part_o, &part_ml, &q, &k_cache, &v_cache, &items, &n_items, &counters, &q_start, &q_len,
+                  &ctx_len, &block_table, &wo, &h, &sync, &err})
+    check_gpu(*t, "attn_o arg");
+  check_dtype(q, at::kBFloat16, "q"); check_dtype(out, at::kBFloat16, "out"); check_dtype(h, at::kBFloat16, "h");
+  check_dtype(wo, at::kBFloat16, "wo");
+  for (auto* t : {&items, &n_items, &counters, &q_start, &q_len, &ctx_len, &block_table, &sync, &err})
+    check_dtype(*t, at::kInt, "attn_o int arg");
+  TORCH_CHECK(q.dim() == 3 && q.size(2) == 128 && out.sizes() == q.sizes() && out.is_contiguous(),
+              "q / out must be [T, H, 128] (out contiguous)");
+  TORCH_CHECK(k_cache.dim() == 5 && v_cache.dim() == 4, "paged K / V caches");
+  TORCH_CHECK(wo.dim() == 4 && wo.size(2) == 64 && wo.size(3) == 8 && wo.is_contiguous(), "wo must be packed");
+  const int T = q.size(0), H = q.size(1), KV = k_cache.size(1);
+  const int N = wo.size(0) * 16, K = wo.size(1) * 32;
+  TORCH_CHECK(h.dim() == 2 && h.size(0) >= T && h.size(1) == N && h.stride(1) == 1 && h.stride(0) % 4 == 0,
+              "h must be [>= T, N] with 8-byte rows");
+  TORCH_CHECK(items.dim() == 2 && items.size(1) == 4 && block_table.dim() == 2, "items / block_table");
+  TORCH_CHECK(part_o.numel() >= items.size(0) * KV * 16 * 128 && part_ml.numel() >= items.size(0) * KV * 16 * 2,
+              "partition workspaces too small");
+  TORCH_CHECK(sync.numel() >= 2 && err.numel() >= 1, "sync[2] / err[1]");
+  const int rc = pa_attn_o(out.data_ptr(), part_o.data_ptr<float>(), part_ml.data_ptr<float>(), q.data_ptr(),
+                           k_cache.data_ptr(), v_cache.data_ptr(), items.data_ptr<int>(), n_items.data_ptr<int>(),
+                           part_size.has_value() ? part_size->data_ptr<int>() : nullptr, counters.data_ptr<int>(),
+                           q_start.data_ptr<int>(), q_len.data_ptr<int>(), ctx_len.data_ptr<int>(),
+                           block_table.data_ptr<int>(), block_table.size(1), H, KV,
+                           (float)(scale * 1.4426950408889634), wo.data_ptr(), h.data_ptr(), T, N, K, h.stride(0),
+                           sync.data_ptr<int>(), err.data_ptr<int>(), cur_stream());
+  TORCH_CHECK(rc >= 0, "attn_o launch failed");
+  return rc == 0;
 }
 
 // y[M, N] = x[M, K] . w[N, K]^T for M <= 128; returns false if the shape is not handled.
@@ -875,6 +916,11 @@ at::Tensor empty_uncached(int64_t numel, at::ScalarType dtype, int64_t device) {
 }
 
 PYBIND11_MODULE(_C, m) {
+  m.def("attn_o", &attn_o, py::arg("out"), py::arg("part_o"), py::arg("part_ml"), py::arg("q"), py::arg("k_cache"),
+        py::arg("v_cache"), py::arg("items"), py::arg("n_items"), py::arg("counters"), py::arg("q_start"),
+        py::arg("q_len"), py::arg("ctx_len"), py::arg("block_table"), py::arg("scale"), py::arg("part_size"),
+        py::arg("wo"), py::arg("h"), py::arg("sync"), py::arg("err"),
+        "decode-sized steps: paged attention + h += out . Wo^T (packed) in one launch; false if not handled");
   m.def("store_test", [](at::Tensor dst, int64_t mode, int64_t grid) {
     check_gpu(dst, "dst");
     TORCH_CHECK(dst.is_contiguous() && dst.nbytes() % 16 == 0, "dst: contiguous, a multiple of 16 bytes");

@@ -172,6 +172,10 @@ class LlamaModel:
     # bench 14.17 / 14.24 -> 14.41 / 14.47 tasks/s, 8-token steps 3.28 -> 3.19-3.20 ms
     # (profiles/r3_attention_8wave.jsonl)
     ATT_DECODE_WAVES = int(os.environ.get("PILOTTAI_ATT_DECODE_WAVES", "8"))
+    # decode-sized steps (T <= DECODE_FUSED_MAX_T, TP = 1, 8-wave attention): attention and the
+    # O projection + residual in ONE launch whose idle workgroups stream the O weights into LDS
+    # while the attention runs (csrc/ops/attention.hip attn_o_kernel); False = two launches
+    ATTN_O_FUSED = os.environ.get("PILOTTAI_ATTN_O_FUSED", "0") == "1"
     # per projection: (largest M, path, config); the first row whose M covers the step is used,
     # for every step on the fused packed-weight path (T > WIDE_MAX_T).
     # "pf": prefill kernel — bn = tile width (256 / 128), variant = kernel family (3: the
@@ -476,18 +480,24 @@ class LlamaModel:
             ops.decode_qkv_rope(h, L["wqkv_p"], eps, q, kv.k[li], kv.v[li], meta.positions, meta.slots,
                                 self.cos_sin, H, KVh)
             attn = torch.empty(T, H, hd, dtype=self.dtype, device=self.device)
-            # the attention grid's idle workgroups read the O projection's weights into
-            # the Infinity Cache while the K/V stream runs (csrc/ops/attention.hip)
-            ops.paged_attention(attn, part_o, part_ml, q, kv.k[li], kv.v[li], meta.items, meta.n_items,
-                                meta.att_counters, meta.q_start, meta.q_len, meta.ctx_len,
-                                meta.block_table, self.scale, num_seqs=meta.num_seqs, part_size=meta.part_size,
-                                queue=meta.att_queue, waves=self.ATT_DECODE_WAVES,
-                                prefetch=L["wo_p"] if pf else None)
-            a2 = attn.view(T, H * hd)
-            if tp:  # all-reduce + residual add in one launch (custom_ar.hip RES epilogue)
-                self.tp.all_reduce_add(ops.decode_gemm(a2, L["wo_p"], "plain"), h)
-            else:
-                ops.decode_gemm(a2, L["wo_p"], "resid", resid=h, out=h)
+            fused = (not tp and self.ATTN_O_FUSED and not pf and meta.att_queue is None
+                     and self.ATT_DECODE_WAVES == 8
+                     and ops.attn_o(attn, part_o, part_ml, q, kv.k[li], kv.v[li], meta.items, meta.n_items,
+                                    meta.att_counters, meta.q_start, meta.q_len, meta.ctx_len, meta.block_table,
+                                    self.scale, L["wo_p"], h, num_seqs=meta.num_seqs, part_size=meta.part_size))
+            if not fused:
+                # the attention grid's idle workgroups read the O projection's weights into
+                # the Infinity Cache while the K/V stream runs (csrc/ops/attention.hip)
+                ops.paged_attention(attn, part_o, part_ml, q, kv.k[li], kv.v[li], meta.items, meta.n_items,
+                                    meta.att_counters, meta.q_start, meta.q_len, meta.ctx_len,
+                                    meta.block_table, self.scale, num_seqs=meta.num_seqs, part_size=meta.part_size,
+                                    queue=meta.att_queue, waves=self.ATT_DECODE_WAVES,
+                                    prefetch=L["wo_p"] if pf else None)
+                a2 = attn.view(T, H * hd)
+                if tp:  # all-reduce + residual add in one launch (custom_ar.hip RES epilogue)
+                    self.tp.all_reduce_add(ops.decode_gemm(a2, L["wo_p"], "plain"), h)
+                else:
+                    ops.decode_gemm(a2, L["wo_p"], "resid", resid=h, out=h)
             a = ops.decode_gemm(h, L["w13_p"], "silu", norm=True, eps=eps)
             if tp:
                 self.tp.all_reduce_add(ops.decode_gemm(a, L["w2_p"], "plain"), h)

@@ -173,6 +173,38 @@ def paged_attention(out, part_o, part_ml, q, k_cache, v_cache, items, n_items, c
     return out
 
 
+_attn_o_sync = {}
+
+
+def attn_o_workspace(device) -> tuple:
+    """(sync[2], err[1]) int32 for attn_o: zero, and left zero by every launch."""
+    key = str(device)
+    if key not in _attn_o_sync:
+        _attn_o_sync[key] = (torch.zeros(2, dtype=torch.int32, device=device),
+                             torch.zeros(1, dtype=torch.int32, device=device))
+    return _attn_o_sync[key]
+
+
+def attn_o(out, part_o, part_ml, q, k_cache, v_cache, items, n_items, counters, q_start, q_len, ctx_len,
+           block_table, scale: float, wo: torch.Tensor, h: torch.Tensor, num_seqs: Optional[int] = None,
+           part_size: Optional[torch.Tensor] = None) -> bool:
+    """Decode-sized steps: paged attention into `out` [T, H, 128] AND h[:T] += out . Wo^T (Wo
+    packed by pack_decode_weight) in one launch (csrc/ops/attention.hip attn_o_kernel: the O
+    tiles' weights stream into LDS while the attention runs, one workgroup per CU).
+    Returns False if the shape / device does not allow it (then nothing ran). CPU: the
+    reference attention + mid_gemm residual path."""
+    if _on_gpu(q):
+        sync, err = attn_o_workspace(q.device)
+        return bool(require_native().attn_o(out, part_o, part_ml, q, k_cache, v_cache, items, n_items, counters,
+                                            q_start, q_len, ctx_len, block_table, float(scale), part_size, wo, h,
+                                            sync, err))
+    paged_attention(out, part_o, part_ml, q, k_cache, v_cache, items, n_items, counters, q_start, q_len, ctx_len,
+                    block_table, scale, num_seqs=num_seqs, part_size=part_size)
+    T = q.shape[0]
+    mid_gemm(out.view(T, -1), wo, "resid", resid=h[:T], out=h[:T])
+    return True
+
+
 def sample_workspace(rows: int, V: int, device) -> torch.Tensor:
     n = require_native().sample_workspace_floats(rows, V)
     return torch.empty(n, dtype=torch.float32, device=device)

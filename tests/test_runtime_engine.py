@@ -379,6 +379,21 @@ def test_fused_decode_path_matches_unfused_logits():
     assert int(a.argmax(-1)[0]) == int(b.argmax(-1)[0]) or float((a - b).abs().max()) < 1e-2
 
 
+def test_attn_o_fused_decode_path_same_tokens(tok):
+    """LlamaModel.ATTN_O_FUSED (attention + O projection + residual in one launch on decode
+    steps) leaves the greedy tokens unchanged (CPU: the op's reference path)."""
+    from pilottai_amd.engine.engine import EngineConfig, LLMEngine
+
+    prompts = [tok.encode("Task: summarize the report."), tok.encode("List three risks of the plan.")]
+    outs = {}
+    for fused in (False, True):
+        eng = LLMEngine(EngineConfig(model="tiny", max_num_seqs=8, use_graphs=False, decode_fused=True,
+                                     num_kv_blocks=256, max_model_len=512,
+                                     model_overrides={"ATTN_O_FUSED": fused}))
+        outs[fused] = [o.token_ids for o in eng.generate(prompts, temperature=0.0, max_tokens=12, ignore_eos=True)]
+    assert outs[True] == outs[False]
+
+
 def test_wide_path_matches_library_path_logits():
     """The packed small-batch forward (16 < T <= 32: folded norms, split-K kernels,
     SwiGLU / residual epilogues) and the library-GEMM forward give the same logits

@@ -1,0 +1,15 @@
+# round-4 GPU job: fused attention + O launch: kernel tests, engine numerics with it on, in-engine A/B
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+O=gpurun_out/r4_attno
+mkdir -p $O
+export TMPDIR=/tmp
+timeout -k 10 300 python -u -m pytest tests/test_attn_o_gpu.py -m gpu -x -v --timeout 120 --timeout-method thread > $O/tests.log 2>&1 || { tail -40 $O/tests.log; exit 1; }
+tail -2 $O/tests.log
+PILOTTAI_ATTN_O_FUSED=1 timeout -k 10 600 python -u -m pytest tests/test_engine_gpu.py -m gpu -x -q --timeout 300 --timeout-method thread > $O/engine_tests.log 2>&1 || { tail -40 $O/engine_tests.log; exit 1; }
+tail -2 $O/engine_tests.log
+echo '[{"ATTN_O_FUSED": false}, {"ATTN_O_FUSED": true}]' > $O/ov.json
+timeout -k 10 600 python -u tools/midrange_ab.py --T 8 --reps 4 --decode 8,600,48 --overrides $O/ov.json --out $O/ab8.jsonl > $O/ab8.log 2>&1 || { tail -20 $O/ab8.log; exit 1; }
+cat $O/ab8.jsonl
+timeout -k 10 600 python -u tools/midrange_ab.py --T 16 --reps 4 --decode 16,800,48 --overrides $O/ov.json --out $O/ab16.jsonl > $O/ab16.log 2>&1 || { tail -20 $O/ab16.log; exit 1; }
+cat $O/ab16.jsonl
