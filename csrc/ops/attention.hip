@@ -860,17 +860,21 @@ __global__ __launch_bounds__(512, 1) void attn_o_kernel(const AttnOArgs A) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's O-tile LDS-DMA landed
   __syncthreads();
 
-  // O tile: 16 columns x <= 16 rows; wave w sums its K / 8 slice
+  // O tile: 16 columns x <= 16 rows; wave w sums its K / 8 = 16 k-steps (K = 4096: the
+  // launcher checks). All 16 x fragments are loaded before the first MFMA: one memory round
+  // trip instead of 16 dependent ones.
+  constexpr int PER = 16;
   const int c = lane & 15, g = lane >> 4;
-  const int per = KS >> 3;
-  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-  const bf16* xrow = A.out + (size_t)min(c, A.T - 1) * A.K + 8 * g;
+  const bf16* xrow = A.out + (size_t)min(c, A.T - 1) * A.K + 8 * g + wid * PER * 32;
   const bool rowok = c < A.T;
-  for (int ks = wid * per; ks < (wid + 1) * per; ++ks) {
-    const bf16x8 wf = *reinterpret_cast<const bf16x8*>(smem + ks * 1024 + lane * 16);
-    bf16x8 xf = *reinterpret_cast<const bf16x8*>(xrow + ks * 32);
-    if (!rowok) xf = bf16x8{};
-    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf, xf, acc, 0, 0, 0);
+  bf16x8 xf[PER];
+#pragma unroll
+  for (int i = 0; i < PER; ++i) xf[i] = *reinterpret_cast<const bf16x8*>(xrow + i * 32);
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const bf16x8 wf = *reinterpret_cast<const bf16x8*>(smem + (wid * PER + i) * 1024 + lane * 16);
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf, rowok ? xf[i] : bf16x8{}, acc, 0, 0, 0);
   }
   f32x4* red = reinterpret_cast<f32x4*>(smem + KS * 1024);
   red[wid * 64 + lane] = acc;
@@ -905,7 +909,7 @@ extern "C" int pa_attn_o(void* out, float* part_o, float* part_ml, const void* q
                          int* counters, const int* q_start, const int* q_len, const int* ctx_len,
                          const int* block_table, int max_blocks, int H, int KV, float scale_log2, const void* wo,
                          void* h, int T, int N, int K, int ldh, int* sync, int* err, hipStream_t st) {
-  if (H % KV != 0 || T <= 0 || T > 16 || N % 16 != 0 || K != H * 128 || (K / 32) % 8 != 0) return 1;
+  if (H % KV != 0 || T <= 0 || T > 16 || N % 16 != 0 || K != H * 128 || K != 4096) return 1;
   const int grid = N / 16;
   static int ncu = 0;
   if (ncu == 0) {
