@@ -35,6 +35,7 @@
 #include "common.h"
 
 #include <algorithm>
+#include <cstdlib>
 
 namespace pa {
 
@@ -806,6 +807,10 @@ struct AttnOArgs {
   int T, N, K, ldh;
   int* sync;  // [2]: published units, departed workgroups (zero between launches)
   int* err;   // 1 if a wait timed out (never in a healthy run)
+  // diagnostics (PILOTTAI_ATTN_O_MODE, default 1): bit 0 = the producer release (without it
+  // the hand-off is NOT safe: timing only); bit 1 = every workgroup loads its O tile only
+  // after the wait (no overlap with the attention)
+  int mode;
 };
 
 template <int G>
@@ -824,7 +829,8 @@ __global__ __launch_bounds__(512, 1) void attn_o_kernel(const AttnOArgs A) {
                                        (att_lds_t*)(smem + ks * 1024), 16, 0, 0);
   };
   const bool att = bid < units;
-  if (!att) load_w();
+  const bool late = A.mode & 2;
+  if (!att && !late) load_w();
   for (int u = bid; u < units; u += nwg) {
     const int kvh = u % A.KV;
     const int4 it = A.items[u / A.KV];
@@ -837,12 +843,14 @@ __global__ __launch_bounds__(512, 1) void attn_o_kernel(const AttnOArgs A) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's output stores
     __syncthreads();
     if (threadIdx.x == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (A.mode & 1) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
       __hip_atomic_fetch_add((gi32*)A.sync, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
-  if (att) {
+  if (att && !late) {
     __syncthreads();  // every wave is done with the attention LDS
     load_w();
   }
@@ -856,6 +864,10 @@ __global__ __launch_bounds__(512, 1) void attn_o_kernel(const AttnOArgs A) {
       }
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  }
+  if (late) {
+    __syncthreads();
+    load_w();
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's O-tile LDS-DMA landed
   __syncthreads();
@@ -922,7 +934,13 @@ extern "C" int pa_attn_o(void* out, float* part_o, float* part_ml, const void* q
   const pa::AttnOArgs a{(pa::bf16*)out, part_o, part_ml, counters, (const pa::bf16*)q, (const pa::bf16*)k_cache,
                         (const pa::bf16*)v_cache, (const int4*)items, n_items, part_size, q_start, q_len, ctx_len,
                         block_table, max_blocks, H, KV, scale_log2, pa::g_handoff_attn, (const pa::bf16*)wo,
-                        (pa::bf16*)h, T, N, K, ldh, sync, err};
+                        (pa::bf16*)h, T, N, K, ldh, sync, err, 1};
+  static int mode_env = -1;
+  if (mode_env < 0) {
+    const char* e = getenv("PILOTTAI_ATTN_O_MODE");
+    mode_env = e ? atoi(e) : 1;
+  }
+  const_cast<pa::AttnOArgs&>(a).mode = mode_env;
 #define PA_AO(GG)                                                                                          \
   do {                                                                                                     \
     static bool attr = false;  /* the whole 160 KiB once: any launch's size fits */                       \
