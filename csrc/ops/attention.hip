@@ -811,6 +811,7 @@ struct AttnOArgs {
   // the hand-off is NOT safe: timing only); bit 1 = every workgroup loads its O tile only
   // after the wait (no overlap with the attention)
   int mode;
+  unsigned long long* stamps;  // diagnostics: per workgroup 8 s_memrealtime stamps (null: none)
 };
 
 template <int G>
@@ -830,6 +831,10 @@ __global__ __launch_bounds__(512, 1) void attn_o_kernel(const AttnOArgs A) {
   };
   const bool att = bid < units;
   const bool late = A.mode & 2;
+  auto stamp = [&](int i) {
+    if (A.stamps && threadIdx.x == 0) A.stamps[(size_t)bid * 8 + i] = __builtin_amdgcn_s_memrealtime();
+  };
+  stamp(0);
   if (!att && !late) load_w();
   for (int u = bid; u < units; u += nwg) {
     const int kvh = u % A.KV;
@@ -850,10 +855,12 @@ __global__ __launch_bounds__(512, 1) void attn_o_kernel(const AttnOArgs A) {
       __hip_atomic_fetch_add((gi32*)A.sync, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
+  stamp(1);
   if (att && !late) {
     __syncthreads();  // every wave is done with the attention LDS
     load_w();
   }
+  stamp(2);
   if (threadIdx.x == 0) {
     unsigned spins = 0;
     while (__hip_atomic_load((gi32*)A.sync, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < units) {
@@ -865,12 +872,14 @@ __global__ __launch_bounds__(512, 1) void attn_o_kernel(const AttnOArgs A) {
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   }
+  stamp(3);
   if (late) {
     __syncthreads();
     load_w();
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's O-tile LDS-DMA landed
   __syncthreads();
+  stamp(4);
 
   // O tile: 16 columns x <= 16 rows; wave w sums its K / 8 = 16 k-steps (K = 4096: the
   // launcher checks). All 16 x fragments are loaded before the first MFMA: one memory round
@@ -903,6 +912,11 @@ __global__ __launch_bounds__(512, 1) void attn_o_kernel(const AttnOArgs A) {
     for (int j = 0; j < 4; ++j) o[j] = (bf16)(v[j] + (float)r[j]);
     *reinterpret_cast<bf16x4*>(dst) = o;
   }
+  if (A.stamps) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    stamp(5);
+  }
   if (threadIdx.x == 0) {  // the last workgroup out resets the counters for the next launch
     const int d = __hip_atomic_fetch_add((gi32*)(A.sync + 1), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (d == nwg - 1) {
@@ -913,6 +927,10 @@ __global__ __launch_bounds__(512, 1) void attn_o_kernel(const AttnOArgs A) {
 }
 
 }  // namespace pa
+
+// diagnostics: when set, the next attn_o launches write per-workgroup phase stamps here
+static unsigned long long* g_attn_o_stamps = nullptr;
+extern "C" void pa_attn_o_set_stamps(void* p) { g_attn_o_stamps = (unsigned long long*)p; }
 
 // Fused attention + O projection (+ residual) for decode-sized steps; returns 1 if the shape
 // or the device does not allow it (the caller then runs the two launches), 0 on success.
@@ -934,7 +952,7 @@ extern "C" int pa_attn_o(void* out, float* part_o, float* part_ml, const void* q
   const pa::AttnOArgs a{(pa::bf16*)out, part_o, part_ml, counters, (const pa::bf16*)q, (const pa::bf16*)k_cache,
                         (const pa::bf16*)v_cache, (const int4*)items, n_items, part_size, q_start, q_len, ctx_len,
                         block_table, max_blocks, H, KV, scale_log2, pa::g_handoff_attn, (const pa::bf16*)wo,
-                        (pa::bf16*)h, T, N, K, ldh, sync, err, 1};
+                        (pa::bf16*)h, T, N, K, ldh, sync, err, 1, g_attn_o_stamps};
   static int mode_env = -1;
   if (mode_env < 0) {
     const char* e = getenv("PILOTTAI_ATTN_O_MODE");

@@ -54,6 +54,7 @@ int pa_mid_gemm(void* y, const void* x, const void* wp, const void* resid, float
                 const float* cos_sin, int H, int KV, hipStream_t st);
 int pa_row_sumsq(float* out, const void* x, int M, int K, int ldx, hipStream_t st);
 int pa_timeline_marker(int id, hipStream_t st);
+void pa_attn_o_set_stamps(void* p);
 int pa_attn_o(void* out, float* part_o, float* part_ml, const void* q, const void* k_cache, const void* v_cache,
               const int* items, const int* n_items, const int* part_size, int* counters, const int* q_start,
               const int* q_len, const int* ctx_len, const int* block_table, int max_blocks, int H, int KV,
@@ -921,6 +922,9 @@ PYBIND11_MODULE(_C, m) {
         py::arg("q_len"), py::arg("ctx_len"), py::arg("block_table"), py::arg("scale"), py::arg("part_size"),
         py::arg("wo"), py::arg("h"), py::arg("sync"), py::arg("err"),
         "decode-sized steps: paged attention + h += out . Wo^T (packed) in one launch; false if not handled");
+  m.def("attn_o_set_stamps", [](c10::optional<at::Tensor> t) {
+    pa_attn_o_set_stamps(t.has_value() ? t->data_ptr() : nullptr);
+  }, py::arg("stamps"), "diagnostics: int64 [>= 8 * grid] buffer for attn_o phase stamps (None: off)");
   m.def("store_test", [](at::Tensor dst, int64_t mode, int64_t grid) {
     check_gpu(dst, "dst");
     TORCH_CHECK(dst.is_contiguous() && dst.nbytes() % 16 == 0, "dst: contiguous, a multiple of 16 bytes");
