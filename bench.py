@@ -259,6 +259,9 @@ async def run_rank(a, rank: int, world: int, device):
 
     if a.warmup > 0:
         await round_(a.warmup, False)
+    from pilottai_amd.utils.gc_tune import freeze_heap
+
+    freeze_heap()  # agents, serve and warm-up state: out of the timed region's GC passes
     await coll(comm.barrier)  # worker ranks keep serving the plane meanwhile
     st0 = dict(eng.stats)  # after the barrier: every rank's warmup work is behind it
     mem0 = dict(lookup.stats, device_s=lookup.lookup_device_seconds()) if lookup is not None else None

@@ -596,6 +596,11 @@ class LLMEngine:
         if sw is not None and sw > 0:
             sys.setswitchinterval(sw)
         self._stop = False
+        # the model, graphs and tokenizer are in place: keep them out of every later GC pass
+        # (a full collection otherwise stalls the engine thread for tens of ms)
+        from pilottai_amd.utils.gc_tune import freeze_heap
+
+        freeze_heap()
         self._thread = threading.Thread(target=self._loop, name="pilottai-engine", daemon=True)
         self._thread.start()
 
