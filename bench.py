@@ -162,12 +162,14 @@ async def run_rank(a, rank: int, world: int, device):
                                     if a.att_wide_min_tokens is not None else {})), device=device)
     register_engine(eng.model_cfg.name, eng)
     if memory is not None and a.embedder == "engine":
-        # queries and write-backs are encoded by the serving model: mean-pooled final hidden
-        # states of embedding requests inside the engine's continuous batch
+        # queries and write-backs are encoded by the serving model: final hidden states (last
+        # token, or mean-pooled) of embedding requests inside the engine's continuous batch (N11)
         from pilottai_amd.memory.embedding import EngineEmbedder
 
         memory.embedder = EngineEmbedder(eng, dim=memory.index.dim, pool="engine", max_tokens=256,
                                          pooling=a.embed_pooling)
+    if memory is not None and a.embedder == "engine" and not a.cpu:
+        eng.capture_embed_graphs()  # embedding requests: no first-use captures while timed
     eng.start()
     llm = LocalLLM(LLMConfig(model_name=eng.model_cfg.name, temperature=a.temperature, max_tokens=1024,
                              retry_attempts=1), engine=eng)

@@ -464,6 +464,13 @@ class LLMEngine:
         d[L["embed_rows"]:L["embed_rows"] + L["max_tokens"]] = L["max_seqs"]
         self._dev_meta.copy_(d.to(self.device))
 
+    def capture_embed_graphs(self):
+        """Capture every bucket's embedding-pooling variant now (before start()), so embedding
+        requests never pay a first-use capture (tens of ms each) while serving."""
+        if self._thread is not None:
+            raise RuntimeError("capture_embed_graphs() runs before start()")
+        self.capture_graphs(embed=True)
+
     def capture_graphs(self, buckets: Optional[Sequence[int]] = None, trunc: bool = False, embed: bool = False):
         """Capture one hipGraph per token bucket (shared memory pool); the top-k/top-p and
         embedding-pooling variants are captured on first use."""
