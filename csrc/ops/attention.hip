@@ -55,7 +55,20 @@ constexpr int ATT_LDS_DECODE_BYTES = att_lds_decode_bytes<4>();
 typedef __attribute__((address_space(1))) unsigned long long gu64;
 typedef __attribute__((address_space(1))) int gi32;
 
-template <int G, int NW = 4>
+// An attention output store (8 bf16): plain, or write-through (sc1: the line is not kept
+// dirty in this XCD's L2, so another workgroup of the same launch can read it after the
+// store drains and a counter says so, without a release / acquire; attn_o_kernel).
+template <bool WT>
+__device__ __forceinline__ void att_store8(bf16* p, const bf16x8 v) {
+  if constexpr (WT) {
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(p, 0, 16, 0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, 0, 0, 16);
+  } else {
+    *reinterpret_cast<bf16x8*>(p) = v;
+  }
+}
+
+template <int G, int NW = 4, bool WT = false>
 __device__ __forceinline__ void decode_item(
     const int4 it, char* smem, bf16* __restrict__ out, float* __restrict__ part_o,
     float* __restrict__ part_ml, int* __restrict__ counters, const bf16* __restrict__ q, const bf16* __restrict__ k_cache,
@@ -276,7 +289,7 @@ __device__ __forceinline__ void decode_item(
     bf16x8 g8;
 #pragma unroll
     for (int j = 0; j < 8; ++j) g8[j] = (bf16)(ga[j] * ginv);
-    *reinterpret_cast<bf16x8*>(out + ((size_t)(q0 + qb + ctq) * H + kvh * G + chg) * ATT_HD + d0) = g8;
+    att_store8<WT>(out + ((size_t)(q0 + qb + ctq) * H + kvh * G + chg) * ATT_HD + d0, g8);
     return;
   }
   if (ctq >= nq || !mthr) return;
@@ -284,7 +297,7 @@ __device__ __forceinline__ void decode_item(
   bf16x8 w8;
 #pragma unroll
   for (int j = 0; j < 8; ++j) w8[j] = (bf16)(acc[j] * inv);
-  *reinterpret_cast<bf16x8*>(out + ((size_t)(q0 + qb + ctq) * H + kvh * G + chg) * ATT_HD + d0) = w8;
+  att_store8<WT>(out + ((size_t)(q0 + qb + ctq) * H + kvh * G + chg) * ATT_HD + d0, w8);
 }
 
 // ---------------------------------------------------------------------------
@@ -359,7 +372,7 @@ __device__ __forceinline__ f32x16 qk_tile(const bf16x8 (&kf)[8], const bf16x8 (&
   return s;
 }
 
-template <int G, int NW = 4>
+template <int G, int NW = 4, bool WT = false>
 __device__ __forceinline__ void prefill_item(
     const int4 it, char* smem, bf16* __restrict__ out, const bf16* __restrict__ q,
     const bf16* __restrict__ k_cache, const bf16* __restrict__ v_cache,
@@ -469,7 +482,7 @@ __device__ __forceinline__ void prefill_item(
     bf16x8 w8;
 #pragma unroll
     for (int j = 0; j < 8; ++j) w8[j] = (bf16)(acc[j] * inv);
-    *reinterpret_cast<bf16x8*>(orow + 8 * c8) = w8;
+    att_store8<WT>(orow + 8 * c8, w8);
   }
 }
 
@@ -615,7 +628,7 @@ __device__ __forceinline__ void prefill_item_wg(
 
 // A q-split item of either width. 8-wave workgroups run no LDS-staged wide items (their 4-wave
 // image layout): a wide item (128/G tokens) runs there as its 32-column sub-items.
-template <int G, int NW>
+template <int G, int NW, bool WT = false>
 __device__ __forceinline__ void prefill_any(
     const int4 it, char* smem, bf16* __restrict__ out, const bf16* __restrict__ q,
     const bf16* __restrict__ k_cache, const bf16* __restrict__ v_cache,
@@ -623,16 +636,17 @@ __device__ __forceinline__ void prefill_any(
     const int* __restrict__ block_table, int max_blocks, int H, int KV, int kvh, float scale_log2) {
   const int nq = it.z & 0xff;
   if (nq <= 32 / G) {
-    prefill_item<G, NW>(it, smem, out, q, k_cache, v_cache, q_start, q_len, ctx_len, block_table, max_blocks, H,
-                        KV, kvh, scale_log2);
+    prefill_item<G, NW, WT>(it, smem, out, q, k_cache, v_cache, q_start, q_len, ctx_len, block_table, max_blocks,
+                            H, KV, kvh, scale_log2);
   } else if constexpr (NW == 4) {
+    static_assert(!WT, "write-through outputs: 8-wave items only");
     prefill_item_wg<G>(it, smem, out, q, k_cache, v_cache, q_start, q_len, ctx_len, block_table, max_blocks, H, KV,
                        kvh, scale_log2);
   } else {
     for (int sb = 0; sb < nq; sb += 32 / G) {
       const int4 sub = {it.x, it.y + sb, min(32 / G, nq - sb) | (it.z & ~0xff), it.w};
-      prefill_item<G, NW>(sub, smem, out, q, k_cache, v_cache, q_start, q_len, ctx_len, block_table, max_blocks,
-                          H, KV, kvh, scale_log2);
+      prefill_item<G, NW, WT>(sub, smem, out, q, k_cache, v_cache, q_start, q_len, ctx_len, block_table,
+                              max_blocks, H, KV, kvh, scale_log2);
       __syncthreads();  // LDS reuse by the next sub-item
     }
   }
@@ -775,15 +789,19 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void paged_attn_kernel(
 //   * workgroups [0, units) run the attention units (item, KV head) exactly as the 8-wave
 //     paged_attn_kernel does; every other workgroup meanwhile loads its O tile's packed
 //     weights (K / 32 KiB, 128 KiB) into LDS by LDS-DMA;
-//   * each attention workgroup publishes its finished unit: stores drained, workgroup
-//     barrier, one agent-scope release, one relaxed ticket on sync[0]; then it loads its own
-//     O tile (its LDS is free again);
-//   * every workgroup waits (one lane, bounded spin, err flag on timeout) until sync[0]
-//     counts every unit, runs one agent-scope acquire, and computes its 16 columns for the
-//     <= 16 rows: 8 waves split K, partial tiles summed through LDS, residual added in place;
+//   * each attention workgroup publishes its finished unit: its output stores are
+//     write-through (sc1) and drained, workgroup barrier, one relaxed ticket on sync[0];
+//   * with units <= nwg / 2 (decode: 8 KV heads x <= 16 items), the o-only workgroup
+//     units + j also owns the attention workgroup j's O tile, held in registers (64 VGPRs a
+//     lane): the attention workgroups publish and leave, no weight byte waits for them;
+//     otherwise each attention workgroup loads its own tile after its units;
+//   * every computing workgroup waits (one lane, bounded spin, err flag on timeout) until
+//     sync[0] counts every unit and computes its 16 (or 2 x 16) columns for the <= 16 rows
+//     from sc1 loads of the attention output: 8 waves split K, partial tiles summed through
+//     LDS, residual added in place;
 //   * the last workgroup to leave resets sync[] (graph replay safe).
 // All workgroups must be resident at once: the launcher requires grid <= CU count and the
-// LDS (137 KiB) allows one workgroup per CU.
+// LDS (144 KiB) allows one workgroup per CU.
 struct AttnOArgs {
   bf16* out;
   float* part_o;
@@ -807,9 +825,10 @@ struct AttnOArgs {
   int T, N, K, ldh;
   int* sync;  // [2]: published units, departed workgroups (zero between launches)
   int* err;   // 1 if a wait timed out (never in a healthy run)
-  // diagnostics (PILOTTAI_ATTN_O_MODE, default 1): bit 0 = the producer release (without it
-  // the hand-off is NOT safe: timing only); bit 1 = every workgroup loads its O tile only
-  // after the wait (no overlap with the attention)
+  // diagnostics (PILOTTAI_ATTN_O_MODE, default 0): bit 0 = an agent-scope release / acquire
+  // pair on top of the write-through hand-off; bit 1 = every workgroup loads its O tile only
+  // after the wait (no overlap with the attention, no split ownership); bit 2 = the o-only
+  // workgroups hold their weight loads ~2 us
   int mode;
   unsigned long long* stamps;  // diagnostics: per workgroup 8 s_memrealtime stamps (null: none)
 };
@@ -818,34 +837,53 @@ template <int G>
 __global__ __launch_bounds__(512, 1) void attn_o_kernel(const AttnOArgs A) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int TPW = 16 / G;
+  constexpr int PER = 16;  // k-steps per wave (K = 4096: the launcher checks)
   const int bid = blockIdx.x, nwg = gridDim.x;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int units = A.n_items[0] * A.KV;
   const int KS = A.K >> 5;
   const int psz = A.part_size ? A.part_size[0] : ATT_PART;
-  const bf16* wt = A.wo + (size_t)bid * KS * 512;
-  auto load_w = [&]() {  // k-step ks of the tile -> smem + ks KiB (lane-linear, as packed)
+  const bool att = bid < units;
+  const bool late = A.mode & 2;
+  // split ownership (units <= nwg / 2): the o-only workgroup units + j also computes the
+  // attention workgroup j's tile from registers (wave w holds that tile's k-steps
+  // [16 w, 16 w + 16): 64 VGPRs), loaded while the attention runs; attention workgroups
+  // then only publish and leave. Otherwise every workgroup computes its own tile.
+  const bool split = 2 * units <= nwg && !late;
+  const int rt = bid - units;  // split: the register tile of an o-only workgroup (< units)
+  const bool has_rt = split && !att && rt < units;
+  auto load_w = [&]() {  // k-step ks of tile bid -> smem + ks KiB (lane-linear, as packed)
+    const bf16* wt = A.wo + (size_t)bid * KS * 512;
     for (int ks = wid; ks < KS; ks += 8)
       __builtin_amdgcn_global_load_lds((att_gbl_t*)(wt + (size_t)ks * 512 + lane * 8),
                                        (att_lds_t*)(smem + ks * 1024), 16, 0, 0);
   };
-  const bool att = bid < units;
-  const bool late = A.mode & 2;
   auto stamp = [&](int i) {
     if (A.stamps && threadIdx.x == 0) A.stamps[(size_t)bid * 8 + i] = __builtin_amdgcn_s_memrealtime();
   };
   stamp(0);
-  if (!att && !late) load_w();
+  bf16x8 wr[PER];
+  if (!att && !late) {
+    if (A.mode & 4) {  // pacing (diagnostics): hold the weight stream ~2 us off the attention
+      const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+      while (__builtin_amdgcn_s_memrealtime() - t0 < 200) __builtin_amdgcn_s_sleep(8);
+    }
+    load_w();
+  }
   for (int u = bid; u < units; u += nwg) {
     const int kvh = u % A.KV;
     const int4 it = A.items[u / A.KV];
     if ((it.z & 0xff) <= TPW)
-      decode_item<G, 8>(it, smem, A.out, A.part_o, A.part_ml, A.counters, A.q, A.k_cache, A.v_cache, A.q_start,
-                        A.q_len, A.ctx_len, A.block_table, A.max_blocks, A.H, A.KV, kvh, A.scale_log2, psz, A.acq);
+      decode_item<G, 8, true>(it, smem, A.out, A.part_o, A.part_ml, A.counters, A.q, A.k_cache, A.v_cache,
+                              A.q_start, A.q_len, A.ctx_len, A.block_table, A.max_blocks, A.H, A.KV, kvh,
+                              A.scale_log2, psz, A.acq);
     else
-      prefill_any<G, 8>(it, smem, A.out, A.q, A.k_cache, A.v_cache, A.q_start, A.q_len, A.ctx_len, A.block_table,
-                        A.max_blocks, A.H, A.KV, kvh, A.scale_log2);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's output stores
+      prefill_any<G, 8, true>(it, smem, A.out, A.q, A.k_cache, A.v_cache, A.q_start, A.q_len, A.ctx_len,
+                              A.block_table, A.max_blocks, A.H, A.KV, kvh, A.scale_log2);
+    // publish: the output went out write-through (sc1) and every wave drains it before the
+    // barrier; the consumers read it with sc1 loads, so no cache maintenance is needed
+    // (mode bit 0 adds an agent-scope release anyway: diagnostics)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
       if (A.mode & 1) {
@@ -856,61 +894,78 @@ __global__ __launch_bounds__(512, 1) void attn_o_kernel(const AttnOArgs A) {
     }
   }
   stamp(1);
-  if (att && !late) {
-    __syncthreads();  // every wave is done with the attention LDS
-    load_w();
+  if (has_rt) {  // (after the loop, which an o-only workgroup skips: wr is not live across it)
+    const bf16* w2 = A.wo + ((size_t)rt * KS + wid * PER) * 512 + lane * 8;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) wr[i] = *reinterpret_cast<const bf16x8*>(w2 + (size_t)i * 512);
   }
-  stamp(2);
-  if (threadIdx.x == 0) {
-    unsigned spins = 0;
-    while (__hip_atomic_load((gi32*)A.sync, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < units) {
-      __builtin_amdgcn_s_sleep(1);
-      if (++spins > (1u << 24)) {
-        __hip_atomic_store((gi32*)A.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
-      }
+  if (att && split) {
+    stamp(2);
+    stamp(3);
+    stamp(4);
+  } else {
+    if (att && !late) {
+      __syncthreads();  // every wave is done with the attention LDS
+      load_w();
     }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  }
-  stamp(3);
-  if (late) {
+    stamp(2);
+    if (threadIdx.x == 0) {
+      unsigned spins = 0;
+      while (__hip_atomic_load((gi32*)A.sync, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < units) {
+        __builtin_amdgcn_s_sleep(1);
+        if (++spins > (1u << 24)) {
+          __hip_atomic_store((gi32*)A.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+      }
+      if (A.mode & 1) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    }
+    stamp(3);
+    if (late) {
+      __syncthreads();
+      load_w();
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's O-tile loads landed
     __syncthreads();
-    load_w();
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's O-tile LDS-DMA landed
-  __syncthreads();
-  stamp(4);
+    stamp(4);
 
-  // O tile: 16 columns x <= 16 rows; wave w sums its K / 8 = 16 k-steps (K = 4096: the
-  // launcher checks). All 16 x fragments are loaded before the first MFMA: one memory round
-  // trip instead of 16 dependent ones.
-  constexpr int PER = 16;
-  const int c = lane & 15, g = lane >> 4;
-  const bf16* xrow = A.out + (size_t)min(c, A.T - 1) * A.K + 8 * g + wid * PER * 32;
-  const bool rowok = c < A.T;
-  bf16x8 xf[PER];
+    // O tiles: 16 columns x <= 16 rows; wave w sums its 16 k-steps. The x fragments are sc1
+    // loads (the attention output was stored write-through by other workgroups), all issued
+    // before the first MFMA.
+    const int c = lane & 15, g = lane >> 4;
+    const bool rowok = c < A.T;
+    const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(A.out, 0, A.T * A.K * 2, 0x00020000);
+    const int xoff = (min(c, A.T - 1) * A.K + 8 * g + wid * PER * 32) * 2;
+    bf16x8 xf[PER];
 #pragma unroll
-  for (int i = 0; i < PER; ++i) xf[i] = *reinterpret_cast<const bf16x8*>(xrow + i * 32);
-  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < PER; ++i)
+      xf[i] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rx, xoff + i * 64, 0, 16));
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f}, acc2 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int i = 0; i < PER; ++i) {
-    const bf16x8 wf = *reinterpret_cast<const bf16x8*>(smem + (wid * PER + i) * 1024 + lane * 16);
-    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf, rowok ? xf[i] : bf16x8{}, acc, 0, 0, 0);
-  }
-  f32x4* red = reinterpret_cast<f32x4*>(smem + KS * 1024);
-  red[wid * 64 + lane] = acc;
-  __syncthreads();
-  if (wid == 0 && rowok) {
-    f32x4 v = red[lane];
+    for (int i = 0; i < PER; ++i) {
+      const bf16x8 xi = rowok ? xf[i] : bf16x8{};
+      const bf16x8 wf = *reinterpret_cast<const bf16x8*>(smem + (wid * PER + i) * 1024 + lane * 16);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf, xi, acc, 0, 0, 0);
+      if (has_rt) acc2 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wr[i], xi, acc2, 0, 0, 0);
+    }
+    f32x4* red = reinterpret_cast<f32x4*>(smem + KS * 1024);
+    red[wid * 64 + lane] = acc;
+    if (has_rt) red[512 + wid * 64 + lane] = acc2;
+    __syncthreads();
+    // wave 0 finishes tile bid, wave 1 the register tile
+    if ((wid == 0 || (wid == 1 && has_rt)) && rowok) {
+      const f32x4* rr = red + wid * 512;
+      f32x4 v = rr[lane];
 #pragma unroll
-    for (int w = 1; w < 8; ++w) v += red[w * 64 + lane];
-    // lane (g, c): columns 16 bid + 4 g .. + 3 of row c
-    bf16* dst = A.h + (size_t)c * A.ldh + bid * 16 + 4 * g;
-    const bf16x4 r = *reinterpret_cast<const bf16x4*>(dst);
-    bf16x4 o;
+      for (int w = 1; w < 8; ++w) v += rr[w * 64 + lane];
+      // lane (g, c): columns 16 tile + 4 g .. + 3 of row c
+      bf16* dst = A.h + (size_t)c * A.ldh + (wid == 0 ? bid : rt) * 16 + 4 * g;
+      const bf16x4 r = *reinterpret_cast<const bf16x4*>(dst);
+      bf16x4 o;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) o[j] = (bf16)(v[j] + (float)r[j]);
-    *reinterpret_cast<bf16x4*>(dst) = o;
+      for (int j = 0; j < 4; ++j) o[j] = (bf16)(v[j] + (float)r[j]);
+      *reinterpret_cast<bf16x4*>(dst) = o;
+    }
   }
   if (A.stamps) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -947,7 +1002,7 @@ extern "C" int pa_attn_o(void* out, float* part_o, float* part_ml, const void* q
     if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
       ncu = -1;
   }
-  const int lds = std::max(pa::ATT_LDS_BYTES8, (K / 32) * 1024 + 8 * 1024);
+  const int lds = std::max(pa::ATT_LDS_BYTES8, (K / 32) * 1024 + 16 * 1024);
   if (ncu <= 0 || grid > ncu || lds > 160 * 1024) return 1;
   const pa::AttnOArgs a{(pa::bf16*)out, part_o, part_ml, counters, (const pa::bf16*)q, (const pa::bf16*)k_cache,
                         (const pa::bf16*)v_cache, (const int4*)items, n_items, part_size, q_start, q_len, ctx_len,
@@ -956,7 +1011,7 @@ extern "C" int pa_attn_o(void* out, float* part_o, float* part_ml, const void* q
   static int mode_env = -1;
   if (mode_env < 0) {
     const char* e = getenv("PILOTTAI_ATTN_O_MODE");
-    mode_env = e ? atoi(e) : 1;
+    mode_env = e ? atoi(e) : 0;
   }
   const_cast<pa::AttnOArgs&>(a).mode = mode_env;
 #define PA_AO(GG)                                                                                          \
