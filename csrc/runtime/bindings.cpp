@@ -131,6 +131,7 @@ PYBIND11_MODULE(_runtime, m) {
         if (d.contains("align_slack")) c.align_slack = d["align_slack"].cast<int32_t>();
         if (d.contains("small_step_tokens")) c.small_step_tokens = d["small_step_tokens"].cast<int32_t>();
         if (d.contains("small_step_part")) c.small_step_part = d["small_step_part"].cast<int32_t>();
+        if (d.contains("decode_part_target")) c.decode_part_target = d["decode_part_target"].cast<int32_t>();
         if (d.contains("eos_ids")) c.eos_ids = d["eos_ids"].cast<std::vector<int32_t>>();
         return std::make_unique<Scheduler>(c);
       }))

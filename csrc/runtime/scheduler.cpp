@@ -351,6 +351,29 @@ int32_t Scheduler::schedule(int32_t* buf) {
     for (const Planned& p : last_plan_) t_step += p.n;
     if (cfg_.small_step_part > 0 && t_step <= cfg_.small_step_tokens && parts512 * kv < target)
       psz = std::max(psz, cfg_.small_step_part);
+    if (cfg_.decode_part_target > 0 && t_step > cfg_.small_step_tokens) {
+      // one balanced round of workgroups instead of 512-key parts + short remainders
+      int64_t ndec = 0, maxc = 0;
+      for (const Planned& p : last_plan_)
+        if (p.n <= tpw) {
+          ++ndec;
+          maxc = std::max<int64_t>(maxc, p.s->num_computed + p.n);
+        }
+      if (ndec > 0) {
+        const int64_t tgt = cfg_.decode_part_target;
+        int64_t cand;
+        if (ndec * kv >= tgt) {
+          cand = std::max<int64_t>(maxc, 32);  // whole contexts: nparts = 1 everywhere
+        } else {
+          const int64_t np = (tgt + ndec * kv - 1) / (ndec * kv);
+          cand = std::max<int64_t>(128, ((maxc + np - 1) / np + 31) / 32 * 32);
+        }
+        int64_t parts = 0;
+        for (const Planned& p : last_plan_)
+          if (p.n <= tpw) parts += std::max<int64_t>(1, (p.s->num_computed + p.n + cand - 1) / cand);
+        if (nprefill + parts <= L.max_items) psz = (int32_t)cand;
+      }
+    }
   }
   buf[L.part_size] = psz;
 

@@ -49,6 +49,11 @@ struct SchedulerConfig {
   // steps run 8-wave attention workgroups, which stream a whole context without a merge
   int32_t small_step_tokens = 0;
   int32_t small_step_part = 0;
+  // > 0: steps above small_step_tokens size their decode partitions for about this many
+  // (partition, KV head) workgroups: no split once the decode rows alone reach it, otherwise
+  // equal partitions of the longest context (multiples of 32 keys, >= 128); 0 = the 512 / 256-key
+  // rule
+  int32_t decode_part_target = 0;
   // GEMM-friendly step sizes: when a step has T > token_align tokens and
   // T % token_align <= align_slack, the tail of the multi-token chunks (prefill /
   // jump-forward) is deferred so that T is a multiple of token_align (library

@@ -76,6 +76,9 @@ class EngineConfig:
     prefix_caching: bool = True
     dedup_inflight_prefix: bool = True  # requests wait for an identical prefix another request is prefilling
     split_decode: bool = True
+    # > 0: mid / large steps size their decode partitions for about this many (partition, KV
+    # head) workgroups (scheduler.h decode_part_target); 0 = 512 / 256-key partitions
+    decode_part_target: int = 0
     use_graphs: bool = True
     token_buckets: Optional[List[int]] = None
     seed: int = 0
@@ -263,6 +266,7 @@ class LLMEngine:
             "kv_heads": self.model.kv_local,
             "small_step_tokens": small_step,
             "small_step_part": 4096 if small_step else 0,
+            "decode_part_target": int(cfg.decode_part_target),
             "eos_ids": list(self.tok.eos_ids)})
         L = self.L = self.sched.layout()
         pin = self.on_gpu

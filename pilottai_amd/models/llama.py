@@ -172,6 +172,8 @@ class LlamaModel:
     # bench 14.17 / 14.24 -> 14.41 / 14.47 tasks/s, 8-token steps 3.28 -> 3.19-3.20 ms
     # (profiles/r3_attention_8wave.jsonl)
     ATT_DECODE_WAVES = int(os.environ.get("PILOTTAI_ATT_DECODE_WAVES", "8"))
+    # waves per attention workgroup on the mid path (DECODE_FUSED_MAX_T < T <= MID_MAX_T)
+    ATT_MID_WAVES = int(os.environ.get("PILOTTAI_ATT_MID_WAVES", "4"))
     # decode-sized steps (T <= DECODE_FUSED_MAX_T, TP = 1, 8-wave attention): attention and the
     # O projection + residual in ONE launch whose idle workgroups stream the O weights into LDS
     # while the attention runs (csrc/ops/attention.hip attn_o_kernel); False = two launches
@@ -686,7 +688,7 @@ class LlamaModel:
             ops.paged_attention(attn, part_o, part_ml, q, kv.k[li], kv.v[li], meta.items, meta.n_items,
                                 meta.att_counters, meta.q_start, meta.q_len, meta.ctx_len,
                                 meta.block_table, self.scale, num_seqs=meta.num_seqs, part_size=meta.part_size,
-                                queue=meta.att_queue)
+                                queue=meta.att_queue, waves=self.ATT_MID_WAVES)
             a2 = attn.view(T, H * hd)
             if tp:  # all-reduce + residual + the next norm's row statistics in one launch;
                 # ss_b was zeroed by the previous down all-reduce (or above), ss_a is zeroed here

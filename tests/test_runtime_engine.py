@@ -720,3 +720,40 @@ def test_scheduler_lists_attention_items_heaviest_first():
     ref_items, _ = build_attention_items(list(ql), list(cl), 4, part=part, qcols=128, wide_min_tokens=0)
     assert [tuple(int(v) for v in x) for x in items] == ref_items
     assert T == int(ql.sum())
+
+
+@pytest.mark.parametrize("rows", [16, 64])
+def test_scheduler_decode_part_target_one_balanced_round(rows):
+    """decode_part_target (csrc/runtime/scheduler.cpp): a mid / large step sizes its decode
+    partitions for ~target (partition, KV head) workgroups -- no split once the decode rows
+    alone reach it (64 rows x 8 KV heads), else equal multiples of 32 keys (16 rows: 4 parts of
+    160 keys for ~600-key contexts) instead of 512-key parts + short remainders."""
+    cfg = {"num_blocks": 4096, "block_size": 16, "max_num_seqs": 64, "max_num_batched_tokens": 2048,
+           "max_prefill_tokens": 2048, "max_model_len": 4096, "gqa_group": 4, "kv_heads": 8,
+           "decode_part_target": 512, "eos_ids": [128009]}
+    s = _runtime.Scheduler(cfg)
+    L = s.layout()
+    buf = np.zeros(L["total"], dtype=np.int32)
+    rng = np.random.default_rng(1)
+    for rid in range(rows):
+        s.add_request(rid, list(rng.integers(1000, 9000, 599)), 0.0, 50, rid, True, [], None)
+    for _ in range(200):  # prefill every prompt (each row then samples its first token)
+        T = s.schedule(buf.ctypes.data)
+        c = buf[L["counts"]:L["counts"] + 8]
+        s.commit(np.full(max(1, int(c[2])), 7, np.int32).ctypes.data, int(c[2]))
+        if all(x[4] >= 599 for x in s.debug_state()):
+            break
+    T = s.schedule(buf.ctypes.data)
+    assert T == rows  # a pure decode step
+    c = buf[L["counts"]:L["counts"] + 8]
+    items = buf[L["items"]:L["items"] + 4 * c[3]].reshape(-1, 4)
+    part = int(buf[L["part_size"]])
+    nparts = items[:, 2] >> 20
+    if rows == 64:
+        assert part >= 600 and len(items) == 64 and (nparts == 1).all()
+    else:
+        assert part == 160 and len(items) == 16 * 4 and (nparts == 4).all()
+    # the ops.attn_meta mirror builds the same list for that part size
+    ql, cl = buf[L["q_len"]:L["q_len"] + c[1]], buf[L["ctx_len"]:L["ctx_len"] + c[1]]
+    ref_items, _ = build_attention_items(list(ql), list(cl), 4, part=part)
+    assert [tuple(int(v) for v in x) for x in items] == ref_items

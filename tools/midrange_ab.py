@@ -35,6 +35,7 @@ def main():
     from pilottai_amd.engine.engine import EngineConfig, LLMEngine
 
     Ts = [int(t) for t in a.T.split(",")]
+    seqs = max(64, int(a.decode.split(",")[0])) if a.decode else 64
     engines = {}
     if a.overrides:
         ovs = json.load(open(a.overrides)) if a.overrides.endswith(".json") else json.loads(a.overrides)
@@ -43,14 +44,14 @@ def main():
             # UPPER-case keys: LlamaModel tunables; lower-case: EngineConfig fields
             eng_kw = {k: v for k, v in o.items() if not k.isupper()}
             mod = {k: v for k, v in o.items() if k.isupper()}
-            engines[c] = LLMEngine(EngineConfig(model="llama-3-8b", max_num_seqs=64, max_num_batched_tokens=2048,
+            engines[c] = LLMEngine(EngineConfig(model="llama-3-8b", max_num_seqs=seqs, max_num_batched_tokens=2048,
                                                 kv_cache_gb=8, prefix_caching=False, token_buckets=sorted(set(Ts)),
                                                 model_overrides=mod, capture_on_start=True, **eng_kw))
     else:
         cfgs = [c for c in a.configs.split(";")]
         for c in cfgs:
             kinds = [k for k in c.split(",") if k and k != "none"]
-            engines[c] = LLMEngine(EngineConfig(model="llama-3-8b", max_num_seqs=64, max_num_batched_tokens=2048,
+            engines[c] = LLMEngine(EngineConfig(model="llama-3-8b", max_num_seqs=seqs, max_num_batched_tokens=2048,
                                                 kv_cache_gb=8, prefix_caching=False, token_buckets=sorted(set(Ts)),
                                                 pf_midrange=kinds, capture_on_start=True))
     rng = random.Random(0)
