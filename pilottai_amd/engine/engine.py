@@ -77,8 +77,11 @@ class EngineConfig:
     dedup_inflight_prefix: bool = True  # requests wait for an identical prefix another request is prefilling
     split_decode: bool = True
     # > 0: mid / large steps size their decode partitions for about this many (partition, KV
-    # head) workgroups (scheduler.h decode_part_target); 0 = 512 / 256-key partitions
-    decode_part_target: int = 0
+    # head) workgroups (scheduler.h decode_part_target): no split once the decode rows fill a
+    # round of 4-wave attention workgroups (2 per CU), equal partitions otherwise; 0 = the
+    # 512 / 256-key partitions. 32 / 64 / 128-row steps (ctx 600) 4.10 / 4.87 / 5.54 ->
+    # 4.05 / 4.67 / 5.45 ms (profiles/r4_att_mid_options_ab.jsonl)
+    decode_part_target: int = int(os.environ.get("PILOTTAI_DECODE_PART_TARGET", "512"))
     use_graphs: bool = True
     token_buckets: Optional[List[int]] = None
     seed: int = 0
