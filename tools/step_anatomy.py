@@ -34,16 +34,23 @@ def main():
     rng = random.Random(0)
     prefix = [rng.randrange(1000, 100000) for _ in range(a.cached)]
     eng.generate([prefix], temperature=0.0, max_tokens=1, ignore_eos=True)  # cache the prefix
+    from pilottai_amd.ops import kernels
+
+    C = kernels.require_native()
     times = []
     for r in range(a.reps):
         prompts = [prefix + [rng.randrange(1000, 100000) for _ in range(a.new)] for _ in range(a.seqs)]
         torch.cuda.synchronize()
+        if r == 1:  # rep 0 warms up; markers bound the rest (prof_summary.py --between-markers)
+            C.timeline_marker(0)
         s0 = eng.stats["steps"]
         t0 = time.perf_counter()
         eng.generate(prompts, temperature=0.0, max_tokens=1, ignore_eos=True)
         torch.cuda.synchronize()
         times.append((time.perf_counter() - t0) * 1e3)
         print(json.dumps({"rep": r, "ms": round(times[-1], 2), "steps": eng.stats["steps"] - s0}), flush=True)
+    C.timeline_marker(1)
+    torch.cuda.synchronize()
     print(json.dumps({"seqs": a.seqs, "new": a.new, "cached": a.cached, "ms_median": sorted(times)[len(times) // 2],
                       "buckets": {str(k): v for k, v in eng.bucket_hist.items()}}), flush=True)
 
