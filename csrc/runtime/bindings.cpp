@@ -132,6 +132,7 @@ PYBIND11_MODULE(_runtime, m) {
         if (d.contains("small_step_tokens")) c.small_step_tokens = d["small_step_tokens"].cast<int32_t>();
         if (d.contains("small_step_part")) c.small_step_part = d["small_step_part"].cast<int32_t>();
         if (d.contains("decode_part_target")) c.decode_part_target = d["decode_part_target"].cast<int32_t>();
+        if (d.contains("small_step_target")) c.small_step_target = d["small_step_target"].cast<int32_t>();
         if (d.contains("eos_ids")) c.eos_ids = d["eos_ids"].cast<std::vector<int32_t>>();
         return std::make_unique<Scheduler>(c);
       }))

@@ -351,7 +351,8 @@ int32_t Scheduler::schedule(int32_t* buf) {
     for (const Planned& p : last_plan_) t_step += p.n;
     if (cfg_.small_step_part > 0 && t_step <= cfg_.small_step_tokens && parts512 * kv < target)
       psz = std::max(psz, cfg_.small_step_part);
-    if (cfg_.decode_part_target > 0 && t_step > cfg_.small_step_tokens) {
+    const int32_t dpt = t_step > cfg_.small_step_tokens ? cfg_.decode_part_target : cfg_.small_step_target;
+    if (dpt > 0 && (t_step > cfg_.small_step_tokens || cfg_.small_step_part > 0)) {
       // one balanced round of workgroups instead of 512-key parts + short remainders
       int64_t ndec = 0, maxc = 0;
       for (const Planned& p : last_plan_)
@@ -360,7 +361,7 @@ int32_t Scheduler::schedule(int32_t* buf) {
           maxc = std::max<int64_t>(maxc, p.s->num_computed + p.n);
         }
       if (ndec > 0) {
-        const int64_t tgt = cfg_.decode_part_target;
+        const int64_t tgt = dpt;
         int64_t cand;
         if (ndec * kv >= tgt) {
           cand = std::max<int64_t>(maxc, 32);  // whole contexts: nparts = 1 everywhere

@@ -54,6 +54,9 @@ struct SchedulerConfig {
   // equal partitions of the longest context (multiples of 32 keys, >= 128); 0 = the 512 / 256-key
   // rule
   int32_t decode_part_target = 0;
+  // the same rule for the decode-sized steps that run 8-wave attention (small_step_part > 0,
+  // t_step <= small_step_tokens; one 8-wave workgroup per CU): 0 = small_step_part
+  int32_t small_step_target = 0;
   // GEMM-friendly step sizes: when a step has T > token_align tokens and
   // T % token_align <= align_slack, the tail of the multi-token chunks (prefill /
   // jump-forward) is deferred so that T is a multiple of token_align (library

@@ -82,6 +82,12 @@ class EngineConfig:
     # 512 / 256-key partitions. 32 / 64 / 128-row steps (ctx 600) 4.10 / 4.87 / 5.54 ->
     # 4.05 / 4.67 / 5.45 ms (profiles/r4_att_mid_options_ab.jsonl)
     decode_part_target: int = int(os.environ.get("PILOTTAI_DECODE_PART_TARGET", "512"))
+    # decode-sized steps on 8-wave attention (scheduler.h small_step_part): the smallest
+    # flash-decoding partition they use; 4096 = whole contexts (no merge) up to 4,096 keys
+    small_step_part: int = int(os.environ.get("PILOTTAI_SMALL_STEP_PART", "4096"))
+    # > 0: decode-sized steps size their partitions for about this many (partition, KV head)
+    # 8-wave workgroups (scheduler.h small_step_target); 0 = small_step_part alone
+    small_step_target: int = int(os.environ.get("PILOTTAI_SMALL_STEP_TARGET", "0"))
     use_graphs: bool = True
     token_buckets: Optional[List[int]] = None
     seed: int = 0
@@ -268,7 +274,8 @@ class LLMEngine:
             "token_align": cfg.token_align, "align_slack": cfg.align_slack,
             "kv_heads": self.model.kv_local,
             "small_step_tokens": small_step,
-            "small_step_part": 4096 if small_step else 0,
+            "small_step_part": int(cfg.small_step_part) if small_step else 0,
+            "small_step_target": int(cfg.small_step_target) if small_step else 0,
             "decode_part_target": int(cfg.decode_part_target),
             "eos_ids": list(self.tok.eos_ids)})
         L = self.L = self.sched.layout()

@@ -757,3 +757,35 @@ def test_scheduler_decode_part_target_one_balanced_round(rows):
     ql, cl = buf[L["q_len"]:L["q_len"] + c[1]], buf[L["ctx_len"]:L["ctx_len"] + c[1]]
     ref_items, _ = build_attention_items(list(ql), list(cl), 4, part=part)
     assert [tuple(int(v) for v in x) for x in items] == ref_items
+
+
+def test_scheduler_small_step_target_splits_few_rows():
+    """small_step_target (csrc/runtime/scheduler.cpp): a decode-sized step on 8-wave attention
+    (small_step_tokens / small_step_part set) with 8 rows x 8 KV heads = 64 workgroups splits
+    each ~600-key context into 3 equal partitions (~192 workgroups) instead of running whole
+    contexts; without the target the step keeps small_step_part (whole contexts)."""
+    for target, want_parts in ((192, 3), (0, 1)):
+        cfg = {"num_blocks": 1024, "block_size": 16, "max_num_seqs": 16, "max_num_batched_tokens": 1024,
+               "max_prefill_tokens": 1024, "max_model_len": 4096, "gqa_group": 4, "kv_heads": 8,
+               "small_step_tokens": 16, "small_step_part": 4096, "small_step_target": target,
+               "decode_part_target": 512, "eos_ids": [128009]}
+        s = _runtime.Scheduler(cfg)
+        L = s.layout()
+        buf = np.zeros(L["total"], dtype=np.int32)
+        rng = np.random.default_rng(2)
+        for rid in range(8):
+            s.add_request(rid, list(rng.integers(1000, 9000, 599)), 0.0, 50, rid, True, [], None)
+        for _ in range(50):
+            s.schedule(buf.ctypes.data)
+            c = buf[L["counts"]:L["counts"] + 8]
+            s.commit(np.full(max(1, int(c[2])), 7, np.int32).ctypes.data, int(c[2]))
+            if all(x[4] >= 599 for x in s.debug_state()):
+                break
+        assert s.schedule(buf.ctypes.data) == 8
+        c = buf[L["counts"]:L["counts"] + 8]
+        items = buf[L["items"]:L["items"] + 4 * c[3]].reshape(-1, 4)
+        part = int(buf[L["part_size"]])
+        assert ((items[:, 2] >> 20) == want_parts).all(), (target, part, items[:, 2] >> 20)
+        assert len(items) == 8 * want_parts
+        if target:
+            assert part == 224  # ceil(601 / 3) rounded up to 32 keys
