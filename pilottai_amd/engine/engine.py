@@ -86,8 +86,10 @@ class EngineConfig:
     # flash-decoding partition they use; 4096 = whole contexts (no merge) up to 4,096 keys
     small_step_part: int = int(os.environ.get("PILOTTAI_SMALL_STEP_PART", "4096"))
     # > 0: decode-sized steps size their partitions for about this many (partition, KV head)
-    # 8-wave workgroups (scheduler.h small_step_target); 0 = small_step_part alone
-    small_step_target: int = int(os.environ.get("PILOTTAI_SMALL_STEP_TARGET", "0"))
+    # 8-wave workgroups (scheduler.h small_step_target); 0 = small_step_part alone. 8-row steps
+    # (ctx 600 / 1,200) 3.228 / 3.461 -> 3.172 / 3.331 ms, 16 rows unchanged
+    # (profiles/r4_small_step_partitions_ab.jsonl)
+    small_step_target: int = int(os.environ.get("PILOTTAI_SMALL_STEP_TARGET", "192"))
     use_graphs: bool = True
     token_buckets: Optional[List[int]] = None
     seed: int = 0
