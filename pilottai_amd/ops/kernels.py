@@ -190,9 +190,13 @@ def attn_o(out, part_o, part_ml, q, k_cache, v_cache, items, n_items, counters, 
            part_size: Optional[torch.Tensor] = None) -> bool:
     """Decode-sized steps: paged attention into `out` [T, H, 128] AND h[:T] += out . Wo^T (Wo
     packed by pack_decode_weight) in one launch (csrc/ops/attention.hip attn_o_kernel: the O
-    tiles' weights stream into LDS while the attention runs, one workgroup per CU).
-    Returns False if the shape / device does not allow it (then nothing ran). CPU: the
-    reference attention + mid_gemm residual path."""
+    tiles' weights stream into LDS / registers of the workgroups without an attention unit
+    while the attention runs, one workgroup per CU; the attention output is handed over by
+    write-through stores and sc1 loads). Measured slower than the two launches in the engine
+    (BENCHMARKS.md), so LlamaModel.ATTN_O_FUSED is off by default. Diagnostics:
+    PILOTTAI_ATTN_O_MODE bits (attention.hip AttnOArgs.mode). Returns False if the shape /
+    device does not allow it (then nothing ran). CPU: the reference attention + mid_gemm
+    residual path."""
     if _on_gpu(q):
         sync, err = attn_o_workspace(q.device)
         return bool(require_native().attn_o(out, part_o, part_ml, q, k_cache, v_cache, items, n_items, counters,
