@@ -80,8 +80,9 @@ class EngineConfig:
     # head) workgroups (scheduler.h decode_part_target): no split once the decode rows fill a
     # round of 4-wave attention workgroups (2 per CU), equal partitions otherwise; 0 = the
     # 512 / 256-key partitions. 32 / 64 / 128-row steps (ctx 600) 4.10 / 4.87 / 5.54 ->
-    # 4.05 / 4.67 / 5.45 ms (profiles/r4_att_mid_options_ab.jsonl)
-    decode_part_target: int = int(os.environ.get("PILOTTAI_DECODE_PART_TARGET", "512"))
+    # 4.05 / 4.67 / 5.45 ms (profiles/r4_att_mid_options_ab.jsonl); headline bench, same box:
+    # 1,024 2 % worse than 512, 384 1 % better (profiles/r4_engine_knobs_ab.jsonl)
+    decode_part_target: int = int(os.environ.get("PILOTTAI_DECODE_PART_TARGET", "384"))
     # decode-sized steps on 8-wave attention (scheduler.h small_step_part): the smallest
     # flash-decoding partition they use; 4096 = whole contexts (no merge) up to 4,096 keys
     small_step_part: int = int(os.environ.get("PILOTTAI_SMALL_STEP_PART", "4096"))
