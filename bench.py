@@ -66,8 +66,6 @@ def parse():
     ap.add_argument("--steps-per-task", type=int, default=1)
     ap.add_argument("--fused-max-t", type=int, default=None,
                     help="largest step on the fused packed-weight decode path (default: the model's)")
-    ap.add_argument("--wide-max-t", type=int, default=None,
-                    help="largest step on the packed small-batch path (default: the model's)")
     ap.add_argument("--mid-max-t", type=int, default=None,
                     help="largest step on the LDS-DMA tiled mid-size path (default: the model's; 0 = off)")
     ap.add_argument("--prefill-max-t", type=int, default=None,
@@ -76,15 +74,12 @@ def parse():
                     help="prefill tokens per step from which attention uses the 4-wave LDS-staged items")
     ap.add_argument("--no-prefix-dedup", action="store_true",
                     help="admit requests whose prefix another request is prefilling right away (no deferral)")
-    ap.add_argument("--no-prefetch", action="store_true", help="decode steps without the side-stream weight prefetch")
     ap.add_argument("--token-align", type=int, default=256, help="GEMM-friendly step sizes (0 = off)")
     ap.add_argument("--pf-midrange", default=None,
                     help="comma-separated projections (qkv,o,gate_up,down) on the prefill kernels at <= 256 tokens "
                          "per LlamaModel.PF_CFG; 'none' = mid kernel only (default: model's)")
     ap.add_argument("--att-decode-waves", type=int, default=None, choices=[4, 8],
                     help="attention workgroup width on decode-sized steps (default: model's)")
-    ap.add_argument("--att-queue", type=int, default=None, choices=[0, 1],
-                    help="persistent work-queue attention launch (default: engine's)")
     ap.add_argument("--async-steps", type=int, default=None, choices=[0, 1],
                     help="pipelined engine steps (schedule/launch step N+1 while step N runs); default: engine's")
     ap.add_argument("--align-slack", type=int, default=96)
@@ -134,12 +129,14 @@ async def run_rank(a, rank: int, world: int, device):
 
     n_local = len(shard_workers(a.workers, world, rank))
     t_init = time.time()
+    if a.hybrid_latency > 0 and a.memory_rows > 0 and world > 1:
+        raise SystemExit("--memory-rows needs an engine on every rank: not with --hybrid-latency")
     if a.hybrid_latency > 0 and rank > 0:
         return await run_cpu_rank(a, rank, world, n_local)
     memory = lookup = None
     if a.memory_rows > 0:
         # before the engine sizes its KV pool: the index is resident beside the model
-        memory, lookup = build_memory(a, device)
+        memory, lookup = build_memory(a, device, rank, world, node=a.dp_mode == "node" and world > 1)
     eng = LLMEngine(EngineConfig(model=a.model if not a.cpu else "tiny", max_num_seqs=max(64, 2 * n_local),
                                  max_num_batched_tokens=a.max_batched_tokens,
                                  max_prefill_tokens=a.max_batched_tokens,
@@ -148,13 +145,11 @@ async def run_rank(a, rank: int, world: int, device):
                                  kv_cache_fraction=0.85,
                                  num_kv_blocks=4096 if a.cpu else None, seed=1234 + rank,
                                  token_align=a.token_align, align_slack=a.align_slack,
-                                 decode_fused_max_t=a.fused_max_t, wide_max_t=a.wide_max_t,
+                                 decode_fused_max_t=a.fused_max_t,
                                  mid_max_t=a.mid_max_t, prefill_max_t=a.prefill_max_t,
                                  reply_tokens=a.reply_tokens,
-                                 prefetch_weights=False if a.no_prefetch else None,
                                  dedup_inflight_prefix=not a.no_prefix_dedup,
                                  **({"async_steps": bool(a.async_steps)} if a.async_steps is not None else {}),
-                                 **({"att_queue": bool(a.att_queue)} if a.att_queue is not None else {}),
                                  **({"att_decode_waves": a.att_decode_waves} if a.att_decode_waves is not None else {}),
                                  **({"pf_midrange": [k for k in a.pf_midrange.split(",") if k and k != "none"]}
                                     if a.pf_midrange is not None else {}),
@@ -294,6 +289,9 @@ async def run_rank(a, rank: int, world: int, device):
     if lookup is not None:
         dev_s = lookup.lookup_device_seconds()
         mem = {"rows": memory.index.count, "index_gb": round(memory.index.memory_bytes() / 2**30, 2),
+               # node mode: ONE node-wide store, rows sharded over the ranks (memory/node_store.py)
+               "store": "node-sharded" if hasattr(memory, "search_rows_blocking") else "single-index",
+               "node_rounds": memory.stats.get("rounds") if hasattr(memory, "search_rows_blocking") else None,
                "lookups": lookup.stats["lookups"] - mem0["lookups"],
                # the encoder's work when the serving model embeds (--embedder engine):
                # embedding requests and their prefilled tokens inside the continuous batch
@@ -330,9 +328,13 @@ async def run_rank(a, rank: int, world: int, device):
             await ag.stop()
     else:
         await serve.stop()
+    if memory is not None and hasattr(memory, "search_rows_blocking"):
+        await asyncio.to_thread(memory.stop)  # leaves once every rank has stopped
     eng.stop()
     local = {
         "dt": dt, "tasks": len(latencies), "lat": latencies, "init_s": init_s, "requeued": requeued,
+        "device": _device_identity(device),
+        "mem_rows": memory.index.count if memory is not None else 0,
         "loop_lag": sorted(lags), "executions_by_rank": by_rank,
         "managers": 1 if serve is not None else 0, "dp_mode": a.dp_mode if world > 1 else "single",
         "tokens": st1["tokens"] - st0["tokens"], "steps": st1["steps"] - st0["steps"],
@@ -397,32 +399,53 @@ async def run_cpu_rank(a, rank: int, world: int, n_local: int):
     zero = {k: 0 for k in ("tokens", "steps", "sampled", "busy_s", "prefix_hit", "prefix_defers", "spec_rows",
                            "spec_voided", "bucket_tokens", "prompt_total", "hbm_used_gb", "graph_captures")}
     return dict(zero, dt=dt, tasks=0, lat=[], init_s=init_s, requeued=0, loop_lag=[], executions_by_rank=None,
+                device=_device_identity(None),
                 managers=0, dp_mode="node", calls=len(llm.calls) if hasattr(llm, "calls") else 0, prompt_tokens=0,
                 completion_tokens=0, async_steps=False, host_phases={}, req_lat={}, memory=None, node_load=None,
                 buckets={}, cpu_rank=True)
 
 
-def build_memory(a, device):
-    """Semantic memory co-resident with the engine: an EnhancedMemory
-    whose HBM index holds `a.memory_rows` rows (random unit vectors standing in for an
-    archive of past findings, filled on the device in 1M-row chunks) plus whatever the
-    agents write back; one MemoryLookupBatcher shared by the rank's agents."""
+def _device_identity(device) -> dict:
+    """What this rank actually ran on: the torch device and, for a GPU, the physical card's
+    identity (UUID / PCI bus id) -- so the driver can check that an N-GPU line used N cards."""
+    if device is None or device.type != "cuda":
+        return {"device": "cpu", "physical": None}
+    import torch
+
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    props = torch.cuda.get_device_properties(idx)
+    dom, bus, dev = (getattr(props, k, None) for k in ("pci_domain_id", "pci_bus_id", "pci_device_id"))
+    if bus is not None:
+        phys = f"pci:{int(dom or 0):04x}:{int(bus):02x}:{int(dev or 0):02x}"
+    else:
+        phys = f"visible:{os.environ.get('HIP_VISIBLE_DEVICES', os.environ.get('CUDA_VISIBLE_DEVICES', ''))}/{idx}"
+    return {"device": f"cuda:{idx}", "physical": phys, "name": props.name, "uuid": str(getattr(props, "uuid", ""))}
+
+
+def build_memory(a, device, rank: int = 0, world: int = 1, node: bool = False):
+    """Semantic memory co-resident with the engine: `a.memory_rows` rows
+    (random unit vectors standing in for an archive of past findings, filled on the device in
+    1M-row chunks) plus whatever the agents write back; one MemoryLookupBatcher shared by the
+    rank's agents. Single rank: an EnhancedMemory over one HBM index. Node mode (N ranks): ONE
+    node-wide store (memory/node_store.py) -- this rank holds its 1/N shard of the rows
+    (global row = local row * N + rank), every lookup scans all shards in a lockstep round."""
     import torch
 
     from pilottai_amd.memory.batcher import MemoryLookupBatcher
     from pilottai_amd.memory.enhanced_memory import EnhancedMemory
 
     dim = 1024
-    cap = a.memory_rows + 65536  # room for the run's write-backs
-    mem = EnhancedMemory(max_size=cap, device=device, dim=dim,
-                         fallback_text=lambda r: f"archived finding {r}: prior document review notes")
+    fallback = lambda r: f"archived finding {r}: prior document review notes"  # noqa: E731
+    rows = a.memory_rows // world + (1 if rank < a.memory_rows % world else 0) if node else a.memory_rows
+    cap = rows + 65536  # room for the run's write-backs
+    mem = EnhancedMemory(max_size=cap, device=device, dim=dim, fallback_text=fallback)
     idx = mem.index
     idx._grow(cap)
-    g = torch.Generator(device=device).manual_seed(7)
+    g = torch.Generator(device=device).manual_seed(7 + rank)
     tags = [idx.tags.bit(t) for t in ("archive", "finance", "ops", "legal")]
     done = 0
-    while done < a.memory_rows:
-        m = min(1 << 20, a.memory_rows - done)
+    while done < rows:
+        m = min(1 << 20, rows - done)
         v = torch.randn(m, dim, device=device, generator=g, dtype=torch.float32)
         pr = torch.randint(0, 3, (m,), device=device, dtype=torch.int32, generator=g)
         tb = (1 << tags[0]) | (1 << torch.randint(1, 4, (m,), device=device, generator=g)).to(torch.int64)
@@ -430,6 +453,17 @@ def build_memory(a, device):
         done += m
     if device.type == "cuda":
         torch.cuda.synchronize(device)
+    if node:
+        import torch.distributed as dist
+
+        from pilottai_amd.memory.node_store import NodeSemanticStore
+
+        # the store's own groups (every rank creates them in this order): device collectives
+        # on the job's backend (RCCL), host metadata on gloo
+        grp = dist.new_group(backend=dist.get_backend())
+        cpu_grp = dist.new_group(backend="gloo") if dist.get_backend() != "gloo" else grp
+        mem = NodeSemanticStore(idx, embedder=mem.embedder, group=grp, cpu_group=cpu_grp, fallback_text=fallback)
+        mem.start()
     return mem, MemoryLookupBatcher(mem, min_batch=a.memory_min_batch, max_wait_s=a.memory_wait_ms / 1000.0)
 
 
@@ -486,11 +520,19 @@ def main():
         lat0 = gathered[0]["req_lat"]  # rank 0's request timings (per-GPU engines are alike)
         calls = max(1, tot("calls"))
         value = tasks / dt if dt > 0 else 0.0
+        # scale-run evidence: physical GPUs the ranks actually used (a --share-gpu or hybrid
+        # rehearsal of N ranks on one card reports n_gpus 1), the process group RCCL / gloo saw
+        phys = sorted({g["device"]["physical"] for g in gathered if g["device"]["physical"]})
+        rehearsal = "hybrid" if a.hybrid_latency > 0 else ("share-gpu" if a.share_gpu and world > 1 else None)
+        import torch.distributed as dist
+
+        dist_backend = str(dist.get_backend()) if dist.is_initialized() else None
+        dist_world = dist.get_world_size() if dist.is_initialized() else 1
         out = {
             "metric": METRIC,
             "value": round(value, 3),
             "unit": "tasks/s",
-            "n_gpus": world if not a.cpu else 0,
+            "n_gpus": len(phys),
             "steps": a.steps,
             "warmup": a.warmup,
             "ms_per_step": round(1000.0 * dt / max(1, a.steps), 3),
@@ -550,7 +592,14 @@ def main():
                                               ("p99", 0.99, gathered[0]["loop_lag"]))},
             "executions_by_rank": gathered[0]["executions_by_rank"],
             "hybrid_latency_s": a.hybrid_latency or None,
-            "memory": gathered[0]["memory"],
+            "rehearsal": rehearsal,
+            "dist_backend": dist_backend,
+            "world_size": dist_world,
+            "devices": [g["device"]["device"] for g in gathered],
+            "physical_devices": phys,
+            "memory": (dict(gathered[0]["memory"], rows_per_rank=[g.get("mem_rows", 0) for g in gathered],
+                            rows_total=sum(g.get("mem_rows", 0) for g in gathered))
+                       if gathered[0]["memory"] else None),
             "node_load": gathered[0]["node_load"],
             "notes": "BASELINE.md publishes no number for this config (vs_baseline null); the reference's "
                      "structural bound with a remote LLM is ~0.8 tasks/s per LLMHandler (BASELINE.md §2).",

@@ -61,25 +61,45 @@ async def run(clients: int, n_tasks: int):
     await serve.start()
     lat = []
     per = max(1, n_tasks // clients)
+    # client interleaving: which client submitted each task (in submission order) and how
+    # many tasks were in flight at once -- with truly concurrent clients the submissions of
+    # different clients alternate and ~clients tasks are in flight (Little's law: mean
+    # latency ~= clients / throughput)
+    order = []
+    state = {"inflight": 0, "max_inflight": 0}
 
     async def client(ci):
         for j in range(per):
             t0 = time.perf_counter()
+            order.append(ci)
+            state["inflight"] += 1
+            state["max_inflight"] = max(state["max_inflight"], state["inflight"])
             r = await serve.execute_task(Task(description=f"echo {ci}-{j}"))
+            state["inflight"] -= 1
             lat.append(time.perf_counter() - t0)
             if not r.success:
                 raise RuntimeError(r.error)
 
     await asyncio.gather(*(client(i) for i in range(clients)))  # warmup pass
     lat.clear()
+    order.clear()
+    state["max_inflight"] = 0
     t0 = time.perf_counter()
     await asyncio.gather(*(client(i) for i in range(clients)))
     dt = time.perf_counter() - t0
     await serve.stop()
     lat.sort()
     n = len(lat)
+    switches = sum(1 for a_, b_ in zip(order, order[1:]) if a_ != b_)
+    mean_ms = 1000 * sum(lat) / n
     return {"clients": clients, "tasks": n, "tasks_per_s": round(n / dt, 1),
             "p50_ms": round(1000 * lat[n // 2], 3), "p99_ms": round(1000 * lat[min(n - 1, int(0.99 * n))], 3),
+            "mean_ms": round(mean_ms, 3),
+            # Little's law check: clients / throughput (ms) vs the measured mean latency
+            "littles_law_ms": round(1000 * clients / (n / dt), 3),
+            # fraction of consecutive submissions made by different clients (1 client: 0)
+            "interleave_frac": round(switches / max(1, len(order) - 1), 3),
+            "max_inflight": state["max_inflight"],
             "reference_tasks_per_s": REF.get(clients, (None,))[0], "reference_p50_ms": REF.get(clients, (0, None))[1]}
 
 

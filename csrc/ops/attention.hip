@@ -55,20 +55,10 @@ constexpr int ATT_LDS_DECODE_BYTES = att_lds_decode_bytes<4>();
 typedef __attribute__((address_space(1))) unsigned long long gu64;
 typedef __attribute__((address_space(1))) int gi32;
 
-// An attention output store (8 bf16): plain, or write-through (sc1: the line is not kept
-// dirty in this XCD's L2, so another workgroup of the same launch can read it after the
-// store drains and a counter says so, without a release / acquire; attn_o_kernel).
-template <bool WT>
-__device__ __forceinline__ void att_store8(bf16* p, const bf16x8 v) {
-  if constexpr (WT) {
-    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(p, 0, 16, 0x00020000);
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, 0, 0, 16);
-  } else {
-    *reinterpret_cast<bf16x8*>(p) = v;
-  }
-}
+// An attention output store (8 bf16, one 16-B vector store)
+__device__ __forceinline__ void att_store8(bf16* p, const bf16x8 v) { *reinterpret_cast<bf16x8*>(p) = v; }
 
-template <int G, int NW = 4, bool WT = false>
+template <int G, int NW = 4>
 __device__ __forceinline__ void decode_item(
     const int4 it, char* smem, bf16* __restrict__ out, float* __restrict__ part_o,
     float* __restrict__ part_ml, int* __restrict__ counters, const bf16* __restrict__ q, const bf16* __restrict__ k_cache,
@@ -289,7 +279,7 @@ __device__ __forceinline__ void decode_item(
     bf16x8 g8;
 #pragma unroll
     for (int j = 0; j < 8; ++j) g8[j] = (bf16)(ga[j] * ginv);
-    att_store8<WT>(out + ((size_t)(q0 + qb + ctq) * H + kvh * G + chg) * ATT_HD + d0, g8);
+    att_store8(out + ((size_t)(q0 + qb + ctq) * H + kvh * G + chg) * ATT_HD + d0, g8);
     return;
   }
   if (ctq >= nq || !mthr) return;
@@ -297,7 +287,7 @@ __device__ __forceinline__ void decode_item(
   bf16x8 w8;
 #pragma unroll
   for (int j = 0; j < 8; ++j) w8[j] = (bf16)(acc[j] * inv);
-  att_store8<WT>(out + ((size_t)(q0 + qb + ctq) * H + kvh * G + chg) * ATT_HD + d0, w8);
+  att_store8(out + ((size_t)(q0 + qb + ctq) * H + kvh * G + chg) * ATT_HD + d0, w8);
 }
 
 // ---------------------------------------------------------------------------
@@ -372,7 +362,7 @@ __device__ __forceinline__ f32x16 qk_tile(const bf16x8 (&kf)[8], const bf16x8 (&
   return s;
 }
 
-template <int G, int NW = 4, bool WT = false>
+template <int G, int NW = 4>
 __device__ __forceinline__ void prefill_item(
     const int4 it, char* smem, bf16* __restrict__ out, const bf16* __restrict__ q,
     const bf16* __restrict__ k_cache, const bf16* __restrict__ v_cache,
@@ -482,7 +472,7 @@ __device__ __forceinline__ void prefill_item(
     bf16x8 w8;
 #pragma unroll
     for (int j = 0; j < 8; ++j) w8[j] = (bf16)(acc[j] * inv);
-    att_store8<WT>(orow + 8 * c8, w8);
+    att_store8(orow + 8 * c8, w8);
   }
 }
 
@@ -628,7 +618,7 @@ __device__ __forceinline__ void prefill_item_wg(
 
 // A q-split item of either width. 8-wave workgroups run no LDS-staged wide items (their 4-wave
 // image layout): a wide item (128/G tokens) runs there as its 32-column sub-items.
-template <int G, int NW, bool WT = false>
+template <int G, int NW>
 __device__ __forceinline__ void prefill_any(
     const int4 it, char* smem, bf16* __restrict__ out, const bf16* __restrict__ q,
     const bf16* __restrict__ k_cache, const bf16* __restrict__ v_cache,
@@ -636,16 +626,15 @@ __device__ __forceinline__ void prefill_any(
     const int* __restrict__ block_table, int max_blocks, int H, int KV, int kvh, float scale_log2) {
   const int nq = it.z & 0xff;
   if (nq <= 32 / G) {
-    prefill_item<G, NW, WT>(it, smem, out, q, k_cache, v_cache, q_start, q_len, ctx_len, block_table, max_blocks,
+    prefill_item<G, NW>(it, smem, out, q, k_cache, v_cache, q_start, q_len, ctx_len, block_table, max_blocks,
                             H, KV, kvh, scale_log2);
   } else if constexpr (NW == 4) {
-    static_assert(!WT, "write-through outputs: 8-wave items only");
     prefill_item_wg<G>(it, smem, out, q, k_cache, v_cache, q_start, q_len, ctx_len, block_table, max_blocks, H, KV,
                        kvh, scale_log2);
   } else {
     for (int sb = 0; sb < nq; sb += 32 / G) {
       const int4 sub = {it.x, it.y + sb, min(32 / G, nq - sb) | (it.z & ~0xff), it.w};
-      prefill_item<G, NW, WT>(sub, smem, out, q, k_cache, v_cache, q_start, q_len, ctx_len, block_table,
+      prefill_item<G, NW>(sub, smem, out, q, k_cache, v_cache, q_start, q_len, ctx_len, block_table,
                               max_blocks, H, KV, kvh, scale_log2);
       __syncthreads();  // LDS reuse by the next sub-item
     }
@@ -662,442 +651,84 @@ constexpr int ATT_LDS_BYTES = ATT_LDS_BYTES0 > PW_NBUF * PW_TILE ? ATT_LDS_BYTES
 // One launch serves a whole ragged step: items (seq, q_begin, nq | part<<8 |
 // nparts<<20, partial slot) are strided over the grid, so the shape-stable
 // (graph-captured) grid can be sized to the chip rather than to the worst case.
-// MODE 0: every item of the step (one launch); MODE 1: the decode / short items only,
-// items [n_items[1], n_items[0]); MODE 2: the prefill (q-split) items only, items
-// [0, n_items[1]) -- the scheduler lists them first. Split into two launches, each kernel
-// gets the register budget of its own paths (the mixed kernel carries 254 VGPRs, 2 waves
-// per SIMD, for the wide prefill path's sake).
-// MODE 3 (the engine's default): a persistent 1-D grid of 2 workgroups per CU, work-queue
-// scheduled. Workgroup b serves KV head b % KV -- with KV = 8 that is its XCD under the
-// round-robin dispatch, so every K/V page of a head is read through one XCD's L2 -- and
-// takes item b / KV first, then pulls further items from the head's queue counter
-// (queue[kvh]; queue[KV + kvh] counts the workgroups done, and the last one resets both
-// for the next launch). The scheduler lists the items heaviest first, so the workgroups
-// that finish a short prefill item pick up the decode items: in a mixed step they run
-// beside the long prefill items instead of in a second wave after them (MODE 0 holds the
-// decode items until a prefill item retires, and its padded grid's empty workgroups are
-// dispatched between the real ones).
-template <int G, int MODE, int NW = 4>
+// (Round 4 measured and removed two alternatives: a persistent work-queue launch and idle
+// workgroups warming the next projection's weights into the Infinity Cache; neither paid
+// end to end, BENCHMARKS.md.)
+template <int G, int NW = 4>
 __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void paged_attn_kernel(
     bf16* __restrict__ out, float* __restrict__ part_o, float* __restrict__ part_ml,
     int* __restrict__ counters, const bf16* __restrict__ q, const bf16* __restrict__ k_cache,
     const bf16* __restrict__ v_cache, const int4* __restrict__ items,
     const int* __restrict__ n_items, const int* __restrict__ part_size, const int* __restrict__ q_start,
     const int* __restrict__ q_len, const int* __restrict__ ctx_len,
-    const int* __restrict__ block_table, int max_blocks, int H, int KV, float scale_log2,
-    const u32x4* __restrict__ pf, long long pf_lines, u32x4* __restrict__ pf_sink, int acq,
-    int* __restrict__ queue) {
+    const int* __restrict__ block_table, int max_blocks, int H, int KV, float scale_log2, int acq) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int TPW = 16 / G;
   const int psz_q = part_size ? part_size[0] : ATT_PART;
-  if (MODE == 3) {
-    __shared__ int s_next;
-    const int kvh = (int)blockIdx.x % KV;
-    const int nslot = (int)gridDim.x / KV;
-    const int slot = (int)blockIdx.x / KV;
-    const int n = n_items[0];
-    int item = slot;
-    if (item >= n && pf_lines > 0) {  // no item at all: prefetch as in the grid modes
-      const long long idle = (long long)(nslot - n) * KV;
-      const long long me = (long long)kvh * (nslot - n) + (slot - n);
-      const long long per = (pf_lines + idle - 1) / idle;
-      const long long l1 = min(pf_lines, (me + 1) * per);
-      u32x4 acc = {0u, 0u, 0u, 0u};
-      for (long long l = me * per + threadIdx.x; l < l1; l += blockDim.x) acc ^= pf[4 * l];
-      if (acc.x == 0x9E3779B9u && acc.y == 0x7F4A7C15u && acc.z == 0xF39CC060u && acc.w == 0x5CEDC834u)
-        pf_sink[threadIdx.x] = acc;
-    }
-    while (item < n) {
-      const int4 it = items[item];
-      // the next item is claimed while this one runs: the claim's return is only consumed
-      // after the item (older than the item's loads, it only makes their counted waits
-      // conservative in wave 0)
-      int claimed = 0;
-      if (threadIdx.x == 0)
-        claimed = nslot + __hip_atomic_fetch_add((gi32*)(queue + kvh), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const int nq = it.z & 0xff;
-      if (nq <= TPW)
-        decode_item<G, NW>(it, smem, out, part_o, part_ml, counters, q, k_cache, v_cache, q_start, q_len, ctx_len,
-                           block_table, max_blocks, H, KV, kvh, scale_log2, psz_q, acq);
-      else
-        prefill_any<G, NW>(it, smem, out, q, k_cache, v_cache, q_start, q_len, ctx_len, block_table, max_blocks, H,
-                           KV, kvh, scale_log2);
-      if (threadIdx.x == 0) s_next = claimed;
-      __syncthreads();  // LDS reuse by the next item; s_next visible to every wave
-      item = s_next;
-      __syncthreads();
-    }
-    // every workgroup of this head is past its last claim: the last one resets the queue
-    if (threadIdx.x == 0) {
-      const int d = __hip_atomic_fetch_add((gi32*)(queue + KV + kvh), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (d == nslot - 1) {
-        __hip_atomic_store((gi32*)(queue + kvh), 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store((gi32*)(queue + KV + kvh), 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
-    return;
-  }
   // The first item is loaded together with the item count, not after it: one dependent
   // memory round trip less before the K/V stream starts (decode steps with few rows are
   // latency-bound). In bounds: the host sizes the grid to gridDim.x <= max_items, the
   // length of `items`.
-  const int i0 = MODE == 1 ? n_items[1] : 0;
-  const int n = MODE == 2 ? n_items[1] : n_items[0];
-  int4 it_next = items[min((int)blockIdx.x + i0, max(n - 1, 0))];
-  if (MODE == 2 && (int)blockIdx.x + i0 >= n) return;
-  if ((int)blockIdx.x + i0 >= n) {
-    // A workgroup without an item (the grid is sized for the bucket's largest item
-    // list; a decode step of 8 rows uses ~1/70 of it): read a slice of the next
-    // projection's weights so they are in the Infinity Cache when it starts (the
-    // attention K/V stream leaves most of HBM's bandwidth idle at small batch).
-    if (pf_lines > 0) {
-      const long long idle = (long long)(gridDim.x - (n - i0)) * gridDim.y;
-      const long long me = (long long)blockIdx.y * (gridDim.x - (n - i0)) + (blockIdx.x - (n - i0));
-      const long long per = (pf_lines + idle - 1) / idle;
-      const long long l1 = min(pf_lines, (me + 1) * per);
-      u32x4 acc = {0u, 0u, 0u, 0u};
-      for (long long l = me * per + threadIdx.x; l < l1; l += blockDim.x) acc ^= pf[4 * l];  // 16 B per 64-B line
-      if (acc.x == 0x9E3779B9u && acc.y == 0x7F4A7C15u && acc.z == 0xF39CC060u && acc.w == 0x5CEDC834u)
-        pf_sink[threadIdx.x] = acc;  // never in practice: keeps the loads
-    }
-    return;
-  }
+  const int n = n_items[0];
+  int4 it_next = items[min((int)blockIdx.x, max(n - 1, 0))];
+  if ((int)blockIdx.x >= n) return;  // the grid is sized for the bucket's largest item list
   const int psz = psz_q;  // decode partition (keys), per step
   const int kvh = blockIdx.y;
-  for (int item = blockIdx.x + i0; item < n; item += gridDim.x) {
+  for (int item = blockIdx.x; item < n; item += gridDim.x) {
     const int4 it = it_next;
     if (item + (int)gridDim.x < n) it_next = items[item + gridDim.x];
     const int nq = it.z & 0xff;
-    if (MODE != 2 && nq <= TPW)
+    if (nq <= TPW)
       decode_item<G, NW>(it, smem, out, part_o, part_ml, counters, q, k_cache, v_cache, q_start, q_len, ctx_len,
                          block_table, max_blocks, H, KV, kvh, scale_log2, psz, acq);
-    else if (MODE != 1)
+    else
       prefill_any<G, NW>(it, smem, out, q, k_cache, v_cache, q_start, q_len, ctx_len, block_table, max_blocks, H,
                          KV, kvh, scale_log2);
     __syncthreads();  // LDS reuse by the next item
   }
 }
 
-// ---------------------------------------------------------------------------
-// Decode-sized steps (<= 16 tokens): attention and the O projection (+ residual) in ONE
-// launch (a persistent per-layer structure for the decode regime).
-//
-// Separate launches cost the O projection its whole weight stream (33.5 MB, ~8 us at
-// M = 8, 4.1 TB/s) after the attention launch (~12 us, latency-bound on 64 workgroups for
-// 8 rows) and a kernel boundary. Here the grid is one workgroup per CU (N / 16 = 256 O
-// tiles of 16 output columns for Llama-3-8B):
-//   * workgroups [0, units) run the attention units (item, KV head) exactly as the 8-wave
-//     paged_attn_kernel does; every other workgroup meanwhile loads its O tile's packed
-//     weights (K / 32 KiB, 128 KiB) into LDS by LDS-DMA;
-//   * each attention workgroup publishes its finished unit: its output stores are
-//     write-through (sc1) and drained, workgroup barrier, one relaxed ticket on sync[0];
-//   * with units <= nwg / 2 (decode: 8 KV heads x <= 16 items), the o-only workgroup
-//     units + j also owns the attention workgroup j's O tile, held in registers (64 VGPRs a
-//     lane): the attention workgroups publish and leave, no weight byte waits for them;
-//     otherwise each attention workgroup loads its own tile after its units;
-//   * every computing workgroup waits (one lane, bounded spin, err flag on timeout) until
-//     sync[0] counts every unit and computes its 16 (or 2 x 16) columns for the <= 16 rows
-//     from sc1 loads of the attention output: 8 waves split K, partial tiles summed through
-//     LDS, residual added in place;
-//   * the last workgroup to leave resets sync[] (graph replay safe).
-// All workgroups must be resident at once: the launcher requires grid <= CU count and the
-// LDS (144 KiB) allows one workgroup per CU.
-struct AttnOArgs {
-  bf16* out;
-  float* part_o;
-  float* part_ml;
-  int* counters;
-  const bf16* q;
-  const bf16* k_cache;
-  const bf16* v_cache;
-  const int4* items;
-  const int* n_items;
-  const int* part_size;
-  const int* q_start;
-  const int* q_len;
-  const int* ctx_len;
-  const int* block_table;
-  int max_blocks, H, KV;
-  float scale_log2;
-  int acq;
-  const bf16* wo;  // packed [N / 16][K / 32][64][8]
-  bf16* h;         // [T, ldh], += out . Wo^T in place
-  int T, N, K, ldh;
-  int* sync;  // [2]: published units, departed workgroups (zero between launches)
-  int* err;   // 1 if a wait timed out (never in a healthy run)
-  // diagnostics (PILOTTAI_ATTN_O_MODE, default 0): bit 0 = an agent-scope release / acquire
-  // pair on top of the write-through hand-off; bit 1 = every workgroup loads its O tile only
-  // after the wait (no overlap with the attention, no split ownership); bit 2 = the o-only
-  // workgroups hold their weight loads ~2 us
-  int mode;
-  unsigned long long* stamps;  // diagnostics: per workgroup 8 s_memrealtime stamps (null: none)
-};
-
-template <int G>
-__global__ __launch_bounds__(512, 1) void attn_o_kernel(const AttnOArgs A) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  constexpr int TPW = 16 / G;
-  constexpr int PER = 16;  // k-steps per wave (K = 4096: the launcher checks)
-  const int bid = blockIdx.x, nwg = gridDim.x;
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int units = A.n_items[0] * A.KV;
-  const int KS = A.K >> 5;
-  const int psz = A.part_size ? A.part_size[0] : ATT_PART;
-  const bool att = bid < units;
-  const bool late = A.mode & 2;
-  // split ownership (units <= nwg / 2): the o-only workgroup units + j also computes the
-  // attention workgroup j's tile from registers (wave w holds that tile's k-steps
-  // [16 w, 16 w + 16): 64 VGPRs), loaded while the attention runs; attention workgroups
-  // then only publish and leave. Otherwise every workgroup computes its own tile.
-  const bool split = 2 * units <= nwg && !late;
-  const int rt = bid - units;  // split: the register tile of an o-only workgroup (< units)
-  const bool has_rt = split && !att && rt < units;
-  auto load_w = [&]() {  // k-step ks of tile bid -> smem + ks KiB (lane-linear, as packed)
-    const bf16* wt = A.wo + (size_t)bid * KS * 512;
-    for (int ks = wid; ks < KS; ks += 8)
-      __builtin_amdgcn_global_load_lds((att_gbl_t*)(wt + (size_t)ks * 512 + lane * 8),
-                                       (att_lds_t*)(smem + ks * 1024), 16, 0, 0);
-  };
-  auto stamp = [&](int i) {
-    if (A.stamps && threadIdx.x == 0) A.stamps[(size_t)bid * 8 + i] = __builtin_amdgcn_s_memrealtime();
-  };
-  stamp(0);
-  bf16x8 wr[PER];
-  if (!att && !late) {
-    if (A.mode & 4) {  // pacing (diagnostics): hold the weight stream ~2 us off the attention
-      const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-      while (__builtin_amdgcn_s_memrealtime() - t0 < 200) __builtin_amdgcn_s_sleep(8);
-    }
-    load_w();
-  }
-  for (int u = bid; u < units; u += nwg) {
-    const int kvh = u % A.KV;
-    const int4 it = A.items[u / A.KV];
-    if ((it.z & 0xff) <= TPW)
-      decode_item<G, 8, true>(it, smem, A.out, A.part_o, A.part_ml, A.counters, A.q, A.k_cache, A.v_cache,
-                              A.q_start, A.q_len, A.ctx_len, A.block_table, A.max_blocks, A.H, A.KV, kvh,
-                              A.scale_log2, psz, A.acq);
-    else
-      prefill_any<G, 8, true>(it, smem, A.out, A.q, A.k_cache, A.v_cache, A.q_start, A.q_len, A.ctx_len,
-                              A.block_table, A.max_blocks, A.H, A.KV, kvh, A.scale_log2);
-    // publish: the output went out write-through (sc1) and every wave drains it before the
-    // barrier; the consumers read it with sc1 loads, so no cache maintenance is needed
-    // (mode bit 0 adds an agent-scope release anyway: diagnostics)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      if (A.mode & 1) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-      __hip_atomic_fetch_add((gi32*)A.sync, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-  stamp(1);
-  if (has_rt) {  // (after the loop, which an o-only workgroup skips: wr is not live across it)
-    const bf16* w2 = A.wo + ((size_t)rt * KS + wid * PER) * 512 + lane * 8;
-#pragma unroll
-    for (int i = 0; i < PER; ++i) wr[i] = *reinterpret_cast<const bf16x8*>(w2 + (size_t)i * 512);
-  }
-  if (att && split) {
-    stamp(2);
-    stamp(3);
-    stamp(4);
-  } else {
-    if (att && !late) {
-      __syncthreads();  // every wave is done with the attention LDS
-      load_w();
-    }
-    stamp(2);
-    if (threadIdx.x == 0) {
-      unsigned spins = 0;
-      while (__hip_atomic_load((gi32*)A.sync, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < units) {
-        __builtin_amdgcn_s_sleep(1);
-        if (++spins > (1u << 24)) {
-          __hip_atomic_store((gi32*)A.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          break;
-        }
-      }
-      if (A.mode & 1) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    }
-    stamp(3);
-    if (late) {
-      __syncthreads();
-      load_w();
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's O-tile loads landed
-    __syncthreads();
-    stamp(4);
-
-    // O tiles: 16 columns x <= 16 rows; wave w sums its 16 k-steps. The x fragments are sc1
-    // loads (the attention output was stored write-through by other workgroups), all issued
-    // before the first MFMA.
-    const int c = lane & 15, g = lane >> 4;
-    const bool rowok = c < A.T;
-    const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(A.out, 0, A.T * A.K * 2, 0x00020000);
-    const int xoff = (min(c, A.T - 1) * A.K + 8 * g + wid * PER * 32) * 2;
-    bf16x8 xf[PER];
-#pragma unroll
-    for (int i = 0; i < PER; ++i)
-      xf[i] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rx, xoff + i * 64, 0, 16));
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f}, acc2 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      const bf16x8 xi = rowok ? xf[i] : bf16x8{};
-      const bf16x8 wf = *reinterpret_cast<const bf16x8*>(smem + (wid * PER + i) * 1024 + lane * 16);
-      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf, xi, acc, 0, 0, 0);
-      if (has_rt) acc2 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wr[i], xi, acc2, 0, 0, 0);
-    }
-    f32x4* red = reinterpret_cast<f32x4*>(smem + KS * 1024);
-    red[wid * 64 + lane] = acc;
-    if (has_rt) red[512 + wid * 64 + lane] = acc2;
-    __syncthreads();
-    // wave 0 finishes tile bid, wave 1 the register tile
-    if ((wid == 0 || (wid == 1 && has_rt)) && rowok) {
-      const f32x4* rr = red + wid * 512;
-      f32x4 v = rr[lane];
-#pragma unroll
-      for (int w = 1; w < 8; ++w) v += rr[w * 64 + lane];
-      // lane (g, c): columns 16 tile + 4 g .. + 3 of row c
-      bf16* dst = A.h + (size_t)c * A.ldh + (wid == 0 ? bid : rt) * 16 + 4 * g;
-      const bf16x4 r = *reinterpret_cast<const bf16x4*>(dst);
-      bf16x4 o;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) o[j] = (bf16)(v[j] + (float)r[j]);
-      *reinterpret_cast<bf16x4*>(dst) = o;
-    }
-  }
-  if (A.stamps) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    stamp(5);
-  }
-  if (threadIdx.x == 0) {  // the last workgroup out resets the counters for the next launch
-    const int d = __hip_atomic_fetch_add((gi32*)(A.sync + 1), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (d == nwg - 1) {
-      __hip_atomic_store((gi32*)A.sync, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store((gi32*)(A.sync + 1), 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-}
-
 }  // namespace pa
 
-// diagnostics: when set, the next attn_o launches write per-workgroup phase stamps here
-static unsigned long long* g_attn_o_stamps = nullptr;
-extern "C" void pa_attn_o_set_stamps(void* p) { g_attn_o_stamps = (unsigned long long*)p; }
-
-// Fused attention + O projection (+ residual) for decode-sized steps; returns 1 if the shape
-// or the device does not allow it (the caller then runs the two launches), 0 on success.
-extern "C" int pa_attn_o(void* out, float* part_o, float* part_ml, const void* q, const void* k_cache,
-                         const void* v_cache, const int* items, const int* n_items, const int* part_size,
-                         int* counters, const int* q_start, const int* q_len, const int* ctx_len,
-                         const int* block_table, int max_blocks, int H, int KV, float scale_log2, const void* wo,
-                         void* h, int T, int N, int K, int ldh, int* sync, int* err, hipStream_t st) {
-  if (H % KV != 0 || T <= 0 || T > 16 || N % 16 != 0 || K != H * 128 || K != 4096) return 1;
-  const int grid = N / 16;
-  static int ncu = 0;
-  if (ncu == 0) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-      ncu = -1;
-  }
-  const int lds = std::max(pa::ATT_LDS_BYTES8, (K / 32) * 1024 + 16 * 1024);
-  if (ncu <= 0 || grid > ncu || lds > 160 * 1024) return 1;
-  const pa::AttnOArgs a{(pa::bf16*)out, part_o, part_ml, counters, (const pa::bf16*)q, (const pa::bf16*)k_cache,
-                        (const pa::bf16*)v_cache, (const int4*)items, n_items, part_size, q_start, q_len, ctx_len,
-                        block_table, max_blocks, H, KV, scale_log2, pa::g_handoff_attn, (const pa::bf16*)wo,
-                        (pa::bf16*)h, T, N, K, ldh, sync, err, 1, g_attn_o_stamps};
-  static int mode_env = -1;
-  if (mode_env < 0) {
-    const char* e = getenv("PILOTTAI_ATTN_O_MODE");
-    mode_env = e ? atoi(e) : 0;
-  }
-  const_cast<pa::AttnOArgs&>(a).mode = mode_env;
-#define PA_AO(GG)                                                                                          \
-  do {                                                                                                     \
-    static bool attr = false;  /* the whole 160 KiB once: any launch's size fits */                       \
-    if (!attr) {                                                                                           \
-      (void)hipFuncSetAttribute((const void*)pa::attn_o_kernel<GG>, hipFuncAttributeMaxDynamicSharedMemorySize, \
-                                160 * 1024);                                                               \
-      attr = true;                                                                                         \
-    }                                                                                                      \
-    hipLaunchKernelGGL((pa::attn_o_kernel<GG>), dim3(grid), dim3(512), lds, st, a);                        \
-  } while (0)
-  switch (H / KV) {
-    case 1: PA_AO(1); break;
-    case 2: PA_AO(2); break;
-    case 4: PA_AO(4); break;
-    case 8: PA_AO(8); break;
-    default: return 1;
-  }
-#undef PA_AO
-  return (int)hipGetLastError() == 0 ? 0 : -2;
-}
-
-// split_prefill > 0: two launches -- the prefill items [0, n_items[1]) on their own kernel
-// with a grid of split_prefill workgroups per KV head, then the decode items.
 extern "C" int pa_paged_attention(void* out, float* part_o, float* part_ml, const void* q,
                                   const void* k_cache, const void* v_cache, const int* items,
-                                  const int* n_items, int max_items, int split_prefill, const int* part_size,
-                                  int* counters,
-                                  const int* q_start,
-                                  const int* q_len, const int* ctx_len, const int* block_table,
-                                  int max_blocks, int H, int KV, float scale_log2,
-                                  const void* pf, long long pf_bytes, void* pf_sink,
-                                  int* queue, int waves, hipStream_t st) {
+                                  const int* n_items, int max_items, const int* part_size, int* counters,
+                                  const int* q_start, const int* q_len, const int* ctx_len, const int* block_table,
+                                  int max_blocks, int H, int KV, float scale_log2, int waves, hipStream_t st) {
   if (H % KV != 0) return -1;
   if (waves != 4 && waves != 8) return -1;
-  if (pf_bytes > 0 && (pf == nullptr || pf_sink == nullptr || (reinterpret_cast<uintptr_t>(pf) & 15))) return -1;
-  const long long pf_lines = pf_bytes > 0 ? pf_bytes / 64 : 0;
   const int G = H / KV;
   // items are strided over the grid: ~8 resident workgroups per CU over all KV heads
   const int gx = max_items < 1 ? 1 : (max_items < 2048 / KV ? max_items : (2048 / KV > 0 ? 2048 / KV : 1));
-  dim3 grid(gx, KV);
-  // queue mode: 2 workgroups per CU (256 CUs), a multiple of KV, at most one slot per item
-  const int qslots = std::max(1, std::min(max_items, 512 / std::max(1, KV)));
-  dim3 qgrid(qslots * KV);
-#define PA_ATT1(GG, MD, GRID, PFP, PFL)                                                         \
-  do {                                                                                          \
-    if (waves == 8) {                                                                           \
-      static bool attr8_##GG##_##MD = false;                                                    \
-      if (!attr8_##GG##_##MD) {                                                                 \
-        (void)hipFuncSetAttribute((const void*)pa::paged_attn_kernel<GG, MD, 8>,                \
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, pa::ATT_LDS_BYTES8); \
-        attr8_##GG##_##MD = true;                                                               \
-      }                                                                                         \
-      hipLaunchKernelGGL((pa::paged_attn_kernel<GG, MD, 8>), GRID, dim3(512), pa::ATT_LDS_BYTES8, st, \
-                         (pa::bf16*)out, part_o, part_ml, counters, (const pa::bf16*)q,         \
-                         (const pa::bf16*)k_cache, (const pa::bf16*)v_cache, (const int4*)items, \
-                         n_items, part_size, q_start, q_len, ctx_len, block_table, max_blocks, H, \
-                         KV, scale_log2, (const pa::u32x4*)PFP, PFL, (pa::u32x4*)pf_sink,      \
-                         pa::g_handoff_attn, queue);                                           \
-      break;                                                                                    \
-    }                                                                                           \
-    static bool attr_##GG##_##MD = false;                                                       \
-    if (!attr_##GG##_##MD) {                                                                    \
-      (void)hipFuncSetAttribute((const void*)pa::paged_attn_kernel<GG, MD>,                     \
-                                hipFuncAttributeMaxDynamicSharedMemorySize, pa::ATT_LDS_BYTES); \
-      attr_##GG##_##MD = true;                                                                  \
-    }                                                                                           \
-    hipLaunchKernelGGL((pa::paged_attn_kernel<GG, MD>), GRID, dim3(256), pa::ATT_LDS_BYTES, st,  \
-                       (pa::bf16*)out, part_o, part_ml, counters, (const pa::bf16*)q,          \
-                       (const pa::bf16*)k_cache, (const pa::bf16*)v_cache, (const int4*)items, \
-                       n_items, part_size, q_start, q_len, ctx_len, block_table, max_blocks, H, \
-                       KV, scale_log2, (const pa::u32x4*)PFP, PFL, (pa::u32x4*)pf_sink,        \
-                       pa::g_handoff_attn, queue);                                           \
-  } while (0)
+  const dim3 grid(gx, KV);
 #define PA_ATT(GG)                                                                              \
   do {                                                                                          \
     if (max_items <= 0) break;                                                                  \
-    if (queue != nullptr) {                                                                     \
-      PA_ATT1(GG, 3, qgrid, pf, pf_lines);                                                      \
-    } else if (split_prefill > 0) {                                                             \
-      PA_ATT1(GG, 2, dim3(std::min(split_prefill, max_items), KV), nullptr, 0LL);              \
-      PA_ATT1(GG, 1, grid, pf, pf_lines);                                                       \
-    } else {                                                                                    \
-      PA_ATT1(GG, 0, grid, pf, pf_lines);                                                       \
+    if (waves == 8) {                                                                           \
+      static bool attr8 = false;                                                                \
+      if (!attr8) {                                                                             \
+        (void)hipFuncSetAttribute((const void*)pa::paged_attn_kernel<GG, 8>,                    \
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, pa::ATT_LDS_BYTES8); \
+        attr8 = true;                                                                           \
+      }                                                                                         \
+      hipLaunchKernelGGL((pa::paged_attn_kernel<GG, 8>), grid, dim3(512), pa::ATT_LDS_BYTES8, st, \
+                         (pa::bf16*)out, part_o, part_ml, counters, (const pa::bf16*)q,         \
+                         (const pa::bf16*)k_cache, (const pa::bf16*)v_cache, (const int4*)items, \
+                         n_items, part_size, q_start, q_len, ctx_len, block_table, max_blocks, H, \
+                         KV, scale_log2, pa::g_handoff_attn);                                   \
+      break;                                                                                    \
     }                                                                                           \
+    static bool attr4 = false;                                                                  \
+    if (!attr4) {                                                                               \
+      (void)hipFuncSetAttribute((const void*)pa::paged_attn_kernel<GG, 4>,                      \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, pa::ATT_LDS_BYTES); \
+      attr4 = true;                                                                             \
+    }                                                                                           \
+    hipLaunchKernelGGL((pa::paged_attn_kernel<GG, 4>), grid, dim3(256), pa::ATT_LDS_BYTES, st,  \
+                       (pa::bf16*)out, part_o, part_ml, counters, (const pa::bf16*)q,           \
+                       (const pa::bf16*)k_cache, (const pa::bf16*)v_cache, (const int4*)items,   \
+                       n_items, part_size, q_start, q_len, ctx_len, block_table, max_blocks, H,  \
+                       KV, scale_log2, pa::g_handoff_attn);                                     \
   } while (0)
   switch (G) {
     case 1: PA_ATT(1); break;
@@ -1108,6 +739,5 @@ extern "C" int pa_paged_attention(void* out, float* part_o, float* part_ml, cons
     default: return -2;
   }
 #undef PA_ATT
-#undef PA_ATT1
   return (int)hipGetLastError();
 }

@@ -16,10 +16,9 @@ int pa_rope_cache(void* q_out, void* k_cache, void* v_cache, const void* qkv, co
 int pa_silu_mul(void* out, const void* in, int T, int F, hipStream_t st);
 int pa_paged_attention(void* out, float* part_o, float* part_ml, const void* q, const void* k_cache,
                        const void* v_cache, const int* items, const int* n_items, int max_items,
-                       int split_prefill, const int* part_size, int* counters, const int* q_start,
+                       const int* part_size, int* counters, const int* q_start,
                        const int* q_len, const int* ctx_len, const int* block_table,
-                       int max_blocks, int H, int KV, float scale_log2, const void* pf, long long pf_bytes,
-                       void* pf_sink, int* queue, int waves, hipStream_t st);
+                       int max_blocks, int H, int KV, float scale_log2, int waves, hipStream_t st);
 int pa_sample_workspace_floats(int rows, int V);
 int pa_patch_pending_ids(int* ids, const int* sampled, int T, int n_sampled, hipStream_t st);
 int pa_sample(int* out_tokens, float* out_keys, float* workspace, const void* logits, int rows,
@@ -42,9 +41,6 @@ int pa_decode_qkv_rope(const void* x, const void* wp, int M, int N, int K, int l
                        void* k_cache, void* v_cache, const int* positions, const int* slots,
                        const float* cos_sin, int H, int KV, int nt, int waves, int splits, float* ws,
                        long long ws_floats, int* counters, int n_counters, hipStream_t st);
-int pa_wide_gemm(void* y, const void* x, const void* wp, const void* resid, float* ws, long long ws_floats,
-                 int* counters, int n_counters, int M, int N, int K, int ldx, int ldy, int ldr, int epi, int norm,
-                 float eps, int ntw, int waves, int splits, hipStream_t st);
 int pa_mid_gemm_plan(int M, int N, int K, int epi, int* fm, int* fn, int* S);
 long long pa_mid_gemm_ws_floats(int M, int N, int K, int fm, int fn, int S);
 int pa_mid_gemm(void* y, const void* x, const void* wp, const void* resid, float* ws, long long ws_floats,
@@ -54,12 +50,6 @@ int pa_mid_gemm(void* y, const void* x, const void* wp, const void* resid, float
                 const float* cos_sin, int H, int KV, hipStream_t st);
 int pa_row_sumsq(float* out, const void* x, int M, int K, int ldx, hipStream_t st);
 int pa_timeline_marker(int id, hipStream_t st);
-void pa_attn_o_set_stamps(void* p);
-int pa_attn_o(void* out, float* part_o, float* part_ml, const void* q, const void* k_cache, const void* v_cache,
-              const int* items, const int* n_items, const int* part_size, int* counters, const int* q_start,
-              const int* q_len, const int* ctx_len, const int* block_table, int max_blocks, int H, int KV,
-              float scale_log2, const void* wo, void* h, int T, int N, int K, int ldh, int* sync, int* err,
-              hipStream_t st);
 int pa_store_test(void* dst, long long n16, int mode, int grid, hipStream_t st);
 long long pa_stream_gemm_ws_floats(int M, int N, int K, int mg, int rg, int tpw, int wt, int wk, int S);
 void pa_stream_gemm_plan(int M, int N, int K, int epi, int* plan);
@@ -77,7 +67,6 @@ int pa_prefill_gemm(void* y, const void* x, const void* wp, const void* resid, f
                     const float* ss_in, float* ss_out, float* ss_zero, float eps, int full, int splits, int bn,
                     void* q_out, void* k_cache, void* v_cache, const int* positions, const int* slots,
                     const float* cos_sin, int H, int KV, int kernel_variant, hipStream_t st);
-int pa_prefetch(const void* p, long long bytes, void* sink, int wgs, hipStream_t st);
 long long pa_cosine_topk_workspace_bytes(int Q, int N, int K);
 int pa_cosine_topk(float* out_scores, int* out_rows, void* workspace, const void* queries,
                    const void* index, int Q, int N, int D, int K, const int* row_priority,
@@ -109,14 +98,6 @@ void check_dtype(const at::Tensor& t, at::ScalarType dt, const char* name) {
 void check_rc(int rc, const char* what) {
   TORCH_CHECK(rc == 0, what, " launch failed with code ", rc, " (",
               rc > 0 ? hipGetErrorString((hipError_t)rc) : "bad arguments", ")");
-}
-
-void prefetch(at::Tensor t, at::Tensor sink, int64_t wgs) {
-  check_gpu(t, "t"); check_gpu(sink, "sink");
-  TORCH_CHECK(sink.numel() * sink.element_size() >= 256 * 16, "prefetch sink must hold 4 KiB");
-  check_rc(pa_prefetch(t.data_ptr(), (long long)t.numel() * t.element_size(), sink.data_ptr(), (int)wgs,
-                       cur_stream()),
-           "prefetch");
 }
 
 void rmsnorm(at::Tensor out, at::Tensor x, at::Tensor w, double eps) {
@@ -183,9 +164,7 @@ void paged_attention(at::Tensor out, at::Tensor part_o, at::Tensor part_ml, at::
                      at::Tensor k_cache, at::Tensor v_cache, at::Tensor items, at::Tensor n_items,
                      at::Tensor counters, at::Tensor q_start, at::Tensor q_len,
                      at::Tensor ctx_len, at::Tensor block_table, double scale,
-                     c10::optional<at::Tensor> part_size, c10::optional<at::Tensor> prefetch,
-                     c10::optional<at::Tensor> prefetch_sink, int64_t split_prefill,
-                     c10::optional<at::Tensor> queue, int64_t waves) {
+                     c10::optional<at::Tensor> part_size, int64_t waves) {
   for (auto* t : {&out, &part_o, &part_ml, &q, &k_cache, &v_cache, &items, &n_items, &counters,
                   &q_start, &q_len, &ctx_len, &block_table})
     check_gpu(*t, "paged_attention arg");
@@ -207,73 +186,16 @@ void paged_attention(at::Tensor out, at::Tensor part_o, at::Tensor part_ml, at::
   TORCH_CHECK(part_ml.numel() >= (int64_t)max_items * KV * 16 * 2, "part_ml workspace too small");
   TORCH_CHECK(counters.numel() >= block_table.size(0) * KV,
               "counters must hold one zero-initialised int per (sequence, KV head)");
-  int* qptr = nullptr;
-  if (queue.has_value()) {  // work-queue launch (attention.hip MODE 3): 2 * KV zeroed ints
-    check_gpu(*queue, "queue");
-    check_dtype(*queue, at::kInt, "queue");
-    TORCH_CHECK(queue->numel() >= 2 * KV, "queue must hold 2 * KV zero-initialised ints");
-    qptr = queue->data_ptr<int>();
-  }
   const float scale_log2 = (float)(scale * 1.4426950408889634);
-  const void* pf = nullptr;
-  long long pf_bytes = 0;
-  void* pf_sink = nullptr;
-  if (prefetch.has_value()) {  // weights to warm with the idle workgroups (see attention.hip)
-    check_gpu(*prefetch, "prefetch");
-    TORCH_CHECK(prefetch_sink.has_value() && prefetch_sink->is_cuda() &&
-                    prefetch_sink->numel() * prefetch_sink->element_size() >= 256 * 16,
-                "prefetch needs a >= 4 KiB prefetch_sink");
-    pf = prefetch->data_ptr();
-    pf_bytes = (long long)prefetch->numel() * prefetch->element_size();
-    pf_sink = prefetch_sink->data_ptr();
-  }
   check_rc(pa_paged_attention(out.data_ptr(), part_o.data_ptr<float>(), part_ml.data_ptr<float>(),
                               q.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(),
                               items.data_ptr<int>(), n_items.data_ptr<int>(), max_items,
-                              n_items.numel() >= 2 ? (int)split_prefill : 0,
                               part_size.has_value() ? part_size->data_ptr<int>() : nullptr,
                               counters.data_ptr<int>(),
                               q_start.data_ptr<int>(), q_len.data_ptr<int>(),
                               ctx_len.data_ptr<int>(), block_table.data_ptr<int>(),
-                              block_table.size(1), H, KV, scale_log2, pf, pf_bytes, pf_sink, qptr, (int)waves,
-                              cur_stream()),
+                              block_table.size(1), H, KV, scale_log2, (int)waves, cur_stream()),
            "paged_attention");
-}
-
-// Decode-sized steps: paged attention and h += out . Wo^T (packed) in one launch; false if
-// the shape / device does not allow it (attention.hip attn_o_kernel).
-bool attn_o(at::Tensor out, at::Tensor part_o, at::Tensor part_ml, at::Tensor q, at::Tensor k_cache,
-            at::Tensor v_cache, at::Tensor items, at::Tensor n_items, at::Tensor counters, at::Tensor q_start,
-            at::Tensor q_len, at::Tensor ctx_len, at::Tensor block_table, double scale,
-            c10::optional<at::Tensor> part_size, at::Tensor wo, at::Tensor h, at::Tensor sync, at::Tensor err) {
-  for (auto* t : {&out, &part_o, &part_ml, &q, &k_cache, &v_cache, &items, &n_items, &counters, &q_start, &q_len,
-                  &ctx_len, &block_table, &wo, &h, &sync, &err})
-    check_gpu(*t, "attn_o arg");
-  check_dtype(q, at::kBFloat16, "q"); check_dtype(out, at::kBFloat16, "out"); check_dtype(h, at::kBFloat16, "h");
-  check_dtype(wo, at::kBFloat16, "wo");
-  for (auto* t : {&items, &n_items, &counters, &q_start, &q_len, &ctx_len, &block_table, &sync, &err})
-    check_dtype(*t, at::kInt, "attn_o int arg");
-  TORCH_CHECK(q.dim() == 3 && q.size(2) == 128 && out.sizes() == q.sizes() && out.is_contiguous(),
-              "q / out must be [T, H, 128] (out contiguous)");
-  TORCH_CHECK(k_cache.dim() == 5 && v_cache.dim() == 4, "paged K / V caches");
-  TORCH_CHECK(wo.dim() == 4 && wo.size(2) == 64 && wo.size(3) == 8 && wo.is_contiguous(), "wo must be packed");
-  const int T = q.size(0), H = q.size(1), KV = k_cache.size(1);
-  const int N = wo.size(0) * 16, K = wo.size(1) * 32;
-  TORCH_CHECK(h.dim() == 2 && h.size(0) >= T && h.size(1) == N && h.stride(1) == 1 && h.stride(0) % 4 == 0,
-              "h must be [>= T, N] with 8-byte rows");
-  TORCH_CHECK(items.dim() == 2 && items.size(1) == 4 && block_table.dim() == 2, "items / block_table");
-  TORCH_CHECK(part_o.numel() >= items.size(0) * KV * 16 * 128 && part_ml.numel() >= items.size(0) * KV * 16 * 2,
-              "partition workspaces too small");
-  TORCH_CHECK(sync.numel() >= 2 && err.numel() >= 1, "sync[2] / err[1]");
-  const int rc = pa_attn_o(out.data_ptr(), part_o.data_ptr<float>(), part_ml.data_ptr<float>(), q.data_ptr(),
-                           k_cache.data_ptr(), v_cache.data_ptr(), items.data_ptr<int>(), n_items.data_ptr<int>(),
-                           part_size.has_value() ? part_size->data_ptr<int>() : nullptr, counters.data_ptr<int>(),
-                           q_start.data_ptr<int>(), q_len.data_ptr<int>(), ctx_len.data_ptr<int>(),
-                           block_table.data_ptr<int>(), block_table.size(1), H, KV,
-                           (float)(scale * 1.4426950408889634), wo.data_ptr(), h.data_ptr(), T, N, K, h.stride(0),
-                           sync.data_ptr<int>(), err.data_ptr<int>(), cur_stream());
-  TORCH_CHECK(rc >= 0, "attn_o launch failed");
-  return rc == 0;
 }
 
 // y[M, N] = x[M, K] . w[N, K]^T for M <= 128; returns false if the shape is not handled.
@@ -368,41 +290,6 @@ void decode_qkv_rope(at::Tensor x, at::Tensor wp, double eps, at::Tensor q_out, 
                                     slots.data_ptr<int>(), cos_sin.data_ptr<float>(), (int)H, (int)KV, 0, 0,
                                     (int)splits, wsp, wsn, cp, cn, cur_stream());
   check_rc(rc < 0 ? rc : (rc > 0 ? -1 : 0), "decode_qkv_rope");
-}
-
-// y = epi(rownorm(x) . W^T) for 16 < M <= 128 on packed weights (csrc/ops/gemm_wide.hip).
-// epi 0 plain, 1 silu(gate)*up (y has N/2 columns), 2 resid + acc, 3 plain with the
-// RoPE tile permutation of the packed QKV undone. ws/counters: split-K slabs and
-// zeroed tickets. Returns false if the shape/config is not handled.
-bool wide_gemm(at::Tensor y, at::Tensor x, at::Tensor wp, c10::optional<at::Tensor> resid, at::Tensor ws,
-               at::Tensor counters, int64_t epi, bool norm, double eps, int64_t ntw, int64_t waves, int64_t splits) {
-  check_gpu(wp, "wp"); check_gpu(ws, "ws"); check_gpu(counters, "counters");
-  TORCH_CHECK(x.is_cuda() && x.dim() == 2 && x.stride(1) == 1, "x must be a 2-D GPU tensor, unit inner stride");
-  TORCH_CHECK(y.is_cuda() && y.dim() == 2 && y.stride(1) == 1, "y must be a 2-D GPU tensor, unit inner stride");
-  check_dtype(x, at::kBFloat16, "x"); check_dtype(wp, at::kBFloat16, "wp"); check_dtype(y, at::kBFloat16, "y");
-  check_dtype(ws, at::kFloat, "ws"); check_dtype(counters, at::kInt, "counters");
-  TORCH_CHECK(wp.dim() == 4 && wp.size(2) == 64 && wp.size(3) == 8, "wp must be packed [N/16, K/32, 64, 8]");
-  const int M = x.size(0), K = x.size(1), N = wp.size(0) * 16;
-  TORCH_CHECK(wp.size(1) * 32 == K, "packed weight K mismatch");
-  TORCH_CHECK(x.stride(0) % 8 == 0, "x rows must be 16-byte aligned");
-  const int NO = epi == 1 ? N / 2 : N;
-  TORCH_CHECK(y.size(0) == M && y.size(1) == NO, "y shape mismatch");
-  const void* rp = nullptr;
-  int ldr = 0;
-  if (epi == 2) {
-    TORCH_CHECK(resid.has_value(), "epi=2 needs resid");
-    const auto& r = *resid;
-    TORCH_CHECK(r.is_cuda() && r.dim() == 2 && r.stride(1) == 1 && r.size(0) == M && r.size(1) == N,
-                "resid must be [M, N] with unit inner stride");
-    check_dtype(r, at::kBFloat16, "resid");
-    rp = r.data_ptr();
-    ldr = r.stride(0);
-  }
-  const int rc = pa_wide_gemm(y.data_ptr(), x.data_ptr(), wp.data_ptr(), rp, ws.data_ptr<float>(), ws.numel(),
-                              counters.data_ptr<int>(), counters.numel(), M, N, K, x.stride(0), y.stride(0), ldr,
-                              (int)epi, norm ? 1 : 0, (float)eps, (int)ntw, (int)waves, (int)splits, cur_stream());
-  TORCH_CHECK(rc >= 0, "wide_gemm launch failed");
-  return rc == 0;
 }
 
 const float* opt_rows(const c10::optional<at::Tensor>& t, int M, const char* name) {
@@ -917,14 +804,6 @@ at::Tensor empty_uncached(int64_t numel, at::ScalarType dtype, int64_t device) {
 }
 
 PYBIND11_MODULE(_C, m) {
-  m.def("attn_o", &attn_o, py::arg("out"), py::arg("part_o"), py::arg("part_ml"), py::arg("q"), py::arg("k_cache"),
-        py::arg("v_cache"), py::arg("items"), py::arg("n_items"), py::arg("counters"), py::arg("q_start"),
-        py::arg("q_len"), py::arg("ctx_len"), py::arg("block_table"), py::arg("scale"), py::arg("part_size"),
-        py::arg("wo"), py::arg("h"), py::arg("sync"), py::arg("err"),
-        "decode-sized steps: paged attention + h += out . Wo^T (packed) in one launch; false if not handled");
-  m.def("attn_o_set_stamps", [](c10::optional<at::Tensor> t) {
-    pa_attn_o_set_stamps(t.has_value() ? t->data_ptr() : nullptr);
-  }, py::arg("stamps"), "diagnostics: int64 [>= 8 * grid] buffer for attn_o phase stamps (None: off)");
   m.def("store_test", [](at::Tensor dst, int64_t mode, int64_t grid) {
     check_gpu(dst, "dst");
     TORCH_CHECK(dst.is_contiguous() && dst.nbytes() % 16 == 0, "dst: contiguous, a multiple of 16 bytes");
@@ -936,7 +815,6 @@ PYBIND11_MODULE(_C, m) {
   m.def("empty_uncached", &empty_uncached, py::arg("numel"), py::arg("dtype"), py::arg("device"),
         "zero-filled device tensor in uncached memory (hipDeviceMallocUncached)");
   m.doc() = "pilottai_amd CDNA4 (gfx950) HIP kernels";
-  m.def("prefetch", &prefetch, py::arg("t"), py::arg("sink"), py::arg("wgs") = 64);
   m.def("rmsnorm", &rmsnorm);
   m.def("fused_add_rmsnorm", &fused_add_rmsnorm);
   m.def("rope_cache", &rope_cache);
@@ -955,9 +833,6 @@ PYBIND11_MODULE(_C, m) {
         py::arg("k_cache"), py::arg("v_cache"), py::arg("positions"), py::arg("slots"), py::arg("cos_sin"),
         py::arg("H"), py::arg("KV"), py::arg("splits") = 0, py::arg("ws") = py::none(),
         py::arg("counters") = py::none());
-  m.def("wide_gemm", &wide_gemm, py::arg("y"), py::arg("x"), py::arg("wp"), py::arg("resid"), py::arg("ws"),
-        py::arg("counters"), py::arg("epi") = 0, py::arg("norm") = false, py::arg("eps") = 1e-5, py::arg("ntw") = 0,
-        py::arg("waves") = 0, py::arg("splits") = 0);
   m.def("mid_gemm", &mid_gemm, py::arg("y"), py::arg("x"), py::arg("wp"), py::arg("resid"), py::arg("ws"),
         py::arg("counters"), py::arg("epi") = 0, py::arg("ss_in") = py::none(), py::arg("ss_out") = py::none(),
         py::arg("ss_zero") = py::none(), py::arg("eps") = 1e-5, py::arg("fm") = 0, py::arg("fn") = 0,
@@ -990,8 +865,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("paged_attention", &paged_attention, py::arg("out"), py::arg("part_o"), py::arg("part_ml"), py::arg("q"),
         py::arg("k_cache"), py::arg("v_cache"), py::arg("items"), py::arg("n_items"), py::arg("counters"),
         py::arg("q_start"), py::arg("q_len"), py::arg("ctx_len"), py::arg("block_table"), py::arg("scale"),
-        py::arg("part_size") = py::none(), py::arg("prefetch") = py::none(), py::arg("prefetch_sink") = py::none(),
-        py::arg("split_prefill") = 0, py::arg("queue") = py::none(), py::arg("waves") = 4);
+        py::arg("part_size") = py::none(), py::arg("waves") = 4);
   m.def("sample_workspace_floats", &sample_workspace_floats);
   m.def("patch_pending_ids", &patch_pending_ids);
   m.def("sample", &sample, py::arg("out_tokens"), py::arg("out_keys"), py::arg("workspace"),

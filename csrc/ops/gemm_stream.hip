@@ -29,9 +29,12 @@
 //     on a per-group counter and waits for the others (all S slices of a group are resident:
 //     the grid is at most one workgroup per CU), then reduces 1/S of the group's fragments
 //     and runs the epilogue on them (RMSNorm row scale, SwiGLU, residual + the next norm's row
-//     statistics, RoPE + paged KV write: packed_epi.h). A departure counter resets both
-//     counters, so they are zero between launches (hipGraph replay safe). Every spin is
-//     bounded (err flag).
+//     statistics, RoPE + paged KV write: packed_epi.h). Publish = sc1 slab stores, every
+//     wave's vmcnt(0), the workgroup barrier, one lane's agent-scope release + drain, relaxed
+//     arrive; consume = relaxed poll, agent-scope acquire + drain, barrier, sc1 loads. A
+//     departure counter resets both counters, so they are zero between launches (hipGraph
+//     replay safe). Every spin is bounded: a timed-out group barrier sets the err word, which
+//     the engine reads back with every step and fails on (LLMEngine._health_check).
 #include "common.h"
 #include "packed_epi.h"
 
@@ -71,8 +74,11 @@ struct Args {
   const int* slots;
   const float* cos_sin;
   int H, KV;
-  // bit 0: agent-scope release (L2 write-back) before arriving (diagnostics); bit 1: each
-  // workgroup starts its K slice at a different chunk (rotated order; HBM channel spread)
+  // bit 0: agent-scope release (buffer_wbl2 sc1 + drain) before arriving -- the host's default
+  // (ops.STREAM_REL): the LLVM AMDGPU memory model's agent-scope release, which waits for the
+  // write-through slab stores to complete at memory; without it the arrive can overtake them
+  // (round 4: 5 of 10,000 poisoned decode runs). bit 1: each workgroup starts its K slice at a
+  // different chunk (rotated order; HBM channel spread)
   int rel;
   // diagnostics (null in the engine): per workgroup 8 wall-clock stamps (s_memrealtime, 100 MHz):
   // [0] start, [1] first chunk in LDS, [2] main loop done, [3] group barrier passed, [4] end
@@ -105,10 +111,12 @@ __device__ __forceinline__ void group_barrier(int* arrive, int n, int* err, int 
     }
     const int tk = __hip_atomic_fetch_add((gi32*)arrive, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (tk != n - 1) {
-      unsigned spins = 0;
+      // bounded by wall time (s_memrealtime runs at 100 MHz): after 1 s a partner never ran;
+      // give up and raise the err word (the engine fails the step) rather than hang
+      const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
       while (__hip_atomic_load((gi32*)arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < n) {
         __builtin_amdgcn_s_sleep(1);
-        if (++spins > (1u << 24)) {  // ~1 s: a partner never ran; give up rather than hang
+        if (__builtin_amdgcn_s_memrealtime() - t0 > 100000000ull) {
           __hip_atomic_store((gi32*)err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           break;
         }

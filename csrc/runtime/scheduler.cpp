@@ -354,20 +354,27 @@ int32_t Scheduler::schedule(int32_t* buf) {
     const int32_t dpt = t_step > cfg_.small_step_tokens ? cfg_.decode_part_target : cfg_.small_step_target;
     if (dpt > 0 && (t_step > cfg_.small_step_tokens || cfg_.small_step_part > 0)) {
       // one balanced round of workgroups instead of 512-key parts + short remainders
-      int64_t ndec = 0, maxc = 0;
+      int64_t ndec = 0, maxc = 0, sumc = 0;
       for (const Planned& p : last_plan_)
         if (p.n <= tpw) {
           ++ndec;
-          maxc = std::max<int64_t>(maxc, p.s->num_computed + p.n);
+          const int64_t c = p.s->num_computed + p.n;
+          maxc = std::max<int64_t>(maxc, c);
+          sumc += c;
         }
       if (ndec > 0) {
         const int64_t tgt = dpt;
+        // the balanced share of all decode keys per (partition, KV head) workgroup: no
+        // partition is longer than that, so one long row among many short ones is split
+        // instead of becoming the one serial work item of every layer (uniform contexts are
+        // unaffected: there the share is at least the longest context / the parts below)
+        const int64_t share = ((sumc * kv + tgt - 1) / tgt + 31) / 32 * 32;
         int64_t cand;
         if (ndec * kv >= tgt) {
-          cand = std::max<int64_t>(maxc, 32);  // whole contexts: nparts = 1 everywhere
+          cand = std::max<int64_t>(32, std::min(maxc, std::max<int64_t>(share, 128)));
         } else {
           const int64_t np = (tgt + ndec * kv - 1) / (ndec * kv);
-          cand = std::max<int64_t>(128, ((maxc + np - 1) / np + 31) / 32 * 32);
+          cand = std::max<int64_t>(128, std::min(((maxc + np - 1) / np + 31) / 32 * 32, share));
         }
         int64_t parts = 0;
         for (const Planned& p : last_plan_)

@@ -100,7 +100,6 @@ class EngineConfig:
     align_slack: int = 96
     decode_fused: Optional[bool] = None  # packed-weight fused decode path; None = when it fits in HBM
     decode_fused_max_t: Optional[int] = None  # largest step (tokens) on that path; None = model default
-    wide_max_t: Optional[int] = None  # largest step on the packed small-batch path; None = model default
     mid_max_t: Optional[int] = None  # largest step on the LDS-DMA tiled mid-size path; None = model default
     # largest step on the fused packed-weight path with the 256 x 256 prefill kernels (above
     # mid_max_t); 0 = such steps take the library (hipBLASLt) path; None = model default
@@ -115,15 +114,10 @@ class EngineConfig:
     # ... used only for steps with at least this many prefill tokens (1,024: 1,024-2,048-token steps
     # 1-2 % faster than with 2,048, which most mixed steps never reached; profiles/r2_att_wide_min_ab.jsonl)
     att_wide_min_tokens: int = 1024
-    # persistent work-queue attention launch (2 workgroups per CU, KV head = XCD, items pulled
-    # heaviest first: decode items run beside a mixed step's prefill items); False = the
-    # grid-strided launch
-    att_queue: bool = False
     # attention workgroup width on decode-sized steps (<= the model's DECODE_FUSED_MAX_T
     # tokens): 8 waves stream a whole context per workgroup (the scheduler then skips the
     # flash-decoding split for such steps when they have few rows); None = model default
     att_decode_waves: Optional[int] = None
-    prefetch_weights: Optional[bool] = None  # decode-step MALL prefetch on a side stream (None: model default)
     reply_tokens: Optional[int] = None  # fixed length of every reply schema's free-text slot (grammar.py)
     # interpreter thread-switch interval while the engine thread runs (sys.setswitchinterval);
     # None = env PILOTTAI_GIL_SWITCH_S or the interpreter default (5 ms)
@@ -131,6 +125,12 @@ class EngineConfig:
     # pipelined steps: step N+1 is scheduled and launched while step N runs;
     # rows sampling in N continue speculatively (runtime/scheduler.h). TP = 1 only.
     async_steps: bool = False
+    # start(): gc.freeze() everything alive (model, graphs, tokenizer) so later cyclic
+    # collections skip it (a full pass stalled the engine thread 60-85 ms). PROCESS-GLOBAL:
+    # frozen objects are never reclaimed by the cycle collector until stop() unfreezes, so it
+    # is opt-in, for serving entry points that build one engine (bench.py freezes after its
+    # warm-up instead; the HTTP server sets it)
+    freeze_heap: bool = False
 
 
 # TP step header: [op, T, ns, nsamp, bucket, masks_changed, n_copy, truncate, embed]
@@ -216,8 +216,6 @@ class LLMEngine:
                                 decode_pack=cfg.decode_fused)
         if cfg.decode_fused_max_t is not None:
             self.model.DECODE_FUSED_MAX_T = int(cfg.decode_fused_max_t)
-        if cfg.wide_max_t is not None:
-            self.model.WIDE_MAX_T = int(cfg.wide_max_t)
         if cfg.mid_max_t is not None:
             self.model.MID_MAX_T = int(cfg.mid_max_t)
         if cfg.prefill_max_t is not None:
@@ -230,8 +228,6 @@ class LLMEngine:
             self.model.ATT_DECODE_WAVES = int(cfg.att_decode_waves)
         if cfg.pf_midrange is not None:
             self.model.PF_MIDRANGE = frozenset(cfg.pf_midrange)
-        if cfg.prefetch_weights is not None:
-            self.model.PREFETCH_WEIGHTS = bool(cfg.prefetch_weights)
         self.load_time = time.time() - t0
         self.max_model_len = min(cfg.max_model_len, mc.max_position)
         # ---- KV cache sizing (288 GB HBM: the default leaves room for graphs/activations)
@@ -294,8 +290,6 @@ class LLMEngine:
         self._dev_meta = torch.zeros(L["total"], dtype=torch.int32, device=self.device) \
             if (self.on_gpu or self._async) else self._host_meta
         self._att_counters = torch.zeros(L["max_seqs"] * kv_local, dtype=torch.int32, device=self.device)
-        self._att_queue = torch.zeros(2 * kv_local, dtype=torch.int32, device=self.device) \
-            if (cfg.att_queue and self.on_gpu) else None
         self._init_views()
         V = mc.vocab_size
         self._mask_words = (V + 31) // 32
@@ -359,7 +353,19 @@ class LLMEngine:
         # instead of hanging; the word is copied back with every step and checked after the
         # step's synchronize, failing the engine rather than continuing on partial sums
         self._car = getattr(self.tp, "custom", None) if self.tp.size > 1 else None
-        self._car_err_host = torch.zeros(1, dtype=torch.int32, pin_memory=pin) if self._car is not None else None
+        # device health words read back with every step (non-blocking, behind the step) and
+        # checked after its synchronize: [0] the custom all-reduce's barrier timeout, [1] the
+        # weight-streaming GEMM's split-K group-barrier timeout (gemm_stream.hip: a partner
+        # workgroup never became resident, so the reduced slabs would be partial)
+        self._health_dev = []
+        if self._car is not None:
+            self._health_dev.append(("custom all-reduce barrier timed out (a TP peer stalled > 5 s): "
+                                     "the step's activations are partial", self._car.err))
+        if self.on_gpu:
+            self._health_dev.append(("weight-streaming GEMM split-K group barrier timed out (a "
+                                     "partner workgroup never ran): the step's projections are partial",
+                                     ops.stream_workspace(self.device)[2]))
+        self._health_host = torch.zeros(max(1, len(self._health_dev)), dtype=torch.int32, pin_memory=pin)
         self._tp_ring = None
         if self.tp.size > 1:
             self._open_tp_ring()
@@ -387,7 +393,6 @@ class LLMEngine:
             items=sl("items", 4 * L["max_items"]).view(L["max_items"], 4),
             n_items=sl("n_items", 1),
             att_counters=self._att_counters,
-            att_queue=self._att_queue,
             part_size=sl("part_size", 1),
             logit_rows=sl("logit_rows", ms))
         self._temp = sl("temperature", ms).view(torch.float32)
@@ -415,7 +420,7 @@ class LLMEngine:
         n_it = self._items_for_bucket(bucket, s_b)
         return StepMeta(m.input_ids, m.positions, m.slots, m.q_start, m.q_len, m.ctx_len,
                         m.block_table, m.items[:n_it], m.n_items, m.att_counters, m.logit_rows, num_seqs=ns,
-                        part_size=m.part_size, att_queue=m.att_queue)
+                        part_size=m.part_size)
 
     def _forward_and_sample(self, bucket: int, s_b: int, ns: int, trunc: bool = False, embed: bool = False):
         meta = self._meta_for(bucket, s_b, ns)
@@ -620,11 +625,12 @@ class LLMEngine:
         if sw is not None and sw > 0:
             sys.setswitchinterval(sw)
         self._stop = False
-        # the model, graphs and tokenizer are in place: keep them out of every later GC pass
-        # (a full collection otherwise stalls the engine thread for tens of ms)
-        from pilottai_amd.utils.gc_tune import freeze_heap
+        if self.cfg.freeze_heap:
+            # the model, graphs and tokenizer are in place: keep them out of every later GC
+            # pass (a full collection otherwise stalls the engine thread for tens of ms)
+            from pilottai_amd.utils.gc_tune import freeze_heap
 
-        freeze_heap()
+            self._froze = freeze_heap() > 0
         self._thread = threading.Thread(target=self._loop, name="pilottai-engine", daemon=True)
         self._thread.start()
 
@@ -634,6 +640,11 @@ class LLMEngine:
         if self._thread is not None:
             self._thread.join(timeout=30)
             self._thread = None
+        if getattr(self, "_froze", False):  # give the frozen heap back to the collector
+            import gc
+
+            gc.unfreeze()
+            self._froze = False
         self.release_followers()
 
     # ------------------------------------------------------------------ TP
@@ -722,22 +733,24 @@ class LLMEngine:
                     self.tp.broadcast(self._class_masks)
                 self.tp.broadcast(self._dev_meta[:n_copy])
                 self._run(bucket, ns, bool(trunc), n_copy, bool(embed))
-                self._car_fetch()
+                self._health_fetch()
                 if self.on_gpu:
                     torch.cuda.current_stream().synchronize()
-                self._car_check()
+                self._health_check()
                 n += 1
         self.stats["steps"] += n
         return n
 
-    def _car_fetch(self):
-        if self._car is not None:
-            self._car_err_host.copy_(self._car.err, non_blocking=True)
+    def _health_fetch(self):
+        for i, (_, w) in enumerate(self._health_dev):
+            self._health_host[i:i + 1].copy_(w[:1], non_blocking=True)
 
-    def _car_check(self):
-        if self._car is not None and int(self._car_err_host[0]) != 0:
-            raise RuntimeError("custom all-reduce barrier timed out (a TP peer stalled > 5 s): "
-                               "the step's activations are partial; engine stopped")
+    def _health_check(self):
+        """Fail the engine (rather than continue on partial sums) if a device health word is
+        set; call after the step's synchronize."""
+        for i, (what, _) in enumerate(self._health_dev):
+            if int(self._health_host[i]) != 0:
+                raise RuntimeError(f"{what}; engine stopped")
 
     @property
     def failed(self) -> Optional[BaseException]:
@@ -830,7 +843,7 @@ class LLMEngine:
             self._run(bucket, ns, trunc, n_copy, embed)
         if nsamp:
             self._sampled_host[:nsamp].copy_(self._sampled_dev[:nsamp], non_blocking=self.on_gpu)
-        self._car_fetch()
+        self._health_fetch()
         t_launch = time.perf_counter()
         # the previous step's finished requests are handed to their callers while this step
         # runs on the GPU (host/device overlap): delivery needs nothing from it
@@ -838,7 +851,7 @@ class LLMEngine:
         t_flush = time.perf_counter()
         if self.on_gpu:
             torch.cuda.current_stream().synchronize()
-        self._car_check()
+        self._health_check()
         t_sync = time.perf_counter()
         with trace_range("engine.commit"):
             outs = self.sched.commit(self._sampled_host.data_ptr(), nsamp)
@@ -910,6 +923,7 @@ class LLMEngine:
             self._sampled_hosts[slot][:nsamp].copy_(self._sampled_dev[:nsamp], non_blocking=self.on_gpu)
         if embed:
             self._embed_hosts[slot].copy_(self._embed_pool, non_blocking=self.on_gpu)
+        self._health_fetch()
         ev = None
         if self.on_gpu:
             ev = torch.cuda.Event()
@@ -929,6 +943,7 @@ class LLMEngine:
         t_w = time.perf_counter()
         if ev is not None:
             ev.synchronize()
+        self._health_check()
         t_sync = time.perf_counter()
         with trace_range("engine.commit"):
             outs = self.sched.commit(self._sampled_hosts[slot].data_ptr(), nsamp)

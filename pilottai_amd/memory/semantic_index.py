@@ -372,6 +372,11 @@ class SemanticIndex:
             raise ValueError(f"unsupported index checkpoint version {meta.get('version')}")
         n, dim = int(meta["count"]), int(meta["dim"])
         cap = max(int(capacity or meta["capacity"]), n, 1)
+        if int(meta["size"]) > int(meta["capacity"]) and cap != int(meta["capacity"]):
+            # a wrapped ring: its write position is size % capacity and every row is live; under
+            # another capacity that position moves and count would take in never-written rows
+            raise ValueError(f"index checkpoint is a wrapped ring of capacity {meta['capacity']}: "
+                             f"it can only be restored at that capacity, not {cap}")
         idx = cls(dim=dim, capacity=cap, device=device, growable=growable,
                   max_capacity=max_capacity or max(cap, int(meta["capacity"])))
         packed = np.load(path / "packed.npy", mmap_mode="r", allow_pickle=False)

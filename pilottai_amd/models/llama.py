@@ -112,9 +112,6 @@ class StepMeta:
     logit_rows: torch.Tensor
     num_seqs: int = 0  # host-side count, used only by the CPU reference path
     part_size: Optional[torch.Tensor] = None  # device int[1]: decode partition size of the step
-    # persistent zeroed int[2 * KV]: the attention work queue (csrc/ops/attention.hip MODE 3);
-    # None = the grid-strided launch
-    att_queue: Optional[torch.Tensor] = None
 
 
 class KVCache:
@@ -137,13 +134,7 @@ class LlamaModel:
     # decode steps of at most this many tokens run the fused packed-weight path
     # (csrc/ops/gemm_decode.hip; tools/decode_gemm_bench.py, profiles/r1_decode_gemm.md)
     DECODE_FUSED_MAX_T = 16
-    # steps of up to this many tokens (above DECODE_FUSED_MAX_T) run the packed-weight
-    # small-batch kernels (csrc/ops/gemm_wide.hip; tools/wide_gemm_bench.py)
-    # (off by default since the mid path and the nt weight streams landed: 48-token steps run
-    # 4.07-4.34 ms on the mid path against 4.6-4.7 on this one, 32-token steps 3.83-3.90 against
-    # 3.92-3.97; profiles/r2_wide_max_t_ab.jsonl. EngineConfig.wide_max_t = 48 turns it back on)
-    WIDE_MAX_T = 16
-    # steps of up to this many tokens (above WIDE_MAX_T) run the LDS-DMA tiled projections
+    # steps of up to this many tokens (above DECODE_FUSED_MAX_T) run the LDS-DMA tiled projections
     # (csrc/ops/gemm_mid.hip) with every norm / SwiGLU / residual / RoPE + KV write fused
     MID_MAX_T = 256
     # steps above MID_MAX_T and up to this many tokens run the same fused packed-weight layer
@@ -162,7 +153,7 @@ class LlamaModel:
     # profiles/r3_midrange_inengine_ab.jsonl — 160 / 192 / 256-token steps 6.20 / 6.35 / 6.73 ms
     # with the mid kernel, 5.96 / 6.11 / 6.59 with gate_up here, 6.72 / 6.89 / 7.22 with all four)
     PF_MIDRANGE = frozenset({"gate_up"})
-    # steps of at most this many tokens (above WIDE_MAX_T) run the QKV projection on the
+    # steps of at most this many tokens (above DECODE_FUSED_MAX_T) run the QKV projection on the
     # packed decode kernel (all rows per workgroup, norm from x, RoPE + KV write; csrc/ops/
     # gemm_decode.hip handles M <= 64) instead of the mid kernel; 0 = off
     DEC_QKV_MAX_T = 0
@@ -174,12 +165,8 @@ class LlamaModel:
     ATT_DECODE_WAVES = int(os.environ.get("PILOTTAI_ATT_DECODE_WAVES", "8"))
     # waves per attention workgroup on the mid path (DECODE_FUSED_MAX_T < T <= MID_MAX_T)
     ATT_MID_WAVES = int(os.environ.get("PILOTTAI_ATT_MID_WAVES", "4"))
-    # decode-sized steps (T <= DECODE_FUSED_MAX_T, TP = 1, 8-wave attention): attention and the
-    # O projection + residual in ONE launch whose idle workgroups stream the O weights into LDS
-    # while the attention runs (csrc/ops/attention.hip attn_o_kernel); False = two launches
-    ATTN_O_FUSED = os.environ.get("PILOTTAI_ATTN_O_FUSED", "0") == "1"
     # per projection: (largest M, path, config); the first row whose M covers the step is used,
-    # for every step on the fused packed-weight path (T > WIDE_MAX_T).
+    # for every step on the fused packed-weight path (T > DECODE_FUSED_MAX_T).
     # "pf": prefill kernel — bn = tile width (256 / 128), variant = kernel family (3: the
     # ping-pong kernels of gemm_pingpong.h, 1: the read-ahead 256 x 256 / 3-stage 256 x 128
     # kernels), full / splits = the decomposition (-1 / 0: the kernel's plan); "mid": mid
@@ -203,7 +190,7 @@ class LlamaModel:
     # (csrc/ops/gemm_stream.hip; shape = (rg, tpw, wt, wk, S, D): row groups, 16-column tiles
     # per wave, waves along N, waves along K, K-split, ring depth; the rows per group follow
     # from the step, _stream_plan); the first row whose M covers a mid-size step
-    # (WIDE_MAX_T < T <= MID_MAX_T) replaces PF_CFG / MID_CFG there.
+    # (DECODE_FUSED_MAX_T < T <= MID_MAX_T) replaces PF_CFG / MID_CFG there.
     # Rows only where tools/stream_gemm_bench.py (graph-replayed, cold weights, engine
     # epilogues) measured it ahead of the round-3 choice (profiles/r4_stream_gemm_*.jsonl).
     # (profiles/r4_stream_gemm_sweep_final.jsonl, interleaved, cold weights, us stream vs round 3:
@@ -224,14 +211,6 @@ class LlamaModel:
     # (profiles/r4_stream_lm_head_sweep.jsonl: 24 / 48 / 64 / 128 rows 166 / 172 / 175 / 197 us
     # vs 176 (packed decode kernel) / 210 / 210 / 235 (hipBLASLt); 17-32 rows included)
     LM_HEAD_STREAM: list = [(32, (1, 3, 4, 1, 1, 2)), (64, (1, 4, 4, 1, 1, 2)), (128, (1, 2, 8, 1, 1, 2))]
-    # decode/small steps: let the attention launch's idle workgroups read the O
-    # projection's weights into the Infinity Cache (MALL-resident weights run the 34 MB
-    # O projection at M=8 in 8.7 us vs 12.8 us cold, profiles/r2_mall_warm.jsonl). Off by
-    # default: end to end it did not pay (8-row steps 3.67 -> 3.72 ms, 16-row 4.01 -> 4.10:
-    # the prefetching workgroups compete with the K/V stream), and a side-stream prefetch
-    # inside the graph was worse still (+1 ms per step from the fork/join nodes);
-    # profiles/r2_prefetch_ab.jsonl. EngineConfig.prefetch_weights turns it on.
-    PREFETCH_WEIGHTS = False
     # (largest M, fm, fn, K-slices) per projection, best of tools/mid_gemm_bench.py on MI355X
     # (profiles/r2_mid_gemm_sweep.jsonl); the first row whose M covers the step is used
     # 32-row tiles (fm = 1) from profiles/r2_mid_fm1_sweep.jsonl: 2-16 % faster at 17-64 rows
@@ -291,14 +270,12 @@ class LlamaModel:
             L["w2_p"] = ops.pack_decode_weight(L["w2"])
         self.lm_head_p = ops.pack_decode_weight(self.lm_head)
         if self.device.type == "cuda":
-            ops.wide_workspace(self.device)  # split-K slabs + tickets, before any graph capture
+            ops.decode_workspace(self.device)  # split-K slabs + tickets, before any graph capture
             ops.mid_workspace(self.device)
             ops.prefill_workspace(self.device)
             ops.stream_workspace(self.device)
         # RMSNorm row statistics handed from each residual epilogue to the next projection
         self._ss = torch.zeros(2, 1 << 15, dtype=torch.float32, device=self.device)
-        if self.device.type == "cuda":
-            ops.kernels._prefetch_sink(self.device)  # before any graph capture
         self.decode_packed = True
 
     # -- weights -----------------------------------------------------------------
@@ -427,8 +404,6 @@ class LlamaModel:
         T = num_tokens
         if self.decode_packed and T <= self.DECODE_FUSED_MAX_T:
             return self._forward_decode(meta, kv, T, num_logit_rows, part_o, part_ml, embed)
-        if self.decode_packed and T <= self.WIDE_MAX_T:
-            return self._forward_wide(meta, kv, T, num_logit_rows, part_o, part_ml, embed)
         if self.decode_packed and (T <= self.MID_MAX_T or T <= self.PREFILL_MAX_T):
             return self._forward_mid(meta, kv, T, num_logit_rows, part_o, part_ml, embed)
         H, KVh, hd = self.h_local, self.kv_local, cfg.head_dim
@@ -443,8 +418,7 @@ class LlamaModel:
             attn = torch.empty(T, H, hd, dtype=self.dtype, device=self.device)
             ops.paged_attention(attn, part_o, part_ml, q, kv.k[li], kv.v[li], meta.items, meta.n_items,
                                 meta.att_counters, meta.q_start, meta.q_len, meta.ctx_len,
-                                meta.block_table, self.scale, num_seqs=meta.num_seqs, part_size=meta.part_size,
-                                queue=meta.att_queue)
+                                meta.block_table, self.scale, num_seqs=meta.num_seqs, part_size=meta.part_size)
             o = ops.linear(attn.view(T, H * hd), L["wo"], "o")
             if self.tp.size > 1:
                 self.tp.all_reduce(o)
@@ -476,30 +450,20 @@ class LlamaModel:
         h = self._embed(ids)
         if not h.is_contiguous():
             h = h.contiguous()
-        pf = self.PREFETCH_WEIGHTS and self.device.type == "cuda"
         for li, L in enumerate(self.layers):
             q = torch.empty(T, H, hd, dtype=self.dtype, device=self.device)
             ops.decode_qkv_rope(h, L["wqkv_p"], eps, q, kv.k[li], kv.v[li], meta.positions, meta.slots,
                                 self.cos_sin, H, KVh)
             attn = torch.empty(T, H, hd, dtype=self.dtype, device=self.device)
-            fused = (not tp and self.ATTN_O_FUSED and not pf and meta.att_queue is None
-                     and self.ATT_DECODE_WAVES == 8
-                     and ops.attn_o(attn, part_o, part_ml, q, kv.k[li], kv.v[li], meta.items, meta.n_items,
-                                    meta.att_counters, meta.q_start, meta.q_len, meta.ctx_len, meta.block_table,
-                                    self.scale, L["wo_p"], h, num_seqs=meta.num_seqs, part_size=meta.part_size))
-            if not fused:
-                # the attention grid's idle workgroups read the O projection's weights into
-                # the Infinity Cache while the K/V stream runs (csrc/ops/attention.hip)
-                ops.paged_attention(attn, part_o, part_ml, q, kv.k[li], kv.v[li], meta.items, meta.n_items,
-                                    meta.att_counters, meta.q_start, meta.q_len, meta.ctx_len,
-                                    meta.block_table, self.scale, num_seqs=meta.num_seqs, part_size=meta.part_size,
-                                    queue=meta.att_queue, waves=self.ATT_DECODE_WAVES,
-                                    prefetch=L["wo_p"] if pf else None)
-                a2 = attn.view(T, H * hd)
-                if tp:  # all-reduce + residual add in one launch (custom_ar.hip RES epilogue)
-                    self.tp.all_reduce_add(ops.decode_gemm(a2, L["wo_p"], "plain"), h)
-                else:
-                    ops.decode_gemm(a2, L["wo_p"], "resid", resid=h, out=h)
+            ops.paged_attention(attn, part_o, part_ml, q, kv.k[li], kv.v[li], meta.items, meta.n_items,
+                                meta.att_counters, meta.q_start, meta.q_len, meta.ctx_len,
+                                meta.block_table, self.scale, num_seqs=meta.num_seqs, part_size=meta.part_size,
+                                waves=self.ATT_DECODE_WAVES)
+            a2 = attn.view(T, H * hd)
+            if tp:  # all-reduce + residual add in one launch (custom_ar.hip RES epilogue)
+                self.tp.all_reduce_add(ops.decode_gemm(a2, L["wo_p"], "plain"), h)
+            else:
+                ops.decode_gemm(a2, L["wo_p"], "resid", resid=h, out=h)
             a = ops.decode_gemm(h, L["w13_p"], "silu", norm=True, eps=eps)
             if tp:
                 self.tp.all_reduce_add(ops.decode_gemm(a, L["w2_p"], "plain"), h)
@@ -519,53 +483,6 @@ class LlamaModel:
         M = 16 against 27.6 for the 2-tile x 16-wave x 2-slice config that 9-16-row steps
         used before; profiles/r3_decode_cfg_sweep.jsonl, tools/decode_cfg_sweep.py)."""
         return {"nt": 1, "waves": 8}
-
-    def _forward_wide(self, meta: StepMeta, kv: KVCache, T: int, num_logit_rows: int,
-                      part_o: torch.Tensor, part_ml: torch.Tensor, embed=None) -> torch.Tensor:
-        """Small-batch step (DECODE_FUSED_MAX_T < T <= WIDE_MAX_T: decode rows plus
-        grammar jump-forward runs or a short prefill chunk) on the packed weights:
-        x staged once per workgroup through LDS, split-K for the narrow projections,
-        RMSNorm folded into QKV / gate_up, SwiGLU and residual adds in the epilogues
-        (csrc/ops/gemm_wide.hip); the QKV projection runs on the decode kernel with RoPE +
-        paged KV write fused (csrc/ops/gemm_decode.hip)."""
-        cfg = self.cfg
-        H, KVh, hd = self.h_local, self.kv_local, cfg.head_dim
-        eps = cfg.rms_eps
-        tp = self.tp.size > 1
-        ids = meta.input_ids[:T].long() if self.device.type == "cpu" else meta.input_ids[:T]
-        h = self._embed(ids)
-        if not h.is_contiguous():
-            h = h.contiguous()
-        for li, L in enumerate(self.layers):
-            # QKV with RoPE + KV write in the epilogue (the decode kernel handles M <= 64 rows):
-            # at 32 rows 16.8 us against 18.6 + 7 us for wide_gemm + rope_cache
-            q = torch.empty(T, H, hd, dtype=self.dtype, device=self.device)
-            ops.decode_qkv_rope(h, L["wqkv_p"], eps, q, kv.k[li], kv.v[li], meta.positions, meta.slots,
-                                self.cos_sin, H, KVh)
-            attn = torch.empty(T, H, hd, dtype=self.dtype, device=self.device)
-            ops.paged_attention(attn, part_o, part_ml, q, kv.k[li], kv.v[li], meta.items, meta.n_items,
-                                meta.att_counters, meta.q_start, meta.q_len, meta.ctx_len,
-                                meta.block_table, self.scale, num_seqs=meta.num_seqs, part_size=meta.part_size,
-                                queue=meta.att_queue,
-                                prefetch=L["wo_p"] if self.PREFETCH_WEIGHTS and self.device.type == "cuda" else None)
-            a2 = attn.view(T, H * hd)
-            if tp:
-                self.tp.all_reduce_add(ops.wide_gemm(a2, L["wo_p"], "plain"), h)
-            else:
-                ops.wide_gemm(a2, L["wo_p"], "resid", resid=h, out=h)
-            a = ops.wide_gemm(h, L["w13_p"], "silu", norm=True, eps=eps)
-            if tp:
-                self.tp.all_reduce_add(ops.wide_gemm(a, L["w2_p"], "plain"), h)
-            else:
-                ops.wide_gemm(a, L["w2_p"], "resid", resid=h, out=h)
-        if embed is not None:
-            self._pool_embed(ops.rmsnorm(h, self.norm, eps), T, embed)
-        rows = meta.logit_rows[:num_logit_rows]
-        rows = rows.long() if self.device.type == "cpu" else rows
-        xs = ops.rmsnorm(h.index_select(0, rows), self.norm, eps)
-        # decode_gemm beats hipBLASLt on the LM head up to 32 rows (24: 180 vs 191 us, 32: 184.5
-        # vs 196; 48: 221 vs 204; profiles/r2_decode_sweep_nt*.jsonl)
-        return self._lm_head(xs, num_logit_rows)
 
     @staticmethod
     def _pool_embed(hn: torch.Tensor, T: int, embed):
@@ -656,7 +573,7 @@ class LlamaModel:
 
     def _forward_mid(self, meta: StepMeta, kv: KVCache, T: int, num_logit_rows: int,
                      part_o: torch.Tensor, part_ml: torch.Tensor, embed=None) -> torch.Tensor:
-        """Mid-size and prefill-heavy steps (T > WIDE_MAX_T: decode rows plus prefill chunks)
+        """Mid-size and prefill-heavy steps (T > DECODE_FUSED_MAX_T: decode rows plus prefill chunks)
         on the packed weights, 4 projection launches + attention per layer
         (csrc/ops/gemm_mid.hip up to MID_MAX_T tokens; above it the 256 x 256 tiles of
         csrc/ops/gemm_prefill.hip for the projections PF_CFG assigns to them):
@@ -688,7 +605,7 @@ class LlamaModel:
             ops.paged_attention(attn, part_o, part_ml, q, kv.k[li], kv.v[li], meta.items, meta.n_items,
                                 meta.att_counters, meta.q_start, meta.q_len, meta.ctx_len,
                                 meta.block_table, self.scale, num_seqs=meta.num_seqs, part_size=meta.part_size,
-                                queue=meta.att_queue, waves=self.ATT_MID_WAVES)
+                                waves=self.ATT_MID_WAVES)
             a2 = attn.view(T, H * hd)
             if tp:  # all-reduce + residual + the next norm's row statistics in one launch;
                 # ss_b was zeroed by the previous down all-reduce (or above), ss_a is zeroed here

@@ -73,28 +73,6 @@ def empty_handoff(numel: int, dtype=torch.float32, device=None) -> torch.Tensor:
     return torch.zeros(int(numel), dtype=dtype, device=device)
 
 
-_PF_SINKS: dict = {}
-
-
-def _prefetch_sink(device) -> torch.Tensor:
-    """A 4 KiB device buffer per device that prefetching kernels could write (never do in
-    practice). Allocated on first use — the model calls it at load time, outside any
-    graph capture."""
-    key = str(device)
-    t = _PF_SINKS.get(key)
-    if t is None:
-        t = _PF_SINKS[key] = torch.zeros(1024, dtype=torch.int32, device=device)
-    return t
-
-
-def prefetch(t: torch.Tensor, sink: torch.Tensor, wgs: int = 64):
-    """Read `t` once so its lines land in the Infinity Cache (csrc/ops/prefetch.hip); meant
-    for a side stream while a latency-bound kernel runs. `sink` (>= 4 KiB, on t's device)
-    is never written in practice. No-op off the GPU."""
-    if _on_gpu(t):
-        require_native().prefetch(t, sink, int(wgs))
-
-
 def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float, out: Optional[torch.Tensor] = None):
     if _on_gpu(x):
         out = torch.empty_like(x) if out is None else out
@@ -148,22 +126,16 @@ def rope_cache(q_out, k_cache, v_cache, qkv, positions, slot_mapping, cos_sin, H
 
 def paged_attention(out, part_o, part_ml, q, k_cache, v_cache, items, n_items, counters,
                     q_start, q_len, ctx_len, block_table, scale: float, num_seqs: Optional[int] = None,
-                    part_size: Optional[torch.Tensor] = None, prefetch: Optional[torch.Tensor] = None,
-                    queue: Optional[torch.Tensor] = None, waves: int = 4):
+                    part_size: Optional[torch.Tensor] = None, waves: int = 4):
     """Attention over the paged cache. On GPU `items` must be a device int32
     [max, 4] tensor with a device count (graph-capturable) and `counters` a
     zero-initialised int32 tensor of >= seqs * KV entries (partition tickets; the
-    kernel leaves it zeroed); on CPU the reference path ignores both. `prefetch`: a
-    tensor (e.g. the next projection's packed weights) that the grid's idle workgroups
-    read into the Infinity Cache. `queue`: a zero-initialised device int32 [>= 2 * KV]
-    (left zeroed) selects the persistent work-queue launch (csrc/ops/attention.hip MODE 3).
-    `waves` 8: 512-thread workgroups for the decode and 32-column prefill items (small decode
+    kernel leaves it zeroed); on CPU the reference path ignores both. `waves` 8: 512-thread workgroups for the decode and 32-column prefill items (small decode
     batches; wide items run as their 32-column sub-items)."""
     if _on_gpu(q):
-        sink = _prefetch_sink(q.device) if prefetch is not None else None
         require_native().paged_attention(out, part_o, part_ml, q, k_cache, v_cache, items, n_items,
                                          counters, q_start, q_len, ctx_len, block_table,
-                                         float(scale), part_size, prefetch, sink, 0, queue, int(waves))
+                                         float(scale), part_size, int(waves))
         return out
     ns = len(q_len) if num_seqs is None else num_seqs
     r = ref.paged_attention(q, k_cache, v_cache, q_start[:ns], q_len[:ns], ctx_len[:ns],
@@ -171,42 +143,6 @@ def paged_attention(out, part_o, part_ml, q, k_cache, v_cache, items, n_items, c
     n_tok = int(q_start[ns - 1] + q_len[ns - 1]) if ns > 0 else 0
     out[:n_tok].copy_(r[:n_tok])
     return out
-
-
-_attn_o_sync = {}
-
-
-def attn_o_workspace(device) -> tuple:
-    """(sync[2], err[1]) int32 for attn_o: zero, and left zero by every launch."""
-    key = str(device)
-    if key not in _attn_o_sync:
-        _attn_o_sync[key] = (torch.zeros(2, dtype=torch.int32, device=device),
-                             torch.zeros(1, dtype=torch.int32, device=device))
-    return _attn_o_sync[key]
-
-
-def attn_o(out, part_o, part_ml, q, k_cache, v_cache, items, n_items, counters, q_start, q_len, ctx_len,
-           block_table, scale: float, wo: torch.Tensor, h: torch.Tensor, num_seqs: Optional[int] = None,
-           part_size: Optional[torch.Tensor] = None) -> bool:
-    """Decode-sized steps: paged attention into `out` [T, H, 128] AND h[:T] += out . Wo^T (Wo
-    packed by pack_decode_weight) in one launch (csrc/ops/attention.hip attn_o_kernel: the O
-    tiles' weights stream into LDS / registers of the workgroups without an attention unit
-    while the attention runs, one workgroup per CU; the attention output is handed over by
-    write-through stores and sc1 loads). Measured slower than the two launches in the engine
-    (BENCHMARKS.md), so LlamaModel.ATTN_O_FUSED is off by default. Diagnostics:
-    PILOTTAI_ATTN_O_MODE bits (attention.hip AttnOArgs.mode). Returns False if the shape /
-    device does not allow it (then nothing ran). CPU: the reference attention + mid_gemm
-    residual path."""
-    if _on_gpu(q):
-        sync, err = attn_o_workspace(q.device)
-        return bool(require_native().attn_o(out, part_o, part_ml, q, k_cache, v_cache, items, n_items, counters,
-                                            q_start, q_len, ctx_len, block_table, float(scale), part_size, wo, h,
-                                            sync, err))
-    paged_attention(out, part_o, part_ml, q, k_cache, v_cache, items, n_items, counters, q_start, q_len, ctx_len,
-                    block_table, scale, num_seqs=num_seqs, part_size=part_size)
-    T = q.shape[0]
-    mid_gemm(out.view(T, -1), wo, "resid", resid=h[:T], out=h[:T])
-    return True
 
 
 def sample_workspace(rows: int, V: int, device) -> torch.Tensor:
@@ -372,7 +308,7 @@ def decode_gemm(x: torch.Tensor, wp: torch.Tensor, epi: str = "plain", norm: boo
     if out is None:
         out = torch.empty(M, NO, dtype=x.dtype, device=x.device)
     if _on_gpu(x):
-        ws, cnt = wide_workspace(x.device)
+        ws, cnt = decode_workspace(x.device)
         if not require_native().decode_gemm(out, x, wp, resid, code, bool(norm), float(eps), int(nt), int(waves),
                                             int(splits), ws, cnt):
             raise ValueError(f"decode_gemm does not handle M={M} N={N} K={K} epi={epi} nt={nt} waves={waves}")
@@ -420,7 +356,7 @@ def decode_qkv_rope(x: torch.Tensor, wp: torch.Tensor, eps: float, q_out: torch.
     into the packed weights), RoPE and the paged KV write fused in the epilogue:
     replaces rmsnorm + QKV GEMM + rope_cache on decode-sized steps."""
     if _on_gpu(x):
-        ws, cnt = wide_workspace(x.device)
+        ws, cnt = decode_workspace(x.device)
         require_native().decode_qkv_rope(x, wp, float(eps), q_out, k_cache, v_cache, positions, slots,
                                          cos_sin, int(H), int(KV), int(splits), ws, cnt)
         return q_out
@@ -431,59 +367,19 @@ def decode_qkv_rope(x: torch.Tensor, wp: torch.Tensor, eps: float, q_out: torch.
     return q_out
 
 
-# ---------------------------------------------------------------------------
-# Small-batch projections (16 < M <= 256) on the packed weights (csrc/ops/gemm_wide.hip)
-
-WIDE_EPI = {"plain": 0, "silu": 1, "resid": 2, "rope_perm": 3}
-WIDE_WS_FLOATS = 8 << 20  # 32 MB of split-K slabs per device
-_wide_ws = {}
+# split-K slabs + tickets of the packed decode kernels (decode_gemm / decode_qkv_rope)
+DECODE_WS_FLOATS = 8 << 20  # 32 MB of split-K slabs per device
+_decode_ws = {}
 
 
-def wide_workspace(device):
-    """(slabs, tickets) for wide_gemm on `device`; allocate before hipGraph capture
-    (the tickets must start zeroed; every launch leaves them zeroed)."""
+def decode_workspace(device):
+    """(slabs, tickets) for decode_gemm / decode_qkv_rope on `device`; allocate before
+    hipGraph capture (the tickets must start zeroed; every launch leaves them zeroed)."""
     key = str(device)
-    if key not in _wide_ws:
-        _wide_ws[key] = (empty_handoff(WIDE_WS_FLOATS, torch.float32, device),
-                         torch.zeros(16384, dtype=torch.int32, device=device))
-    return _wide_ws[key]
-
-
-def wide_gemm(x: torch.Tensor, wp: torch.Tensor, epi: str = "plain", resid: Optional[torch.Tensor] = None,
-              out: Optional[torch.Tensor] = None, norm: bool = False, eps: float = 1e-5, ntw: int = 0,
-              waves: int = 0, splits: int = 0) -> torch.Tensor:
-    """y = epi(rownorm(x) @ W.T) for 16 < M <= 128 with W packed by pack_decode_weight
-    (gate_up: pack_decode_gate_up + epi "silu"; QKV: pack_decode_qkv_rope + epi
-    "rope_perm", which returns the natural column order); "resid": resid + acc.
-    `norm` scales rows by rsqrt(mean(x^2) + eps) (RMSNorm weight folded into W)."""
-    M, K = x.shape
-    N = wp.shape[0] * 16
-    code = WIDE_EPI[epi]
-    NO = N // 2 if code == 1 else N
-    if out is None:
-        out = torch.empty(M, NO, dtype=x.dtype, device=x.device)
-    if _on_gpu(x):
-        ws, cnt = wide_workspace(x.device)
-        if not require_native().wide_gemm(out, x, wp, resid, ws, cnt, code, bool(norm), float(eps), int(ntw),
-                                          int(waves), int(splits)):
-            raise ValueError(f"wide_gemm does not handle M={M} N={N} K={K} epi={epi} ntw={ntw} waves={waves}")
-        return out
-    if code == 3:
-        W = unpack_decode_qkv_rope(wp)
-    elif code == 1:
-        W = unpack_decode_gate_up(wp)
-    else:
-        W = unpack_decode_weight(wp)
-    xf = x.float()
-    acc = xf @ W.float().T
-    if norm:
-        acc = acc * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps)
-    if code == 1:
-        acc = torch.nn.functional.silu(acc[:, :NO]) * acc[:, NO:]
-    elif code == 2:
-        acc = acc + resid.float()
-    out.copy_(acc.to(out.dtype))
-    return out
+    if key not in _decode_ws:
+        _decode_ws[key] = (empty_handoff(DECODE_WS_FLOATS, torch.float32, device),
+                           torch.zeros(16384, dtype=torch.int32, device=device))
+    return _decode_ws[key]
 
 
 # ---------------------------------------------------------------------------
@@ -571,6 +467,14 @@ def mid_gemm(x: torch.Tensor, wp: torch.Tensor, epi: str = "plain", resid: Optio
 STREAM_EPI = {"plain": 0, "silu": 1, "resid": 2, "rope_perm": 3}
 STREAM_WS_FLOATS = 24 << 20  # 96 MB of split-K partial fragments per device (uncached)
 _stream_ws = {}
+# Split-K group hand-off of gemm_stream.hip (rel bit 0): the producer's agent-scope release
+# (buffer_wbl2 sc1 + drain) before it arrives on the group counter, i.e. the LLVM AMDGPU
+# memory model's release at agent scope, paired with the acquire after the poll. Without it
+# the protocol rests on when a write-through store's vmcnt ack comes back relative to the
+# fabric write (the round-4 decode QKV+RoPE case failed 5 of 10,000 poisoned runs that way
+# on uncached slabs: profiles/r4_handoff_uncached.md, profiles/r5_handoff_*). 0 = the sc1-only
+# form, for the A/B tools only.
+STREAM_REL = int(os.environ.get("PILOTTAI_STREAM_REL", "1"))
 
 
 def stream_workspace(device):
@@ -594,14 +498,14 @@ def stream_gemm_plan(M: int, N: int, K: int, epi: str = "plain"):
 def stream_gemm(x: torch.Tensor, wp: torch.Tensor, epi: str = "plain", resid: Optional[torch.Tensor] = None,
                 out: Optional[torch.Tensor] = None, norm: bool = False, eps: float = 1e-5,
                 ss_in: Optional[torch.Tensor] = None, ss_out: Optional[torch.Tensor] = None,
-                ss_zero: Optional[torch.Tensor] = None, plan=None, rel: int = 0,
+                ss_zero: Optional[torch.Tensor] = None, plan=None, rel: Optional[int] = None,
                 stamps: Optional[torch.Tensor] = None) -> torch.Tensor:
     """y = epi(rownorm(x) @ W.T) for 16 < M <= 256 with W packed by pack_decode_weight (gate_up:
     pack_decode_gate_up + "silu"; QKV: pack_decode_qkv_rope + "rope_perm"); same epilogue and
     row-statistics conventions as mid_gemm. `plan`: (mg, rg, tpw, wt, wk, S, D) or None for
     the kernel's default decomposition (csrc/ops/gemm_stream.hip).
-    rel: bit 0 = producer-side L2 release before the group barrier (diagnostics), bit 1 =
-    each workgroup streams its K slice from a rotated starting chunk."""
+    rel: bit 0 = producer-side agent-scope release before the group barrier, bit 1 = each
+    workgroup streams its K slice from a rotated starting chunk; None = STREAM_REL."""
     M, K = x.shape
     N = wp.shape[0] * 16
     code = STREAM_EPI[epi]
@@ -613,7 +517,8 @@ def stream_gemm(x: torch.Tensor, wp: torch.Tensor, epi: str = "plain", resid: Op
     if _on_gpu(x):
         ws, cnt, err = stream_workspace(x.device)
         if not require_native().stream_gemm(out, x, wp, resid, ws, cnt, err, code, ss_in if norm else None, ss_out,
-                                             ss_zero, float(eps), list(plan) if plan else [], rel=int(rel),
+                                             ss_zero, float(eps), list(plan) if plan else [],
+                                             rel=int(STREAM_REL if rel is None else rel),
                                              stamps=stamps):
             raise ValueError(f"stream_gemm does not handle M={M} N={N} K={K} epi={epi} plan={plan}")
         return out
@@ -623,7 +528,7 @@ def stream_gemm(x: torch.Tensor, wp: torch.Tensor, epi: str = "plain", resid: Op
 
 def stream_qkv_rope(x: torch.Tensor, wp: torch.Tensor, eps: float, q_out: torch.Tensor, k_cache, v_cache,
                     positions, slots, cos_sin, H: int, KV: int, ss_in: Optional[torch.Tensor] = None, plan=None,
-                    rel: int = 0) -> torch.Tensor:
+                    rel: Optional[int] = None) -> torch.Tensor:
     """QKV projection for 16 < M <= 256 (RMSNorm folded, row statistics ss_in) with RoPE and the
     paged KV write in the epilogue (csrc/ops/gemm_stream.hip, EP_ROPEKV)."""
     if ss_in is None:
@@ -632,7 +537,7 @@ def stream_qkv_rope(x: torch.Tensor, wp: torch.Tensor, eps: float, q_out: torch.
         ws, cnt, err = stream_workspace(x.device)
         if not require_native().stream_gemm(None, x, wp, None, ws, cnt, err, 4, ss_in, None, None, float(eps),
                                              list(plan) if plan else [], q_out, k_cache, v_cache, positions, slots,
-                                             cos_sin, int(H), int(KV), int(rel)):
+                                             cos_sin, int(H), int(KV), int(STREAM_REL if rel is None else rel)):
             raise ValueError(f"stream_qkv_rope does not handle M={x.shape[0]} K={x.shape[1]} plan={plan}")
         return q_out
     return mid_qkv_rope(x, wp, eps, q_out, k_cache, v_cache, positions, slots, cos_sin, H, KV, ss_in=ss_in)

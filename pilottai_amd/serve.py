@@ -332,6 +332,13 @@ class Serve:
                 for st in subtasks:
                     await self._enqueue(st)
                 return task.id
+        if inline:
+            # yield the loop once per task before running it in the caller's coroutine: when the
+            # LLM and tool calls complete without suspending, a caller-runs client would
+            # otherwise run its whole batch before any other client, heartbeat or plane RPC got
+            # a turn (the reference's single queue consumer interleaves clients,
+            # pilott/pilott.py:272-303); the slot test below then sees the state after the yield
+            await asyncio.sleep(0)
         if inline and self._queue.empty() and self._active < self.config.max_concurrent_tasks \
                 and not any(d in self.tasks and d not in self.completed_tasks for d in task.dependencies):
             # caller-runs: a free concurrency slot and nothing queued ahead — run the

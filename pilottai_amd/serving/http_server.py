@@ -213,7 +213,8 @@ def main():
         dev = torch.device("cuda", 0) if torch.cuda.is_available() else torch.device("cpu")
         eng = LLMEngine(EngineConfig(model=a.model if dev.type == "cuda" else "tiny",
                                      kv_cache_gb=a.kv_gb if dev.type == "cuda" else None,
-                                     num_kv_blocks=None if dev.type == "cuda" else 1024), device=dev)
+                                     num_kv_blocks=None if dev.type == "cuda" else 1024,
+                                     freeze_heap=True), device=dev)
         eng.start()
         llm = LocalLLM(LLMConfig(model_name=eng.model_cfg.name, max_tokens=1024), engine=eng)
         app = create_app(llm, eng.model_cfg.name, engine=eng)

@@ -60,7 +60,7 @@ def test_sampling_batch_invariance(engine):
     as the steps run the same kernels (the packed decode path here: every step of
     both runs has <= 16 tokens, every context < 128 keys). Rows are independent in
     every kernel and the sampler's RNG is keyed per request, so the tokens are
-    bit-identical; across kernel paths (a 200-token prefill step on hipBLASLt vs a
+    bit-identical; across kernel paths (a 200-token step on the mid / stream kernels vs a
     6-token one on the decode kernels) only bf16 rounding may differ."""
     tok = engine.tok
     p = tok.encode("batch invariance probe prompt")
@@ -168,22 +168,6 @@ def test_llama3_8b_production_large_steps(gpu, lens):
     for p, o in zip(prompts, outs):
         assert len(o.token_ids) == 5
         _check_greedy(eng, p, o.token_ids)
-
-
-def test_llama3_8b_layer_dims_small_batch_path(gpu):
-    """The packed small-batch path (csrc/ops/gemm_wide.hip; off by default, EngineConfig
-    wide_max_t turns it on) on a 17-48-token prefill step at the exact Llama-3-8B dims."""
-    from pilottai_amd.engine.engine import EngineConfig, LLMEngine
-
-    eng = LLMEngine(EngineConfig(model="llama-3-8b-2l", max_num_seqs=8, max_num_batched_tokens=512,
-                                 max_model_len=1024, num_kv_blocks=256, prefix_caching=False,
-                                 token_buckets=[16, 48, 128, 256, 512], token_align=0, wide_max_t=48),
-                    device=gpu)
-    assert eng.model.WIDE_MAX_T == 48
-    tok = eng.tok
-    prompt = tok.encode(("agents plan tasks and tools while the orchestrator checks every result " * 8))[:30]
-    out = eng.generate([prompt], temperature=0.0, max_tokens=6, ignore_eos=True)[0]
-    _check_greedy(eng, prompt, out.token_ids)
 
 
 _ENG8B = {}

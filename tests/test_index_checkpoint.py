@@ -57,6 +57,23 @@ def test_index_ring_position_survives(tmp_path):
     assert a == b == [36, 37, 38]
 
 
+def test_index_wrapped_ring_keeps_its_capacity(tmp_path):
+    """a wrapped ring restored under another capacity would move its write position
+    and count never-written rows; load refuses it, and an unwrapped index may still grow."""
+    idx = SemanticIndex(dim=32, capacity=64, device="cpu", growable=False)
+    rng = np.random.default_rng(4)
+    idx.add(rng.standard_normal((100, 32)), [0] * 100, [()] * 100, [None] * 100)
+    idx.save(tmp_path / "w")
+    with pytest.raises(ValueError, match="wrapped ring"):
+        SemanticIndex.load(tmp_path / "w", device="cpu", capacity=128)
+    assert SemanticIndex.load(tmp_path / "w", device="cpu", capacity=64).count == 64
+    small = SemanticIndex(dim=32, capacity=64, device="cpu", growable=False)
+    small.add(rng.standard_normal((40, 32)), [0] * 40, [()] * 40, [None] * 40)
+    small.save(tmp_path / "u")
+    back = SemanticIndex.load(tmp_path / "u", device="cpu", capacity=256)
+    assert back.count == 40 and back.add(rng.standard_normal((1, 32)), [0], [()], [None]) == [40]
+
+
 def test_index_checkpoint_rejects_mismatch(tmp_path):
     idx, _ = _filled(100)
     idx.save(tmp_path / "m")

@@ -70,7 +70,7 @@ def test_rope_cache(gpu):
 
 
 def _run_attention(gpu, H, KV, q_lens, ctx_lens, seed=0, split=True, part=512, qcols=128, pad=1,
-                   prefetch=None, queue=False, launches=1, waves=4):
+                   launches=1, waves=4):
     torch.manual_seed(seed)
     G = H // KV
     blk = 16
@@ -99,15 +99,12 @@ def _run_attention(gpu, H, KV, q_lens, ctx_lens, seed=0, split=True, part=512, q
     out = torch.zeros(T, H, 128, dtype=torch.bfloat16, device=gpu)
     scale = 1.0 / math.sqrt(128)
     dev_i = lambda a: torch.tensor(a, dtype=torch.int32, device=gpu)  # noqa: E731
-    qt = torch.zeros(2 * KV, dtype=torch.int32, device=gpu) if queue else None
-    for _ in range(launches):  # the work queue must reset itself for the next launch
+    for _ in range(launches):  # the partition tickets must reset themselves for the next launch
         ops.paged_attention(out, part_o, part_ml, q, kc, vc, it, n_it, cnt, dev_i(q_start),
                             dev_i(q_lens), dev_i(ctx_lens), bt.to(gpu), scale, part_size=dev_i([part]),
-                            prefetch=prefetch, queue=qt, waves=waves)
+                            waves=waves)
     torch.cuda.synchronize()
     assert int(cnt.abs().sum()) == 0, "partition tickets must be left zeroed"
-    if qt is not None:
-        assert int(qt.abs().sum()) == 0, "the work queue must be left zeroed"
     r = ref.paged_attention(q.cpu(), kc.cpu(), vc.cpu(), q_start, q_lens, ctx_lens, bt, scale)
     return out.cpu().float(), r.float()
 
@@ -117,20 +114,6 @@ def test_attention_decode(gpu, H, KV):
     ctx = [1, 15, 16, 17, 33, 100, 511, 512, 513, 1500, 2049, 64]
     o, r = _run_attention(gpu, H, KV, [1] * len(ctx), ctx)
     torch.testing.assert_close(o, r, atol=2e-2, rtol=2e-2)
-
-
-def test_attention_idle_workgroups_prefetch(gpu):
-    """The engine's decode graphs size the attention grid for the bucket's largest item
-    list; the idle workgroups read the next projection's weights (MALL prefetch). The
-    attention result must be bit-identical with and without it, and equal to fp32."""
-    ctx = [1, 15, 100, 511, 513, 1500, 2049, 64]
-    w = torch.randn(4096 * 4096 + 24, device=gpu).to(torch.bfloat16)  # 34 MB, not a multiple of 64 B
-    o0, r = _run_attention(gpu, 32, 8, [1] * len(ctx), ctx, seed=3, pad=140)
-    o1, _ = _run_attention(gpu, 32, 8, [1] * len(ctx), ctx, seed=3, pad=140, prefetch=w)
-    torch.testing.assert_close(o1, r, atol=2e-2, rtol=2e-2)
-    assert torch.equal(o0, o1)
-    with pytest.raises(RuntimeError):  # a prefetch tensor on the wrong device fails loudly
-        _run_attention(gpu, 32, 8, [1], [10], pad=4, prefetch=w.cpu())
 
 
 @pytest.mark.parametrize("qcols", [32, 128])
@@ -163,12 +146,10 @@ def test_attention_small_partitions(gpu, part):
 
 
 @pytest.mark.parametrize("case", ["decode", "mixed32", "mixed128", "tiles", "kv1", "kv16", "small_part", "step2048"])
-def test_attention_work_queue_matches_grid_launch(gpu, case):
-    """Persistent work-queue launch (attention.hip MODE 3: 2 workgroups per CU, KV head =
-    blockIdx % KV, items claimed from a per-head counter, last workgroup resets it):
-    bit-identical to the grid-strided launch (same device code per item, the same
-    partition-merge order) and equal to fp32, over three back-to-back launches on one
-    queue tensor, with padded item lists as the engine's graphs have."""
+def test_attention_repeated_padded_launches(gpu, case):
+    """Three back-to-back launches on one ticket buffer with padded item lists, as the
+    engine's graphs replay them: bit-identical to a single launch (the partition tickets
+    reset themselves, the merge order is fixed) and equal to fp32."""
     cfg = {
         "decode": dict(H=32, KV=8, q=[1] * 12, c=[1, 15, 16, 17, 33, 100, 511, 512, 513, 1500, 2049, 64]),
         "mixed32": dict(H=32, KV=8, q=[37, 1, 100, 3, 16, 5, 250, 129, 33], c=[37, 700, 164, 40, 16, 1029, 260, 1000, 2100],
@@ -182,12 +163,12 @@ def test_attention_work_queue_matches_grid_launch(gpu, case):
     }[case]
     kw = dict(seed=17, qcols=cfg.get("qcols", 128), part=cfg.get("part", 512), pad=200)
     og, r = _run_attention(gpu, cfg["H"], cfg["KV"], cfg["q"], cfg["c"], **kw)
-    oq, _ = _run_attention(gpu, cfg["H"], cfg["KV"], cfg["q"], cfg["c"], queue=True, launches=3, **kw)
+    oq, _ = _run_attention(gpu, cfg["H"], cfg["KV"], cfg["q"], cfg["c"], launches=3, **kw)
     torch.testing.assert_close(oq, r, atol=2e-2, rtol=2e-2)
     assert torch.equal(oq, og)
 
 
-@pytest.mark.parametrize("case", ["decode", "small_part", "mixed32", "mixed128_wide", "kv1", "queue"])
+@pytest.mark.parametrize("case", ["decode", "small_part", "mixed32", "mixed128_wide", "kv1", "rows9"])
 def test_attention_eight_wave_workgroups(gpu, case):
     """512-thread workgroups (waves=8, the engine's decode-sized steps): decode items split
     their 32-key tiles over 8 waves, 32-column prefill items too, and wide (128-column)
@@ -200,9 +181,9 @@ def test_attention_eight_wave_workgroups(gpu, case):
         "mixed128_wide": dict(H=32, KV=8, q=[37, 1, 100, 3, 16, 5, 250, 129, 33],
                               c=[37, 700, 164, 40, 16, 1029, 260, 1000, 2100]),
         "kv1": dict(H=8, KV=1, q=[1, 1, 2, 12, 1], c=[100, 600, 33, 40, 2000]),
-        "queue": dict(H=32, KV=8, q=[1] * 8 + [5], c=[600] * 8 + [300], queue=True),
+        "rows9": dict(H=32, KV=8, q=[1] * 8 + [5], c=[600] * 8 + [300]),
     }[case]
-    kw = dict(seed=23, qcols=cfg.get("qcols", 128), part=cfg.get("part", 256), pad=50, queue=cfg.get("queue", False))
+    kw = dict(seed=23, qcols=cfg.get("qcols", 128), part=cfg.get("part", 256), pad=50)
     o4, r = _run_attention(gpu, cfg["H"], cfg["KV"], cfg["q"], cfg["c"], **kw)
     o8, _ = _run_attention(gpu, cfg["H"], cfg["KV"], cfg["q"], cfg["c"], waves=8, launches=2, **kw)
     torch.testing.assert_close(o8, r, atol=2e-2, rtol=2e-2)
@@ -428,37 +409,6 @@ def test_decode_qkv_rope(gpu, M, H, KV, K, splits):
     torch.testing.assert_close(q.float().cpu(), rq, atol=3e-2, rtol=2e-2)
     torch.testing.assert_close(kc.float().cpu(), rk, atol=3e-2, rtol=2e-2)
     torch.testing.assert_close(vc.float().cpu(), rv, atol=3e-2, rtol=2e-2)
-
-
-@pytest.mark.parametrize("M,N,K,epi,norm,ntw,waves,splits", [
-    (17, 4096, 4096, "plain", False, 0, 0, 0), (48, 6144, 4096, "rope_perm", True, 0, 0, 0),
-    (128, 28672, 4096, "silu", True, 0, 0, 0), (64, 4096, 14336, "resid", False, 0, 0, 0),
-    (33, 1024, 512, "silu", True, 2, 4, 2), (100, 768, 512, "rope_perm", False, 1, 4, 1),
-    (120, 4096, 4096, "resid", False, 1, 8, 3), (90, 6144, 4096, "plain", True, 2, 4, 5),
-    (64, 2048, 1024, "plain", False, 2, 8, 1), (29, 4096, 4096, "plain", True, 1, 4, 4),
-    # SwiGLU with one tile per wave (gate/up handed over through LDS), split-K and 8 waves
-    (24, 28672, 4096, "silu", True, 1, 4, 0), (33, 1024, 512, "silu", True, 1, 4, 3),
-    (40, 1024, 512, "silu", False, 1, 8, 0)])
-def test_wide_gemm(gpu, M, N, K, epi, norm, ntw, waves, splits):
-    """Small-batch packed-weight GEMM (csrc/ops/gemm_wide.hip) vs fp32, every epilogue
-    and the folded row norm, with and without split-K; run twice so the
-    self-resetting split-K tickets are exercised."""
-    torch.manual_seed(15)
-    x = _bf(M, K, dev=gpu)
-    w = _bf(N, K, dev=gpu, scale=0.05)
-    resid = _bf(M, N, dev=gpu) if epi == "resid" else None
-    pack = {"silu": ops.pack_decode_gate_up, "rope_perm": ops.pack_decode_qkv_rope}.get(epi, ops.pack_decode_weight)
-    wp = pack(w)
-    acc = x.float() @ w.float().T
-    if norm:
-        acc = acc * torch.rsqrt(x.float().pow(2).mean(-1, keepdim=True) + 1e-5)
-    if epi == "silu":
-        acc = torch.nn.functional.silu(acc[:, :N // 2]) * acc[:, N // 2:]
-    elif epi == "resid":
-        acc = acc + resid.float()
-    for _ in range(2):
-        y = ops.wide_gemm(x, wp, epi, resid=resid, norm=norm, ntw=ntw, waves=waves, splits=splits)
-        torch.testing.assert_close(y.float(), acc, atol=3e-2, rtol=2e-2)
 
 
 @pytest.mark.parametrize("M,N,K,epi,norm,fm,fn,splits", [

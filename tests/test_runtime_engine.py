@@ -360,7 +360,6 @@ def test_fused_decode_path_matches_unfused_logits():
         assert eng.model.decode_packed
         if not fused:
             eng.model.DECODE_FUSED_MAX_T = 0
-            eng.model.WIDE_MAX_T = 0
             eng.model.MID_MAX_T = 0
         seen = []
         fwd = eng.model.forward
@@ -377,52 +376,6 @@ def test_fused_decode_path_matches_unfused_logits():
     assert a.shape == b.shape
     torch.testing.assert_close(a, b, atol=0.05 * float(b.abs().max()), rtol=0.05)
     assert int(a.argmax(-1)[0]) == int(b.argmax(-1)[0]) or float((a - b).abs().max()) < 1e-2
-
-
-def test_attn_o_fused_decode_path_same_tokens(tok):
-    """LlamaModel.ATTN_O_FUSED (attention + O projection + residual in one launch on decode
-    steps) leaves the greedy tokens unchanged (CPU: the op's reference path)."""
-    from pilottai_amd.engine.engine import EngineConfig, LLMEngine
-
-    prompts = [tok.encode("Task: summarize the report."), tok.encode("List three risks of the plan.")]
-    outs = {}
-    for fused in (False, True):
-        eng = LLMEngine(EngineConfig(model="tiny", max_num_seqs=8, use_graphs=False, decode_fused=True,
-                                     num_kv_blocks=256, max_model_len=512,
-                                     model_overrides={"ATTN_O_FUSED": fused}))
-        outs[fused] = [o.token_ids for o in eng.generate(prompts, temperature=0.0, max_tokens=12, ignore_eos=True)]
-    assert outs[True] == outs[False]
-
-
-def test_wide_path_matches_library_path_logits():
-    """The packed small-batch forward (16 < T <= 32: folded norms, split-K kernels,
-    SwiGLU / residual epilogues) and the library-GEMM forward give the same logits
-    for a 24-token prefill step on a tiny model (CPU references of both paths)."""
-    import torch
-
-    from pilottai_amd.engine.engine import EngineConfig, LLMEngine
-
-    logits = {}
-    for wide in (True, False):
-        eng = LLMEngine(EngineConfig(model="tiny", max_num_seqs=8, use_graphs=False, decode_fused=True,
-                                     num_kv_blocks=256, max_model_len=512))
-        if not wide:
-            eng.model.WIDE_MAX_T = 0
-            eng.model.MID_MAX_T = 0
-        seen = []
-        fwd = eng.model.forward
-
-        def rec(*a, _f=fwd, _s=seen, **k):
-            out = _f(*a, **k)
-            _s.append((a[2], out.float().clone()))
-            return out
-
-        eng.model.forward = rec
-        eng.generate([list(range(1, 25))], max_tokens=2, temperature=0.0, ignore_eos=True)
-        assert 16 < seen[0][0] <= 32
-        logits[wide] = seen[0][1]
-    a, b = logits[True], logits[False]
-    torch.testing.assert_close(a, b, atol=0.05 * float(b.abs().max()), rtol=0.05)
 
 
 def test_mid_path_matches_library_path_logits():
@@ -538,9 +491,31 @@ def test_engine_fails_on_custom_allreduce_timeout():
     eng = LLMEngine(EngineConfig(model="tiny", max_num_seqs=4, use_graphs=False, num_kv_blocks=64,
                                  max_model_len=256))
     eng._car = types.SimpleNamespace(err=torch.ones(1, dtype=torch.int32))
-    eng._car_err_host = torch.zeros(1, dtype=torch.int32)
+    eng._health_dev = [("custom all-reduce barrier timed out", eng._car.err)]
+    eng._health_host = torch.zeros(1, dtype=torch.int32)
     eng.submit([1, 2, 3], lambda o: None, max_tokens=2)
     with pytest.raises(RuntimeError, match="custom all-reduce"):
+        for _ in range(4):
+            eng.step()
+
+
+def test_engine_fails_on_stream_gemm_group_barrier_timeout():
+    """the weight-streaming GEMM's split-K group barrier sets an error word when a
+    partner workgroup never arrives (its reduced slabs would be partial); the engine reads that
+    word back with every step and must stop instead of serving wrong logits."""
+    import torch
+
+    from pilottai_amd.engine.engine import EngineConfig, LLMEngine
+
+    eng = LLMEngine(EngineConfig(model="tiny", max_num_seqs=4, use_graphs=False, num_kv_blocks=64,
+                                 max_model_len=256))
+    err = torch.zeros(1, dtype=torch.int32)
+    eng._health_dev = [("weight-streaming GEMM split-K group barrier timed out", err)]
+    eng._health_host = torch.zeros(1, dtype=torch.int32)
+    eng.submit([1, 2, 3], lambda o: None, max_tokens=8)
+    assert eng.step()  # healthy step
+    err[0] = 1  # a timed-out group barrier in the next step
+    with pytest.raises(RuntimeError, match="group barrier timed out"):
         for _ in range(4):
             eng.step()
 
@@ -755,6 +730,43 @@ def test_scheduler_decode_part_target_one_balanced_round(rows):
         assert part == 160 and len(items) == 16 * 4 and (nparts == 4).all()
     # the ops.attn_meta mirror builds the same list for that part size
     ql, cl = buf[L["q_len"]:L["q_len"] + c[1]], buf[L["ctx_len"]:L["ctx_len"] + c[1]]
+    ref_items, _ = build_attention_items(list(ql), list(cl), 4, part=part)
+    assert [tuple(int(v) for v in x) for x in items] == ref_items
+
+
+def test_scheduler_decode_part_target_splits_a_long_row_among_short_ones():
+    """with 48 decode rows x 8 KV heads >= the 384 target, decode_part_target used to
+    set the partition to the LONGEST context, so one long row ran as a single serial work item
+    beside 47 short ones. The partition is now capped at the balanced share of all decode keys
+    per workgroup: the 4,000-key row is split, the ~600-key rows are not."""
+    cfg = {"num_blocks": 8192, "block_size": 16, "max_num_seqs": 64, "max_num_batched_tokens": 2048,
+           "max_prefill_tokens": 2048, "max_model_len": 8192, "gqa_group": 4, "kv_heads": 8,
+           "decode_part_target": 384, "eos_ids": [128009]}
+    s = _runtime.Scheduler(cfg)
+    L = s.layout()
+    buf = np.zeros(L["total"], dtype=np.int32)
+    rng = np.random.default_rng(3)
+    lens = [599] * 47 + [3999]
+    for rid, n in enumerate(lens):
+        s.add_request(rid, list(rng.integers(1000, 9000, n)), 0.0, 50, rid, True, [], None)
+    for _ in range(400):
+        s.schedule(buf.ctypes.data)
+        c = buf[L["counts"]:L["counts"] + 8]
+        s.commit(np.full(max(1, int(c[2])), 7, np.int32).ctypes.data, int(c[2]))
+        if all(x[4] >= lens[x[0]] for x in s.debug_state()):
+            break
+    assert s.schedule(buf.ctypes.data) == 48  # a pure decode step
+    c = buf[L["counts"]:L["counts"] + 8]
+    items = buf[L["items"]:L["items"] + 4 * c[3]].reshape(-1, 4)
+    part = int(buf[L["part_size"]])
+    cl = buf[L["ctx_len"]:L["ctx_len"] + c[1]]
+    share = -(-int(cl.sum()) * 8 // 384)
+    assert part == (share + 31) // 32 * 32 and part < 4000
+    nparts = {int(it[0]): int(it[2] >> 20) for it in items}
+    long_row = int(np.argmax(cl))
+    assert nparts[long_row] == -(-int(cl[long_row]) // part) >= 5
+    assert all(v == 1 for k, v in nparts.items() if k != long_row)
+    ql = buf[L["q_len"]:L["q_len"] + c[1]]
     ref_items, _ = build_attention_items(list(ql), list(cl), 4, part=part)
     assert [tuple(int(v) for v in x) for x in items] == ref_items
 

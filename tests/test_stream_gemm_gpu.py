@@ -26,7 +26,7 @@ def _ref(x, w, epi, norm, resid):
     return acc
 
 
-def _check(gpu, M, N, K, epi, norm, plan, reps=3, rel=0):
+def _check(gpu, M, N, K, epi, norm, plan, reps=3, rel=None):
     torch.manual_seed(31 + M)
     x = _bf(M, K, dev=gpu)
     w = _bf(N, K, dev=gpu, scale=0.05)
@@ -79,7 +79,7 @@ def test_stream_gemm_plans(gpu, M, N, K, epi, norm, plan):
 def test_stream_gemm_rotated_chunk_order(gpu, M, N, K, epi, norm, plan):
     """rel bit 1: every workgroup streams its K slice from a different starting chunk (the
     accumulation order changes, the result must not beyond rounding)."""
-    _check(gpu, M, N, K, epi, norm, plan, rel=2)
+    _check(gpu, M, N, K, epi, norm, plan, rel=2 | ops.kernels.STREAM_REL)
 
 
 def test_stream_gemm_asymmetric_identity(gpu):
@@ -176,4 +176,27 @@ def test_stream_gemm_poisoned_handoff(gpu):
         got = ops.stream_gemm(x, wp, "plain", plan=(4, 1, 2, 4, 1, 8, 4))
         torch.cuda.synchronize()
         assert torch.equal(got, base), rep
+    assert int(err[0]) == 0
+
+
+def test_stream_gemm_group_barrier_timeout_sets_err(gpu):
+    """a split-K group whose partner never arrives (injected: the group's arrive
+    counter starts far below zero, so no workgroup ever sees all S arrivals) must give up after
+    its bounded spin and set the err word the engine reads back, not hang and not stay silent;
+    the departure path then leaves the counters zeroed for the next launch."""
+    torch.manual_seed(35)
+    _, cnt, err = ops.stream_workspace(gpu)
+    x = _bf(64, 4096, dev=gpu)
+    w = _bf(4096, 4096, dev=gpu, scale=0.05)
+    wp = ops.pack_decode_weight(w)
+    plan = (4, 1, 1, 4, 1, 4, 4)  # 64 groups x 4 K-slices
+    err.zero_()
+    cnt[0] = -(1 << 20)  # group 0: its arrivals can never reach S
+    ops.stream_gemm(x, wp, "plain", plan=plan)
+    torch.cuda.synchronize()
+    assert int(err[0]) == 1
+    assert int(cnt[0]) == 0 and int(cnt[1]) == 0  # reset by the last departure
+    err.zero_()
+    y = ops.stream_gemm(x, wp, "plain", plan=plan)  # healthy again
+    torch.testing.assert_close(y.float(), x.float() @ w.float().T, atol=4e-2, rtol=2e-2)
     assert int(err[0]) == 0

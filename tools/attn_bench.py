@@ -58,14 +58,14 @@ def setup(q_lens, ctx_lens, H=32, KV=8, pad_items=0, dev="cuda", part=512, qcols
     return args, kv_bytes, flops, n_items
 
 
-def timeit(args, iters, queue=None, waves=4):
+def timeit(args, iters, waves=4):
     for _ in range(3):
-        ops.paged_attention(*args, queue=queue, waves=waves)
+        ops.paged_attention(*args, waves=waves)
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     for _ in range(iters):
-        ops.paged_attention(*args, queue=queue, waves=waves)
+        ops.paged_attention(*args, waves=waves)
     e1.record()
     torch.cuda.synchronize()
     return e0.elapsed_time(e1) * 1000 / iters
@@ -79,7 +79,6 @@ def main():
     ap.add_argument("--small", action="store_true", help="small-batch decode (8/16 rows) over partition sizes")
     ap.add_argument("--cases", default="", help="comma-separated subset of the step cases")
     ap.add_argument("--qcols", default="32,128", help="prefill item widths to time")
-    ap.add_argument("--queue", default="0", help="0 = grid-strided launch, 1 = work-queue launch (attention.hip MODE 3)")
     ap.add_argument("--waves", default="4", help="waves per workgroup to time (4, 8), comma-separated")
     a = ap.parse_args()
     torch.manual_seed(0)
@@ -114,11 +113,9 @@ def main():
     for name, (ql, cl) in cases.items():
         for qcols in [int(x) for x in a.qcols.split(",")]:
             for pad in ((0,) if a.scan else (0, a.pad)):
-              for qm in [int(x) for x in a.queue.split(",")]:
                 args, kvb, fl, n = setup(ql, cl, pad_items=pad, qcols=qcols)
-                qt = torch.zeros(16, dtype=torch.int32, device="cuda") if qm else None
-                us = timeit(args, a.iters, qt)
-                print(json.dumps({"case": name, "qcols": qcols, "queue": qm, "items": n, "grid_items": args[6].shape[0],
+                us = timeit(args, a.iters)
+                print(json.dumps({"case": name, "qcols": qcols, "items": n, "grid_items": args[6].shape[0],
                                   "us": round(us, 1), "kv_TBps": round(kvb / us / 1e6, 2),
                                   "TFLOPs": round(fl / us / 1e6, 1)}), flush=True)
 

@@ -54,12 +54,12 @@ ALLOC = {"uncached": kernels.empty_handoff,
          "cached": lambda n, dt=torch.float32, device=None: torch.zeros(int(n), dtype=dt, device=device)}
 WS = {}
 for kind, fn in ALLOC.items():  # one split-K workspace set per allocation kind
-    WS[kind] = {"wide": (fn(kernels.WIDE_WS_FLOATS, torch.float32, dev), torch.zeros(16384, dtype=torch.int32, device=dev)),
+    WS[kind] = {"decode": (fn(kernels.DECODE_WS_FLOATS, torch.float32, dev), torch.zeros(16384, dtype=torch.int32, device=dev)),
                 "mid": (fn(kernels.MID_WS_FLOATS, torch.float32, dev), torch.zeros(16384, dtype=torch.int32, device=dev))}
 
 
 def use_ws(kind):
-    kernels._wide_ws[str(dev)] = WS[kind]["wide"]
+    kernels._decode_ws[str(dev)] = WS[kind]["decode"]
     kernels._mid_ws[str(dev)] = WS[kind]["mid"]
 
 

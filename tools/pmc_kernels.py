@@ -3,8 +3,8 @@ case each, cache-cold (weights rotate over >= 1.5 GB of copies):
 
   dec_gateup_m8   packed decode GEMM, gate_up + norm + SwiGLU, M = 8   (top kernel at 8 workers)
   dec_o_m8        packed decode GEMM, o_proj + residual, M = 8
-  wide_down_m32   small-batch packed GEMM, down + residual, M = 32
-  wide_down_m128  small-batch packed GEMM, down + residual, M = 128
+  mid_down_m32    mid-size packed GEMM, down + residual, M = 32
+  mid_down_m128   mid-size packed GEMM, down + residual, M = 128
   lib_down_m128   hipBLASLt (F.linear), down, M = 128
   attn_dec8       paged attention, 8 decode rows, ctx 1000, 256-key partitions
   attn_mix        paged attention, 64 decode rows (ctx 512) + 2 x 320 prefill
@@ -53,13 +53,13 @@ run(lambda i: kernels.decode_gemm(x, wp[i], "resid", resid=r), len(wp))
 del ws, wp
 torch.cuda.empty_cache()
 
-# down projection: small-batch packed kernel at M = 32 and 128, hipBLASLt at 128
+# down projection: mid-size packed kernel at M = 32 and 128, hipBLASLt at 128
 ws = copies(4096, 14336)
 wp = [kernels.pack_decode_weight(w) for w in ws]
 for M in (32, 128):
     xm = torch.randn(M, 14336, device="cuda").bfloat16()
     rm = torch.randn(M, 4096, device="cuda").bfloat16()
-    run(lambda i: kernels.wide_gemm(xm, wp[i], "resid", resid=rm), len(wp))
+    run(lambda i: kernels.mid_gemm(xm, wp[i], "resid", resid=rm), len(wp))
 run(lambda i: torch.nn.functional.linear(xm, ws[i]), len(ws))
 del ws, wp
 torch.cuda.empty_cache()

@@ -60,7 +60,7 @@ def emit(rec):
 
 
 def poison_ws():
-    kernels.wide_workspace(dev)[0].fill_(NAN)
+    kernels.decode_workspace(dev)[0].fill_(NAN)
     kernels.mid_workspace(dev)[0].fill_(NAN)
     kernels.prefill_workspace(dev)[0].fill_(NAN)
 
@@ -164,10 +164,7 @@ def gemm_case(M, N, K, epi, splits, kind, **cfg):
             else:
                 kernels.stream_workspace(dev)[0].fill_(NAN)
                 ops.stream_gemm(x, wp, epi, resid=r if epi == "resid" else None, out=out, norm=(epi == "silu"),
-                                plan=kw["plan"], rel=kw.get("rel", 0))
-        elif kind == "wide":
-            ops.wide_gemm(x, wp, epi, resid=r if epi == "resid" else None, out=out, norm=(epi == "silu"),
-                          splits=s, **kw)
+                                plan=kw["plan"], rel=kw.get("rel"))
         else:
             ops.mid_gemm(x, wp, epi, resid=r if epi == "resid" else None, out=out, norm=(epi == "silu"),
                          splits=s, **kw)
@@ -228,7 +225,6 @@ for M in (9, 16):
     cases.append((f"decode_down_resid M{M} S2 (engine)",
                   lambda M=M: gemm_case(M, 4096, 14336, "resid", 2, "decode", nt=2, waves=16)))
 cases.append(("decode_silu M12 S2", lambda: gemm_case(12, 2 * 14336, 4096, "silu", 2, "decode")))
-cases.append(("wide_down_resid M32 S8", lambda: gemm_case(32, 4096, 14336, "resid", 8, "wide")))
 cases.append(("mid_qkv_rope M32 fm1 fn2 S2 (engine)", lambda: qkv_rope_case(32, 2, mid=True, fm=1, fn=2)))
 for M, fm, fn, S in ((32, 1, 2, 4), (64, 1, 2, 2), (128, 2, 2, 2)):
     cases.append((f"mid_o_resid M{M} fm{fm} fn{fn} S{S} (engine)",
