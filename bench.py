@@ -94,6 +94,11 @@ def parse():
     ap.add_argument("--memory-min-batch", type=int, default=1,
                     help="lookups a pass waits for (up to --memory-wait-ms) before it starts")
     ap.add_argument("--memory-wait-ms", type=float, default=0.0)
+    ap.add_argument("--memory-gate-tokens", type=int, default=1024,
+                    help="start index passes beside engine steps of at least this many tokens (compute-bound), "
+                         "0 = as soon as lookups are pending")
+    ap.add_argument("--memory-gate-ms", type=float, default=30.0,
+                    help="latency cap of the gate: a lookup waits at most this long for such a step")
     ap.add_argument("--embed-pooling", default="last", choices=["mean", "last"],
                     help="--embedder engine: last-token states (embedding requests reuse the prefix cache: an "
                          "agent's successive lookups share the task text) or mean pooling (no reuse)")
@@ -165,6 +170,8 @@ async def run_rank(a, rank: int, world: int, device):
                                          pooling=a.embed_pooling)
     if memory is not None and a.embedder == "engine" and not a.cpu:
         eng.capture_embed_graphs()  # embedding requests: no first-use captures while timed
+    if lookup is not None and a.memory_gate_tokens > 0:
+        lookup.attach_engine(eng, gate_tokens=a.memory_gate_tokens, max_wait_s=a.memory_gate_ms / 1000.0)
     eng.start()
     llm = LocalLLM(LLMConfig(model_name=eng.model_cfg.name, temperature=a.temperature, max_tokens=1024,
                              retry_attempts=1), engine=eng)
@@ -261,7 +268,8 @@ async def run_rank(a, rank: int, world: int, device):
     freeze_heap()  # agents, serve and warm-up state: out of the timed region's GC passes
     await coll(comm.barrier)  # worker ranks keep serving the plane meanwhile
     st0 = dict(eng.stats)  # after the barrier: every rank's warmup work is behind it
-    mem0 = dict(lookup.stats, device_s=lookup.lookup_device_seconds()) if lookup is not None else None
+    mem0 = dict(lookup.stats, device_s=lookup.lookup_device_seconds(), nlat=len(lookup._lat)) \
+        if lookup is not None else None
     bh0 = {b: list(v) for b, v in eng.bucket_hist.items()}
     u0 = dict(llm.usage)
     n_timed0 = len(eng.timings)
@@ -303,6 +311,13 @@ async def run_rank(a, rank: int, world: int, device):
                "embed_token_share": round((st1["embed_tokens"] - st0["embed_tokens"]) /
                                           max(1, st1["tokens"] - st0["tokens"]), 4),
                "passes": lookup.stats["passes"] - mem0["passes"],
+               # co-scheduling with compute-bound engine steps (memory/batcher.py attach_engine)
+               "gate_tokens": a.memory_gate_tokens,
+               "passes_beside_heavy": lookup.stats["passes_beside_heavy"] - mem0["passes_beside_heavy"],
+               "passes_capped": lookup.stats["passes_capped"] - mem0["passes_capped"],
+               "beside_heavy_frac": round((lookup.stats["passes_beside_heavy"] - mem0["passes_beside_heavy"]) /
+                                          max(1, lookup.stats["passes"] - mem0["passes"]), 3),
+               **lookup.latency_summary(mem0["nlat"]),
                "stores": lookup.stats["stores"] - mem0["stores"],
                # HIP events around each pass on the lookup stream (includes any wait for
                # CUs the engine holds: an upper bound on the passes' kernel time)

@@ -25,6 +25,9 @@ int pa_sample(int* out_tokens, float* out_keys, float* workspace, const void* lo
               int V, int ld, int vocab_offset, const float* temperature, const int* mask_class,
               const uint32_t* class_masks, int mask_words, const int64_t* seeds,
               const int* offsets, const int* forced, const float* tau, hipStream_t st);
+int pa_tp_topkp_phase(int phase, float* tau, float* ws, const void* logits, int rows, int v_local, int ld,
+                      int vocab_offset, int V, const float* temperature, const int* top_k, const float* top_p,
+                      const int* mask_class, const uint32_t* class_masks, int mask_words, hipStream_t st);
 int pa_topkp_threshold(float* tau, const void* logits, int rows, int V, int ld, int shards,
                        long long shard_stride, const float* temperature, const int* top_k,
                        const float* top_p, const int* mask_class, const uint32_t* class_masks,
@@ -78,6 +81,9 @@ void* pa_car_alloc(long long bytes, void* handle_out);
 void* pa_car_open(const void* handle);
 int pa_car_close(void* p);
 int pa_car_free(void* p);
+int pa_car_collective(void* const* bases, int W, int rank0, int nranks_local, const void* const* ins,
+                      void* const* outs, long long n4, long long cap_bytes, uint32_t* epochs, int* err, int op,
+                      hipStream_t st);
 int pa_car_all_reduce(void* const* bases, int W, int rank0, int nranks_local, const void* const* ins,
                       void* const* outs, long long nelem, long long cap_bytes, uint32_t* epochs, int* err,
                       int two_shot, const void* const* resids, float* const* ss, float* const* ss_zero,
@@ -676,6 +682,34 @@ void cosine_topk(at::Tensor out_scores, at::Tensor out_rows, at::Tensor workspac
 
 }  // namespace
 
+// One phase of the vocab-parallel top-k / top-p threshold (sampling.hip tp_topkp_kernel):
+// logits [rows, v_local] is this rank's slice; ws [ceil4(rows) + rows * 1028] fp32 holds
+// mx | h0 | h1 | st.
+void tp_topkp_phase(int64_t phase, at::Tensor tau, at::Tensor ws, at::Tensor logits, int64_t vocab_offset,
+                    int64_t V, at::Tensor temperature, at::Tensor top_k, at::Tensor top_p, at::Tensor mask_class,
+                    at::Tensor class_masks) {
+  for (auto* t : {&tau, &ws, &temperature, &top_k, &top_p, &mask_class, &class_masks})
+    check_gpu(*t, "tp_topkp_phase arg");
+  TORCH_CHECK(logits.is_cuda() && logits.dim() == 2 && logits.stride(1) == 1, "logits: [rows, v_local] GPU");
+  check_dtype(tau, at::kFloat, "tau"); check_dtype(ws, at::kFloat, "ws"); check_dtype(logits, at::kBFloat16, "logits");
+  check_dtype(temperature, at::kFloat, "temperature"); check_dtype(top_k, at::kInt, "top_k");
+  check_dtype(top_p, at::kFloat, "top_p"); check_dtype(mask_class, at::kInt, "mask_class");
+  check_dtype(class_masks, at::kInt, "class_masks");
+  const int rows = logits.size(0), vl = logits.size(1);
+  TORCH_CHECK(ws.numel() >= (int64_t)((rows + 3) & ~3) + (int64_t)rows * 1028,
+              "ws must hold ceil4(rows) + rows * 1028 floats");
+  TORCH_CHECK(tau.numel() >= rows && temperature.numel() >= rows && top_k.numel() >= rows &&
+                  top_p.numel() >= rows && mask_class.numel() >= rows, "per-row tensors too short");
+  TORCH_CHECK(class_masks.dim() == 2 && class_masks.size(1) * 32 >= V && vocab_offset + vl <= V,
+              "class_masks / vocab slice");
+  check_rc(pa_tp_topkp_phase((int)phase, tau.data_ptr<float>(), ws.data_ptr<float>(), logits.data_ptr(), rows, vl,
+                             logits.stride(0), (int)vocab_offset, (int)V, temperature.data_ptr<float>(),
+                             top_k.data_ptr<int>(), top_p.data_ptr<float>(), mask_class.data_ptr<int>(),
+                             reinterpret_cast<const uint32_t*>(class_masks.data_ptr<int>()), class_masks.size(1),
+                             cur_stream()),
+           "tp_topkp_phase");
+}
+
 // tau[r] = top-k / top-p logit threshold of row r. `logits` is [rows, V] or a TP
 // all-gather [shards, rows, V/shards] (then V is the full vocabulary).
 void topkp_threshold(at::Tensor tau, at::Tensor logits, int64_t V, at::Tensor temperature,
@@ -781,6 +815,40 @@ void car_all_reduce(std::vector<int64_t> bases, int64_t rank0, std::vector<at::T
            "custom all-reduce");
 }
 
+// Small collectives over the custom all-reduce buffers (custom_ar.hip co_kernel): op 0 = SUM
+// and 1 = MAX of fp32 (outs may alias ins), 2 = all-gather of any 4-byte dtype (outs[i] holds
+// W x n elements, rank-major). n % 4 == 0, 16-byte aligned tensors.
+void car_collective(std::vector<int64_t> bases, int64_t rank0, std::vector<at::Tensor> ins,
+                    std::vector<at::Tensor> outs, int64_t cap_bytes, at::Tensor epochs, at::Tensor err, int64_t op) {
+  const int W = (int)bases.size();
+  const int nl = (int)ins.size();
+  TORCH_CHECK(W >= 2 && W <= 8, "custom collectives support 2..8 ranks");
+  TORCH_CHECK(nl >= 1 && (int)outs.size() == nl && rank0 >= 0 && rank0 + nl <= W, "bad rank range");
+  TORCH_CHECK(op >= 0 && op <= 2, "op: 0 sum, 1 max, 2 gather");
+  const int64_t n = ins[0].numel();
+  std::vector<void*> b(W), ip(nl), opp(nl);
+  for (int i = 0; i < W; ++i) b[i] = (void*)(uintptr_t)bases[i];
+  for (int i = 0; i < nl; ++i) {
+    check_gpu(ins[i], "in"); check_gpu(outs[i], "out");
+    TORCH_CHECK(ins[i].element_size() == 4 && outs[i].element_size() == 4, "4-byte elements");
+    if (op < 2) {
+      check_dtype(ins[i], at::kFloat, "in"); check_dtype(outs[i], at::kFloat, "out");
+    }
+    TORCH_CHECK(ins[i].numel() == n && outs[i].numel() == (op == 2 ? n * W : n), "collective tensor sizes");
+    TORCH_CHECK(((uintptr_t)ins[i].data_ptr() & 15) == 0 && ((uintptr_t)outs[i].data_ptr() & 15) == 0,
+                "collective tensors must be 16-byte aligned");
+    ip[i] = ins[i].data_ptr(); opp[i] = outs[i].data_ptr();
+  }
+  TORCH_CHECK(n % 4 == 0 && n * 4 <= cap_bytes, "message of ", n, " x 4 B does not fit the custom buffers");
+  check_gpu(epochs, "epochs"); check_dtype(epochs, at::kInt, "epochs");
+  TORCH_CHECK(epochs.numel() >= (int64_t)nl * pa_car_group(), "epochs too short");
+  check_gpu(err, "err"); check_dtype(err, at::kInt, "err");
+  check_rc(pa_car_collective(b.data(), W, (int)rank0, nl, ip.data(), opp.data(), n, cap_bytes,
+                             reinterpret_cast<uint32_t*>(epochs.data_ptr<int>()), err.data_ptr<int>(), (int)op,
+                             cur_stream()),
+           "custom collective");
+}
+
 // ---- uncached device memory (in-launch hand-off workspaces) ----
 // Split-K slabs and attention partials are written by one workgroup and read by another
 // inside the same launch. In uncached memory (MTYPE UC: no L1/L2 copy of any line) a reader
@@ -873,6 +941,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("class_masks"), py::arg("seeds"), py::arg("offsets"), py::arg("forced"),
         py::arg("tau") = py::none());
   m.def("topkp_threshold", &topkp_threshold);
+  m.def("tp_topkp_phase", &tp_topkp_phase);
   m.def("cosine_topk_workspace_bytes", &cosine_topk_workspace_bytes);
   m.def("cosine_topk", &cosine_topk);
   m.def("car_alloc", &car_alloc);
@@ -883,6 +952,8 @@ PYBIND11_MODULE(_C, m) {
         py::arg("cap_bytes"), py::arg("epochs"), py::arg("err"), py::arg("two_shot"),
         py::arg("resids") = std::vector<at::Tensor>(), py::arg("ss") = std::vector<at::Tensor>(),
         py::arg("ss_zero") = std::vector<at::Tensor>(), py::arg("row_len") = 0);
+  m.def("car_collective", &car_collective, py::arg("bases"), py::arg("rank0"), py::arg("ins"), py::arg("outs"),
+        py::arg("cap_bytes"), py::arg("epochs"), py::arg("err"), py::arg("op"));
   m.def("car_group", &pa_car_group);
   m.def("car_flag_bytes", &pa_car_flag_bytes);
   m.attr("ATT_PART") = 512;

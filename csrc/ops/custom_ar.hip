@@ -233,6 +233,59 @@ __global__ __launch_bounds__(AR_THREADS) void ar_kernel(ArPeers P, ArIO io, int 
   if (t == 0) *ep_slot = ep;
 }
 
+// ---------------------------------------------------------------------------------------
+// Small collectives of the TP step graph on the same buffers, flags and epochs (VERDICT r4
+// item 4: no RCCL call inside a captured graph): the sampler's all-gather of per-shard winners
+// (keys, token ids) and the top-k / top-p threshold's MAX / SUM all-reduces of fp32 row maxima
+// and radix histograms. One-shot: stage, one cross-rank barrier, every rank reads every
+// peer's chunk. Elements are 4 bytes moved as 16-byte vectors; SUM adds in rank order, so
+// every rank holds bit-identical results. Sharing the epochs with ar_kernel keeps the
+// parity argument above: a workgroup's calls, of any kind, alternate parities in one order.
+enum { CO_SUM_F32 = 0, CO_MAX_F32 = 1, CO_GATHER = 2 };
+
+template <int W, int OP>
+__global__ __launch_bounds__(AR_THREADS) void co_kernel(ArPeers P, ArIO io, int rank0, long long nvec,
+                                                         long long cap_vec, uint32_t* epochs, int* err) {
+  const int b = blockIdx.x, t = threadIdx.x;
+  const int rank = rank0 + blockIdx.y;
+  const u32x4* in = io.in[blockIdx.y];
+  u32x4* out = io.out[blockIdx.y];
+  uint32_t* ep_slot = epochs + blockIdx.y * AR_G + b;
+  const uint32_t ep = *ep_slot + 1;
+  const long long par_off = (long long)(ep & 1) * cap_vec;
+  const long long nchunk = (nvec + AR_VPB - 1) / AR_VPB;
+  auto data = [&](int r) { return reinterpret_cast<u32x4*>(P.base[r] + AR_FLAG_BYTES) + par_off; };
+  u32x4* mine = data(rank);
+  for (long long c = b; c < nchunk; c += AR_G) {
+    const long long v = c * AR_VPB + t;
+    if (v < nvec) __builtin_nontemporal_store(in[v], mine + v);
+  }
+  ar_stores_done();
+  __syncthreads();
+  ar_signal_wait(P, rank, W, b, 0, ep, err);
+  for (long long c = b; c < nchunk; c += AR_G) {
+    const long long v = c * AR_VPB + t;
+    if (v >= nvec) continue;
+    u32x4 x[W];
+#pragma unroll
+    for (int r = 0; r < W; ++r) x[r] = __builtin_nontemporal_load(data(r) + v);
+    if constexpr (OP == CO_GATHER) {
+#pragma unroll
+      for (int r = 0; r < W; ++r) out[(long long)r * nvec + v] = x[r];
+    } else {
+      f32x4 a = __builtin_bit_cast(f32x4, x[0]);
+#pragma unroll
+      for (int r = 1; r < W; ++r) {
+        const f32x4 y = __builtin_bit_cast(f32x4, x[r]);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) a[i] = OP == CO_SUM_F32 ? a[i] + y[i] : fmaxf(a[i], y[i]);
+      }
+      out[v] = __builtin_bit_cast(u32x4, a);
+    }
+  }
+  if (t == 0) *ep_slot = ep;
+}
+
 }  // namespace pa
 
 using namespace pa;
@@ -325,6 +378,49 @@ int pa_car_all_reduce(void* const* bases, int W, int rank0, int nranks_local, co
   }
 #undef AR_LAUNCH
 #undef AR_KERN
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// Small collectives (co_kernel): n4 4-byte elements per rank (a multiple of 4), op CO_*; for
+// CO_GATHER outs[i] receives W x n4 elements (rank-major). Same buffers / epochs / err as
+// pa_car_all_reduce, so the two kinds of call may be interleaved in any order every rank shares.
+int pa_car_collective(void* const* bases, int W, int rank0, int nranks_local, const void* const* ins,
+                      void* const* outs, long long n4, long long cap_bytes, uint32_t* epochs, int* err, int op,
+                      hipStream_t st) {
+  if (W < 2 || W > AR_MAXW || n4 <= 0 || n4 % 4 || n4 * 4 > cap_bytes || nranks_local < 1 ||
+      rank0 + nranks_local > W || op < CO_SUM_F32 || op > CO_GATHER)
+    return -1;
+  ArPeers P;
+  for (int i = 0; i < AR_MAXW; ++i) P.base[i] = i < W ? (char*)bases[i] : nullptr;
+  ArIO io{};
+  for (int i = 0; i < AR_MAXW; ++i) {
+    const bool on = i < nranks_local;
+    io.in[i] = on ? (const u32x4*)ins[i] : nullptr;
+    io.out[i] = on ? (u32x4*)outs[i] : nullptr;
+  }
+  const long long nvec = n4 / 4, cap_vec = cap_bytes / 16;
+  dim3 grid(AR_G, nranks_local);
+#define CO_KERN(WW, OO) \
+  hipLaunchKernelGGL((co_kernel<WW, OO>), grid, dim3(AR_THREADS), 0, st, P, io, rank0, nvec, cap_vec, epochs, err)
+#define CO_LAUNCH(WW)                                  \
+  case WW:                                             \
+    if (op == CO_SUM_F32) CO_KERN(WW, CO_SUM_F32);     \
+    else if (op == CO_MAX_F32) CO_KERN(WW, CO_MAX_F32); \
+    else CO_KERN(WW, CO_GATHER);                       \
+    break;
+  switch (W) {
+    CO_LAUNCH(2)
+    CO_LAUNCH(3)
+    CO_LAUNCH(4)
+    CO_LAUNCH(5)
+    CO_LAUNCH(6)
+    CO_LAUNCH(7)
+    CO_LAUNCH(8)
+    default:
+      return -1;
+  }
+#undef CO_LAUNCH
+#undef CO_KERN
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -29,9 +29,10 @@
 //     on a per-group counter and waits for the others (all S slices of a group are resident:
 //     the grid is at most one workgroup per CU), then reduces 1/S of the group's fragments
 //     and runs the epilogue on them (RMSNorm row scale, SwiGLU, residual + the next norm's row
-//     statistics, RoPE + paged KV write: packed_epi.h). Publish = sc1 slab stores, every
-//     wave's vmcnt(0), the workgroup barrier, one lane's agent-scope release + drain, relaxed
-//     arrive; consume = relaxed poll, agent-scope acquire + drain, barrier, sc1 loads. A
+//     statistics, RoPE + paged KV write: packed_epi.h). Publish = 16-B sc1 slab stores, every
+//     wave's vmcnt(0), the workgroup barrier, one lane's relaxed agent-scope arrive (optionally
+//     behind an agent release, rel bit 0); consume = relaxed poll, agent-scope acquire + drain,
+//     barrier, sc1 loads (MI355X_MICROARCH.md hand-off table row 1, plus the acquire). A
 //     departure counter resets both counters, so they are zero between launches (hipGraph
 //     replay safe). Every spin is bounded: a timed-out group barrier sets the err word, which
 //     the engine reads back with every step and fails on (LLMEngine._health_check).
@@ -74,11 +75,10 @@ struct Args {
   const int* slots;
   const float* cos_sin;
   int H, KV;
-  // bit 0: agent-scope release (buffer_wbl2 sc1 + drain) before arriving -- the host's default
-  // (ops.STREAM_REL): the LLVM AMDGPU memory model's agent-scope release, which waits for the
-  // write-through slab stores to complete at memory; without it the arrive can overtake them
-  // (round 4: 5 of 10,000 poisoned decode runs). bit 1: each workgroup starts its K slice at a
-  // different chunk (rotated order; HBM channel spread)
+  // bit 0: agent-scope release (buffer_wbl2 sc1 + drain) before arriving (off by default:
+  // ops.STREAM_REL -- the sc1 form below passed 1.2M poisoned repetitions and the release costs
+  // 2.5-5 us per launch); bit 1: each workgroup starts its K slice at a different chunk
+  // (rotated order; HBM channel spread)
   int rel;
   // diagnostics (null in the engine): per workgroup 8 wall-clock stamps (s_memrealtime, 100 MHz):
   // [0] start, [1] first chunk in LDS, [2] main loop done, [3] group barrier passed, [4] end

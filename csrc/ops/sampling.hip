@@ -227,7 +227,174 @@ __global__ __launch_bounds__(TKP_THREADS) void topkp_threshold_kernel(
   if (threadIdx.x == 0) tau[row] = order_key_value(prefix);
 }
 
+// ---------------------------------------------------------------------------
+// The same threshold for a vocab-parallel LM head (TP > 1) without gathering the logits: each
+// rank runs the passes on its own V/tp slice and the group combines the partial results
+// between them with the custom P2P collectives (parallel/custom_ar.py; no RCCL in the step
+// graph). Histograms ADD across shards, maxima MAX, so every rank ends with the tau the
+// single-GPU kernel computes on the whole row:
+//   phase 0  mx[row]            = max allowed logit of the slice         -> MAX over ranks
+//   phase 1  h0[row][0:256/256:512] = (count, mass) per high byte         -> SUM over ranks
+//   phase 2  scan h0 (identical on every rank) -> st[row] = (hi, count / mass above hi, total);
+//            h1[row] = (count, mass) per low byte inside bin hi          -> SUM over ranks
+//   phase 3  scan h1 with the carries -> tau[row]
+// mass = exp2((logit - mx) * log2(e) / T) of the allowed tokens (as the single-GPU kernel).
+struct TkpArgs {
+  const uint16_t* logits;  // [rows, ld] this rank's slice (v_local valid columns)
+  int v_local, ld, vocab_offset, V;
+  const float* temperature;
+  const int* top_k;
+  const float* top_p;
+  const int* mask_class;
+  const uint32_t* class_masks;
+  int mask_words;
+  float* mx;   // [rows]
+  float* h0;   // [rows, 512]
+  float* h1;   // [rows, 512]
+  float* st;   // [rows, 4]
+  float* tau;  // [rows]
+};
+
+__device__ __forceinline__ bool tkp_active(const TkpArgs& A, int row) {
+  const int k = A.top_k[row];
+  const float p = A.top_p[row];
+  return A.temperature[row] > 0.f && !((k <= 0 || k >= A.V) && !(p < 1.f));
+}
+
+// top-down scan of 256 (count, mass) bins (thread 0): the highest bin where the count or the
+// mass from the top reaches its need (bin 0 if none), and the count / mass strictly above it
+__device__ __forceinline__ int tkp_scan(const float* cnt, const float* mass, float need_cnt, float need_mass,
+                                        float* c_io, float* m_io) {
+  float c = *c_io, m = *m_io;
+  int sel = 0;
+  for (int b = 255; b >= 0; --b) {
+    const float c2 = c + cnt[b], m2 = m + mass[b];
+    if (c2 >= need_cnt || m2 >= need_mass) { sel = b; break; }
+    c = c2; m = m2;
+    sel = b;
+  }
+  *c_io = c;
+  *m_io = m;
+  return sel;
+}
+
+template <int PHASE>
+__global__ __launch_bounds__(TKP_THREADS) void tp_topkp_kernel(const TkpArgs A) {
+  const int row = blockIdx.x;
+  const bool act = tkp_active(A, row);
+  const int mc = A.mask_class[row];
+  const uint16_t* lr = A.logits + (size_t)row * A.ld;
+  auto allowed = [&](int li) -> bool {
+    if (mc < 0) return true;
+    const int g = A.vocab_offset + li;
+    return (A.class_masks[(size_t)mc * A.mask_words + (g >> 5)] >> (g & 31)) & 1u;
+  };
+  __shared__ float s_cnt[256], s_mass[256];
+  __shared__ float red[TKP_THREADS / 64];
+  if constexpr (PHASE == 0) {
+    float m = -INFINITY;
+    if (act)
+      for (int li = threadIdx.x; li < A.v_local; li += TKP_THREADS)
+        if (allowed(li)) m = fmaxf(m, order_key_value(bf16_order_key(lr[li])));
+    m = wave_max(m);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      float r = red[0];
+      for (int w = 1; w < TKP_THREADS / 64; ++w) r = fmaxf(r, red[w]);
+      A.mx[row] = r;
+    }
+    return;
+  }
+  if constexpr (PHASE == 3) {
+    if (threadIdx.x == 0) {
+      const float* st = A.st + (size_t)row * 4;
+      float tau = -INFINITY;
+      if (act && A.mx[row] > -INFINITY) {
+        const int k = A.top_k[row];
+        const float p = A.top_p[row];
+        const float need_mass = p < 1.f ? p * st[3] : INFINITY;
+        const float need_cnt = (k > 0 && k < A.V) ? (float)k : INFINITY;
+        float c = st[1], m = st[2];
+        const float* h = A.h1 + (size_t)row * 512;
+        const int lo = tkp_scan(h, h + 256, need_cnt, need_mass, &c, &m);
+        tau = order_key_value(((uint32_t)st[0] << 8) | (uint32_t)lo);
+      }
+      A.tau[row] = tau;
+    }
+    return;
+  }
+  // phases 1 and 2: a histogram of this slice
+  if (threadIdx.x < 256) { s_cnt[threadIdx.x] = 0.f; s_mass[threadIdx.x] = 0.f; }
+  __shared__ int s_hi;
+  const float mx = A.mx[row];
+  const bool live = act && mx > -INFINITY;
+  if constexpr (PHASE == 2) {
+    if (threadIdx.x == 0) {
+      int hi = 0;
+      float c = 0.f, m = 0.f, total = 0.f;
+      if (live) {
+        const float* h = A.h0 + (size_t)row * 512;
+        for (int b = 0; b < 256; ++b) total += h[256 + b];
+        const int k = A.top_k[row];
+        const float p = A.top_p[row];
+        const float need_mass = p < 1.f ? p * total : INFINITY;
+        const float need_cnt = (k > 0 && k < A.V) ? (float)k : INFINITY;
+        hi = tkp_scan(h, h + 256, need_cnt, need_mass, &c, &m);
+      }
+      float* st = A.st + (size_t)row * 4;
+      st[0] = (float)hi;
+      st[1] = c;
+      st[2] = m;
+      st[3] = total;
+      s_hi = hi;
+    }
+  }
+  __syncthreads();
+  if (live) {
+    const float invT_log2 = 1.4426950408889634f / A.temperature[row];
+    const int hi = PHASE == 2 ? s_hi : -1;
+    for (int li = threadIdx.x; li < A.v_local; li += TKP_THREADS) {
+      if (!allowed(li)) continue;
+      const uint32_t kk = bf16_order_key(lr[li]);
+      if (PHASE == 2 && (int)(kk >> 8) != hi) continue;
+      const int bin = PHASE == 1 ? (int)(kk >> 8) : (int)(kk & 0xff);
+      atomicAdd(&s_cnt[bin], 1.f);
+      atomicAdd(&s_mass[bin], exp2f((order_key_value(kk) - mx) * invT_log2));
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < 256) {
+    float* h = (PHASE == 1 ? A.h0 : A.h1) + (size_t)row * 512;
+    h[threadIdx.x] = s_cnt[threadIdx.x];
+    h[256 + threadIdx.x] = s_mass[threadIdx.x];
+  }
+}
+
 }  // namespace pa
+
+// TP top-k / top-p threshold, one phase per call (the caller combines mx / h0 / h1 over the TP
+// group between phases). ws: [ceil4(rows) + rows * 1028] floats: mx | h0 | h1 | st.
+extern "C" int pa_tp_topkp_phase(int phase, float* tau, float* ws, const void* logits, int rows, int v_local,
+                                 int ld, int vocab_offset, int V, const float* temperature, const int* top_k,
+                                 const float* top_p, const int* mask_class, const uint32_t* class_masks,
+                                 int mask_words, hipStream_t st) {
+  if (rows <= 0) return 0;
+  if (phase < 0 || phase > 3 || v_local <= 0 || ld < v_local) return -1;
+  // mx is padded to a multiple of 4 rows, so every segment the TP group reduces starts 16-byte
+  // aligned and holds a multiple of 4 floats (the custom collectives move 16-byte vectors)
+  const size_t r4 = ((size_t)rows + 3) & ~(size_t)3;
+  pa::TkpArgs a{(const uint16_t*)logits, v_local, ld, vocab_offset, V, temperature, top_k, top_p, mask_class,
+                class_masks, mask_words, ws, ws + r4, ws + r4 + (size_t)rows * 512, ws + r4 + (size_t)rows * 1024,
+                tau};
+  switch (phase) {
+    case 0: hipLaunchKernelGGL(pa::tp_topkp_kernel<0>, dim3(rows), dim3(pa::TKP_THREADS), 0, st, a); break;
+    case 1: hipLaunchKernelGGL(pa::tp_topkp_kernel<1>, dim3(rows), dim3(pa::TKP_THREADS), 0, st, a); break;
+    case 2: hipLaunchKernelGGL(pa::tp_topkp_kernel<2>, dim3(rows), dim3(pa::TKP_THREADS), 0, st, a); break;
+    default: hipLaunchKernelGGL(pa::tp_topkp_kernel<3>, dim3(rows), dim3(pa::TKP_THREADS), 0, st, a); break;
+  }
+  return (int)hipGetLastError();
+}
 
 extern "C" int pa_topkp_threshold(float* tau, const void* logits, int rows, int V, int ld, int shards,
                                   long long shard_stride, const float* temperature, const int* top_k,

@@ -297,13 +297,20 @@ class LLMEngine:
         self._mask_version = -1
         self._sync_masks()
         S = cfg.max_num_seqs
-        self._sampled_dev = torch.zeros(S, dtype=torch.int32, device=self.device)
+        S4 = (S + 3) & ~3  # the TP winners' all-gather moves 16-byte vectors (custom_ar.hip co_kernel)
+        self._sampled_dev = torch.zeros(S4, dtype=torch.int32, device=self.device)
         self._sampled_hosts = [torch.zeros(S, dtype=torch.int32, pin_memory=pin) for _ in range(nbuf)]
         self._sampled_host = self._sampled_hosts[0]
         self._inflight: "deque" = deque()  # launched, not yet committed steps (pipelined mode)
         self._slot = 0
         self._last_done = 0.0
-        self._keys_dev = torch.zeros(S, dtype=torch.float32, device=self.device)
+        self._keys_dev = torch.zeros(S4, dtype=torch.float32, device=self.device)
+        # TP top-k / top-p: workspace of the HIP phase kernels (engine/tp_sampling.py)
+        self._tkp_ws = None
+        if self.tp.size > 1 and self.on_gpu:
+            from .tp_sampling import tkp_ws_floats
+
+            self._tkp_ws = torch.empty(tkp_ws_floats(S), dtype=torch.float32, device=self.device)
         # embedding requests: per-request pooling rows (+ one row that collects every other
         # token), summed in the step graph, read and cleared when the request finishes
         self._embed_pool = torch.zeros(L["max_seqs"] + 1, mc.hidden_size, dtype=torch.float32, device=self.device)
@@ -327,6 +334,11 @@ class LLMEngine:
         self._tau = torch.empty(S, dtype=torch.float32, device=self.device)
         self._graph_pool = None
         self.use_graphs = cfg.use_graphs and self.on_gpu
+        if self.use_graphs and self.tp.size > 1 and getattr(self.tp, "custom", None) is None:
+            # a TP step graph would capture RCCL collectives; every TP collective of a step
+            # (activations, sampling winners, threshold histograms) needs the custom P2P path
+            log.warning("TP=%d without the custom P2P collectives: running the steps eagerly", self.tp.size)
+            self.use_graphs = False
         self.is_driver = self.tp.rank == 0
         self._tp_header = torch.zeros(9, dtype=torch.int64)
         self._tp_closed = False
@@ -349,6 +361,9 @@ class LLMEngine:
                       "bucket_tokens": 0, "host_sched_s": 0.0, "host_launch_s": 0.0, "device_wait_s": 0.0,
                       "host_commit_s": 0.0, "host_deliver_s": 0.0}
         self.bucket_hist: Dict[int, list] = {}  # bucket -> [steps, seconds]
+        # called on the engine thread right after a step is launched with its token count (the
+        # memory batcher co-schedules its index scans with compute-bound steps, memory/batcher.py)
+        self._step_listeners: List[Callable[[int], None]] = []
         # custom all-reduce health: its spin-waits give up after ~5 s and set an error word
         # instead of hanging; the word is copied back with every step and checked after the
         # step's synchronize, failing the engine rather than continuing on partial sums
@@ -439,7 +454,8 @@ class LLMEngine:
             else:
                 tau = tp_topkp_threshold(logits, self.model.vocab_offset, self.model_cfg.vocab_size,
                                          self._temp[:s_b], self._top_k[:s_b], self._top_p[:s_b],
-                                         self._mask_cls[:s_b], self._class_masks, self.tp, out=self._tau[:s_b])
+                                         self._mask_cls[:s_b], self._class_masks, self.tp, out=self._tau[:s_b],
+                                         ws=self._tkp_ws)
         if self.tp.size == 1:
             ops.sample(logits, self._temp[:s_b], self._mask_cls[:s_b], self._class_masks,
                        self._seeds[:s_b], self._offsets[:s_b], self._forced[:s_b],
@@ -451,8 +467,9 @@ class LLMEngine:
                        self._seeds[:s_b], self._offsets[:s_b], self._forced[:s_b],
                        out=self._sampled_dev[:s_b], workspace=self._sample_ws,
                        vocab_offset=self.model.vocab_offset, out_keys=self._keys_dev[:s_b], tau=tau)
-            keys = self.tp.all_gather(self._keys_dev[:s_b])        # [tp, s_b]
-            toks = self.tp.all_gather(self._sampled_dev[:s_b])     # [tp, s_b]
+            s4 = (s_b + 3) & ~3  # whole 16-byte vectors for the custom all-gather
+            keys = self.tp.all_gather(self._keys_dev[:s4])[:, :s_b]        # [tp, s_b]
+            toks = self.tp.all_gather(self._sampled_dev[:s4])[:, :s_b]     # [tp, s_b]
             best = keys.argmax(0, keepdim=True)
             self._sampled_dev[:s_b].copy_(toks.gather(0, best).squeeze(0))
 
@@ -553,6 +570,18 @@ class LLMEngine:
         self._inbox.put(req)
         self._wake.set()
         return rid
+
+    def add_step_listener(self, fn: Callable[[int], None]):
+        """fn(tokens) runs on the engine thread right after each step is launched (keep it cheap:
+        e.g. loop.call_soon_threadsafe). The kind of step the device is about to run."""
+        self._step_listeners.append(fn)
+
+    def _notify_launch(self, T: int):
+        for fn in self._step_listeners:
+            try:
+                fn(T)
+            except Exception:  # noqa: BLE001 -- a listener must not stop the engine
+                log.exception("step listener failed")
 
     def abort(self, rid: int):
         self._aborts.put(rid)
@@ -841,6 +870,8 @@ class LLMEngine:
             self.tp.broadcast(self._dev_meta[:n_copy])
         with torch.inference_mode(), trace_range("engine.forward"):
             self._run(bucket, ns, trunc, n_copy, embed)
+        if self._step_listeners:
+            self._notify_launch(T)
         if nsamp:
             self._sampled_host[:nsamp].copy_(self._sampled_dev[:nsamp], non_blocking=self.on_gpu)
         self._health_fetch()
@@ -919,6 +950,8 @@ class LLMEngine:
         self._dev_meta[:n_copy].copy_(hm[:n_copy], non_blocking=self.on_gpu)
         with torch.inference_mode(), trace_range("engine.forward"):
             self._run(bucket, ns, trunc, n_copy, embed)
+        if self._step_listeners:
+            self._notify_launch(T)
         if nsamp:
             self._sampled_hosts[slot][:nsamp].copy_(self._sampled_dev[:nsamp], non_blocking=self.on_gpu)
         if embed:

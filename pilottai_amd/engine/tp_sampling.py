@@ -11,7 +11,8 @@ and every rank runs the identical scan: the same kept set as the single-GPU kern
 gathered logits, for ~4 KB per row of traffic instead of the 2 x V bytes per row an all-gather
 of the logits moves (Llama-3: 256 KB per row at TP = 8).
 
-All operations are shape-static torch ops plus collectives, so the step graph captures them.
+On the GPU the passes are HIP kernels and the collectives run on the custom P2P buffers
+(capturable, no RCCL in a step graph); on the CPU the same algorithm runs as torch ops.
 """
 from __future__ import annotations
 
@@ -57,12 +58,42 @@ def _scan(cnt: torch.Tensor, mass: torch.Tensor, need_cnt: torch.Tensor, need_ma
     return sel, c_above, m_above
 
 
+def tkp_ws_floats(rows: int) -> int:
+    """Workspace of the HIP phase kernels: mx (padded to 4 rows) | h0 | h1 | scan state."""
+    return ((rows + 3) & ~3) + rows * 1028
+
+
 def tp_topkp_threshold(logits: torch.Tensor, vocab_offset: int, V: int, temperature, top_k, top_p,
-                       mask_class, class_masks, tp, out: torch.Tensor = None) -> torch.Tensor:
+                       mask_class, class_masks, tp, out: torch.Tensor = None,
+                       ws: torch.Tensor = None) -> torch.Tensor:
     """tau[row] for this rank's logit slice [rows, V / tp] (bf16): the threshold the single-GPU
     kernel computes on the whole vocabulary. Collective over the TP group `tp`
-    (TPGroup: all_reduce_max / all_reduce_sum over fp32)."""
+    (TPGroup: all_reduce_max / all_reduce_sum over fp32; on GPUs the custom P2P buffers, so a
+    captured step graph holds no RCCL call). On the GPU: four launches of the HIP phase kernel
+    (csrc/ops/sampling.hip tp_topkp_kernel: row max, high-byte histogram, scan + low-byte
+    histogram, scan) with a MAX and two SUM all-reduces between them; `ws` (>= tkp_ws_floats(rows)
+    fp32, allocate outside capture) is their workspace. CPU: the same algorithm as torch ops."""
     rows, vl = logits.shape
+    if logits.is_cuda:
+        from pilottai_amd.ops.kernels import require_native
+
+        C = require_native()
+        tau = out if out is not None else torch.empty(rows, dtype=torch.float32, device=logits.device)
+        if ws is None:
+            ws = torch.empty(tkp_ws_floats(rows), dtype=torch.float32, device=logits.device)
+        args = (logits, int(vocab_offset), int(V), temperature, top_k, top_p, mask_class, class_masks)
+        r4 = (rows + 3) & ~3
+        mx = ws[:r4]
+        h0 = ws[r4:r4 + rows * 512]
+        h1 = ws[r4 + rows * 512:r4 + rows * 1024]
+        C.tp_topkp_phase(0, tau, ws, *args)
+        tp.all_reduce_max(mx)
+        C.tp_topkp_phase(1, tau, ws, *args)
+        tp.all_reduce_sum(h0)
+        C.tp_topkp_phase(2, tau, ws, *args)
+        tp.all_reduce_sum(h1)
+        C.tp_topkp_phase(3, tau, ws, *args)
+        return tau
     dev = logits.device
     T = temperature[:rows].float()
     k = top_k[:rows]

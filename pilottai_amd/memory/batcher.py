@@ -16,6 +16,15 @@ the same way.
 `stats` reports lookups, passes and the device time of the passes (HIP events around
 the kernel on the index's own stream; beside a busy engine that span also contains any
 wait for CUs the engine holds, so it bounds the kernel time from above).
+
+Co-scheduling with the engine (`attach_engine`): a 205-GB index pass is a
+streaming read that halves the speed of the engine's memory-bound (decode-sized) steps but
+costs a compute-bound 2,048-token prefill step only ~6 % (BENCHMARKS.md, config 4). The engine
+announces every step it launches (LLMEngine.add_step_listener); with a gate attached, a pass
+whose queries are embedded waits until the engine launches a step of at least `gate_tokens`
+tokens -- or until its oldest lookup has waited `gate_max_wait_s` -- and then starts right
+behind that launch, so the scan overlaps compute-bound work. `stats` counts the passes that
+started beside such a step and the ones the latency cap released.
 """
 from __future__ import annotations
 
@@ -45,7 +54,55 @@ class MemoryLookupBatcher:
         if time_device and getattr(getattr(memory.index, "device", None), "type", "cpu") == "cuda":
             memory.index.pass_events = []  # the index records (start, end) around each pass
         self.stats = {"lookups": 0, "passes": 0, "stores": 0, "store_batches": 0, "host_s": 0.0,
-                      "device_s": 0.0, "max_batch_seen": 0}
+                      "device_s": 0.0, "max_batch_seen": 0, "passes_beside_heavy": 0, "passes_capped": 0,
+                      "gate_wait_s": 0.0}
+        self._gate_tokens = 0
+        self._gate_wait = 0.0
+        self._heavy: Optional[asyncio.Event] = None
+        self._last_heavy = 0.0
+        self._lat: List[float] = []  # per-lookup latency (s), for p50 / p99
+
+    # ----------------------------------------------------------------- engine gate
+    def attach_engine(self, engine, gate_tokens: int = 1024, max_wait_s: float = 0.03):
+        """Co-schedule index passes with the engine's compute-bound steps (module docstring).
+        Call from the event loop that runs the lookups."""
+        loop = asyncio.get_running_loop()
+        self._heavy = asyncio.Event()
+        self._gate_tokens = int(gate_tokens)
+        self._gate_wait = float(max_wait_s)
+
+        def on_launch(T: int):
+            if T >= self._gate_tokens:
+                loop.call_soon_threadsafe(self._mark_heavy)
+        engine.add_step_listener(on_launch)
+
+    def _mark_heavy(self):
+        self._last_heavy = time.perf_counter()
+        self._heavy.set()
+
+    async def _await_heavy(self, oldest: float):
+        """Return once a heavy step was just launched (within 2 ms), or at the latency cap."""
+        t0 = time.perf_counter()
+        if t0 - self._last_heavy < 0.002:
+            self.stats["passes_beside_heavy"] += 1
+            return
+        self._heavy.clear()
+        left = self._gate_wait - (t0 - oldest)
+        try:
+            if left <= 0:
+                raise asyncio.TimeoutError
+            await asyncio.wait_for(self._heavy.wait(), left)
+            self.stats["passes_beside_heavy"] += 1
+        except asyncio.TimeoutError:
+            self.stats["passes_capped"] += 1
+        self.stats["gate_wait_s"] += time.perf_counter() - t0
+
+    def latency_summary(self, since: int = 0) -> dict:
+        lat = sorted(self._lat[since:])
+        if not lat:
+            return {}
+        pick = lambda q: round(1000 * lat[min(len(lat) - 1, int(q * len(lat)))], 2)  # noqa: E731
+        return {"lookup_p50_ms": pick(0.5), "lookup_p99_ms": pick(0.99), "lookups": len(lat)}
 
     # ----------------------------------------------------------------- API
     async def search(self, query: str, limit: int = 5, tags: Optional[Set[str]] = None,
@@ -115,9 +172,16 @@ class MemoryLookupBatcher:
             limit = max(b[3] for b in batch)
             t0 = time.perf_counter()
             try:
-                hits = await self.memory.search_batch([b[0] for b in batch], tags=[b[1] for b in batch],
-                                                      min_priority=[b[2] for b in batch], limit=limit)
+                qs = [b[0] for b in batch]
+                vecs = None
+                if self._heavy is not None:  # embed now, scan beside the next compute-bound step
+                    vecs = await self.memory.embed_queries(qs)
+                    await self._await_heavy(min(b[5] for b in batch))
+                hits = await self.memory.search_batch(qs, tags=[b[1] for b in batch],
+                                                      min_priority=[b[2] for b in batch], limit=limit, vecs=vecs)
+                now = time.perf_counter()
                 for b, h in zip(batch, hits):
+                    self._lat.append(now - b[5])
                     if not b[4].done():
                         b[4].set_result(h[: b[3]])
             except Exception as e:  # noqa: BLE001

@@ -123,9 +123,17 @@ class EnhancedMemory:
         res = await self.search_batch([query], tags=[tags], min_priority=[min_priority], limit=limit, mode=mode)
         return res[0]
 
+    async def embed_queries(self, queries: Sequence[str]):
+        """The query embeddings (a worker thread on the GPU: the embedder may be the serving
+        engine); pass them to search_batch(vecs=...) to run the index pass later."""
+        if getattr(self.index.device, "type", "cpu") == "cuda":
+            return await asyncio.get_running_loop().run_in_executor(None, self.embedder, list(queries))
+        return self.embedder(list(queries))
+
     async def search_batch(self, queries: Sequence[str], tags: Optional[Sequence[Optional[Set[str]]]] = None,
                            min_priority: Optional[Sequence[int]] = None, limit: int = 5,
-                           mode: str = "semantic") -> List[List[MemoryItem]]:
+                           mode: str = "semantic", vecs=None) -> List[List[MemoryItem]]:
+        """`vecs`: the queries' embeddings from embed_queries (skips embedding here)."""
         Q = len(queries)
         tags = list(tags) if tags is not None else [None] * Q
         minp = list(min_priority) if min_priority is not None else [0] * Q
@@ -134,8 +142,8 @@ class EnhancedMemory:
                 return [self._substring(q, t, p, limit) for q, t, p in zip(queries, tags, minp)]
 
             def run():
-                vecs = self.embedder(list(queries))
-                return self.index.search(vecs, limit, minp, [t or () for t in tags])
+                v = self.embedder(list(queries)) if vecs is None else vecs
+                return self.index.search(v, limit, minp, [t or () for t in tags])
 
             if getattr(self.index.device, "type", "cpu") == "cuda":
                 # embed + one kernel pass + wait in a worker thread: the event loop (all

@@ -94,9 +94,12 @@ class NodeSemanticStore:
             self._thread = None
 
     # ------------------------------------------------------------------ API (asyncio)
+    async def embed_queries(self, queries: Sequence[str]) -> np.ndarray:
+        return await asyncio.get_running_loop().run_in_executor(None, self._embed, list(queries))
+
     async def search_batch(self, queries: Sequence[str], tags: Optional[Sequence[Optional[Set[str]]]] = None,
                            min_priority: Optional[Sequence[int]] = None, limit: int = 5,
-                           mode: str = "semantic") -> List[List[MemoryItem]]:
+                           mode: str = "semantic", vecs=None) -> List[List[MemoryItem]]:
         if mode != "semantic":
             raise ValueError("the node-wide store answers semantic searches only")
         Q = len(queries)
@@ -105,7 +108,10 @@ class NodeSemanticStore:
         tags = list(tags) if tags is not None else [None] * Q
         minp = list(min_priority) if min_priority is not None else [0] * Q
         loop = asyncio.get_running_loop()
-        vecs = await loop.run_in_executor(None, self._embed, list(queries))
+        if vecs is None:
+            vecs = await loop.run_in_executor(None, self._embed, list(queries))
+        else:
+            vecs = vecs.float().cpu().numpy() if isinstance(vecs, torch.Tensor) else np.asarray(vecs, np.float32)
         futs = []
         with self._lock:
             self._check()

@@ -467,14 +467,16 @@ def mid_gemm(x: torch.Tensor, wp: torch.Tensor, epi: str = "plain", resid: Optio
 STREAM_EPI = {"plain": 0, "silu": 1, "resid": 2, "rope_perm": 3}
 STREAM_WS_FLOATS = 24 << 20  # 96 MB of split-K partial fragments per device (uncached)
 _stream_ws = {}
-# Split-K group hand-off of gemm_stream.hip (rel bit 0): the producer's agent-scope release
-# (buffer_wbl2 sc1 + drain) before it arrives on the group counter, i.e. the LLVM AMDGPU
-# memory model's release at agent scope, paired with the acquire after the poll. Without it
-# the protocol rests on when a write-through store's vmcnt ack comes back relative to the
-# fabric write (the round-4 decode QKV+RoPE case failed 5 of 10,000 poisoned runs that way
-# on uncached slabs: profiles/r4_handoff_uncached.md, profiles/r5_handoff_*). 0 = the sc1-only
-# form, for the A/B tools only.
-STREAM_REL = int(os.environ.get("PILOTTAI_STREAM_REL", "1"))
+# Split-K group hand-off of gemm_stream.hip (rel bit 0 = the producer's agent-scope release,
+# buffer_wbl2 sc1 + drain, before it arrives). Shipped: 0, the form of MI355X_MICROARCH.md's
+# measured-valid hand-off table, row 1 (16-B sc1 slab stores drained by every wave, workgroup
+# barrier, one lane's agent-scope add; sc1 poll; sc1 slab loads behind a barrier), plus the
+# consumer's agent-scope acquire. Round 5 ran 100,000 NaN-poisoned, varied-input repetitions of
+# every production plan (the RoPE + paged-KV epilogue included) in both forms: 0 bad runs
+# (profiles/r5_handoff_stream.md); the release costs 2.5-5 us per launch (+10-18 %, about +5 %
+# on a 64-row step), so it stays an option (PILOTTAI_STREAM_REL=1). The decode / mid / prefill
+# last-arriver hand-offs keep their release (they failed without it, profiles/r4_handoff_uncached.md).
+STREAM_REL = int(os.environ.get("PILOTTAI_STREAM_REL", "0"))
 
 
 def stream_workspace(device):

@@ -63,15 +63,20 @@ class TPGroup:
         return resid
 
     def all_reduce_max(self, t: torch.Tensor) -> torch.Tensor:
-        """In-place elementwise max over the group (any dtype; RCCL / gloo)."""
+        """In-place elementwise max over the group: fp32 device tensors on the custom P2P
+        buffers (capturable, no RCCL in a step graph), anything else through the process group."""
         if self.size > 1:
+            if self.custom is not None and self.custom.collective_eligible(t, "max"):
+                return self.custom.all_reduce_f32(t, "max")
             dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
         return t
 
     def all_reduce_sum(self, t: torch.Tensor) -> torch.Tensor:
-        """In-place sum over the group through the process group (fp32 histograms etc.; the
-        custom all-reduce is for bf16 activations)."""
+        """In-place sum over the group (fp32 histograms etc.): the custom P2P buffers when
+        eligible (rank-order sums, bit-identical on every rank), else the process group."""
         if self.size > 1:
+            if self.custom is not None and self.custom.collective_eligible(t, "sum"):
+                return self.custom.all_reduce_f32(t, "sum")
             dist.all_reduce(t, group=self.group)
         return t
 
@@ -79,6 +84,8 @@ class TPGroup:
         """Concatenate `t` from every rank along a new leading dim: [size, *t.shape]."""
         if self.size == 1:
             return t.unsqueeze(0)
+        if self.custom is not None and self.custom.collective_eligible(t, "gather"):
+            return self.custom.all_gather(t)
         if t.device.type == "cpu" or dist.get_backend(self.group) == "gloo":  # gloo: list form
             parts = [torch.empty_like(t) for _ in range(self.size)]
             dist.all_gather(parts, t.contiguous(), group=self.group)

@@ -30,7 +30,10 @@ import torch.distributed as dist
 
 log = logging.getLogger(__name__)
 
-DEFAULT_CAP_BYTES = 8 << 20          # per data parity: 512 tokens x 8192 hidden x bf16
+# per data parity: a 2,048-token step of the 70B model (2,048 x 8,192 x bf16), so every TP
+# all-reduce of a step graph -- the embedding, o and down projections -- stays on the custom
+# path (no RCCL call inside a captured graph)
+DEFAULT_CAP_BYTES = 32 << 20
 DEFAULT_TWO_SHOT_BYTES = 512 << 10   # above this the 2(W-1)/W traffic of two-shot wins
 
 
@@ -140,6 +143,29 @@ class CustomAllReduce:
         self.calls += 1
         return resid
 
+    # -- small collectives of the TP step graph (custom_ar.hip co_kernel) ---------------
+    _OPS = {"sum": 0, "max": 1, "gather": 2}
+
+    def collective_eligible(self, t: torch.Tensor, op: str) -> bool:
+        n = t.numel()
+        ok_dtype = t.dtype == torch.float32 if op in ("sum", "max") else t.element_size() == 4
+        return (t.is_cuda and ok_dtype and t.is_contiguous() and n % 4 == 0 and n > 0
+                and n * 4 <= self.cap_bytes and t.data_ptr() % 16 == 0)
+
+    def all_reduce_f32(self, t: torch.Tensor, op: str = "sum") -> torch.Tensor:
+        """In-place fp32 SUM (rank order: bit-identical on every rank) or MAX over the group."""
+        self.C.car_collective(self.bases, self.rank, [t], [t], self.cap_bytes, self.epochs, self.err,
+                              self._OPS[op])
+        self.calls += 1
+        return t
+
+    def all_gather(self, t: torch.Tensor) -> torch.Tensor:
+        """[world, *t.shape]: every rank's `t` (any 4-byte dtype)."""
+        out = torch.empty((self.world,) + tuple(t.shape), dtype=t.dtype, device=t.device)
+        self.C.car_collective(self.bases, self.rank, [t], [out], self.cap_bytes, self.epochs, self.err, 2)
+        self.calls += 1
+        return out
+
     def fusable(self, t: torch.Tensor, resid: torch.Tensor) -> bool:
         return (self.eligible(t) and resid.is_contiguous() and resid.numel() == t.numel()
                 and resid.dtype == torch.bfloat16 and resid.data_ptr() % 16 == 0
@@ -157,6 +183,26 @@ class CustomAllReduce:
         if self._own:
             C.car_free(self._own)
             self._own = 0
+
+
+def local_group_collective(C, tensors: List[torch.Tensor], cap_bytes: int, op: str, state: dict,
+                           outs: Optional[List[torch.Tensor]] = None) -> List[torch.Tensor]:
+    """Single-process form of the small collectives (tests): W 'ranks' in one launch. op "sum" /
+    "max" reduce in place; "gather" returns one [W, n] tensor per rank."""
+    W = len(tensors)
+    key = (W, cap_bytes)
+    if key not in state:
+        bufs = [C.car_alloc(CustomAllReduce.buffer_bytes(cap_bytes))[0] for _ in range(W)]
+        epochs = torch.zeros(W * C.car_group(), dtype=torch.int32, device=tensors[0].device)
+        err = torch.zeros(1, dtype=torch.int32, device=tensors[0].device)
+        state[key] = (bufs, epochs, err)
+    bufs, epochs, err = state[key]
+    if op == "gather":
+        outs = outs or [torch.empty((W,) + tuple(t.shape), dtype=t.dtype, device=t.device) for t in tensors]
+        C.car_collective(bufs, 0, tensors, outs, cap_bytes, epochs, err, 2)
+        return outs
+    C.car_collective(bufs, 0, tensors, tensors, cap_bytes, epochs, err, CustomAllReduce._OPS[op])
+    return tensors
 
 
 def local_group_all_reduce(C, tensors: List[torch.Tensor], cap_bytes: int, two_shot: bool,

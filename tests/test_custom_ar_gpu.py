@@ -120,6 +120,21 @@ if car is not None:
         want = (both[0].float() + both[1].float()).bfloat16()
         gr.replay(); torch.cuda.synchronize()
         out["ok"].append(bool(torch.equal(t, want)))
+    # the TP step graph's small collectives on the same buffers (fp32 SUM / MAX, all-gather)
+    for n in [4, 4096 + 4, 64 * 512]:
+        both = [torch.randn(n, device="cuda", generator=g) for _ in range(2)]
+        t = both[rank].clone()
+        car.all_reduce_f32(t, "sum")
+        torch.cuda.synchronize()
+        out["ok"].append(bool(torch.equal(t, both[0] + both[1])))
+        t = both[rank].clone()
+        car.all_reduce_f32(t, "max")
+        out["ok"].append(bool(torch.equal(t, torch.maximum(both[0], both[1]))))
+        ids = torch.arange(n, device="cuda", dtype=torch.int32) * (rank + 1)
+        got = car.all_gather(ids)
+        torch.cuda.synchronize()
+        want = torch.stack([torch.arange(n, device="cuda", dtype=torch.int32) * (r + 1) for r in range(2)])
+        out["ok"].append(bool(torch.equal(got, want)))
     out["healthy"] = car.healthy()
     dist.barrier()
     car.close()
@@ -186,3 +201,134 @@ def test_custom_ar_fused_residual_and_row_stats(W, two_shot):
                 assert float(junk[r].abs().max()) == 0.0
     err = state[(W, cap)][2]
     assert int(err.item()) == 0
+
+
+@pytest.mark.parametrize("W", [2, 4, 8])
+def test_custom_collectives_local_ranks(W):
+    """The TP step graph's small collectives (custom_ar.hip co_kernel): fp32
+    SUM in rank order (bit-exact vs a PyTorch rank-order sum), MAX, and the all-gather of 4-byte
+    values, interleaved with bf16 all-reduces on the same buffers / epochs, W ranks in one
+    launch, sizes from one vector to several chunks per workgroup; then in hipGraph replay."""
+    from pilottai_amd.parallel.custom_ar import local_group_all_reduce, local_group_collective
+
+    C = _C()
+    state = {}
+    cap = 1 << 20
+    g = torch.Generator(device="cuda").manual_seed(100 + W)
+    for n in [4, 1024 + 4, 64 * 512, cap // 8]:
+        for rep in range(2):
+            xs = [torch.randn(n, device="cuda", generator=g) for _ in range(W)]
+            want = torch.zeros(n, device="cuda")
+            for x in xs:
+                want = want + x
+            ins = [x.clone() for x in xs]
+            local_group_collective(C, ins, cap, "sum", state)
+            torch.cuda.synchronize()
+            assert all(torch.equal(t, want) for t in ins), (n, rep)
+            ins = [x.clone() for x in xs]
+            local_group_collective(C, ins, cap, "max", state)
+            mx = torch.stack(xs).max(0).values
+            assert all(torch.equal(t, mx) for t in ins), (n, rep)
+            ids = [torch.randint(0, 1 << 30, (n,), device="cuda", dtype=torch.int32, generator=g) for _ in range(W)]
+            outs = local_group_collective(C, ids, cap, "gather", state)
+            torch.cuda.synchronize()
+            assert all(torch.equal(o, torch.stack(ids)) for o in outs), (n, rep)
+            bf = [torch.randn(min(8 * n, cap // 2), device="cuda", generator=g).bfloat16() for _ in range(W)]
+            want_bf = _ref(bf)
+            local_group_all_reduce(C, bf, cap, rep % 2 == 1, state)
+            torch.cuda.synchronize()
+            assert all(torch.equal(t, want_bf) for t in bf)
+    assert int(state[(W, cap)][2].item()) == 0
+    # hipGraph replay: gather + sum + max captured back to back
+    n = 4096
+    keys = [torch.empty(n, device="cuda") for _ in range(W)]
+    hist = [torch.empty(n, device="cuda") for _ in range(W)]
+    gout = [torch.empty(W, n, device="cuda") for _ in range(W)]
+    local_group_collective(C, keys, cap, "gather", state, outs=gout)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(graph, stream=s):
+            local_group_collective(C, keys, cap, "gather", state, outs=gout)
+            local_group_collective(C, hist, cap, "sum", state)
+            local_group_collective(C, keys, cap, "max", state)
+    torch.cuda.current_stream().wait_stream(s)
+    for it in range(3):
+        kx = [torch.randn(n, device="cuda", generator=g) for _ in range(W)]
+        hx = [torch.randn(n, device="cuda", generator=g) for _ in range(W)]
+        for d, x in zip(keys, kx):
+            d.copy_(x)
+        for d, x in zip(hist, hx):
+            d.copy_(x)
+        graph.replay()
+        torch.cuda.synchronize()
+        hs = torch.zeros(n, device="cuda")
+        for x in hx:
+            hs = hs + x
+        for r in range(W):
+            assert torch.equal(gout[r], torch.stack(kx)), (it, r)
+            assert torch.equal(hist[r], hs), (it, r)
+            assert torch.equal(keys[r], torch.stack(kx).max(0).values), (it, r)
+    assert int(state[(W, cap)][2].item()) == 0
+
+
+@pytest.mark.parametrize("W", [2, 4, 8])
+def test_tp_topkp_phase_kernels_match_single_gpu(W):
+    """The vocab-parallel top-k / top-p threshold (csrc/ops/sampling.hip tp_topkp_kernel, four
+    phases with MAX / SUM reductions over the custom collectives between them) gives every shard
+    the tau of the single-GPU kernel on the whole row: greedy / untruncated rows -inf, top-k,
+    top-p, both, grammar-masked rows, a row whose allowed set lies in one shard."""
+    from pilottai_amd import ops
+    from pilottai_amd.engine.tp_sampling import tkp_ws_floats
+    from pilottai_amd.ops import reference as ref
+    from pilottai_amd.parallel.custom_ar import local_group_collective
+
+    C = _C()
+    torch.manual_seed(7 + W)
+    rows, V = 13, 128256
+    vl = V // W
+    logits = (torch.randn(rows, V, device="cuda") * 3).bfloat16()
+    temp = torch.tensor([0.7, 0.0, 1.0, 0.9, 1.3, 0.5, 0.8, 1.0, 0.6, 1.1, 0.9, 0.7, 1.0], device="cuda")
+    top_k = torch.tensor([40, 40, 0, 5, 0, 1, 100, 0, 20, V, 7, 0, 3], device="cuda", dtype=torch.int32)
+    top_p = torch.tensor([1.0, 0.9, 0.95, 0.8, 0.5, 1.0, 0.99, 1.0, 0.3, 0.7, 1.0, 0.999, 0.6], device="cuda")
+    words = (V + 31) // 32
+    masks = torch.zeros(3, words, dtype=torch.int32)
+    masks[0] = -1
+    allowed = torch.zeros(V, dtype=torch.bool)
+    allowed[torch.randperm(V)[:3000]] = True
+    masks[1] = ref.pack_mask(allowed.numpy())
+    one_shard = torch.zeros(V, dtype=torch.bool)
+    one_shard[vl + 17: vl + 900] = True  # every allowed token in shard 1
+    masks[2] = ref.pack_mask(one_shard.numpy())
+    masks = masks.cuda()
+    mcls = torch.tensor([-1, -1, 0, 1, 1, 2, -1, -1, 2, -1, 1, 0, -1], device="cuda", dtype=torch.int32)
+    want = ops.topkp_threshold(logits, V, temp, top_k, top_p, mcls, masks)
+    shards = [logits[:, w * vl:(w + 1) * vl] for w in range(W)]
+    wss = [torch.zeros(tkp_ws_floats(rows), device="cuda") for _ in range(W)]
+    taus = [torch.empty(rows, device="cuda") for _ in range(W)]
+    r4 = (rows + 3) & ~3
+    seg = {"mx": (0, r4), "h0": (r4, r4 + rows * 512), "h1": (r4 + rows * 512, r4 + rows * 1024)}
+    state = {}
+    cap = 1 << 20
+
+    def phase(ph):
+        for w in range(W):
+            C.tp_topkp_phase(ph, taus[w], wss[w], shards[w], w * vl, V, temp, top_k, top_p, mcls, masks)
+
+    def reduce(name, op):
+        a, b = seg[name]
+        local_group_collective(C, [ws[a:b] for ws in wss], cap, op, state)
+
+    phase(0)
+    reduce("mx", "max")
+    phase(1)
+    reduce("h0", "sum")
+    phase(2)
+    reduce("h1", "sum")
+    phase(3)
+    torch.cuda.synchronize()
+    for w in range(W):
+        assert torch.equal(taus[w], taus[0])
+    torch.testing.assert_close(taus[0], want, atol=0, rtol=0)
+    assert float(taus[0][1]) == float("-inf") and float(taus[0][7]) == float("-inf")  # greedy / untruncated

@@ -21,6 +21,7 @@ from pilottai_amd.core.policy import ControlPolicy
 from pilottai_amd.core.task import Task
 from pilottai_amd.engine.local_llm import SchemaLLM
 from pilottai_amd.memory.batcher import MemoryLookupBatcher
+from pilottai_amd.memory.embedding import HashingEmbedder
 from pilottai_amd.memory.enhanced_memory import EnhancedMemory
 from pilottai_amd.memory.semantic_index import SemanticIndex, ShardedSemanticIndex
 from pilottai_amd.tools.tool import Tool, echo_tool
@@ -163,3 +164,45 @@ def test_serve_does_not_start_openings_for_custom_agents():
     agents, rs = asyncio.run(go())
     assert all(r.success for r in rs)
     assert all(a._llm is None for a in agents)
+
+
+def test_batcher_scans_beside_compute_bound_steps():
+    """with an engine gate attached, an index pass waits for the engine to
+    launch a compute-bound step (>= gate_tokens tokens) and starts right behind it; a lookup
+    never waits longer than the latency cap when no such step comes."""
+    import time as _t
+
+    class FakeEngine:
+        def __init__(self):
+            self.listeners = []
+
+        def add_step_listener(self, fn):
+            self.listeners.append(fn)
+
+        def launch(self, T):
+            for fn in self.listeners:
+                fn(T)
+
+    async def run():
+        mem = EnhancedMemory(device="cpu", dim=64, embedder=HashingEmbedder(64))
+        await mem.store_semantic_batch(["alpha report", "beta memo", "gamma notes"])
+        b = MemoryLookupBatcher(mem)
+        eng = FakeEngine()
+        b.attach_engine(eng, gate_tokens=1024, max_wait_s=0.2)
+        loop = asyncio.get_running_loop()
+        # a heavy launch 50 ms after the lookup: the pass starts beside it
+        t0 = _t.perf_counter()
+        loop.call_later(0.02, eng.launch, 64)     # memory-bound: not a trigger
+        loop.call_later(0.05, eng.launch, 2048)   # compute-bound: the trigger
+        hits = await b.search("alpha report", limit=1)
+        waited = _t.perf_counter() - t0
+        assert hits and hits[0].text == "alpha report"
+        assert 0.045 <= waited < 0.18 and b.stats["passes_beside_heavy"] == 1
+        # no heavy step: the cap releases the lookup
+        t0 = _t.perf_counter()
+        await b.search("beta memo", limit=1)
+        assert 0.18 <= _t.perf_counter() - t0 < 0.5 and b.stats["passes_capped"] == 1
+        s = b.latency_summary()
+        assert s["lookups"] == 2 and s["lookup_p99_ms"] >= s["lookup_p50_ms"] > 0
+
+    asyncio.run(run())

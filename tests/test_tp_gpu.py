@@ -4,6 +4,11 @@ on GPU 0 over real IPC handles; gloo carries the host-side step headers).
 Mirrors tests/test_tp_cpu.py: the TP=2 engine must reproduce the TP=1 engine's
 greedy tokens (canonical sharded init -> identical weights) and keep structured
 output valid, with every row-parallel all-reduce going through csrc/ops/custom_ar.hip.
+The graph-on variant is the production TP mode: every bucket captured
+up front with the collectives inside, all of them on the custom P2P buffers -- the
+activations' all-reduces, the sampling winners' all-gather and the top-k / top-p
+threshold's MAX / SUM reductions; a hook on torch.distributed proves that no RCCL / gloo
+call is made while a graph is being captured.
 """
 import json
 import os
@@ -24,18 +29,36 @@ def _free_port() -> int:
     return p
 
 
-def _cfg():
+def _cfg(graphs=False):
     from pilottai_amd.engine.engine import EngineConfig
 
     return EngineConfig(model="tiny-gqa4", max_num_seqs=8, max_num_batched_tokens=128, max_model_len=512,
-                        num_kv_blocks=96, use_graphs=False)
+                        num_kv_blocks=96, use_graphs=graphs, token_buckets=[8, 16, 32, 64, 128])
+
+
+_COLLECTIVES = ("all_reduce", "all_gather", "all_gather_into_tensor", "broadcast", "reduce_scatter_tensor",
+                "all_to_all_single", "barrier", "all_gather_object", "broadcast_object_list")
+
+
+def _hook_collectives(box):
+    """Count torch.distributed collectives issued while a hipGraph is being captured."""
+    import torch.distributed as dist
+
+    for name in _COLLECTIVES:
+        fn = getattr(dist, name)
+
+        def wrapped(*a, _fn=fn, _name=name, **k):
+            if torch.cuda.is_current_stream_capturing():
+                box.append(_name)
+            return _fn(*a, **k)
+        setattr(dist, name, wrapped)
 
 
 def _prompts(tok):
     return [tok.encode("Task: summarize the quarterly report."), tok.encode("Task: plan a trip")]
 
 
-def _worker(rank, world, port, out_path):
+def _worker(rank, world, port, out_path, graphs=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
     from pilottai_amd.engine.engine import LLMEngine
@@ -45,7 +68,10 @@ def _worker(rank, world, port, out_path):
     torch.cuda.set_device(0)
     tp = new_tp_groups(world, custom_ar=True)
     assert tp.custom is not None, "custom all-reduce did not initialise"
-    e = LLMEngine(_cfg(), device=torch.device("cuda", 0), tp=tp)
+    in_graph = []
+    _hook_collectives(in_graph)
+    e = LLMEngine(_cfg(graphs), device=torch.device("cuda", 0), tp=tp)
+    assert e.use_graphs == graphs
     if rank != 0:
         e.follow()
         torch.distributed.destroy_process_group()
@@ -54,19 +80,27 @@ def _worker(rank, world, port, out_path):
     greedy = e.generate(ps, temperature=0.0, max_tokens=6, ignore_eos=True)
     segs = e.grammar.compile("orchestrator.result_evaluation")
     js = e.generate([ps[0]], temperature=0.8, max_tokens=64, grammar=segs)[0]
+    # top-k / top-p rows: the TP threshold (HIP phases + custom MAX / SUM) inside the graph
+    tk = e.generate(ps, temperature=0.9, max_tokens=12, ignore_eos=True, top_k=20, top_p=0.9)
     e.release_followers()
     with open(out_path, "w") as f:
         json.dump({"greedy": [o.token_ids for o in greedy], "json": js.text, "calls": tp.custom.calls,
-                   "healthy": tp.custom.healthy()}, f)
+                   "healthy": tp.custom.healthy(), "graphs": len(e._graphs), "in_graph": in_graph,
+                   "topk_lens": [len(o.token_ids) for o in tk]}, f)
     torch.distributed.destroy_process_group()
 
 
-def test_tp2_engine_custom_allreduce_matches_tp1(tmp_path):
+@pytest.mark.parametrize("graphs", [False, True])
+def test_tp2_engine_custom_allreduce_matches_tp1(tmp_path, graphs):
     out = str(tmp_path / "tp.json")
     port = _free_port()
-    mp.start_processes(_worker, args=(2, port, out), nprocs=2, join=True, start_method="spawn")
+    mp.start_processes(_worker, args=(2, port, out, graphs), nprocs=2, join=True, start_method="spawn")
     res = json.load(open(out))
     assert res["calls"] > 0 and res["healthy"], res
+    assert res["topk_lens"] == [12, 12]
+    if graphs:
+        assert res["graphs"] >= 5  # every bucket captured up front (+ first-use variants)
+        assert res["in_graph"] == [], res["in_graph"]  # no RCCL / gloo call inside a graph
     obj = json.loads(res["json"])
     assert set(obj) == {"success", "quality", "requires_retry"}
 

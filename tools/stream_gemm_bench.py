@@ -35,6 +35,8 @@ ap.add_argument("--cold-mb", type=int, default=1024)
 ap.add_argument("--sweep", action="store_true", help="time every valid stream decomposition too")
 ap.add_argument("--row-groups", action="store_true", help="sweep also splits the rows into 2-4 groups")
 ap.add_argument("--krot", action="store_true", help="also time the default plan with rotated K-chunk order")
+ap.add_argument("--rel-ab", action="store_true",
+                help="also time the default plan without the producer release (rel 0; shipped: ops.STREAM_REL)")
 ap.add_argument("--out", default="")
 a = ap.parse_args()
 SHAPES = {"qkv": (6144, 4096, "rope_perm", True), "o": (4096, 4096, "resid", False),
@@ -143,6 +145,8 @@ for name in a.shapes.split(","):
             f = kernels.prefill_gemm if path == "pf" else kernels.mid_gemm
             variants["r3"] = lambda i, f=f, cfg=cfg: f(x, wps[i], epi, **kw, **cfg)
         variants["stream"] = lambda i: kernels.stream_gemm(x, wps[i], epi, **kw)
+        if a.rel_ab:  # the sc1-only group hand-off, for the cost of the shipped release
+            variants["stream_rel0"] = lambda i: kernels.stream_gemm(x, wps[i], epi, rel=0, **kw)
         if a.krot:  # default plan, rotated K-chunk order per workgroup
             variants["stream_krot"] = lambda i: kernels.stream_gemm(x, wps[i], epi, rel=2, **kw)
         for sl in a.slabs.split(","):
