@@ -41,7 +41,7 @@ def parse():
     ap.add_argument("--no-fault", action="store_true")
     ap.add_argument("--cpu", action="store_true")
     ap.add_argument("--max-batched-tokens", type=int, default=2048)
-    ap.add_argument("--no-graphs", action="store_true", help="eager steps (required with --share-gpu)")
+    ap.add_argument("--no-graphs", action="store_true", help="eager steps")
     ap.add_argument("--share-gpu", action="store_true",
                     help="1-GPU rehearsal of TP=N: every rank on GPU 0, gloo control plane "
                          "(PILOTTAI_DIST_BACKEND=gloo), TP all-reduces through the custom P2P kernel")
@@ -115,7 +115,8 @@ async def drive(a, engine):
     calls = u1["calls"] - u0["calls"]
     return {
         "metric": "hierarchical extract->analyze->summarize workflows/s (delegation + fault tolerance)",
-        "value": round(n / dt, 3), "unit": "workflows/s", "n_gpus": engine.tp.size if not a.cpu else 0,
+        "value": round(n / dt, 3), "unit": "workflows/s", "n_gpus": (1 if a.share_gpu else engine.tp.size) if not a.cpu else 0,
+        "rehearsal": "share-gpu" if a.share_gpu else None,
         "higher_is_better": True, "dtype": "bf16", "data": "synthetic documents, random-init weights",
         "config": {"model": engine.model_cfg.name if not a.cpu else "tiny(cpu-smoke)",
                    "parallelism": f"tp{engine.tp.size}", "clients": a.clients, "replicas_per_stage": a.replicas,
@@ -142,11 +143,9 @@ def main():
     from pilottai_amd.parallel import comm
 
     rank, world, local = comm.init_distributed()
-    if a.share_gpu:
-        # gloo cannot carry >8 MiB GPU all-reduces quickly nor be graph-captured: keep every
-        # row-parallel message on the custom kernel (tokens x hidden x 2 B <= 8 MiB) and run eagerly
-        a.no_graphs = True
-        a.max_batched_tokens = min(a.max_batched_tokens, 256)
+    # every TP collective of a step (activations up to 2,048 x 8,192 bf16, sampling winners,
+    # top-k / top-p histograms) runs on the custom P2P buffers, so the step graphs capture the
+    # TP=2 shared-GPU rehearsal too; --no-graphs keeps the eager steps
     tp = comm.new_tp_groups(world, custom_ar=True if a.share_gpu else None)
     if a.cpu or not torch.cuda.is_available():
         a.cpu = True
@@ -176,6 +175,9 @@ def main():
         finally:
             eng.stop()  # also releases the follower ranks
         out["init_s"] = round(init_s, 1)
+        out["graphs"] = {"use_graphs": eng.use_graphs, "captured": len(eng._graphs),
+                         "replays": eng.stats.get("graph_replays", 0), "tp": tp.size,
+                         "custom_collective_calls": tp.custom.calls if getattr(tp, "custom", None) else None}
         if eng.on_gpu:
             out["hbm_used_gb_per_gpu"] = round(torch.cuda.max_memory_allocated(device) / 2**30, 1)
         print(json.dumps(out), flush=True)

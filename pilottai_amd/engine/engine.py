@@ -131,6 +131,9 @@ class EngineConfig:
     # is opt-in, for serving entry points that build one engine (bench.py freezes after its
     # warm-up instead; the HTTP server sets it)
     freeze_heap: bool = False
+    # keep every captured hipGraph's node list (torch keep_graph=True) so tools can count its
+    # kernels (utils/tracing.py graph_node_counts); costs host memory, off in serving
+    keep_graphs: bool = False
 
 
 # TP step header: [op, T, ns, nsamp, bucket, masks_changed, n_copy, truncate, embed]
@@ -529,9 +532,11 @@ class LLMEngine:
                 for _ in range(2):
                     self._forward_and_sample(b, s_b, 0, trunc, embed)
             torch.cuda.current_stream().wait_stream(st)
-            g = torch.cuda.CUDAGraph()
+            g = torch.cuda.CUDAGraph(keep_graph=True) if self.cfg.keep_graphs else torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, pool=self._graph_pool):
                 self._forward_and_sample(b, s_b, 0, trunc, embed)
+            if self.cfg.keep_graphs:
+                g.instantiate()
             self._graphs[(b, trunc, embed)] = g
         if embed:
             self._embed_pool.zero_()  # the capture's dummy steps pooled into row max_seqs only

@@ -22,8 +22,7 @@ streaming read that halves the speed of the engine's memory-bound (decode-sized)
 costs a compute-bound 2,048-token prefill step only ~6 % (BENCHMARKS.md, config 4). The engine
 announces every step it launches (LLMEngine.add_step_listener); with a gate attached, a pass
 whose queries are embedded waits until the engine launches a step of at least `gate_tokens`
-tokens -- or until its oldest lookup has waited `gate_max_wait_s` -- and then starts right
-behind that launch, so the scan overlaps compute-bound work. `stats` counts the passes that
+tokens -- or for at most `gate_max_wait_s` -- and then starts right behind that launch, so the scan overlaps compute-bound work. `stats` counts the passes that
 started beside such a step and the ones the latency cap released.
 """
 from __future__ import annotations
@@ -80,14 +79,15 @@ class MemoryLookupBatcher:
         self._last_heavy = time.perf_counter()
         self._heavy.set()
 
-    async def _await_heavy(self, oldest: float):
-        """Return once a heavy step was just launched (within 2 ms), or at the latency cap."""
+    async def _await_heavy(self):
+        """Return once a heavy step was just launched (within 2 ms), or at the latency cap
+        (counted from here: the queries are embedded, only the scan waits)."""
         t0 = time.perf_counter()
         if t0 - self._last_heavy < 0.002:
             self.stats["passes_beside_heavy"] += 1
             return
         self._heavy.clear()
-        left = self._gate_wait - (t0 - oldest)
+        left = self._gate_wait
         try:
             if left <= 0:
                 raise asyncio.TimeoutError
@@ -176,7 +176,7 @@ class MemoryLookupBatcher:
                 vecs = None
                 if self._heavy is not None:  # embed now, scan beside the next compute-bound step
                     vecs = await self.memory.embed_queries(qs)
-                    await self._await_heavy(min(b[5] for b in batch))
+                    await self._await_heavy()
                 hits = await self.memory.search_batch(qs, tags=[b[1] for b in batch],
                                                       min_priority=[b[2] for b in batch], limit=limit, vecs=vecs)
                 now = time.perf_counter()

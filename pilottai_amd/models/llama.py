@@ -84,6 +84,12 @@ PRESETS: Dict[str, LlamaConfig] = {
     # the exact Llama-3-8B layer (4096 / 14336 / 32:8 heads / full vocabulary), 2 layers deep:
     # production shapes through every forward path at test cost
     "llama-3-8b-2l": LlamaConfig(name="llama-3-8b-2l", num_layers=2, max_position=4096),
+    # the exact Llama-3-70B layer, 1 / 2 layers deep (per-layer launch counts of the TP step graph:
+    # tools/graph_nodes.py)
+    "llama-3-70b-1l": LlamaConfig(name="llama-3-70b-1l", hidden_size=8192, intermediate_size=28672,
+                                  num_layers=1, num_heads=64, num_kv_heads=8, max_position=4096),
+    "llama-3-70b-2l": LlamaConfig(name="llama-3-70b-2l", hidden_size=8192, intermediate_size=28672,
+                                  num_layers=2, num_heads=64, num_kv_heads=8, max_position=4096),
 }
 
 

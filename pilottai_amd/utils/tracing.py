@@ -77,3 +77,30 @@ class Tracer:
 
 
 GLOBAL_TRACER = Tracer()
+
+
+_HIP_NODE_TYPES = {0: "kernel", 1: "memcpy", 2: "memset", 3: "host", 4: "graph", 5: "empty",
+                   6: "wait_event", 7: "event_record"}
+
+
+def graph_node_counts(graph) -> dict:
+    """Node counts by type of a captured torch.cuda.CUDAGraph made with keep_graph=True
+    (hipGraphGetNodes / hipGraphNodeGetType): how many kernel launches one replay issues."""
+    import ctypes
+
+    lib = ctypes.CDLL("libamdhip64.so")
+    g = ctypes.c_void_p(int(graph.raw_cuda_graph()))
+    n = ctypes.c_size_t(0)
+    if lib.hipGraphGetNodes(g, None, ctypes.byref(n)) != 0:
+        raise RuntimeError("hipGraphGetNodes failed")
+    nodes = (ctypes.c_void_p * n.value)()
+    if lib.hipGraphGetNodes(g, nodes, ctypes.byref(n)) != 0:
+        raise RuntimeError("hipGraphGetNodes failed")
+    out: dict = {}
+    t = ctypes.c_int(0)
+    for i in range(n.value):
+        if lib.hipGraphNodeGetType(ctypes.c_void_p(nodes[i]), ctypes.byref(t)) != 0:
+            raise RuntimeError("hipGraphNodeGetType failed")
+        k = _HIP_NODE_TYPES.get(t.value, f"type{t.value}")
+        out[k] = out.get(k, 0) + 1
+    return out
