@@ -7,7 +7,11 @@ instant fake manager LLM), echo agents, closed-loop clients that submit a task
 and await its result. Reference (8-vCPU Xeon): 5,052 tasks/s p50 0.153 ms at 1
 client; 5,125 tasks/s p50 1.325 ms at 8; 5,312 tasks/s p50 10.426 ms at 64.
 
-    python benchmarks/plumbing.py [--clients 1,8,64] [--tasks 20000]
+    python benchmarks/plumbing.py [--clients 1,8,64] [--tasks 20000] [--same-box-reference]
+
+--same-box-reference runs the reference's own Serve (benchmarks/reference_plumbing.py)
+alternating with ours, on this machine, so the comparison does not depend on BASELINE.md's
+survey-session hardware.
 """
 from __future__ import annotations
 
@@ -108,12 +112,31 @@ def main():
     ap.add_argument("--clients", default="1,8,64")
     ap.add_argument("--tasks", type=int, default=20000)
     ap.add_argument("--repeat", type=int, default=3, help="runs per client count; the median is reported")
+    ap.add_argument("--same-box-reference", action="store_true",
+                    help="also run the reference's own Serve on this machine (benchmarks/reference_plumbing.py), "
+                         "alternating with ours, and report the ratio of the medians")
     a = ap.parse_args()
+    ref_mods = None
+    if a.same_box_reference:
+        from benchmarks import reference_plumbing as rp
+
+        ref_mods = rp._import_reference()
     rows = []
     for c in a.clients.split(","):
-        runs = sorted((asyncio.run(run(int(c), a.tasks)) for _ in range(a.repeat)), key=lambda r: r["tasks_per_s"])
+        ours, theirs = [], []
+        for _ in range(a.repeat):  # interleaved: both see the same machine load
+            ours.append(asyncio.run(run(int(c), a.tasks)))
+            if ref_mods is not None:
+                theirs.append(asyncio.run(rp.run(int(c), a.tasks, ref_mods)))
+        runs = sorted(ours, key=lambda r: r["tasks_per_s"])
         med = dict(runs[len(runs) // 2])
         med["runs_tasks_per_s"] = [r["tasks_per_s"] for r in runs]
+        if theirs:
+            tr = sorted(theirs, key=lambda r: r["tasks_per_s"])
+            rm = tr[len(tr) // 2]
+            med.update(same_box_reference_tasks_per_s=rm["tasks_per_s"], same_box_reference_p50_ms=rm["p50_ms"],
+                       same_box_reference_runs=[r["tasks_per_s"] for r in tr],
+                       vs_same_box_reference=round(med["tasks_per_s"] / rm["tasks_per_s"], 2))
         rows.append(med)
     for r in rows:
         print(json.dumps(r), flush=True)
@@ -122,7 +145,8 @@ def main():
                       "value": best["tasks_per_s"], "unit": "tasks/s", "n_gpus": 0,
                       "p50_task_latency_ms": best["p50_ms"], "clients": best["clients"],
                       "vs_reference": round(best["tasks_per_s"] / REF[best["clients"]][0], 2)
-                      if best["clients"] in REF else None}), flush=True)
+                      if best["clients"] in REF else None,
+                      "vs_same_box_reference": best.get("vs_same_box_reference")}), flush=True)
 
 
 if __name__ == "__main__":

@@ -15,6 +15,7 @@ interoperate. Intended behaviour is implemented where the reference is broken
 from __future__ import annotations
 
 import asyncio
+import os
 import uuid
 from contextlib import asynccontextmanager
 from datetime import datetime
@@ -92,6 +93,15 @@ class TaskPriority(str, Enum):
         return cls(s) if s in _PRIO_RANK else cls.MEDIUM
 
 
+def _uuid4_str() -> str:
+    """str(uuid.uuid4()) at a fifth of its cost (one urandom read, no UUID object)."""
+    b = bytearray(os.urandom(16))
+    b[6] = (b[6] & 0x0F) | 0x40
+    b[8] = (b[8] & 0x3F) | 0x80
+    h = b.hex()
+    return f"{h[:8]}-{h[8:12]}-{h[12:16]}-{h[16:20]}-{h[20:]}"
+
+
 class TaskResult(BaseModel):
     model_config = ConfigDict(arbitrary_types_allowed=True)
 
@@ -99,18 +109,19 @@ class TaskResult(BaseModel):
     output: Any = None
     error: Optional[str] = None
     execution_time: float = 0.0
-    metadata: Dict[str, Any] = {}
+    metadata: Dict[str, Any] = Field(default_factory=dict)
     resources_cleaned: bool = False
     completion_time: Optional[datetime] = None  # set at construction (model_post_init)
-    # Hot-path note: no default_factory / PrivateAttr factories here — pydantic
-    # re-inspects every factory's signature per instance, which alone cost ~40 %
-    # of the orchestration plumbing time (benchmarks/plumbing.py).
+    # Hot-path notes (benchmarks/plumbing.py, pydantic 2.13): mutable defaults use
+    # default_factory (a literal [] / {} default is deep-copied per instance, ~4x the cost),
+    # private attributes are created lazily, and model_post_init writes the instance dict
+    # directly (pydantic's __setattr__ costs ~1-2 us per assignment).
     _file_handles: Optional[Set[Any]] = PrivateAttr(default=None)
     _temp_files: Optional[Set[Path]] = PrivateAttr(default=None)
 
     def model_post_init(self, __ctx):
         if self.completion_time is None:
-            self.completion_time = datetime.now()
+            self.__dict__["completion_time"] = datetime.now()
 
     def register_file_handle(self, h: Any):
         if self._file_handles is None:
@@ -155,18 +166,18 @@ class Task(BaseModel):
     created_at: Optional[datetime] = None  # set at construction
     started_at: Optional[datetime] = None
     completed_at: Optional[datetime] = None
-    context: List["Task"] = []
-    tools: List[str] = []
-    config: Dict[str, Any] = {}
-    dependencies: List[str] = []
+    context: List["Task"] = Field(default_factory=list)
+    tools: List[str] = Field(default_factory=list)
+    config: Dict[str, Any] = Field(default_factory=dict)
+    dependencies: List[str] = Field(default_factory=list)
     output_file: Optional[Path] = None
     result: Optional[TaskResult] = None
     complexity: Optional[int] = None
-    metadata: Dict[str, Any] = {}
+    metadata: Dict[str, Any] = Field(default_factory=dict)
     # fields the reference used but never declared (App. A #15)
     parent_task_id: Optional[str] = None
-    subtasks: List[str] = []
-    required_skills: List[str] = []
+    subtasks: List[str] = Field(default_factory=list)
+    required_skills: List[str] = Field(default_factory=list)
     type: Optional[str] = None
 
     _locks: Optional[Dict[str, asyncio.Lock]] = PrivateAttr(default=None)
@@ -174,18 +185,21 @@ class Task(BaseModel):
     _temp_files: Optional[Set[Path]] = PrivateAttr(default=None)
 
     def model_post_init(self, __ctx):
-        if not self.id:
-            self.id = str(uuid.uuid4())
-        if self.created_at is None:
-            self.created_at = datetime.now()
-        if self._locks is None:
-            self._locks = {}
-        if self._file_handles is None:
-            self._file_handles = set()
-        if self._temp_files is None:
-            self._temp_files = set()
-        if self.id in self.dependencies:
-            raise ValueError(f"Circular dependency: task {self.id} depends on itself")
+        d = self.__dict__  # direct writes: pydantic's __setattr__ is the slow part of a Task
+        if not d["id"]:
+            d["id"] = _uuid4_str()
+        if d["created_at"] is None:
+            d["created_at"] = datetime.now()
+        if d["dependencies"] and d["id"] in d["dependencies"]:
+            raise ValueError(f"Circular dependency: task {d['id']} depends on itself")
+
+    # private resources, created on first use (most tasks never lock or open anything)
+    def _res(self, name: str, make):
+        priv = self.__pydantic_private__
+        v = priv.get(name)
+        if v is None:
+            v = priv[name] = make()
+        return v
 
     # -- validators -----------------------------------------------------------
     @field_validator("priority", mode="before")
@@ -221,7 +235,7 @@ class Task(BaseModel):
     async def acquire_lock(self, resource: str, timeout: float = 5.0) -> bool:
         if not resource:
             raise ValueError("Resource name cannot be empty")
-        lock = self._locks.setdefault(resource, asyncio.Lock())
+        lock = self._res("_locks", dict).setdefault(resource, asyncio.Lock())
         try:
             await asyncio.wait_for(lock.acquire(), timeout=timeout)
             return True
@@ -229,7 +243,7 @@ class Task(BaseModel):
             return False
 
     def release_lock(self, resource: str):
-        lock = self._locks.get(resource)
+        lock = (self._locks or {}).get(resource)
         if lock is not None and lock.locked():
             lock.release()
 
@@ -246,29 +260,32 @@ class Task(BaseModel):
     def register_file_handle(self, h: Any):
         if h is None:
             raise ValueError("File handle cannot be None")
-        self._file_handles.add(h)
+        self._res("_file_handles", set).add(h)
 
     def register_temp_file(self, p):
         if not p:
             raise ValueError("Path cannot be None")
-        self._temp_files.add(Path(p))
+        self._res("_temp_files", set).add(Path(p))
 
     def cleanup_resources(self):
-        for h in list(self._file_handles):
+        for h in list(self._file_handles or ()):
             try:
                 h.close()
             except Exception:  # noqa: BLE001
                 pass
-        self._file_handles.clear()
-        for p in list(self._temp_files):
+        if self._file_handles:
+            self._file_handles.clear()
+        for p in list(self._temp_files or ()):
             try:
                 p.unlink()
             except Exception:  # noqa: BLE001
                 pass
-        self._temp_files.clear()
-        for name in list(self._locks):
+        if self._temp_files:
+            self._temp_files.clear()
+        for name in list(self._locks or ()):
             self.release_lock(name)
-        self._locks.clear()
+        if self._locks:
+            self._locks.clear()
         if self.result is not None:
             self.result.cleanup_resources()
 
@@ -338,7 +355,7 @@ class Task(BaseModel):
         """Copy with updates; a fresh id/status unless keep_id (App. A #18)."""
         data = self.model_dump()
         if not keep_id:
-            data.update(id=str(uuid.uuid4()), status=TaskStatus.PENDING, result=None,
+            data.update(id=_uuid4_str(), status=TaskStatus.PENDING, result=None,
                         started_at=None, completed_at=None)
         data.update(update or {})
         data.update(kwargs)
