@@ -61,12 +61,16 @@ constexpr int PP_BUF = 4 * PP_PART;
 // PH2 (F = 8): two 32-MFMA phases per 64-k tile instead of four 16-MFMA phases (schedule at
 // `body2`); each load segment retires its own LDS reads before its barrier, so a part can be
 // restaged one phase after its last read.
+// F = 6 (PH2 only): 256 x 192 tiles, two 56-KiB buffers of [W: 24 KiB | B0 | B1] (schedule at
+// `body6`): N = 6,144 (Llama-3-8B qkv) is 32 column tiles, so M in (1,280, 2,048] fills the
+// 256 CUs in one round instead of 144-192 256 x 256 tiles.
 template <int EPI, bool NORM, bool STAMP = false, bool BUFLD = false, int F = 8, bool PH2 = false>
 __device__ __forceinline__ void pingpong_tile(const Args& A, const int bid, const int nblocks, char* smem) {
-  static_assert(F == 8 || F == 4, "256- or 128-wide tiles");
-  constexpr int NA = F / 4;                 // W parts per 64-k tile
-  constexpr int BUFB = (NA + 2) * PP_PART;  // bytes per tile buffer
-  constexpr int NBUF = F == 8 ? 2 : 3;
+  static_assert(F == 8 || F == 4 || (F == 6 && PH2 && !BUFLD), "256-, 192- or 128-wide tiles");
+  constexpr int NA = F / 4;                 // W parts per 64-k tile (F = 8, 4)
+  constexpr int WB = F == 6 ? 24 * 1024 : NA * PP_PART;  // W bytes per tile buffer
+  constexpr int BUFB = WB + 2 * PP_PART;    // bytes per tile buffer
+  constexpr int NBUF = F == 4 ? 3 : 2;
   constexpr int SLABF = 256 * 32 * F;       // floats per split slab
   uint64_t st0 = 0, st1 = 0, st2 = 0, rt0 = 0;
   if constexpr (STAMP) {
@@ -121,7 +125,7 @@ __device__ __forceinline__ void pingpong_tile(const Args& A, const int bid, cons
   auto buf = [&](int t) -> char* { return sbase + (NBUF == 2 ? (t & 1) : (t % 3)) * BUFB; };
 
   // flat sources (BUFLD = false)
-  const bf16* wsrc[2];
+  const bf16* wsrc[F == 6 ? 3 : 2];
   const bf16* xsrc[2][2];
   // buffer sources (BUFLD = true): the tile's W panel and x as buffer resources
   const __amdgpu_buffer_rsrc_t wrs =
@@ -136,6 +140,18 @@ __device__ __forceinline__ void pingpong_tile(const Args& A, const int bid, cons
     for (int cc = 0; cc < 2; ++cc)
 #pragma unroll
       for (int h = 0; h < 2; ++h) xoff[cc][h] = (uint32_t)(((size_t)xrow[cc][h] * A.ldx + xunit[cc][h] * 8) * 2);
+  } else if constexpr (F == 6) {
+    // 24 W chunks per 64-k tile, three per wave: chunk q = 3 wid + j is k-half (q & 1) of
+    // n-frag (q % 12) >> 1 of group q / 12, at LDS offset q KiB
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const int q = 3 * wid + j;
+      wsrc[j] = A.wp + ((size_t)(nt * 12 + (q / 12) * 6 + ((q % 12) >> 1)) * KS + (q & 1)) * 512 + lane * 8;
+    }
+#pragma unroll
+    for (int cc = 0; cc < 2; ++cc)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) xsrc[cc][h] = A.x + (size_t)xrow[cc][h] * A.ldx + xunit[cc][h] * 8;
   } else {
 #pragma unroll
     for (int r = 0; r < NA; ++r)
@@ -159,7 +175,7 @@ __device__ __forceinline__ void pingpong_tile(const Args& A, const int bid, cons
     }
   };
   auto issue_x = [&](int cc, int t) {
-    char* dst = buf(t) + (NA + cc) * PP_PART + (2 * wid) * 1024;
+    char* dst = buf(t) + WB + cc * PP_PART + (2 * wid) * 1024;
     if constexpr (BUFLD) {
       const int so = (kt0 + t) * 128;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (lds_t*)dst, 16, xoff[cc][0], so, 0, 0);
@@ -179,8 +195,23 @@ __device__ __forceinline__ void pingpong_tile(const Args& A, const int bid, cons
 #pragma unroll
       for (int h = 0; h < 2; ++h) af[i][h] = *reinterpret_cast<const bf16x8*>(p + (2 * i + h) * 1024);
   };
+  // F = 6: all 24 W chunks of tile t, three per wave
+  auto issue_w6 = [&](int t) {
+    char* dst = buf(t) + (3 * wid) * 1024;
+    const size_t ko = (size_t)(2 * (kt0 + t)) * 512;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) glds16(wsrc[j] + ko, dst + j * 1024);
+  };
+  // F = 6: n-frags 3 p .. 3 p + 2 of this wave's group (x 2 k-halves)
+  auto read_w6 = [&](int p, int t, bf16x8(&af)[3][2]) {
+    const char* s = buf(t) + (G * 12 + 6 * p) * 1024 + lane * 16;
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) af[i][h] = *reinterpret_cast<const bf16x8*>(s + (2 * i + h) * 1024);
+  };
   auto read_x = [&](int cc, int t, bf16x8(&bfr)[2][2]) {
-    const char* p = buf(t) + (NA + cc) * PP_PART;
+    const char* p = buf(t) + WB + cc * PP_PART;
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const int lr = wc * 32 + 16 * j + c;
@@ -228,7 +259,23 @@ __device__ __forceinline__ void pingpong_tile(const Args& A, const int bid, cons
     __builtin_amdgcn_s_setprio(0);
   };
 
+  // 24 MFMAs: n-frags 3 p .. 3 p + 2 x all 4 token frags x K = 64 (F = 6)
+  auto mma24 = [&](auto pp, const bf16x8(&af)[3][2], const bf16x8(&b0)[2][2], const bf16x8(&b1)[2][2]) {
+    constexpr int p = decltype(pp)::value;
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[3 * p + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][h], j < 2 ? b0[j][h] : b1[j - 2][h],
+                                                                      acc[3 * p + i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
   bf16x8 af[4][2], bx0[2][2], bx1[2][2];
+  bf16x8 a6[3][2];
 
   // One 64-k tile. ST: 0 steady (tiles t + 1 and t + 2 exist), 1 = tile nk - 2 (only t + 1
   // left to issue), 2 = the last tile.
@@ -350,8 +397,54 @@ __device__ __forceinline__ void pingpong_tile(const Args& A, const int bid, cons
     raw_barrier();
   };
 
+  // 256 x 192 tiles, two phases per 64-k tile (F = 6):
+  //     phase  reads (tile t)               MFMA                  LDS-DMA issued       vmcnt
+  //     0      W n 0-2 (6), B0 (4), B1 (4)  n 0-2 x (B0, B1)      W of tile t + 1        -
+  //     1      W n 3-5 (6)                  n 3-5 x (B0, B1)      B0, B1 of tile t + 2   4
+  // W of a tile is read in both phases, so W(t + 1) goes into the other buffer after the
+  // barrier that ends tile t - 1; B0 / B1 are read in phase 0 only, so B(t + 2) is restaged
+  // in phase 1. The phase-1 wait leaves only B(t + 2) in flight: W(t + 1) and B(t + 1),
+  // read by the next phase 0, have landed. Every wave issues 3 + 4 LDS-DMA instructions per
+  // tile, so the counted waits hold for all eight.
+  auto body6 = [&](int t, auto st) {
+    constexpr int S = decltype(st)::value;  // 0 steady, 1 tile nk - 2, 2 the last tile
+    read_w6(0, t, a6);
+    read_x(0, t, bx0);
+    read_x(1, t, bx1);
+    if constexpr (S < 2) issue_w6(t + 1);
+    lgkm0();
+    raw_barrier();
+    mma24(ic<0>{}, a6, bx0, bx1);
+    raw_barrier();
+    read_w6(1, t, a6);
+    if constexpr (S == 0) {
+      issue_x(0, t + 2);
+      issue_x(1, t + 2);
+      wait_vm<4>();
+    } else if constexpr (S == 1) {
+      wait_vm<0>();
+    }
+    lgkm0();
+    raw_barrier();
+    mma24(ic<1>{}, a6, bx0, bx1);
+    raw_barrier();
+  };
+
   int t = 0;
-  if constexpr (F == 8 && PH2) {
+  if constexpr (F == 6) {
+    issue_x(0, 0);
+    issue_x(1, 0);
+    issue_w6(0);
+    issue_x(0, 1);
+    issue_x(1, 1);
+    wait_vm<4>();  // B0, B1 and W of tile 0 landed
+    raw_barrier();
+    if (G == 1) raw_barrier();
+    if constexpr (STAMP) st1 = __builtin_amdgcn_s_memtime();
+    for (; t + 2 < nk; ++t) body6(t, ic<0>{});
+    body6(t, ic<1>{});
+    body6(t + 1, ic<2>{});
+  } else if constexpr (F == 8 && PH2) {
     issue_w(0, 0);
     issue_x(0, 0);
     issue_x(1, 0);
@@ -435,7 +528,7 @@ __device__ __forceinline__ void pingpong_tile(const Args& A, const int bid, cons
   }
 
   // ---- register epilogue: acc[i][j] holds token row0 + 64 wc + 16 j + c, columns
-  // 4 g .. 4 g + 3 of 16-column tile nt * 16 + 8 G + i
+  // 4 g .. 4 g + 3 of 16-column tile nt * 2F + F G + i
   const float inv_k = 1.f / (float)A.K;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
@@ -490,7 +583,7 @@ __device__ __forceinline__ void pingpong_tile(const Args& A, const int bid, cons
 // One tile family per launch: the whole grid runs pingpong_tile.
 template <int EPI, bool NORM, bool STAMP = false, bool BUFLD = false, int F = 8, bool PH2 = false>
 __global__ __launch_bounds__(512) void pingpong_gemm_kernel(const Args A) {
-  __shared__ __attribute__((aligned(1024))) char smem[(F == 8 ? 2 * 4 : 3 * 3) * PP_PART];
+  __shared__ __attribute__((aligned(1024))) char smem[(F == 8 ? 2 * 4 : F == 6 ? 7 : 3 * 3) * PP_PART];
   pingpong_tile<EPI, NORM, STAMP, BUFLD, F, PH2>(A, blockIdx.x, gridDim.x, smem);
 }
 

@@ -667,7 +667,7 @@ extern "C" int pa_prefill_gemm(void* y, const void* x, const void* wp, const voi
   using namespace pa::pf;
   if (M <= 0) return 0;
   if (bn <= 0) bn = pick_bn(M, N);
-  if (bn != 128 && bn != 256) return 1;
+  if (bn != 128 && bn != 192 && bn != 256) return 1;
   if (K % 64 != 0 || N % bn != 0 || epi < 0 || epi > 4 || ldx % 8 != 0) return 1;
   const int norm = ss_in != nullptr;
   if (epi == EP_RESID && (!resid || norm)) return 1;
@@ -690,6 +690,7 @@ extern "C" int pa_prefill_gemm(void* y, const void* x, const void* wp, const voi
   // the ping-pong kernel's schedule needs >= 2 k-tiles per work item
   int variant = kernel_variant >= 0 ? kernel_variant : g_pf_variant;
   if (variant >= 3 && (KT < 2 || (S > 1 && (per < 2 || KT - (S - 1) * per < 2)))) variant = 1;
+  if (bn == 192 && variant < 3) return 1;  // 256 x 192 tiles: ping-pong schedule only
   if (full < tiles) {
     const long long need = (long long)(tiles - full) * S * (256 * bn);
     if (!ws || !counters || n_counters < tiles - full || need > ws_floats) return 1;
@@ -740,7 +741,8 @@ extern "C" int pa_prefill_gemm(void* y, const void* x, const void* wp, const voi
 #define PA_PF(E, NRM)                                                                                \
   do {                                                                                               \
     const bool stamp = E == EP_PLAIN && !NRM && full == tiles;                                       \
-    if (bn == 128 && variant == 4 && stamp)                                                          \
+    if (bn == 192) hipLaunchKernelGGL((pingpong_gemm_kernel<E, NRM, false, false, 6, true>), dim3(grid), dim3(512), 0, st, a); \
+    else if (bn == 128 && variant == 4 && stamp)                                                     \
       hipLaunchKernelGGL((pingpong_gemm_kernel<EP_PLAIN, false, true, false, 4>), dim3(grid), dim3(512), 0, st, a); \
     else if (bn == 128 && variant >= 3) hipLaunchKernelGGL((pingpong_gemm_kernel<E, NRM, false, false, 4>), dim3(grid), dim3(512), 0, st, a); \
     else if (bn == 128) hipLaunchKernelGGL((prefill_gemm_n128_kernel<E, NRM>), dim3(grid), dim3(512), 0, st, a); \

@@ -181,10 +181,16 @@ class LlamaModel:
     # 256 rows; profiles/r3_midrange_pf_vs_mid.jsonl: from 192 rows the 256 x 128 prefill tiles
     # beat the mid kernel's 128-256-row tiles, e.g. qkv 50.1 -> 27.5 us and o 40.9 -> 25.8 at
     # 256 rows, because the mid tiles' x panel leaves LDS room for one 64-k chunk in flight;
-    # crossovers from profiles/r3_midrange_fused_sweep.jsonl: qkv above 80 rows, the others above 128)
+    # crossovers from profiles/r3_midrange_fused_sweep.jsonl: qkv above 80 rows, the others above 128).
+    # qkv above 1,280 rows: 256 x 192 tiles (bn 192, N % 192 == 0, else 256) where their whole
+    # rounds beat the 256 x 256 tiles' rounds + split tail: 1,281-2,048 rows (one round of 192-256
+    # tiles instead of 144-192 wide ones) and from 3,841 (profiles/r5_qkv_192_tiles.jsonl: RoPE +
+    # KV-write epilogue 71.9 / 77.1 / 84.7 / 164.3 us at 1,536 / 1,792 / 2,048 / 4,096 rows vs
+    # 83.9 / 87.2 / 94.2 / 181.7 on 256 x 256 tiles; plain 2,048 rows 76.2 us vs hipBLASLt 80.1)
     PF_CFG = {
         "qkv": [(80, "mid", {}), (640, "pf", {"bn": 128, "variant": 1}), (1280, "pf", {"bn": 128, "variant": 3}),
-                (1 << 30, "pf", {"bn": 256, "variant": 3})],
+                (2048, "pf", {"bn": 192, "variant": 3}), (3840, "pf", {"bn": 256, "variant": 3}),
+                (1 << 30, "pf", {"bn": 192, "variant": 3})],
         "o": [(128, "mid", {}), (1280, "pf", {"bn": 128, "variant": 1}),
               (1 << 30, "pf", {"bn": 128, "variant": 3})],
         "gate_up": [(128, "mid", {}), (256, "pf", {"bn": 128, "variant": 1}),
@@ -559,7 +565,12 @@ class LlamaModel:
         if self.device.type == "cuda" and (T > self.MID_MAX_T or kind in self.PF_MIDRANGE):
             for mmax, path, cfg in self.PF_CFG[kind]:
                 if T <= mmax:
-                    return path, (dict(cfg) if path == "pf" else self._mid_cfg(kind, T) | dict(cfg))
+                    if path != "pf":
+                        return path, self._mid_cfg(kind, T) | dict(cfg)
+                    cfg = dict(cfg)
+                    if cfg.get("bn") == 192 and N % 192:  # 256 x 192 tiles need N % 192 == 0
+                        cfg["bn"] = 256
+                    return path, cfg
         return "mid", self._mid_cfg(kind, T)
 
     def _gemm(self, kind: str, T: int, x, wp, epi: str, **kw):

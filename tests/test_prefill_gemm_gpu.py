@@ -1,5 +1,5 @@
-"""Large-M packed-weight projections (csrc/ops/gemm_prefill.hip: 256 x 256 and 256 x 128
-MFMA tiles, LDS-DMA stages, fused epilogues) vs fp32 PyTorch references."""
+"""Large-M packed-weight projections (csrc/ops/gemm_prefill.hip: 256 x 256, 256 x 192 and
+256 x 128 MFMA tiles, LDS-DMA stages, fused epilogues) vs fp32 PyTorch references."""
 import pytest
 import torch
 
@@ -61,11 +61,34 @@ def _check_prefill_gemm(gpu, M, N, K, epi, norm, full, splits, bn):
         torch.testing.assert_close(y.float(), acc, atol=4e-2, rtol=2e-2)
 
 
-@pytest.mark.parametrize("bn", [256, 128])
+@pytest.mark.parametrize("M,N,K,epi,norm,full,splits", [
+    # qkv of Llama-3-8B at 1,280 < M <= 2,048 (one round of 256 x 192 tiles)
+    (2048, 6144, 4096, "rope_perm", True, -1, 0), (1536, 6144, 4096, "plain", False, -1, 1),
+    (1300, 6144, 4096, "plain", True, -1, 0),
+    # K-sliced items, every epilogue, partial row tiles, two k-tiles per item
+    (777, 6144, 4096, "plain", True, 0, 3), (513, 6144, 4096, "silu", True, 10, 2),
+    (1000, 6144, 14336, "resid", False, 0, 4), (300, 1536, 128, "resid", False, -1, 1),
+    (2100, 11520, 512, "rope_perm", True, -1, 0), (64, 384, 256, "plain", False, 0, 2)])
+def test_prefill_gemm_192(gpu, M, N, K, epi, norm, full, splits):
+    """256 x 192 tiles (gemm_pingpong.h F = 6, `body6` schedule) vs fp32: whole tiles and
+    K-slices, every register epilogue."""
+    _check_prefill_gemm(gpu, M, N, K, epi, norm, full, splits, 192)
+
+
+def test_prefill_gemm_192_refuses_other_widths(gpu):
+    """bn = 192 needs N % 192 == 0 and the ping-pong schedule: anything else is refused at
+    the launcher instead of running a partial tile."""
+    x = _bf(512, 512, dev=gpu)
+    wp = ops.pack_decode_weight(_bf(1024, 512, dev=gpu))
+    with pytest.raises(ValueError, match="does not handle"):
+        ops.prefill_gemm(x, wp, "plain", bn=192)
+
+
+@pytest.mark.parametrize("bn", [256, 192, 128])
 def test_prefill_gemm_asymmetric_identity(gpu, bn):
     """x = I (rows), W asymmetric: the output must be exactly W^T's rows (catches a
     transposed or permuted C write, guide §3 'A = I-check with asymmetric B')."""
-    M, N, K = 512, 1024, 512
+    M, N, K = 512, 1152 if bn == 192 else 1024, 512
     x = torch.zeros(M, K, device=gpu)
     x[torch.arange(M), torch.arange(M) % K] = 1.0
     w = (torch.arange(N * K, device=gpu, dtype=torch.float32).view(N, K) % 251 / 64.0).to(torch.bfloat16)
@@ -103,8 +126,9 @@ def test_prefill_gemm_resid_in_place_with_row_stats(gpu, M, S, bn):
 
 
 @pytest.mark.parametrize("M,H,KV,K,full,splits", [
-    (1024, 32, 8, 4096, -1, 0), (333, 32, 8, 4096, 0, 4), (600, 8, 2, 1024, -1, 1), (2048, 32, 8, 4096, 0, 2)])
-@pytest.mark.parametrize("bn", [256, 128])
+    (1024, 32, 8, 4096, -1, 0), (333, 32, 8, 4096, 0, 4), (600, 8, 2, 1024, -1, 1), (2048, 32, 8, 4096, 0, 2),
+    (1792, 32, 8, 4096, -1, 0)])
+@pytest.mark.parametrize("bn", [256, 192, 128])
 def test_prefill_qkv_rope(gpu, M, H, KV, K, full, splits, bn):
     """Norm-folded QKV with RoPE + paged KV write vs fp32 projection + reference rope_cache."""
     torch.manual_seed(23)

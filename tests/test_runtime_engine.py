@@ -479,6 +479,23 @@ def test_stream_routing_is_shape_checked():
     assert m._proj_path("o", 100, 1024, 1024)[0] == "mid"  # beyond the table
 
 
+def test_qkv_wide_tile_routing():
+    """qkv steps above 1,280 rows pick 256 x 192 tiles where they fill whole rounds, and fall
+    back to 256-wide tiles when N is not a multiple of 192 (a TP shard, the 70B model)."""
+    import types
+
+    from pilottai_amd.models.llama import LlamaModel
+
+    m = LlamaModel.__new__(LlamaModel)
+    m.STREAM_CFG, m.STREAM_NK, m.MID_MAX_T, m.PF_MIDRANGE = {}, {}, 256, frozenset()
+    m.PF_CFG, m.MID_CFG = LlamaModel.PF_CFG, LlamaModel.MID_CFG
+    m.device = types.SimpleNamespace(type="cuda")
+    bn = {T: m._proj_path("qkv", T, 6144, 4096)[1]["bn"] for T in (1024, 1536, 2048, 2304, 4096)}
+    assert bn == {1024: 128, 1536: 192, 2048: 192, 2304: 256, 4096: 192}
+    assert m._proj_path("qkv", 2048, 5120, 8192) == ("pf", {"bn": 256, "variant": 3})
+    assert LlamaModel.PF_CFG["qkv"][3][2]["bn"] == 192  # the table itself is not rewritten
+
+
 def test_engine_fails_on_custom_allreduce_timeout():
     """A TP peer that stalls past the custom all-reduce's spin budget sets its error word;
     the engine must stop with an error instead of stepping on with partial sums."""

@@ -120,6 +120,26 @@ for name in a.shapes.split(","):
             "mid_fused": lambda i: kernels.mid_gemm(x, fps[i], epi, out=yf if epi == "silu" else y, resid=resid,
                                                     norm=nrm, ss_in=ss if nrm else None),
         }
+        for bn_ in (192, 256, 128):  # 256 x bn_ ping-pong tiles, plain and fused
+            if N % bn_ == 0:
+                variants[f"pp{bn_}w"] = (lambda bn_: lambda i: v0(lambda: kernels.prefill_gemm(
+                    x, wps[i], "plain", out=y, bn=bn_), 3))(bn_)
+                variants[f"pp{bn_}w_fused"] = (lambda bn_: lambda i: v0(lambda: kernels.prefill_gemm(
+                    x, fps[i], epi, out=yf if epi == "silu" else y, resid=resid, norm=nrm,
+                    ss_in=ss if nrm else None, bn=bn_), 3))(bn_)
+        if name == "qkv":  # the engine's qkv call: RMSNorm folded, RoPE + paged KV write epilogue
+            from pilottai_amd.ops import reference as _ref
+            H, KV = 32, 8
+            NB = (M + 15) // 16 + 4
+            cs = _ref.rope_cos_sin(8192).cuda()
+            pos = torch.arange(M, dtype=torch.int32, device="cuda")
+            slots = torch.arange(M, dtype=torch.int32, device="cuda")
+            kc = torch.zeros(NB, KV, 16, 16, 8, dtype=torch.bfloat16, device="cuda")
+            vc = torch.zeros(NB, KV, 128, 16, dtype=torch.bfloat16, device="cuda")
+            qo = torch.empty(M, H, 128, dtype=torch.bfloat16, device="cuda")
+            for bn_ in (192, 256, 128):
+                variants[f"ropekv{bn_}"] = (lambda bn_: lambda i: kernels.prefill_qkv_rope(
+                    x, fps[i], 1e-5, qo, kc, vc, pos, slots, cs, H, KV, ss_in=ss, bn=bn_, variant=3))(bn_)
         for bn_ in (128, 256):  # fused epilogue on an explicit (whole tiles, K-slices) decomposition
             for S_ in (1, 2, 3, 4):
                 variants[f"pf{bn_}_s{S_}_fused"] = (lambda bn_, S_: lambda i: kernels.prefill_gemm(
@@ -155,6 +175,12 @@ for name in a.shapes.split(","):
             y.fill_(float("nan"))
             yy = v0(lambda: kernels.prefill_gemm(x, wps[0], "plain", out=y, full=-1, splits=1, bn=128), 3)
             row["err_pp128"] = float(((yy.float() - ref).abs().max() / ref.abs().max()))
+        for bn_ in (192, 256, 128):
+            if f"pp{bn_}w" in variants:
+                ref = x.float() @ ws[0].float().T
+                y.fill_(float("nan"))
+                yy = v0(lambda: kernels.prefill_gemm(x, wps[0], "plain", out=y, bn=bn_), 3)
+                row[f"err_pp{bn_}w"] = float(((yy.float() - ref).abs().max() / ref.abs().max()))
         if any(k.startswith("pp") for k in variants):
             ref = x.float() @ ws[0].float().T
             for nm, kw, vv in (("pp", {}, 3), ("pp_whole", dict(full=-1, splits=1), 3), ("pp_s2", dict(full=0, splits=2), 3),
