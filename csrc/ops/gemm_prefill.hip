@@ -592,6 +592,7 @@ __global__ __launch_bounds__(512) void prefill_gemm_n128_kernel(const Args A) {
 }  // namespace pa
 
 #include "gemm_pingpong.h"
+#include "gemm_w4.h"
 
 namespace pa {
 namespace pf {
@@ -601,7 +602,8 @@ namespace pf {
 // three-buffer schedule; items of < 2 k-tiles fall back to 1); 9 = 3 without the mixed tail;
 // 4 = its cycle-stamp build; 6 = the four-phase 256-wide schedule, 7 = its stamp build;
 // 5 = four-phase with buffer_load staging; 1 = read-ahead 8-wave 256 x 256 / 3-stage
-// 256 x 128; 0 = reads in the phase they feed; 2 = read-ahead, 4 waves of 128 x 128
+// 256 x 128; 0 = reads in the phase they feed; 2 = read-ahead, 4 waves of 128 x 128;
+// 10 = one wave per SIMD, 128 x 128 per wave, 32-k steps over four LDS stages (gemm_w4.h)
 constexpr int kPfDefaultVariant = 3;
 static int g_pf_variant = kPfDefaultVariant;
 
@@ -742,6 +744,7 @@ extern "C" int pa_prefill_gemm(void* y, const void* x, const void* wp, const voi
   do {                                                                                               \
     const bool stamp = E == EP_PLAIN && !NRM && full == tiles;                                       \
     if (bn == 192) hipLaunchKernelGGL((pingpong_gemm_kernel<E, NRM, false, false, 6, true>), dim3(grid), dim3(512), 0, st, a); \
+    else if (bn == 256 && variant == 10) hipLaunchKernelGGL((w4_gemm_kernel<E, NRM>), dim3(grid), dim3(256), 0, st, a); \
     else if (bn == 128 && variant == 4 && stamp)                                                     \
       hipLaunchKernelGGL((pingpong_gemm_kernel<EP_PLAIN, false, true, false, 4>), dim3(grid), dim3(512), 0, st, a); \
     else if (bn == 128 && variant >= 3) hipLaunchKernelGGL((pingpong_gemm_kernel<E, NRM, false, false, 4>), dim3(grid), dim3(512), 0, st, a); \

@@ -27,12 +27,13 @@ def _bf(*shape, dev, scale=1.0):
     # tail columns on 256 x 128 tiles in the same launch)
     (1024, 20480, 512, "rope_perm", True, -1, 0), (768, 24576, 256, "resid", False, -1, 0),
     (1000, 28672, 256, "plain", False, -1, 0)])
-@pytest.mark.parametrize("bn,variant", [(256, 3), (256, 9), (256, 6), (256, 1), (128, 3), (128, 1)])
+@pytest.mark.parametrize("bn,variant", [(256, 3), (256, 9), (256, 6), (256, 1), (256, 10), (128, 3), (128, 1)])
 def test_prefill_gemm(gpu, M, N, K, epi, norm, full, splits, bn, variant):
     """Every epilogue and the folded row norm; run twice so the self-resetting tickets of
     the split tail are exercised. Ping-pong kernels (variant 3, the default: two-phase
-    256-wide / three-buffer 128-wide schedules; variant 6: the four-phase 256-wide schedule)
-    and the read-ahead / 3-stage kernels (variant 1, the fallback for < 2 k-tiles)."""
+    256-wide / three-buffer 128-wide schedules; variant 6: the four-phase 256-wide schedule;
+    variant 10: four waves of 128 x 128, gemm_w4.h) and the read-ahead / 3-stage kernels
+    (variant 1, the fallback for < 2 k-tiles)."""
     from pilottai_amd.ops import kernels
 
     kernels.require_native().prefill_set_variant(variant)
@@ -84,15 +85,16 @@ def test_prefill_gemm_192_refuses_other_widths(gpu):
         ops.prefill_gemm(x, wp, "plain", bn=192)
 
 
-@pytest.mark.parametrize("bn", [256, 192, 128])
-def test_prefill_gemm_asymmetric_identity(gpu, bn):
+@pytest.mark.parametrize("bn,variant", [(256, -1), (192, -1), (128, -1), (256, 10)])
+def test_prefill_gemm_asymmetric_identity(gpu, bn, variant):
     """x = I (rows), W asymmetric: the output must be exactly W^T's rows (catches a
     transposed or permuted C write, guide §3 'A = I-check with asymmetric B')."""
     M, N, K = 512, 1152 if bn == 192 else 1024, 512
     x = torch.zeros(M, K, device=gpu)
     x[torch.arange(M), torch.arange(M) % K] = 1.0
     w = (torch.arange(N * K, device=gpu, dtype=torch.float32).view(N, K) % 251 / 64.0).to(torch.bfloat16)
-    y = ops.prefill_gemm(x.to(torch.bfloat16), ops.pack_decode_weight(w), "plain", full=-1, splits=1, bn=bn)
+    y = ops.prefill_gemm(x.to(torch.bfloat16), ops.pack_decode_weight(w), "plain", full=-1, splits=1, bn=bn,
+                         variant=variant)
     want = w.float().T[torch.arange(M) % K]
     assert torch.equal(y.float(), want.to(torch.bfloat16).float())
 

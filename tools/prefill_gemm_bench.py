@@ -127,6 +127,10 @@ for name in a.shapes.split(","):
                 variants[f"pp{bn_}w_fused"] = (lambda bn_: lambda i: v0(lambda: kernels.prefill_gemm(
                     x, fps[i], epi, out=yf if epi == "silu" else y, resid=resid, norm=nrm,
                     ss_in=ss if nrm else None, bn=bn_), 3))(bn_)
+        variants["w4"] = lambda i: v0(lambda: kernels.prefill_gemm(x, wps[i], "plain", out=y, bn=256), 10)
+        variants["w4_fused"] = lambda i: v0(lambda: kernels.prefill_gemm(
+            x, fps[i], epi, out=yf if epi == "silu" else y, resid=resid, norm=nrm, ss_in=ss if nrm else None,
+            bn=256), 10)
         if name == "qkv":  # the engine's qkv call: RMSNorm folded, RoPE + paged KV write epilogue
             from pilottai_amd.ops import reference as _ref
             H, KV = 32, 8
@@ -175,6 +179,11 @@ for name in a.shapes.split(","):
             y.fill_(float("nan"))
             yy = v0(lambda: kernels.prefill_gemm(x, wps[0], "plain", out=y, full=-1, splits=1, bn=128), 3)
             row["err_pp128"] = float(((yy.float() - ref).abs().max() / ref.abs().max()))
+        if "w4" in a.variants.split(","):
+            ref = x.float() @ ws[0].float().T
+            y.fill_(float("nan"))
+            yy = v0(lambda: kernels.prefill_gemm(x, wps[0], "plain", out=y, bn=256), 10)
+            row["err_w4"] = float(((yy.float() - ref).abs().max() / ref.abs().max()))
         for bn_ in (192, 256, 128):
             if f"pp{bn_}w" in variants:
                 ref = x.float() @ ws[0].float().T
