@@ -19,21 +19,14 @@
 //            one 1-KiB chunk per LDS-DMA wave instruction, lane-linear, conflict-free reads),
 //       B0 = token frags 0-1 of every wave, B1 = token frags 2-3 (x rows in full 128-B lines,
 //            16-B units XOR-swizzled by (row >> 1) on the SOURCE address).
-//   * default (PH2) schedule: one 64-k tile = 2 phases of 32 MFMAs, see `body2` (9 % fewer
-//     loop cycles than the four-phase schedule below, which stays as variant 6:
-//     profiles/r3_pingpong_ph2_ab.jsonl); four-phase schedule, one 64-k tile = 4 phases of
-//     16 MFMAs (one output quadrant x K = 64):
-//         phase  reads (this tile)   MFMA quadrant     LDS-DMA issued         vmcnt
-//         0      A0 (8), B0 (4)      n 0-3  x m 0-1    B1 of tile t + 1        8
-//         1      B1 (4)              n 0-3  x m 2-3    A1 of tile t + 1        8
-//         2      A1 (8)              n 4-7  x m 2-3    A0 of tile t + 2        -
-//         3      -                   n 4-7  x m 0-1    B0 of tile t + 2        8
-//     Each part is read in ONE phase, so it can be restaged two phases later (A0 / B0 of
-//     tile t + 2 after phase 0 of tile t) and four parts (64 KiB, ~4 phases) stay in flight
-//     across the raw s_barriers; the counted vmcnt before a phase's first barrier retires
-//     exactly the part(s) the next phase reads (guide: "read a staged buffer one phase after
-//     the wait that retires it"). No vmcnt(0) and no __syncthreads() inside the loop.
-//   * s_setprio(1) around every 16-MFMA cluster (guide §5.5 T5).
+//   * schedule (`body2`): one 64-k tile = 2 phases of 32 MFMAs; each load segment retires
+//     its own LDS reads (lgkmcnt(0)) before its barrier, so a part is restaged one phase after
+//     its last read, and the counted vmcnt before a phase's first barrier retires exactly the
+//     part(s) the next phase reads (guide: "read a staged buffer one phase after the wait that
+//     retires it"). No vmcnt(0) and no __syncthreads() inside the loop. (A four-phase
+//     schedule of 16-MFMA quadrants ran 9 % more loop cycles and was removed:
+//     profiles/r3_pingpong_ph2_ab.jsonl.)
+//   * s_setprio(1) around every MFMA cluster (guide §5.5 T5).
 //
 // Work items are those of the prefill launcher: whole tiles (XCD-aware bijective remap, row
 // tiles of one W panel on one XCD) and, for the remainder, K-slices whose fp32 partials
@@ -54,19 +47,14 @@ constexpr int PP_BUF = 4 * PP_PART;
 // STAMP (diagnostic build, whole tiles only): workgroup b's thread 0 writes s_memtime at
 // entry / after the prologue / after the k-loop / after the epilogue and s_memrealtime at
 // entry and exit to A.ws[8 b ..] (as uint64) -- a buffer no output is computed from.
-// BUFLD: stage through buffer_load ... lds with one per-lane 32-bit voffset per stream and the
-// k advance in the SGPR soffset (no per-issue 64-bit address arithmetic in the load segment).
-// F = W n-frags per wave: 8 -> 256 x 256 tiles (two 64-KiB buffers of parts A0 A1 B0 B1),
-// 4 -> 256 x 128 tiles (three 48-KiB buffers of parts A B0 B1; schedule at `body4`).
-// PH2 (F = 8): two 32-MFMA phases per 64-k tile instead of four 16-MFMA phases (schedule at
-// `body2`); each load segment retires its own LDS reads before its barrier, so a part can be
-// restaged one phase after its last read.
-// F = 6 (PH2 only): 256 x 192 tiles, two 56-KiB buffers of [W: 24 KiB | B0 | B1] (schedule at
-// `body6`): N = 6,144 (Llama-3-8B qkv) is 32 column tiles, so M in (1,280, 2,048] fills the
-// 256 CUs in one round instead of 144-192 256 x 256 tiles.
-template <int EPI, bool NORM, bool STAMP = false, bool BUFLD = false, int F = 8, bool PH2 = false>
+// F = W n-frags per wave: 8 -> 256 x 256 tiles (two 64-KiB buffers of parts A0 A1 B0 B1,
+// schedule at `body2`); 6 -> 256 x 192 tiles (two 56-KiB buffers of [W: 24 KiB | B0 | B1],
+// schedule at `body6`: N = 6,144, Llama-3-8B qkv, is 32 column tiles, so M in
+// (1,280, 2,048] fills the 256 CUs in one round instead of 144-192 256 x 256 tiles);
+// 4 -> 256 x 128 tiles (three 48-KiB buffers of parts A B0 B1, schedule at `body4`).
+template <int EPI, bool NORM, bool STAMP = false, int F = 8>
 __device__ __forceinline__ void pingpong_tile(const Args& A, const int bid, const int nblocks, char* smem) {
-  static_assert(F == 8 || F == 4 || (F == 6 && PH2 && !BUFLD), "256-, 192- or 128-wide tiles");
+  static_assert(F == 8 || F == 6 || F == 4, "256-, 192- or 128-wide tiles");
   constexpr int NA = F / 4;                 // W parts per 64-k tile (F = 8, 4)
   constexpr int WB = F == 6 ? 24 * 1024 : NA * PP_PART;  // W bytes per tile buffer
   constexpr int BUFB = WB + 2 * PP_PART;    // bytes per tile buffer
@@ -124,23 +112,9 @@ __device__ __forceinline__ void pingpong_tile(const Args& A, const int bid, cons
   char* const sbase = smem;
   auto buf = [&](int t) -> char* { return sbase + (NBUF == 2 ? (t & 1) : (t % 3)) * BUFB; };
 
-  // flat sources (BUFLD = false)
   const bf16* wsrc[F == 6 ? 3 : 2];
   const bf16* xsrc[2][2];
-  // buffer sources (BUFLD = true): the tile's W panel and x as buffer resources
-  const __amdgpu_buffer_rsrc_t wrs =
-      __builtin_amdgcn_make_buffer_rsrc((void*)(A.wp + (size_t)nt * 2 * F * KS * 512), 0, 2 * F * KS * 1024, 0x00020000);
-  const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)A.x, 0, (int)min(((long long)(A.M - 1) * A.ldx + A.K) * 2, 0x7fffffffll), 0x00020000);
-  uint32_t woff[2] = {0, 0}, xoff[2][2] = {{0, 0}, {0, 0}};
-  if constexpr (BUFLD) {
-#pragma unroll
-    for (int r = 0; r < NA; ++r) woff[r] = (uint32_t)(((G * F + r * 4 + wc) * KS * 512 + lane * 8) * 2);
-#pragma unroll
-    for (int cc = 0; cc < 2; ++cc)
-#pragma unroll
-      for (int h = 0; h < 2; ++h) xoff[cc][h] = (uint32_t)(((size_t)xrow[cc][h] * A.ldx + xunit[cc][h] * 8) * 2);
-  } else if constexpr (F == 6) {
+  if constexpr (F == 6) {
     // 24 W chunks per 64-k tile, three per wave: chunk q = 3 wid + j is k-half (q & 1) of
     // n-frag (q % 12) >> 1 of group q / 12, at LDS offset q KiB
 #pragma unroll
@@ -163,28 +137,15 @@ __device__ __forceinline__ void pingpong_tile(const Args& A, const int bid, cons
   }
   auto issue_w = [&](int r, int t) {
     char* dst = buf(t) + r * PP_PART + (2 * wid) * 1024;
-    if constexpr (BUFLD) {
-      const int so = (kt0 + t) * 2048;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, (lds_t*)dst, 16, woff[r], so, 0, 0);
-      // (the instruction offset would move the LDS address too: advance soffset instead)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, (lds_t*)(dst + 1024), 16, woff[r], so + 1024, 0, 0);
-    } else {
-      const bf16* s = wsrc[r] + (size_t)(2 * (kt0 + t)) * 512;
-      glds16(s, dst);
-      glds16(s + 512, dst + 1024);
-    }
+    const bf16* s = wsrc[r] + (size_t)(2 * (kt0 + t)) * 512;
+    glds16(s, dst);
+    glds16(s + 512, dst + 1024);
   };
   auto issue_x = [&](int cc, int t) {
     char* dst = buf(t) + WB + cc * PP_PART + (2 * wid) * 1024;
-    if constexpr (BUFLD) {
-      const int so = (kt0 + t) * 128;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (lds_t*)dst, 16, xoff[cc][0], so, 0, 0);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (lds_t*)(dst + 1024), 16, xoff[cc][1], so, 0, 0);
-    } else {
-      const size_t ko = (size_t)(kt0 + t) * 64;
-      glds16(xsrc[cc][0] + ko, dst);
-      glds16(xsrc[cc][1] + ko, dst + 1024);
-    }
+    const size_t ko = (size_t)(kt0 + t) * 64;
+    glds16(xsrc[cc][0] + ko, dst);
+    glds16(xsrc[cc][1] + ko, dst + 1024);
   };
   // fragment reads: W frags of part r (4 n-frags x 2 k-halves), x frags of part cc
   // (2 token frags x 2 k-halves)
@@ -277,54 +238,6 @@ __device__ __forceinline__ void pingpong_tile(const Args& A, const int bid, cons
   bf16x8 af[4][2], bx0[2][2], bx1[2][2];
   bf16x8 a6[3][2];
 
-  // One 64-k tile. ST: 0 steady (tiles t + 1 and t + 2 exist), 1 = tile nk - 2 (only t + 1
-  // left to issue), 2 = the last tile.
-  // STAMP: s_memtime on arrival at each of the 8 barriers of k-tile 8 (lane 0 of every wave)
-  uint64_t tb[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  auto pbar = [&](int t, int k) {
-    if constexpr (STAMP) {
-      if (t == 8) tb[k] = __builtin_amdgcn_s_memtime();
-    }
-    raw_barrier();
-  };
-  auto body = [&](int t, auto st) {
-    constexpr int S = decltype(st)::value;
-    // phase 0
-    read_w(0, t, af);
-    read_x(0, t, bx0);
-    if constexpr (S < 2) issue_x(1, t + 1);
-    if constexpr (S < 2) wait_vm<8>(); else wait_vm<2>();
-    pbar(t, 0);
-    lgkm0();
-    mma(ic<0>{}, ic<0>{}, af, bx0);
-    pbar(t, 1);
-    // phase 1
-    read_x(1, t, bx1);
-    if constexpr (S < 2) issue_w(1, t + 1);
-    if constexpr (S < 2) wait_vm<8>(); else wait_vm<0>();
-    pbar(t, 2);
-    lgkm0();
-    mma(ic<0>{}, ic<1>{}, af, bx1);
-    pbar(t, 3);
-    // phase 2
-    read_w(1, t, af);
-    if constexpr (S == 0) issue_w(0, t + 2);
-    pbar(t, 4);
-    lgkm0();
-    mma(ic<1>{}, ic<1>{}, af, bx1);
-    pbar(t, 5);
-    // phase 3
-    if constexpr (S == 0) {
-      issue_x(0, t + 2);
-      wait_vm<8>();
-    } else if constexpr (S == 1) {
-      wait_vm<4>();
-    }
-    pbar(t, 6);
-    mma(ic<1>{}, ic<0>{}, af, bx0);
-    pbar(t, 7);
-  };
-
   // 256 x 128 tiles: one 64-k tile = 2 phases, three buffers
   //     phase  reads (tile t)   MFMA        LDS-DMA issued            vmcnt
   //     0      A (8), B0 (4)    A x B0      A, B0 of tile t + 2       10
@@ -361,7 +274,7 @@ __device__ __forceinline__ void pingpong_tile(const Args& A, const int bid, cons
     raw_barrier();
   };
 
-  // 256 x 256 tiles, two phases per 64-k tile (PH2):
+  // 256 x 256 tiles, two phases per 64-k tile:
   //     phase  reads (tile t)          MFMA              LDS-DMA issued          vmcnt
   //     0      A0 (8), B0 (4), B1 (4)  A0 x (B0, B1)     B1, A1 of tile t + 1      8
   //     1      A1 (8)                  A1 x (B0, B1)     A0, B0 of tile t + 2      6
@@ -444,7 +357,7 @@ __device__ __forceinline__ void pingpong_tile(const Args& A, const int bid, cons
     for (; t + 2 < nk; ++t) body6(t, ic<0>{});
     body6(t, ic<1>{});
     body6(t + 1, ic<2>{});
-  } else if constexpr (F == 8 && PH2) {
+  } else if constexpr (F == 8) {
     issue_w(0, 0);
     issue_x(0, 0);
     issue_x(1, 0);
@@ -458,21 +371,6 @@ __device__ __forceinline__ void pingpong_tile(const Args& A, const int bid, cons
     for (; t + 2 < nk; ++t) body2(t, ic<0>{});
     body2(t, ic<1>{});
     body2(t + 1, ic<2>{});
-  } else if constexpr (F == 8) {
-    // prologue: parts of tiles 0 and 1 in steady-state issue order
-    issue_w(0, 0);
-    issue_x(0, 0);
-    issue_x(1, 0);
-    issue_w(1, 0);
-    issue_w(0, 1);
-    issue_x(0, 1);
-    wait_vm<8>();  // A0 and B0 of tile 0 landed
-    raw_barrier();
-    if (G == 1) raw_barrier();  // stagger: group 1 runs half a phase behind group 0
-    if constexpr (STAMP) st1 = __builtin_amdgcn_s_memtime();
-    for (; t + 2 < nk; ++t) body(t, ic<0>{});
-    body(t, ic<1>{});
-    body(t + 1, ic<2>{});
   } else {
     issue_w(0, 0);
     issue_x(0, 0);
@@ -571,20 +469,15 @@ __device__ __forceinline__ void pingpong_tile(const Args& A, const int bid, cons
 #pragma unroll
       for (int q = 0; q < 8; ++q) __hip_atomic_store(d + q, v[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    if (lane == 0) {  // per-wave barrier arrivals of k-tile 8: A.ws[8 * nblocks + (b * 8 + wid) * 8 ..]
-      uint64_t* d = reinterpret_cast<uint64_t*>(A.ws) + (size_t)nblocks * 8 + ((size_t)bid * 8 + wid) * 8;
-#pragma unroll
-      for (int q = 0; q < 8; ++q) __hip_atomic_store(d + q, tb[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
   }
 }
 
 
 // One tile family per launch: the whole grid runs pingpong_tile.
-template <int EPI, bool NORM, bool STAMP = false, bool BUFLD = false, int F = 8, bool PH2 = false>
+template <int EPI, bool NORM, bool STAMP = false, int F = 8>
 __global__ __launch_bounds__(512) void pingpong_gemm_kernel(const Args A) {
   __shared__ __attribute__((aligned(1024))) char smem[(F == 8 ? 2 * 4 : F == 6 ? 7 : 3 * 3) * PP_PART];
-  pingpong_tile<EPI, NORM, STAMP, BUFLD, F, PH2>(A, blockIdx.x, gridDim.x, smem);
+  pingpong_tile<EPI, NORM, STAMP, F>(A, blockIdx.x, gridDim.x, smem);
 }
 
 // Full rounds of 256 x 256 tiles, then the remaining columns as 256 x 128 tiles in the same
@@ -595,9 +488,9 @@ template <int EPI, bool NORM>
 __global__ __launch_bounds__(512) void pingpong_mixed_kernel(const Args A, const Args B, const int nbig) {
   __shared__ __attribute__((aligned(1024))) char smem[9 * PP_PART];
   if ((int)blockIdx.x < nbig)
-    pingpong_tile<EPI, NORM, false, false, 8, true>(A, blockIdx.x, nbig, smem);
+    pingpong_tile<EPI, NORM, false, 8>(A, blockIdx.x, nbig, smem);
   else
-    pingpong_tile<EPI, NORM, false, false, 4, false>(B, blockIdx.x - nbig, gridDim.x - nbig, smem);
+    pingpong_tile<EPI, NORM, false, 4>(B, blockIdx.x - nbig, gridDim.x - nbig, smem);
 }
 
 }  // namespace pf

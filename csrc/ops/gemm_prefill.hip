@@ -21,10 +21,11 @@
 //     16-row fragment read conflict-free under the ds_read_b128 lane groups;
 //   * a 64-k tile is four 16-KiB "pieces" [x rows lo | x rows hi | W k0 | W k1] in one of
 //     two buffers (128 KiB LDS, one workgroup per CU). Each of the tile's four phases
-//     (rows lo/hi x k halves, 16 MFMAs per wave) issues one piece of a LATER tile and waits
-//     with a counted vmcnt(8) — four pieces (8 LDS-DMA loads per lane) stay in flight
-//     across the raw s_barrier of every phase; a piece is overwritten only two barriers
-//     after its last read (one barrier per phase, no vmcnt(0) inside the loop);
+//     (rows lo/hi x k halves, 16 MFMAs per wave) reads the NEXT phase's fragments ahead and
+//     issues one piece of tile i + 2 with a counted vmcnt — pieces stay in flight across the
+//     raw s_barrier of every phase (schedule table at the read-ahead body below). This is
+//     the fallback family (variant 1: work items of one k-tile) next to the ping-pong
+//     kernels of gemm_pingpong.h;
 //   * s_setprio(1) around each MFMA cluster keeps hipcc from moving the MFMAs across the
 //     barriers (guide §5.5 T5);
 //   * tiles are numbered row-tile fastest and mapped XCD-aware, so the 8 row tiles that
@@ -98,11 +99,9 @@ constexpr int SLAB = 256 * 256;       // floats per split slab
 template <int V>
 using ic = std::integral_constant<int, V>;
 
-template <int EPI, bool NORM, bool RA, int NW>
-__global__ __launch_bounds__(NW * 64) void prefill_gemm_kernel(const Args A) {
-  // NW = 8: 2 x 4 waves of 128 x 64 outputs; NW = 4: 2 x 2 waves of 128 x 128 (one wave per
-  // SIMD, 256 accumulator registers, half the fragment reads per MFMA)
-  static_assert(NW == 4 || NW == 8, "4 or 8 waves");
+template <int EPI, bool NORM>
+__global__ __launch_bounds__(512) void prefill_gemm_kernel(const Args A) {
+  constexpr int NW = 8;           // 2 x 4 waves of 128 x 64 outputs
   constexpr int WCN = NW / 2;     // wave columns
   constexpr int CPW = 16 / WCN;   // 16-column fragments per wave
   constexpr int LPW = 16 / NW;    // LDS-DMA loads per lane per 16-KiB piece
@@ -200,42 +199,9 @@ __global__ __launch_bounds__(NW * 64) void prefill_gemm_kernel(const Args A) {
 
   char* const b0 = smem;
   char* const b1 = smem + BUF;
-  bf16x8 bk0[CPW], bk1[CPW], af[4];
+  bf16x8 bk0[CPW], bk1[CPW];
 
-  // One 64-k tile in four phases. ISS: pieces of the next tiles are issued (main loop:
-  // B-k1 and x-hi of tile i + 1 in phases 0/1, B-k0 and x-lo of tile i + 2 in phases 2/3);
-  // W0/W1/W3: the counted vmcnt of phases 0, 1 and 3 (-1 = none).
-  auto tile_body = [&](int i, auto iss1, auto iss2, auto w0, auto w1, auto w3) {
-    char* cur = (i & 1) ? b1 : b0;
-    char* oth = (i & 1) ? b0 : b1;
-    // phase 0: rows lo, k 0-31
-    read_b(cur, 0, bk0);
-    read_a(cur, 0, 0, af);
-    if constexpr (decltype(iss1)::value) issue_b(1, kt0 + i + 1, oth);
-    if constexpr (decltype(w0)::value >= 0) wait_vm<decltype(w0)::value * LPW / 2>();
-    raw_barrier();
-    mma(ic<0>{}, af, bk0);
-    // phase 1: rows lo, k 32-63
-    read_b(cur, 1, bk1);
-    read_a(cur, 0, 1, af);
-    if constexpr (decltype(iss1)::value) issue_a(1, kt0 + i + 1, oth);
-    if constexpr (decltype(w1)::value >= 0) wait_vm<decltype(w1)::value * LPW / 2>();
-    raw_barrier();
-    mma(ic<0>{}, af, bk1);
-    // phase 2: rows hi, k 0-31
-    read_a(cur, 1, 0, af);
-    if constexpr (decltype(iss2)::value) issue_b(0, kt0 + i + 2, cur);
-    raw_barrier();
-    mma(ic<1>{}, af, bk0);
-    // phase 3: rows hi, k 32-63
-    read_a(cur, 1, 1, af);
-    if constexpr (decltype(iss2)::value) issue_a(0, kt0 + i + 2, cur);
-    if constexpr (decltype(w3)::value >= 0) wait_vm<decltype(w3)::value * LPW / 2>();
-    raw_barrier();
-    mma(ic<1>{}, af, bk1);
-  };
-
-  if constexpr (RA) {
+  {
     // Read-ahead schedule: each phase's window (between two barriers) issues the LDS reads
     // of the NEXT phase into the other register set, one piece of tile i + 2 (into the
     // current buffer: its region's last reads completed before the window's barrier), then
@@ -310,27 +276,6 @@ __global__ __launch_bounds__(NW * 64) void prefill_gemm_kernel(const Args A) {
     } else {
       body(0, ic<0>{}, ic<0>{}, ic<0>{}, ic<-1>{}, ic<-1>{});
     }
-  } else if (nk >= 2) {
-    issue_b(0, kt0, b0);
-    issue_a(0, kt0, b0);
-    issue_b(1, kt0, b0);
-    issue_a(1, kt0, b0);
-    issue_b(0, kt0 + 1, b1);
-    issue_a(0, kt0 + 1, b1);
-    wait_vm<8 * LPW / 2>();
-    raw_barrier();
-    int i = 0;
-    for (; i + 2 < nk; ++i) tile_body(i, ic<1>{}, ic<1>{}, ic<8>{}, ic<8>{}, ic<8>{});
-    tile_body(i, ic<1>{}, ic<0>{}, ic<8>{}, ic<8>{}, ic<4>{});  // tile nk - 2
-    tile_body(i + 1, ic<0>{}, ic<0>{}, ic<2>{}, ic<0>{}, ic<-1>{});  // tile nk - 1
-  } else if (nk == 1) {
-    issue_b(0, kt0, b0);
-    issue_a(0, kt0, b0);
-    issue_b(1, kt0, b0);
-    issue_a(1, kt0, b0);
-    wait_vm<4 * LPW / 2>();
-    raw_barrier();
-    tile_body(0, ic<0>{}, ic<0>{}, ic<2>{}, ic<0>{}, ic<-1>{});
   }
 
   // ---- split tiles: publish, last arriver sums the other slices into its registers
@@ -592,18 +537,16 @@ __global__ __launch_bounds__(512) void prefill_gemm_n128_kernel(const Args A) {
 }  // namespace pa
 
 #include "gemm_pingpong.h"
-#include "gemm_w4.h"
 
 namespace pa {
 namespace pf {
 
 // Kernel family: 3 = ping-pong wave groups (gemm_pingpong.h; default; 256-wide tiles on the
-// two-phase schedule with the mixed 128-wide tail when it applies, 128-wide tiles on the
-// three-buffer schedule; items of < 2 k-tiles fall back to 1); 9 = 3 without the mixed tail;
-// 4 = its cycle-stamp build; 6 = the four-phase 256-wide schedule, 7 = its stamp build;
-// 5 = four-phase with buffer_load staging; 1 = read-ahead 8-wave 256 x 256 / 3-stage
-// 256 x 128; 0 = reads in the phase they feed; 2 = read-ahead, 4 waves of 128 x 128;
-// 10 = one wave per SIMD, 128 x 128 per wave, 32-k steps over four LDS stages (gemm_w4.h)
+// two-phase schedule with the mixed 128-wide tail when it applies, 192- and 128-wide tiles
+// on their own schedules; items of < 2 k-tiles fall back to 1); 9 = 3 without the mixed
+// tail; 4 = its cycle-stamp build; 1 = read-ahead 8-wave 256 x 256 / 3-stage 256 x 128.
+// (Measured and removed: the four-phase ping-pong schedule, buffer_load staging, 4-wave
+// 128 x 128 kernels -- profiles/r3_pingpong_ph2_ab.jsonl, profiles/r5_w4_experiment.md.)
 constexpr int kPfDefaultVariant = 3;
 static int g_pf_variant = kPfDefaultVariant;
 
@@ -743,22 +686,15 @@ extern "C" int pa_prefill_gemm(void* y, const void* x, const void* wp, const voi
 #define PA_PF(E, NRM)                                                                                \
   do {                                                                                               \
     const bool stamp = E == EP_PLAIN && !NRM && full == tiles;                                       \
-    if (bn == 192) hipLaunchKernelGGL((pingpong_gemm_kernel<E, NRM, false, false, 6, true>), dim3(grid), dim3(512), 0, st, a); \
-    else if (bn == 256 && variant == 10) hipLaunchKernelGGL((w4_gemm_kernel<E, NRM>), dim3(grid), dim3(256), 0, st, a); \
+    if (bn == 192) hipLaunchKernelGGL((pingpong_gemm_kernel<E, NRM, false, 6>), dim3(grid), dim3(512), 0, st, a); \
     else if (bn == 128 && variant == 4 && stamp)                                                     \
-      hipLaunchKernelGGL((pingpong_gemm_kernel<EP_PLAIN, false, true, false, 4>), dim3(grid), dim3(512), 0, st, a); \
-    else if (bn == 128 && variant >= 3) hipLaunchKernelGGL((pingpong_gemm_kernel<E, NRM, false, false, 4>), dim3(grid), dim3(512), 0, st, a); \
+      hipLaunchKernelGGL((pingpong_gemm_kernel<EP_PLAIN, false, true, 4>), dim3(grid), dim3(512), 0, st, a); \
+    else if (bn == 128 && variant >= 3) hipLaunchKernelGGL((pingpong_gemm_kernel<E, NRM, false, 4>), dim3(grid), dim3(512), 0, st, a); \
     else if (bn == 128) hipLaunchKernelGGL((prefill_gemm_n128_kernel<E, NRM>), dim3(grid), dim3(512), 0, st, a); \
     else if (variant == 4 && stamp)                                                                  \
-      hipLaunchKernelGGL((pingpong_gemm_kernel<EP_PLAIN, false, true, false, 8, true>), dim3(grid), dim3(512), 0, st, a); \
-    else if (variant == 7 && stamp)                                                                  \
-      hipLaunchKernelGGL((pingpong_gemm_kernel<EP_PLAIN, false, true, false, 8, false>), dim3(grid), dim3(512), 0, st, a); \
-    else if (variant == 5) hipLaunchKernelGGL((pingpong_gemm_kernel<E, NRM, false, true>), dim3(grid), dim3(512), 0, st, a); \
-    else if (variant == 6 || variant == 7) hipLaunchKernelGGL((pingpong_gemm_kernel<E, NRM>), dim3(grid), dim3(512), 0, st, a); \
-    else if (variant >= 3) hipLaunchKernelGGL((pingpong_gemm_kernel<E, NRM, false, false, 8, true>), dim3(grid), dim3(512), 0, st, a); \
-    else if (variant == 2) hipLaunchKernelGGL((prefill_gemm_kernel<E, NRM, true, 4>), dim3(grid), dim3(256), 0, st, a); \
-    else if (variant == 1) hipLaunchKernelGGL((prefill_gemm_kernel<E, NRM, true, 8>), dim3(grid), dim3(512), 0, st, a); \
-    else hipLaunchKernelGGL((prefill_gemm_kernel<E, NRM, false, 8>), dim3(grid), dim3(512), 0, st, a);                 \
+      hipLaunchKernelGGL((pingpong_gemm_kernel<EP_PLAIN, false, true, 8>), dim3(grid), dim3(512), 0, st, a); \
+    else if (variant >= 3) hipLaunchKernelGGL((pingpong_gemm_kernel<E, NRM, false, 8>), dim3(grid), dim3(512), 0, st, a); \
+    else hipLaunchKernelGGL((prefill_gemm_kernel<E, NRM>), dim3(grid), dim3(512), 0, st, a);          \
   } while (0)
   switch (epi) {
     case EP_PLAIN:

@@ -386,9 +386,9 @@ int32_t Scheduler::schedule(int32_t* buf) {
   buf[L.part_size] = psz;
 
   // prefill (q-split) tiles go first in the item list, heaviest (most keys) first across
-  // all chunks, then the decode items, longest partition first: the attention kernel's
-  // work queue (attention.hip MODE 3) hands them out in this order, so the long items
-  // start first and the short ones fill in behind them
+  // all chunks, then the decode items, longest partition first: the attention grid strides
+  // over the items in this order, so the long items start first and the short ones fill in
+  // behind them
   struct ItemCost {
     int32_t keys, a, b, c, d;
   };

@@ -13,5 +13,5 @@ python3 tools/pmc_summary.py $O/pmc > $O/pmc_summary.json
 timeout -s KILL 120 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt -- python3 tools/pmc_prefill.py --shapes 4096:4096:4096,2048:28672:4096 > $O/kt.log 2>&1 || { tail -20 $O/kt.log; exit 1; }
 find $O/kt -name "*kernel_stats.csv" -exec cut -c1-200 {} \; | head -12
 timeout -k 10 300 python -u tools/prefill_gemm_bench.py --shapes sq,gate_up,down,o --M 2048,4096 --rounds 3 \
-  --variants lib,pp256w,pp256w_fused,pp128w,pp128w_fused,pf_w4,pf_w4_fused --out $O/bench.jsonl > $O/bench.log 2>&1 || { tail -20 $O/bench.log; exit 1; }
+  --variants lib,pp256w,pp256w_fused,pp128w,pp128w_fused --out $O/bench.jsonl > $O/bench.log 2>&1 || { tail -20 $O/bench.log; exit 1; }
 cut -c1-500 $O/bench.jsonl

@@ -23,7 +23,6 @@ SHAPES = {"sq": (4096, 4096), "qkv": (6144, 4096), "o": (4096, 4096), "gate_up":
 ap = argparse.ArgumentParser()
 ap.add_argument("--shapes", default="sq:4096,sq:2048,gate_up:2048,gate_up:1024,down:2048")
 ap.add_argument("--out", default="")
-ap.add_argument("--variant", type=int, default=3, help="3: the default (two-phase) schedule, 6: four-phase")
 a = ap.parse_args()
 C = kernels.require_native()
 out_f = open(a.out, "a") if a.out else None
@@ -37,7 +36,7 @@ for spec in a.shapes.split(","):
     x = torch.randn(M, K, device="cuda").to(torch.bfloat16)
     y = torch.empty(M, N, dtype=torch.bfloat16, device="cuda")
     ws, _ = kernels.prefill_workspace(x.device)
-    C.prefill_set_variant(a.variant)
+    C.prefill_set_variant(3)
     try:
         t_end = time.time() + 2.0
         n = 0
@@ -51,7 +50,7 @@ for spec in a.shapes.split(","):
         e.record()
         e.synchronize()
         us = s.elapsed_time(e) * 1000 / n
-        C.prefill_set_variant(4 if a.variant == 3 else 7)  # the matching stamp build
+        C.prefill_set_variant(4)  # the stamp build
         ws[: 8 * 4096 * 9].zero_()
         kernels.prefill_gemm(x, wp, "plain", out=y, full=-1, splits=1, bn=256)
         torch.cuda.synchronize()
@@ -68,28 +67,12 @@ for spec in a.shapes.split(","):
     start_spread_us = (st[:, 4].max() - st[:, 4].min()).item() / 100
     end_spread_us = (st[:, 5].max() - st[:, 5].min()).item() / 100
     span_us = (st[:, 5].max() - st[:, 4].min()).item() / 100
-    # per-wave barrier arrivals of k-tile 8: group 0 (waves 0-3) barrier k is the hardware
-    # barrier of group 1's (waves 4-7) barrier k - 1 (group 1 runs one barrier behind)
-    wb = ws[tiles * 16: tiles * 16 + tiles * 128].view(torch.int64).view(tiles, 8, 8).cpu().double()
-    seg = {}
-    if wb[:, 0, 0].min().item() > 0:
-        g0, g1 = wb[:, :4, :], wb[:, 4:, :]
-        rel = {}
-        for j in range(1, 8):  # hardware barrier j: group 0 index j, group 1 index j - 1
-            rel[j] = torch.maximum(g0[:, :, j].max(1).values, g1[:, :, j - 1].max(1).values)
-        for j in range(1, 7):
-            w0 = (g0[:, :, j + 1] - rel[j][:, None]).median().item()   # group 0 work after barrier j
-            w1 = (g1[:, :, j] - rel[j][:, None]).median().item()       # group 1 work after barrier j
-            wait0 = (rel[j][:, None] - g0[:, :, j]).median().item()
-            wait1 = (rel[j][:, None] - g1[:, :, j - 1]).median().item()
-            seg["b%d" % j] = [round(w0), round(w1), round(wait0), round(wait1)]
-    row = {"variant": a.variant, "shape": name, "M": M, "N": N, "K": K, "tiles": tiles, "us_per_launch": round(us, 1),
+    row = {"variant": 3, "shape": name, "M": M, "N": N, "K": K, "tiles": tiles, "us_per_launch": round(us, 1),
            "tflops": round(2 * M * N * K / us / 1e6, 1),
            "prologue_cyc_med": statistics.median(pro), "loop_cyc_med": statistics.median(loop),
            "epilogue_cyc_med": statistics.median(epi), "epilogue_cyc_max": max(epi), "total_cyc_med": statistics.median(tot),
            "clock_ghz_med": round(statistics.median(clk), 3), "loop_cyc_per_ktile": round(statistics.median(loop) / (K // 64), 1),
-           "start_spread_us": start_spread_us, "end_spread_us": end_spread_us, "stamped_span_us": span_us,
-           "segments_g0work_g1work_g0wait_g1wait": seg}
+           "start_spread_us": start_spread_us, "end_spread_us": end_spread_us, "stamped_span_us": span_us}
     print(json.dumps(row), flush=True)
     if out_f:
         out_f.write(json.dumps(row) + "\n")

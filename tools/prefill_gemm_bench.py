@@ -52,7 +52,7 @@ def timeit(fn, ncopies):
 C = kernels.require_native()
 
 
-def v0(fn, v=0):  # 256-wide schedule variant v (0: reads in the phase they feed; 2: 4 waves)
+def v0(fn, v=1):  # prefill kernel family v for this call (1 read-ahead, 3 ping-pong, 8 / 9 tail forms)
     C.prefill_set_variant(v)
     try:
         return fn()
@@ -91,21 +91,11 @@ for name in a.shapes.split(","):
             "pf128_s2": lambda i: kernels.prefill_gemm(x, wps[i], "plain", out=y, bn=128, full=0, splits=2),
             "pf128_fused": lambda i: kernels.prefill_gemm(x, fps[i], epi, out=yf if epi == "silu" else y, resid=resid,
                                                           norm=nrm, ss_in=ss if nrm else None, bn=128),
-            "pf_v0": lambda i: v0(lambda: kernels.prefill_gemm(x, wps[i], "plain", out=y, bn=256)),
-            "pf_w4": lambda i: v0(lambda: kernels.prefill_gemm(x, wps[i], "plain", out=y, bn=256), 2),
-            "pf_w4_fused": lambda i: v0(lambda: kernels.prefill_gemm(x, fps[i], epi, out=yf if epi == "silu" else y,
-                                                                     resid=resid, norm=nrm, ss_in=ss if nrm else None,
-                                                                     bn=256), 2),
             "pp": lambda i: v0(lambda: kernels.prefill_gemm(x, wps[i], "plain", out=y, bn=256), 9),
-            "pp_ph4": lambda i: v0(lambda: kernels.prefill_gemm(x, wps[i], "plain", out=y, full=-1, splits=1, bn=256), 6),
-            "pp_ph4_fused": lambda i: v0(lambda: kernels.prefill_gemm(x, fps[i], epi, out=yf if epi == "silu" else y,
-                                                                     resid=resid, norm=nrm, ss_in=ss if nrm else None,
-                                                                     bn=256), 6),
             "pp_mix": lambda i: v0(lambda: kernels.prefill_gemm(x, wps[i], "plain", out=y, bn=256), 8),
             "pp_mix_fused": lambda i: v0(lambda: kernels.prefill_gemm(x, fps[i], epi, out=yf if epi == "silu" else y,
                                                                      resid=resid, norm=nrm, ss_in=ss if nrm else None,
                                                                      bn=256), 8),
-            "pp_buf": lambda i: v0(lambda: kernels.prefill_gemm(x, wps[i], "plain", out=y, full=-1, splits=1, bn=256), 5),
             "pp_whole": lambda i: v0(lambda: kernels.prefill_gemm(x, wps[i], "plain", out=y, full=-1, splits=1, bn=256), 3),
             "pp_s2": lambda i: v0(lambda: kernels.prefill_gemm(x, wps[i], "plain", out=y, full=0, splits=2, bn=256), 3),
             "pp_fused": lambda i: v0(lambda: kernels.prefill_gemm(x, fps[i], epi, out=yf if epi == "silu" else y,
@@ -127,10 +117,6 @@ for name in a.shapes.split(","):
                 variants[f"pp{bn_}w_fused"] = (lambda bn_: lambda i: v0(lambda: kernels.prefill_gemm(
                     x, fps[i], epi, out=yf if epi == "silu" else y, resid=resid, norm=nrm,
                     ss_in=ss if nrm else None, bn=bn_), 3))(bn_)
-        variants["w4"] = lambda i: v0(lambda: kernels.prefill_gemm(x, wps[i], "plain", out=y, bn=256), 10)
-        variants["w4_fused"] = lambda i: v0(lambda: kernels.prefill_gemm(
-            x, fps[i], epi, out=yf if epi == "silu" else y, resid=resid, norm=nrm, ss_in=ss if nrm else None,
-            bn=256), 10)
         if name == "qkv":  # the engine's qkv call: RMSNorm folded, RoPE + paged KV write epilogue
             from pilottai_amd.ops import reference as _ref
             H, KV = 32, 8
@@ -172,18 +158,11 @@ for name in a.shapes.split(","):
             for bn in (256, 128):
                 yy = kernels.prefill_gemm(x, wps[0], "plain", out=y, bn=bn)
                 row[f"err_pf{bn}"] = float(((yy.float() - ref).abs().max() / ref.abs().max()))
-            yy = v0(lambda: kernels.prefill_gemm(x, wps[0], "plain", out=y, bn=256), 2)
-            row["err_pf_w4"] = float(((yy.float() - ref).abs().max() / ref.abs().max()))
         if "pp128" in variants:
             ref = x.float() @ ws[0].float().T
             y.fill_(float("nan"))
             yy = v0(lambda: kernels.prefill_gemm(x, wps[0], "plain", out=y, full=-1, splits=1, bn=128), 3)
             row["err_pp128"] = float(((yy.float() - ref).abs().max() / ref.abs().max()))
-        if "w4" in a.variants.split(","):
-            ref = x.float() @ ws[0].float().T
-            y.fill_(float("nan"))
-            yy = v0(lambda: kernels.prefill_gemm(x, wps[0], "plain", out=y, bn=256), 10)
-            row["err_w4"] = float(((yy.float() - ref).abs().max() / ref.abs().max()))
         for bn_ in (192, 256, 128):
             if f"pp{bn_}w" in variants:
                 ref = x.float() @ ws[0].float().T
@@ -193,7 +172,7 @@ for name in a.shapes.split(","):
         if any(k.startswith("pp") for k in variants):
             ref = x.float() @ ws[0].float().T
             for nm, kw, vv in (("pp", {}, 3), ("pp_whole", dict(full=-1, splits=1), 3), ("pp_s2", dict(full=0, splits=2), 3),
-                               ("pp_buf", dict(full=-1, splits=1), 5), ("pp_ph4", dict(full=-1, splits=1), 6), ("pp_mix", {}, 8)):
+                               ("pp_mix", {}, 8)):
                 if nm not in variants:
                     continue
                 try:
