@@ -22,16 +22,8 @@ streaming read that halves the speed of the engine's memory-bound (decode-sized)
 costs a compute-bound 2,048-token prefill step only ~6 % (BENCHMARKS.md, config 4). The engine
 announces every step it launches (LLMEngine.add_step_listener); with a gate attached, a pass
 whose queries are embedded waits until the engine launches a step of at least `gate_tokens`
-tokens -- or for at most `gate_max_wait_s` -- and then starts right behind that launch, so
-the scan overlaps compute-bound work. `stats` counts the passes that started beside such a
-step and the ones the latency cap released.
-
-Two-stage pipeline (`pipeline_depth`, default 2): a lookup batch is embedded first (with the
-engine embedder that is a request inside the engine's continuous batch, i.e. one or two
-engine steps) and scanned after; the index passes run one at a time in arrival order, but
-batch N + 1 is embedded while batch N scans, so a lookup no longer waits for the previous
-batch's embedding AND its pass. At most `pipeline_depth` batches are in flight; requests
-arriving meanwhile join the next batch. pipeline_depth = 1 is the sequential flush.
+tokens -- or for at most `gate_max_wait_s` -- and then starts right behind that launch, so the scan overlaps compute-bound work. `stats` counts the passes that
+started beside such a step and the ones the latency cap released.
 """
 from __future__ import annotations
 
@@ -44,7 +36,7 @@ from .enhanced_memory import EnhancedMemory, MemoryItem
 
 class MemoryLookupBatcher:
     def __init__(self, memory: EnhancedMemory, max_batch: int = 256, time_device: bool = True,
-                 min_batch: int = 1, max_wait_s: float = 0.0, pipeline_depth: int = 2):
+                 min_batch: int = 1, max_wait_s: float = 0.0):
         """min_batch / max_wait_s: before a pass, wait (in 1 ms sleeps) until `min_batch`
         queries are pending or the oldest has waited `max_wait_s` — more queries share each
         streaming pass over the index (whose cost does not depend on the query count up to
@@ -53,9 +45,6 @@ class MemoryLookupBatcher:
         self.max_batch = max_batch
         self.min_batch = max(1, int(min_batch))
         self.max_wait_s = float(max_wait_s)
-        self.pipeline_depth = max(1, int(pipeline_depth))
-        self._inflight: Set["asyncio.Task"] = set()
-        self._scan_lock: Optional[asyncio.Lock] = None  # one index pass at a time
         self.time_device = time_device
         self._pending: List[Tuple[str, Optional[Set[str]], int, int, "asyncio.Future", float]] = []
         self._writes: List[Tuple[str, Dict[str, Any], Set[str], int, "asyncio.Future"]] = []
@@ -178,45 +167,28 @@ class MemoryLookupBatcher:
                     time.perf_counter() - self._pending[0][5] < self.max_wait_s:
                 await asyncio.sleep(0.001)
             self.stats["coalesce_waits"] = self.stats.get("coalesce_waits", 0) + 1
-        if not self._pending:
-            return
-        if self.pipeline_depth > 1:
-            while len(self._inflight) >= self.pipeline_depth:  # later requests join the next batch
-                await asyncio.wait(set(self._inflight), return_when=asyncio.FIRST_COMPLETED)
-            if not self._pending:
-                return
-        batch, self._pending = self._pending[: self.max_batch], self._pending[self.max_batch:]
-        if self.pipeline_depth > 1:
-            t = asyncio.ensure_future(self._lookup(batch))
-            self._inflight.add(t)
-            t.add_done_callback(self._inflight.discard)
-        else:
-            await self._lookup(batch)
-
-    async def _lookup(self, batch):
-        """Embed the batch's queries, then (one pass at a time) gate and scan."""
-        limit = max(b[3] for b in batch)
-        t0 = time.perf_counter()
-        try:
-            qs = [b[0] for b in batch]
-            vecs = await self.memory.embed_queries(qs)
-            if self._scan_lock is None:
-                self._scan_lock = asyncio.Lock()
-            async with self._scan_lock:
-                if self._heavy is not None:  # scan beside the next compute-bound step
+        if self._pending:
+            batch, self._pending = self._pending[: self.max_batch], self._pending[self.max_batch:]
+            limit = max(b[3] for b in batch)
+            t0 = time.perf_counter()
+            try:
+                qs = [b[0] for b in batch]
+                vecs = None
+                if self._heavy is not None:  # embed now, scan beside the next compute-bound step
+                    vecs = await self.memory.embed_queries(qs)
                     await self._await_heavy()
                 hits = await self.memory.search_batch(qs, tags=[b[1] for b in batch],
                                                       min_priority=[b[2] for b in batch], limit=limit, vecs=vecs)
-            now = time.perf_counter()
-            for b, h in zip(batch, hits):
-                self._lat.append(now - b[5])
-                if not b[4].done():
-                    b[4].set_result(h[: b[3]])
-        except Exception as e:  # noqa: BLE001
-            for b in batch:
-                if not b[4].done():
-                    b[4].set_exception(e)
-        self.stats["host_s"] += time.perf_counter() - t0
-        self.stats["lookups"] += len(batch)
-        self.stats["passes"] += 1
-        self.stats["max_batch_seen"] = max(self.stats["max_batch_seen"], len(batch))
+                now = time.perf_counter()
+                for b, h in zip(batch, hits):
+                    self._lat.append(now - b[5])
+                    if not b[4].done():
+                        b[4].set_result(h[: b[3]])
+            except Exception as e:  # noqa: BLE001
+                for b in batch:
+                    if not b[4].done():
+                        b[4].set_exception(e)
+            self.stats["host_s"] += time.perf_counter() - t0
+            self.stats["lookups"] += len(batch)
+            self.stats["passes"] += 1
+            self.stats["max_batch_seen"] = max(self.stats["max_batch_seen"], len(batch))

@@ -207,49 +207,3 @@ def test_batcher_scans_beside_compute_bound_steps():
 
     asyncio.run(run())
 
-
-def test_batcher_pipelines_embedding_and_scan():
-    """A batch is embedded while the previous batch's index pass runs (two-stage pipeline):
-    with lookups arriving steadily the passes still never overlap each other, every answer
-    is right, and the mean lookup latency is not above the sequential flush's (it is the
-    queueing behind the previous batch's embedding that the pipeline removes)."""
-    class SlowMemory:
-        def __init__(self, mem):
-            self.mem, self.index = mem, mem.index
-            self.scanning, self.overlap, self.embed_during_scan = 0, 0, 0
-
-        async def embed_queries(self, qs):
-            if self.scanning:
-                self.embed_during_scan += 1
-            await asyncio.sleep(0.06)
-            return await self.mem.embed_queries(qs)
-
-        async def search_batch(self, qs, **kw):
-            self.scanning += 1
-            self.overlap = max(self.overlap, self.scanning)
-            await asyncio.sleep(0.05)
-            try:
-                return await self.mem.search_batch(qs, **kw)
-            finally:
-                self.scanning -= 1
-
-    texts = [f"note {i} about topic {chr(97 + i)}" for i in range(12)]
-
-    async def run(depth):
-        mem = EnhancedMemory(device="cpu", dim=64, embedder=HashingEmbedder(64))
-        await mem.store_semantic_batch(texts)
-        slow = SlowMemory(mem)
-        b = MemoryLookupBatcher(slow, pipeline_depth=depth)
-
-        async def one(i):
-            await asyncio.sleep(0.025 * i)  # a steady stream of lookups
-            return await b.search(texts[i], limit=1)
-        hits = await asyncio.gather(*(one(i) for i in range(len(texts))))
-        assert [h[0].text for h in hits] == texts
-        assert slow.overlap == 1  # one index pass at a time
-        return sum(b._lat) / len(b._lat), slow.embed_during_scan
-
-    mean1, e1 = asyncio.run(run(1))
-    mean2, e2 = asyncio.run(run(2))
-    assert e1 == 0 and e2 >= 1  # only the pipelined batcher embeds while a pass runs
-    assert mean2 < 1.02 * mean1, (mean1, mean2)
