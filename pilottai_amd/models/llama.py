@@ -239,6 +239,22 @@ class LlamaModel:
         self.device = torch.device(device)
         self.dtype = dtype
         self.tp = tp or TPGroup.single()
+        # routing-table overrides for in-engine A/Bs (tools/midrange_ab.py style): a JSON object
+        # {"STREAM_CFG": {"qkv": [[64, [1, 1, 6, 1, 4, 4]]]}, "MID_CFG": {...}, "PF_CFG": {...}}
+        # whose per-projection rows replace the class table's rows for that projection
+        ov = os.environ.get("PILOTTAI_ROUTING_JSON")
+        if ov:
+            import json
+
+            for table, rows in json.loads(ov).items():
+                if table not in ("STREAM_CFG", "MID_CFG", "PF_CFG"):
+                    raise ValueError(f"PILOTTAI_ROUTING_JSON: unknown table {table!r}")
+                merged = dict(getattr(self, table))
+                for kind, r in rows.items():
+                    merged[kind] = [tuple(x) if table == "MID_CFG" else
+                                    (x[0], tuple(x[1])) if table == "STREAM_CFG" else (x[0], x[1], dict(x[2]))
+                                    for x in r]
+                setattr(self, table, merged)
         ts = self.tp.size
         if cfg.num_heads % ts or cfg.num_kv_heads % ts or cfg.intermediate_size % ts or cfg.vocab_size % ts:
             raise ValueError(f"{cfg.name} is not divisible by tensor-parallel size {ts}")
