@@ -146,8 +146,9 @@ def test_llama3_8b_layer_dims_every_path(gpu, n_prompt):
 def test_llama3_8b_production_large_steps(gpu, lens):
     """VERDICT r3 missing #4: the bench's 1,024-2,048-token steps as the engine composes them
     (max_num_batched_tokens 2,048, the default token buckets: prefill chunks of long prompts
-    beside the decode rows of short ones, so every PF_CFG row runs: 256 x 128 ping-pong qkv,
-    256 x 256 gate_up / down with split tails, the mixed-tail kernel) at the exact Llama-3-8B
+    beside the decode rows of short ones, so every PF_CFG row runs: 256 x 128 ping-pong qkv up
+    to 1,280 rows and 256 x 192 above, 256 x 256 gate_up / down with split tails, the
+    mixed-tail kernel) at the exact Llama-3-8B
     layer dims; every request's greedy tokens must match the dense fp32 reference forward."""
     from pilottai_amd.engine.engine import EngineConfig, LLMEngine
 
