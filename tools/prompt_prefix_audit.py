@@ -72,6 +72,21 @@ def main():
             print(repr(tok.decode(ids[hit:])))
             shown.add(kind)
     print(f"prompts {len(recs)}, tokens {tot[0]}, best-case block-prefix hits {tot[1]} ({tot[1] / max(1, tot[0]):.3f})")
+    # token-granular ceiling: the longest common prefix with any earlier prompt (what a cache
+    # that also reused a partially matching block could serve)
+    lcp_tot = 0
+    for i, (ids, _) in enumerate(recs):
+        best = 0
+        for prev, _ in recs[:i]:
+            m = 0
+            for x, y in zip(ids, prev):
+                if x != y:
+                    break
+                m += 1
+            best = max(best, m)
+        lcp_tot += min(best, len(ids) - 1)
+    print(f"token-granular ceiling {lcp_tot} ({lcp_tot / max(1, tot[0]):.3f}): "
+          f"{(lcp_tot - tot[1]) / max(1, len(recs)):.1f} tokens per prompt lost to block alignment")
     for kind, (c, n, h) in sorted(by_kind.items(), key=lambda kv: -kv[1][1]):
         print(f"  {kind:>40s}: calls {c:4d}, tokens/call {n / c:7.1f}, cached/call {h / c:7.1f} ({h / max(1, n):.3f})")
 
