@@ -240,13 +240,17 @@ class LlamaModel:
         self.dtype = dtype
         self.tp = tp or TPGroup.single()
         # routing-table overrides for in-engine A/Bs (tools/midrange_ab.py style): a JSON object
-        # {"STREAM_CFG": {"qkv": [[64, [1, 1, 6, 1, 4, 4]]]}, "MID_CFG": {...}, "PF_CFG": {...}}
-        # whose per-projection rows replace the class table's rows for that projection
+        # {"STREAM_CFG": {"qkv": [[64, [1, 1, 6, 1, 4, 4]]]}, "MID_CFG": {...}, "PF_CFG": {...},
+        #  "PF_MIDRANGE": ["gate_up", "qkv"]} whose per-projection rows replace the class table's
+        # rows for that projection (PF_MIDRANGE: the whole set)
         ov = os.environ.get("PILOTTAI_ROUTING_JSON")
         if ov:
             import json
 
             for table, rows in json.loads(ov).items():
+                if table == "PF_MIDRANGE":  # a list of projection kinds
+                    self.PF_MIDRANGE = frozenset(rows)
+                    continue
                 if table not in ("STREAM_CFG", "MID_CFG", "PF_CFG"):
                     raise ValueError(f"PILOTTAI_ROUTING_JSON: unknown table {table!r}")
                 merged = dict(getattr(self, table))

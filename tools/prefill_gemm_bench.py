@@ -131,7 +131,7 @@ for name in a.shapes.split(","):
                 variants[f"ropekv{bn_}"] = (lambda bn_: lambda i: kernels.prefill_qkv_rope(
                     x, fps[i], 1e-5, qo, kc, vc, pos, slots, cs, H, KV, ss_in=ss, bn=bn_, variant=3))(bn_)
         for bn_ in (128, 256):  # fused epilogue on an explicit (whole tiles, K-slices) decomposition
-            for S_ in (1, 2, 3, 4):
+            for S_ in (1, 2, 3, 4, 6, 8, 10):
                 variants[f"pf{bn_}_s{S_}_fused"] = (lambda bn_, S_: lambda i: kernels.prefill_gemm(
                     x, fps[i], epi, out=yf if epi == "silu" else y, resid=resid, norm=nrm,
                     ss_in=ss if nrm else None, bn=bn_, full=0 if S_ > 1 else -1, splits=S_))(bn_, S_)
