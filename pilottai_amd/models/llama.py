@@ -186,16 +186,22 @@ class LlamaModel:
     # rounds beat the 256 x 256 tiles' rounds + split tail: 1,281-2,048 rows (one round of 192-256
     # tiles instead of 144-192 wide ones) and from 3,841 (profiles/r5_qkv_192_tiles.jsonl: RoPE +
     # KV-write epilogue 71.9 / 77.1 / 84.7 / 164.3 us at 1,536 / 1,792 / 2,048 / 4,096 rows vs
-    # 83.9 / 87.2 / 94.2 / 181.7 on 256 x 256 tiles; plain 2,048 rows 76.2 us vs hipBLASLt 80.1)
+    # 83.9 / 87.2 / 94.2 / 181.7 on 256 x 256 tiles; plain 2,048 rows 76.2 us vs hipBLASLt 80.1).
+    # Round 5: the 256 x 128 ping-pong family (variant 3) replaced the 3-stage 256 x 128 kernel
+    # (variant 1) in every row: 10-25 % faster in isolation at 144-1,280 rows for every projection
+    # (profiles/r5_pf_family_sweep.jsonl, r5_midrange_isolated_sweep.jsonl; e.g. o at 512 rows
+    # 32.6 vs 41.8 us, down at 384 rows 64.2 vs 76.2), and in the engine (alternating on one box,
+    # profiles/r5_pf_family_inengine_ab.jsonl): headline bench 43.51 vs 42.89 tasks/s (3 reps),
+    # 256- / 192-row steps 7.94 / 7.08 vs 8.05 / 7.17 ms; qkv of 129-256-row steps stays on the
+    # mid kernel (on the prefill kernel there: 8.34 vs 7.94 ms at 256 rows)
     PF_CFG = {
-        "qkv": [(80, "mid", {}), (640, "pf", {"bn": 128, "variant": 1}), (1280, "pf", {"bn": 128, "variant": 3}),
+        "qkv": [(80, "mid", {}), (1280, "pf", {"bn": 128, "variant": 3}),
                 (2048, "pf", {"bn": 192, "variant": 3}), (3840, "pf", {"bn": 256, "variant": 3}),
                 (1 << 30, "pf", {"bn": 192, "variant": 3})],
-        "o": [(128, "mid", {}), (1280, "pf", {"bn": 128, "variant": 1}),
-              (1 << 30, "pf", {"bn": 128, "variant": 3})],
-        "gate_up": [(128, "mid", {}), (256, "pf", {"bn": 128, "variant": 1}),
+        "o": [(128, "mid", {}), (1 << 30, "pf", {"bn": 128, "variant": 3})],
+        "gate_up": [(128, "mid", {}), (256, "pf", {"bn": 128, "variant": 3}),
                     (1 << 30, "pf", {"bn": 256, "variant": 3})],
-        "down": [(128, "mid", {}), (640, "pf", {"bn": 128, "variant": 1}),
+        "down": [(128, "mid", {}), (512, "pf", {"bn": 128, "variant": 3}),
                  (1 << 30, "pf", {"bn": 256, "variant": 3})],
     }
     # per projection: (largest M, shape) rows for the weight-streaming kernel

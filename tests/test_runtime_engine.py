@@ -493,7 +493,7 @@ def test_qkv_wide_tile_routing():
     bn = {T: m._proj_path("qkv", T, 6144, 4096)[1]["bn"] for T in (1024, 1536, 2048, 2304, 4096)}
     assert bn == {1024: 128, 1536: 192, 2048: 192, 2304: 256, 4096: 192}
     assert m._proj_path("qkv", 2048, 5120, 8192) == ("pf", {"bn": 256, "variant": 3})
-    assert LlamaModel.PF_CFG["qkv"][3][2]["bn"] == 192  # the table itself is not rewritten
+    assert [r[2].get("bn") for r in LlamaModel.PF_CFG["qkv"] if r[0] == 2048] == [192]  # the table is not rewritten
 
 
 def test_engine_fails_on_custom_allreduce_timeout():
