@@ -138,6 +138,7 @@ class BaseAgent:
         self.conversation_history: Deque[Dict[str, str]] = deque(maxlen=self.MAX_HISTORY_SIZE)
         self.execution_locks: Dict[str, asyncio.Lock] = {}
         self._openings: Dict[str, "asyncio.Future"] = {}  # prefetched opening calls by task id
+        self._first_lookups: Dict[str, "asyncio.Future"] = {}  # step 0's memory lookup, by task id
         self._tool_locks: Dict[str, asyncio.Lock] = {}
         self.tasks: Dict[str, Task] = {}
         self.active_tasks: set = set()
@@ -395,12 +396,16 @@ class BaseAgent:
         iterations = 0
         try:
             opening = self._openings.pop(task.id, None)
+            first_lookup = self._first_lookups.pop(task.id, None)
             try:
                 self._validate_task(task)
             except BaseException:
-                if opening is not None:
-                    opening.cancel()
+                for f in (opening, first_lookup):
+                    if f is not None:
+                        f.cancel()
                 raise
+            if first_lookup is None:
+                first_lookup = self._start_first_lookup(task)
             if opening is None:
                 opening = self.prefetch_opening(task, _store=False)
             analysis, selection = await opening
@@ -411,7 +416,8 @@ class BaseAgent:
                 lock = self._tool_locks.setdefault(name, asyncio.Lock())
                 await lock.acquire()
                 held.append(name)
-            steps, iterations = await self._execute_steps(task, chosen)
+            steps, iterations = await self._execute_steps(task, chosen, first_lookup)
+            first_lookup = None
             evaluation = await self._evaluate_result(task, steps)
             ok = bool(evaluation.get("success", False))
             await self._remember(task, ok, evaluation)
@@ -423,6 +429,8 @@ class BaseAgent:
             return TaskResult(success=False, output=None, error=str(e), execution_time=time.perf_counter() - t0,
                               metadata={"agent_id": self.id, "iterations": iterations})
         finally:
+            if first_lookup is not None and not first_lookup.done():
+                first_lookup.cancel()
             for name in reversed(sorted(held)):
                 lock = self._tool_locks.get(name)
                 if lock is not None and lock.locked():
@@ -456,12 +464,26 @@ class BaseAgent:
         fut = asyncio.ensure_future(both())
         if _store:
             self._openings[task.id] = fut
+            lk = self._start_first_lookup(task)
+            if lk is not None:
+                self._first_lookups[task.id] = lk
         return fut
 
     def drop_opening(self, task_id: str):
-        fut = self._openings.pop(task_id, None)
-        if fut is not None and not fut.done():
-            fut.cancel()
+        for d in (self._openings, self._first_lookups):
+            fut = d.pop(task_id, None)
+            if fut is not None and not fut.done():
+                fut.cancel()
+
+    def _start_first_lookup(self, task: Task) -> Optional["asyncio.Future"]:
+        """The first step plan's memory lookup depends only on the task (no step result
+        yet), so it starts with the opening calls instead of after them: its batched index
+        pass and query embedding overlap the analysis / tool-selection round trips rather
+        than adding to the task's critical path. Later steps' lookups read the previous
+        step's result and stay in the loop."""
+        if self.memory_lookup is None or self.memory_top_k <= 0:
+            return None
+        return asyncio.ensure_future(self._memory_context(task, json.dumps(_short(None))))
 
     def _validate_task(self, task: Task):
         if not task.description:
@@ -522,7 +544,7 @@ class BaseAgent:
         return await self._llm_json("tool_selection", self.policy.tool_selection(names),
                                     tools=json.dumps(names), task_description=task.description)
 
-    async def _execute_steps(self, task: Task, tools: List[str]):
+    async def _execute_steps(self, task: Task, tools: List[str], first_lookup: Optional["asyncio.Future"] = None):
         completed: List[Dict[str, Any]] = []
         step_inputs = task.metadata.get("tool_inputs", {}) if isinstance(task.metadata, dict) else {}
         iterations = 0
@@ -535,7 +557,10 @@ class BaseAgent:
             common = dict(task_description=task.description, completed_steps=json.dumps(_short(completed, 800)),
                           available_tools=json.dumps(tools), last_result=last)
             if self.memory_lookup is not None and self.memory_top_k > 0:
-                ctx = await self._memory_context(task, last)
+                if iterations == 0 and first_lookup is not None:
+                    ctx = await first_lookup  # started with the opening calls (same query)
+                else:
+                    ctx = await self._memory_context(task, last)
                 plan = await self._llm_json("step_planning_memory", fixed, schema="step_planning",
                                             memory_context=ctx, **common)
             else:

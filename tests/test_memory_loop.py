@@ -208,3 +208,49 @@ def test_batcher_scans_beside_compute_bound_steps():
 
     asyncio.run(run())
 
+
+
+def test_first_step_lookup_overlaps_the_opening_calls():
+    """The first step plan's memory query depends only on the task, so its lookup starts with
+    the opening (analysis / tool selection) calls and finishes under them: with 50 ms LLM
+    calls and a 60 ms lookup the task takes about one lookup less than in sequence, the
+    step-0 prompt still carries the hits, and a dropped opening cancels the lookup too."""
+    import time as _t
+
+    class SlowLookup(MemoryLookupBatcher):
+        def __init__(self, mem):
+            super().__init__(mem)
+            self.starts = []
+
+        async def search(self, query, limit=5, tags=None, min_priority=0):
+            self.starts.append(_t.perf_counter())
+            await asyncio.sleep(0.06)
+            return await super().search(query, limit=limit, tags=tags, min_priority=min_priority)
+
+    async def go():
+        mem = EnhancedMemory(max_size=1024, device="cpu")
+        await mem.store_semantic_batch(["prior finding: quarterly revenue grew"], tags=[{"worker"}], priorities=[1])
+        lookup = SlowLookup(mem)
+        llm = _RecordingLLM()
+        llm.latency_s = 0.05
+        a = BaseAgent(AgentConfig(role="worker", goal="Summarize documents", max_iterations=2), llm=llm,
+                      tools=[Tool(name="echo", description="identity", function=echo_tool, max_retries=1)],
+                      policy=ControlPolicy("fixed", 2), memory_lookup=lookup, memory_top_k=1)
+        await a.start()
+        t0 = _t.perf_counter()
+        r = await a.execute_task(Task(description="Summarize the quarterly revenue report"))
+        first_start = lookup.starts[0] - t0
+        # a speculative opening that is dropped takes its lookup with it
+        t2 = Task(description="Another report")
+        a.prefetch_opening(t2)
+        lk = a._first_lookups[t2.id]
+        a.drop_opening(t2.id)
+        await asyncio.sleep(0)
+        return r, first_start, llm, lk, len(lookup.starts)
+
+    r, first_start, llm, lk, nstarts = asyncio.run(go())
+    assert r.success
+    assert first_start < 0.02  # issued with the opening calls, not after them (>= 50 ms)
+    mem_prompts = [p for p in llm.prompts if "Relevant memory:" in p]
+    assert len(mem_prompts) == 2 and "quarterly revenue" in mem_prompts[0]
+    assert lk.cancelled() or lk.done()
