@@ -117,6 +117,10 @@ for name in a.shapes.split(","):
                 variants[f"pp{bn_}w_fused"] = (lambda bn_: lambda i: v0(lambda: kernels.prefill_gemm(
                     x, fps[i], epi, out=yf if epi == "silu" else y, resid=resid, norm=nrm,
                     ss_in=ss if nrm else None, bn=bn_), 3))(bn_)
+        # the 3-stage 256 x 128 kernel (variant 1) with the engine's epilogue
+        variants["n128v1_fused"] = lambda i: v0(lambda: kernels.prefill_gemm(
+            x, fps[i], epi, out=yf if epi == "silu" else y, resid=resid, norm=nrm, ss_in=ss if nrm else None,
+            bn=128), 1)
         if name == "qkv":  # the engine's qkv call: RMSNorm folded, RoPE + paged KV write epilogue
             from pilottai_amd.ops import reference as _ref
             H, KV = 32, 8
