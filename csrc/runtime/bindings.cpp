@@ -125,6 +125,7 @@ PYBIND11_MODULE(_runtime, m) {
         if (d.contains("prefix_caching")) c.prefix_caching = d["prefix_caching"].cast<bool>();
         if (d.contains("dedup_inflight_prefix")) c.dedup_inflight_prefix = d["dedup_inflight_prefix"].cast<bool>();
         if (d.contains("max_prefix_defer")) c.max_prefix_defer = d["max_prefix_defer"].cast<int32_t>();
+        if (d.contains("embed_first")) c.embed_first = d["embed_first"].cast<bool>();
         if (d.contains("split_decode")) c.split_decode = d["split_decode"].cast<bool>();
         if (d.contains("token_align")) c.token_align = d["token_align"].cast<int32_t>();
         if (d.contains("kv_heads")) c.kv_heads = d["kv_heads"].cast<int32_t>();

@@ -230,6 +230,8 @@ int32_t Scheduler::schedule(int32_t* buf) {
         const uint64_t k = prefix_key(r);
         if (k) inflight.insert(k);
       }
+  if (cfg_.embed_first)  // embedding requests ahead of generation prompts, arrival order kept
+    std::stable_partition(waiting_.begin(), waiting_.end(), [](const Sequence* s) { return s->embed; });
   std::vector<Sequence*> deferred;
   while (!waiting_.empty() && (int32_t)last_plan_.size() < cfg_.max_num_seqs &&
          (int32_t)running_.size() < cfg_.max_num_seqs && tok_budget > 0 && prefill_budget > 0) {

@@ -43,6 +43,10 @@ struct SchedulerConfig {
   // cache instead of computing the same KV again.
   bool dedup_inflight_prefix = true;
   int32_t max_prefix_defer = 4;
+  // waiting embedding requests (memory lookups / write-backs encoded by the serving model)
+  // are admitted before waiting generation requests: they are short and an agent's next
+  // step waits on them, while a generation prompt behind them loses a few tokens of budget
+  bool embed_first = true;
   bool split_decode = true;            // flash-decoding partitions for long contexts
   // decode-sized steps (<= small_step_tokens tokens) with few decode partitions use
   // small_step_part-key partitions (0 = the general rule); the engine sets it when those

@@ -75,6 +75,8 @@ class EngineConfig:
     kv_reserve_gb: float = 20.0  # HBM always left outside the KV pool (graphs, activations, workspaces)
     prefix_caching: bool = True
     dedup_inflight_prefix: bool = True  # requests wait for an identical prefix another request is prefilling
+    # waiting embedding requests are admitted before waiting generation prompts (scheduler.h)
+    embed_first: bool = os.environ.get("PILOTTAI_EMBED_FIRST", "1") != "0"
     split_decode: bool = True
     # > 0: mid / large steps size their decode partitions for about this many (partition, KV
     # head) workgroups (scheduler.h decode_part_target): no split once the decode rows fill a
@@ -273,6 +275,7 @@ class LLMEngine:
             "att_wide_min_tokens": cfg.att_wide_min_tokens,
             "prefix_caching": cfg.prefix_caching, "split_decode": cfg.split_decode,
             "dedup_inflight_prefix": cfg.dedup_inflight_prefix,
+            "embed_first": bool(cfg.embed_first),
             "token_align": cfg.token_align, "align_slack": cfg.align_slack,
             "kv_heads": self.model.kv_local,
             "small_step_tokens": small_step,

@@ -151,6 +151,24 @@ def test_scheduler_preempts_when_out_of_blocks():
     assert s.total_preemptions >= 1
 
 
+@pytest.mark.parametrize("embed_first", [True, False])
+def test_scheduler_admits_embedding_requests_first(embed_first):
+    """A waiting embedding request (an agent's memory lookup) is admitted ahead of earlier
+    waiting generation prompts that would fill the step's token budget (embed_first, the
+    default); without the option admission is strictly first come, first served."""
+    s = _runtime.Scheduler({"num_blocks": 64, "block_size": 16, "max_num_seqs": 8, "max_num_batched_tokens": 128,
+                            "max_model_len": 512, "prefix_caching": False, "embed_first": embed_first})
+    L = s.layout()
+    buf = np.zeros(L["total"], dtype=np.int32)
+    s.add_request(1, list(range(100, 300)), 0.0, 4, 1, True, [], None)   # 200-token prompt
+    s.add_request(2, list(range(300, 500)), 0.0, 4, 2, True, [], None)
+    s.add_request(3, list(range(600, 620)), 0.0, 1, 3, True, [], None, embed=True)  # 20-token lookup
+    T = s.schedule(buf.ctypes.data)
+    c = buf[L["counts"]:L["counts"] + 8]
+    assert T == 128
+    assert int(c[7]) == (20 if embed_first else 0)  # tokens pooled for embedding requests this step
+
+
 def test_engine_cpu_tiny_end_to_end(tok):
     from pilottai_amd.engine.engine import EngineConfig, LLMEngine
 
