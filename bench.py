@@ -319,6 +319,16 @@ async def run_rank(a, rank: int, world: int, device):
                                           max(1, lookup.stats["passes"] - mem0["passes"]), 3),
                **lookup.latency_summary(mem0["nlat"]),
                "stores": lookup.stats["stores"] - mem0["stores"],
+               # flushes whose writes and queries went through the engine in one embedding call
+               "shared_embeds": lookup.stats.get("shared_embeds", 0) - mem0.get("shared_embeds", 0),
+               # where a lookup's latency goes, ms per pass (embedding through the engine, the
+               # gate's wait for a compute-bound step, the index pass) and per lookup (queued
+               # behind the pass in flight before its own flush starts)
+               "lookup_anatomy_ms": {
+                   k: round(1000 * (lookup.stats.get(k + "_s", 0.0) - mem0.get(k + "_s", 0.0)) /
+                            max(1, (lookup.stats["lookups"] - mem0["lookups"]) if k == "queued"
+                                else (lookup.stats["passes"] - mem0["passes"])), 2)
+                   for k in ("embed", "gate_wait", "search", "queued")},
                # HIP events around each pass on the lookup stream (includes any wait for
                # CUs the engine holds: an upper bound on the passes' kernel time)
                "lookup_device_s": round(dev_s - mem0["device_s"], 3),

@@ -254,3 +254,39 @@ def test_first_step_lookup_overlaps_the_opening_calls():
     mem_prompts = [p for p in llm.prompts if "Relevant memory:" in p]
     assert len(mem_prompts) == 2 and "quarterly revenue" in mem_prompts[0]
     assert lk.cancelled() or lk.done()
+
+
+def test_writes_and_queries_share_one_embedding_call():
+    """With an engine gate attached, the writes pending at a flush and the queries pending
+    beside them are embedded in ONE embedder call (one engine round trip, not two), the
+    writes are in the index before those queries scan it, and the answers match a plain
+    lookup."""
+    class FakeEngine:
+        def add_step_listener(self, fn):
+            pass
+
+    class Counting(HashingEmbedder):
+        def __init__(self, dim):
+            super().__init__(dim)
+            self.calls = []
+
+        def __call__(self, texts):
+            self.calls.append(list(texts))
+            return super().__call__(texts)
+
+    async def run():
+        emb = Counting(64)
+        mem = EnhancedMemory(device="cpu", dim=64, embedder=emb)
+        await mem.store_semantic_batch(["alpha report", "beta memo"])
+        b = MemoryLookupBatcher(mem)
+        b.attach_engine(FakeEngine(), gate_tokens=1024, max_wait_s=0.0)
+        emb.calls.clear()
+        st = asyncio.ensure_future(b.store("gamma notes"))
+        hits = await asyncio.gather(b.search("gamma notes", limit=1), b.search("beta memo", limit=1))
+        await st
+        return emb.calls, hits, b.stats
+
+    calls, hits, stats = asyncio.run(run())
+    assert calls == [["gamma notes", "gamma notes", "beta memo"]]
+    assert [h[0].text for h in hits] == ["gamma notes", "beta memo"]
+    assert stats["shared_embeds"] == 1 and stats["passes"] == 1 and stats["stores"] == 1

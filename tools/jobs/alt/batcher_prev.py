@@ -22,10 +22,8 @@ streaming read that halves the speed of the engine's memory-bound (decode-sized)
 costs a compute-bound 2,048-token prefill step only ~6 % (BENCHMARKS.md, config 4). The engine
 announces every step it launches (LLMEngine.add_step_listener); with a gate attached, a pass
 whose queries are embedded waits until the engine launches a step of at least `gate_tokens`
-tokens -- or for at most `gate_max_wait_s` -- and then starts right behind that launch, so the
-scan overlaps compute-bound work. `stats` counts the passes that started beside such a step and
-the ones the latency cap released. With a gate attached, pending writes and the queries pending
-beside them are embedded in one call (one round trip through the engine, `shared_embeds`).
+tokens -- or for at most `gate_max_wait_s` -- and then starts right behind that launch, so the scan overlaps compute-bound work. `stats` counts the passes that
+started beside such a step and the ones the latency cap released.
 """
 from __future__ import annotations
 
@@ -56,8 +54,7 @@ class MemoryLookupBatcher:
             memory.index.pass_events = []  # the index records (start, end) around each pass
         self.stats = {"lookups": 0, "passes": 0, "stores": 0, "store_batches": 0, "host_s": 0.0,
                       "device_s": 0.0, "max_batch_seen": 0, "passes_beside_heavy": 0, "passes_capped": 0,
-                      "gate_wait_s": 0.0, "shared_embeds": 0,
-                      "embed_s": 0.0, "search_s": 0.0, "queued_s": 0.0}
+                      "gate_wait_s": 0.0}
         self._gate_tokens = 0
         self._gate_wait = 0.0
         self._heavy: Optional[asyncio.Event] = None
@@ -152,23 +149,10 @@ class MemoryLookupBatcher:
 
     async def _flush_once(self):
         writes, self._writes = self._writes, []
-        pre = None  # (batch, query vectors) embedded together with the writes
         if writes:
-            taken = []
             try:
-                wvecs = None
-                if self._heavy is not None and self._pending and self.min_batch <= 1:
-                    # engine embedder: the writes and the pending queries share ONE embedding
-                    # round trip through the engine (they were two in sequence)
-                    taken, self._pending = self._pending[: self.max_batch], self._pending[self.max_batch:]
-                    te = time.perf_counter()
-                    allv = await self.memory.embed_queries([w[0] for w in writes] + [b[0] for b in taken])
-                    self.stats["embed_s"] += time.perf_counter() - te
-                    wvecs, pre = allv[: len(writes)], (taken, allv[len(writes):])
-                    self.stats["shared_embeds"] += 1
                 rows = await self.memory.store_semantic_batch([w[0] for w in writes], [w[1] for w in writes],
-                                                              [w[2] for w in writes], [w[3] for w in writes],
-                                                              vecs=wvecs)
+                                                              [w[2] for w in writes], [w[3] for w in writes])
                 for w, r in zip(writes, rows):
                     if not w[4].done():
                         w[4].set_result(r)
@@ -176,39 +160,28 @@ class MemoryLookupBatcher:
                 for w in writes:
                     if not w[4].done():
                         w[4].set_exception(e)
-                if taken and pre is None:  # the shared embedding failed: the queries go again alone
-                    self._pending = taken + self._pending
             self.stats["stores"] += len(writes)
             self.stats["store_batches"] += 1
-        if pre is None and self._pending and self.min_batch > 1 and self.max_wait_s > 0:
+        if self._pending and self.min_batch > 1 and self.max_wait_s > 0:
             while len(self._pending) < self.min_batch and not self._writes and \
                     time.perf_counter() - self._pending[0][5] < self.max_wait_s:
                 await asyncio.sleep(0.001)
             self.stats["coalesce_waits"] = self.stats.get("coalesce_waits", 0) + 1
-        if pre is not None or self._pending:
-            if pre is not None:
-                batch, vecs = pre
-            else:
-                batch, self._pending = self._pending[: self.max_batch], self._pending[self.max_batch:]
-                vecs = None
+        if self._pending:
+            batch, self._pending = self._pending[: self.max_batch], self._pending[self.max_batch:]
             limit = max(b[3] for b in batch)
             t0 = time.perf_counter()
             try:
                 qs = [b[0] for b in batch]
+                vecs = None
                 if self._heavy is not None:  # embed now, scan beside the next compute-bound step
-                    if vecs is None:
-                        te = time.perf_counter()
-                        vecs = await self.memory.embed_queries(qs)
-                        self.stats["embed_s"] += time.perf_counter() - te
+                    vecs = await self.memory.embed_queries(qs)
                     await self._await_heavy()
-                ts = time.perf_counter()
                 hits = await self.memory.search_batch(qs, tags=[b[1] for b in batch],
                                                       min_priority=[b[2] for b in batch], limit=limit, vecs=vecs)
-                self.stats["search_s"] += time.perf_counter() - ts
                 now = time.perf_counter()
                 for b, h in zip(batch, hits):
                     self._lat.append(now - b[5])
-                    self.stats["queued_s"] += t0 - b[5]
                     if not b[4].done():
                         b[4].set_result(h[: b[3]])
             except Exception as e:  # noqa: BLE001

@@ -89,7 +89,6 @@ class EngineEmbedder:
         # "last": the last token's state — embedding requests then reuse the engine's prefix
         # cache (texts that share a prefix, like an agent's successive lookups, share its work)
         self.pooling = pooling
-        self._stream = None
 
     def embed(self, texts: Sequence[str]) -> np.ndarray:
         import torch
@@ -101,16 +100,8 @@ class EngineEmbedder:
             ids = [self.engine.tok.encode(t)[: self.max_tokens] or [0] for t in texts]
             if not ids:
                 return np.zeros((0, self.dim), np.float32)
-            h = self.engine.embed(ids, pooling=self.pooling)
-            if self.proj.device.type != "cuda":
-                return F.normalize(torch.from_numpy(h) @ self.proj, dim=1).numpy()
-            # the projection on a stream of its own: on the device's default stream it would
-            # queue behind the engine steps already in flight there (1-2 steps of latency)
-            if self._stream is None:
-                self._stream = torch.cuda.Stream(device=self.proj.device, priority=-1)
-            with torch.cuda.stream(self._stream):
-                hd = torch.from_numpy(h).to(self.proj.device)
-                return F.normalize(hd @ self.proj, dim=1).cpu().numpy()
+            h = torch.from_numpy(self.engine.embed(ids, pooling=self.pooling)).to(self.proj.device)
+            return F.normalize(h @ self.proj, dim=1).cpu().numpy()
         with torch.inference_mode():
             if self.pool == "hidden":
                 for i in range(0, len(texts), self.batch_size):

@@ -85,13 +85,10 @@ class EnhancedMemory:
         items = [MemoryItem(text=text, metadata=metadata or {}, tags=set(tags or ()), priority=priority,
                             expires_at=datetime.now() + timedelta(seconds=ttl) if ttl is not None else None)]
         async with self._semantic_lock:
-            if getattr(self.index.device, "type", "cpu") == "cuda":
-                return (await asyncio.get_running_loop().run_in_executor(None, self._store_items, items))[0]
             return self._store_items(items)[0]
 
     async def store_semantic_batch(self, texts: Sequence[str], metadatas=None, tags=None, priorities=None,
-                                   ttl: Optional[float] = None, vecs=None) -> List[int]:
-        """`vecs`: the texts' embeddings when the caller already has them (embed_queries)."""
+                                   ttl: Optional[float] = None) -> List[int]:
         n = len(texts)
         items = [MemoryItem(text=t, metadata=(metadatas[i] if metadatas else {}),
                             tags=set(tags[i]) if tags else set(), priority=(priorities[i] if priorities else 0),
@@ -103,11 +100,12 @@ class EnhancedMemory:
             if not n:
                 return []
             if getattr(self.index.device, "type", "cpu") == "cuda":
-                # the embedder may be the serving engine itself (EngineEmbedder), and the row
-                # writes are host->device copies: both in a worker thread, so the event loop
-                # keeps serving the agents meanwhile
-                return await asyncio.get_running_loop().run_in_executor(None, self._store_items, items, vecs)
-            return self._store_items(items, vecs)
+                # the embedder may be the serving engine itself (EngineEmbedder): embed in a
+                # worker thread so the event loop keeps serving the agents meanwhile
+                vecs = await asyncio.get_running_loop().run_in_executor(
+                    None, self.embedder, [it.text for it in items])
+                return self._store_items(items, vecs)
+            return self._store_items(items)
 
     def _store_items(self, items: List[MemoryItem], vecs=None) -> List[int]:
         if vecs is None:

@@ -153,9 +153,7 @@ class SemanticIndex:
         """Append rows; returns their row ids. `expires_at` is wall-clock time.time() or None."""
         v = torch.as_tensor(np.asarray(vectors, dtype=np.float32))
         n = v.shape[0]
-        # on the index's stream: the host copies below wait for earlier passes only, never
-        # for engine steps queued on the device's default stream
-        with self._lock, self._stream_ctx():
+        with self._lock:
             if self.growable and self.size + n > self.capacity and self.capacity < self.max_capacity:
                 self._grow(self.size + n)
             rows = [(self.size + i) % self.capacity for i in range(n)]
@@ -216,12 +214,11 @@ class SemanticIndex:
         ts = self.row_tags_py.get(row)
         if ts is not None:
             return ts
-        with self._stream_ctx():
-            bits = int(self.tagbits[row].item())
+        bits = int(self.tagbits[row].item())
         return frozenset(t for t, b in self.tags.bits.items() if (bits >> b) & 1)
 
     def delete(self, rows: Sequence[int]):
-        with self._lock, self._stream_ctx():
+        with self._lock:
             idx = torch.tensor(list(rows), dtype=torch.long, device=self.device)
             self.priority.index_fill_(0, idx, -(1 << 30))
             for r in rows:
