@@ -665,18 +665,27 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void paged_attn_kernel(
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int TPW = 16 / G;
   const int psz_q = part_size ? part_size[0] : ATT_PART;
+  // Grid (KV, slots): the KV head is the fastest-varying workgroup index, so workgroups are
+  // dispatched item by item over all KV heads -- the heaviest-first item order the scheduler
+  // builds holds across the heads (with the head as the slow index, head 7's heaviest items
+  // were dispatched after heads 0-6's lightest) -- and the round-robin XCD assignment keeps a
+  // KV head's workgroups on one XCD (KV = 8), whose L2 then holds only that head's K/V.
+  // tools/attn_bench.py: the bench's 2,048-token step 54.8 -> 45.3 us, a 2,048-token prompt
+  // 79.6 -> 67.3 us (profiles/r5_attention_grid_ab.jsonl).
+  const int kvh = blockIdx.x;
+  const int slot = blockIdx.y;
+  const int nslots = gridDim.y;
   // The first item is loaded together with the item count, not after it: one dependent
   // memory round trip less before the K/V stream starts (decode steps with few rows are
-  // latency-bound). In bounds: the host sizes the grid to gridDim.x <= max_items, the
+  // latency-bound). In bounds: the host sizes the grid to nslots <= max_items, the
   // length of `items`.
   const int n = n_items[0];
-  int4 it_next = items[min((int)blockIdx.x, max(n - 1, 0))];
-  if ((int)blockIdx.x >= n) return;  // the grid is sized for the bucket's largest item list
+  int4 it_next = items[min(slot, max(n - 1, 0))];
+  if (slot >= n) return;  // the grid is sized for the bucket's largest item list
   const int psz = psz_q;  // decode partition (keys), per step
-  const int kvh = blockIdx.y;
-  for (int item = blockIdx.x; item < n; item += gridDim.x) {
+  for (int item = slot; item < n; item += nslots) {
     const int4 it = it_next;
-    if (item + (int)gridDim.x < n) it_next = items[item + gridDim.x];
+    if (item + nslots < n) it_next = items[item + nslots];
     const int nq = it.z & 0xff;
     if (nq <= TPW)
       decode_item<G, NW>(it, smem, out, part_o, part_ml, counters, q, k_cache, v_cache, q_start, q_len, ctx_len,
@@ -700,7 +709,7 @@ extern "C" int pa_paged_attention(void* out, float* part_o, float* part_ml, cons
   const int G = H / KV;
   // items are strided over the grid: ~8 resident workgroups per CU over all KV heads
   const int gx = max_items < 1 ? 1 : (max_items < 2048 / KV ? max_items : (2048 / KV > 0 ? 2048 / KV : 1));
-  const dim3 grid(gx, KV);
+  const dim3 grid(KV, gx);
 #define PA_ATT(GG)                                                                              \
   do {                                                                                          \
     if (max_items <= 0) break;                                                                  \
