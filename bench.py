@@ -516,6 +516,8 @@ def main():
 
     from pilottai_amd.parallel import comm
 
+    if a.share_gpu:  # RCCL refuses two ranks on one device: the rehearsal's collectives use gloo
+        os.environ.setdefault("PILOTTAI_DIST_BACKEND", "gloo")
     rank, world, local_rank = comm.init_distributed()
     if world != a.gpus:
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}: launch one rank per GPU")
