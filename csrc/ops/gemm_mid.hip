@@ -298,27 +298,60 @@ __global__ __launch_bounds__(256) void mid_gemm_kernel(const Args A) {
   if (!pa::handoff_last(A.counters + tile_id, A.S, lflag, A.acq)) return;
   const __amdgpu_buffer_rsrc_t rall =
       __builtin_amdgcn_make_buffer_rsrc(slab_base, 0, A.S * BM * BN * 4, 0x00020000);
-  // thread -> (token row, 4 consecutive columns of one tile; pair epilogues: of an even tile)
-  constexpr int QPR = BN / 4;  // column quads per row
-  for (int e = threadIdx.x; e < BM * QPR; e += 256) {
-    const int tl = e / QPR, q4 = (e % QPR) * 4;
-    const int m = row0 + tl;
-    if (m >= A.M) continue;
-    const int lt = q4 >> 4, cq = q4 & 15;
-    if constexpr (pair_epi<EPI>()) {
-      if (lt & 1) continue;
+  // thread -> (token row, 4 consecutive columns of one tile; pair epilogues: of an even tile).
+  // RU quads per thread per pass with every slab load of the pass issued before the first
+  // add (the slabs come from memory: one quad at a time put ~1.5 us of load latency per quad
+  // on the critical path -- 16 quads per thread at BM = BN = 128 -- and made split-K tiles
+  // slower than whole-K ones, profiles/r5_mid_splitk_reduce.jsonl)
+  constexpr int QPR = BN / 4;                          // column quads per row
+  constexpr int QW = pair_epi<EPI>() ? QPR / 2 : QPR;  // quads of work per row
+  constexpr int NQ = BM * QW;
+  constexpr int RU = 4;
+  for (int e0 = threadIdx.x; e0 < NQ; e0 += 256 * RU) {
+    int tl[RU], q4[RU];
+    f32x4 sum[RU], sum2[RU];
+#pragma unroll
+    for (int u = 0; u < RU; ++u) {
+      const int e = min(e0 + u * 256, NQ - 1);
+      tl[u] = e / QW;
+      const int k = e % QW;
+      q4[u] = pair_epi<EPI>() ? (k >> 2) * 32 + (k & 3) * 4 : k * 4;
+      sum[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+      sum2[u] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
-    f32x4 sum = f32x4{0.f, 0.f, 0.f, 0.f}, sum2 = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int p = 0; p < A.S; ++p) {
-      sum += __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rall, ((p * BM + tl) * BN + q4) * 4, 0, 16));
-      if constexpr (pair_epi<EPI>())
-        sum2 += __builtin_bit_cast(f32x4,
-                                   __builtin_amdgcn_raw_buffer_load_b128(rall, ((p * BM + tl) * BN + q4 + 16) * 4, 0, 16));
+    for (int p0 = 0; p0 < A.S; p0 += 4) {
+      f32x4 v[4][RU], v2[4][RU];
+#pragma unroll
+      for (int p = 0; p < 4; ++p)
+#pragma unroll
+        for (int u = 0; u < RU; ++u) {
+          const int pp = min(p0 + p, A.S - 1);
+          v[p][u] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                   rall, ((pp * BM + tl[u]) * BN + q4[u]) * 4, 0, 16));
+          if constexpr (pair_epi<EPI>())
+            v2[p][u] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                      rall, ((pp * BM + tl[u]) * BN + q4[u] + 16) * 4, 0, 16));
+        }
+#pragma unroll
+      for (int p = 0; p < 4; ++p)
+        if (p0 + p < A.S) {
+#pragma unroll
+          for (int u = 0; u < RU; ++u) {
+            sum[u] += v[p][u];
+            if constexpr (pair_epi<EPI>()) sum2[u] += v2[p][u];
+          }
+        }
     }
-    const float rs = row_scale(m);
-    const float sq = store_quad<EPI>(A, m, nt * NTL + lt, cq, sum * rs, sum2 * rs);
-    if constexpr (EPI == EP_RESID) {
-      if (A.ss_out) atomicAdd(rsq + tl, sq);  // LDS
+#pragma unroll
+    for (int u = 0; u < RU; ++u) {
+      const int m = row0 + tl[u];
+      if (e0 + u * 256 >= NQ || m >= A.M) continue;
+      const int lt = q4[u] >> 4, cq = q4[u] & 15;
+      const float rs = row_scale(m);
+      const float sq = store_quad<EPI>(A, m, nt * NTL + lt, cq, sum[u] * rs, sum2[u] * rs);
+      if constexpr (EPI == EP_RESID) {
+        if (A.ss_out) atomicAdd(rsq + tl[u], sq);  // LDS
+      }
     }
   }
   if constexpr (EPI == EP_RESID) {
