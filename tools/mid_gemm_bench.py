@@ -37,11 +37,25 @@ def timeit(fn, ncopies, iters=20):
     return s.elapsed_time(e) * 1000 / iters
 
 
-args = [a for a in sys.argv[1:] if not a.startswith("--")]
+args = [a for i, a in enumerate(sys.argv[1:], 1) if not a.startswith("--") and not sys.argv[i - 1].startswith("--")]
 quick = "--quick" in sys.argv
 fused_sweep = "--fused-sweep" in sys.argv  # time every config in the engine's epilogue form
 Ms = [int(v) for v in (args[0] if args else "64,96,128,192,256,384,512").split(",")]
-CFGS = [(1, fm, fn, 4, S) for fm in (1, 2, 4, 8) for fn in (2, 4) for S in (1, 2, 3, 4, 6)]
+def _opt(name, default):
+    for i, v in enumerate(sys.argv):
+        if v == name and i + 1 < len(sys.argv):
+            return [int(x) for x in sys.argv[i + 1].split(",")]
+    return default
+
+
+_FMS, _FNS, _SS = _opt("--fms", (1, 2, 4, 8)), _opt("--fns", (2, 4)), _opt("--splits", (1, 2, 3, 4, 6))
+_SHAPES = None
+for _i, _v in enumerate(sys.argv):
+    if _v == "--shapes" and _i + 1 < len(sys.argv):
+        _SHAPES = sys.argv[_i + 1].split(",")
+if _SHAPES:
+    shapes = [s for s in shapes if s[2] in _SHAPES]
+CFGS = [(1, fm, fn, 4, S) for fm in _FMS for fn in _FNS for S in _SS]
 torch.manual_seed(0)
 for N, K, name in shapes:
     gb = N * K * 2 / 1e9
