@@ -290,3 +290,5 @@ def test_writes_and_queries_share_one_embedding_call():
     assert calls == [["gamma notes", "gamma notes", "beta memo"]]
     assert [h[0].text for h in hits] == ["gamma notes", "beta memo"]
     assert stats["shared_embeds"] == 1 and stats["passes"] == 1 and stats["stores"] == 1
+    # the lookup latency anatomy bench.py reports (memory.lookup_anatomy_ms)
+    assert stats["embed_s"] > 0 and stats["search_s"] > 0 and stats["queued_s"] >= 0
