@@ -268,7 +268,7 @@ async def run_rank(a, rank: int, world: int, device):
     freeze_heap()  # agents, serve and warm-up state: out of the timed region's GC passes
     await coll(comm.barrier)  # worker ranks keep serving the plane meanwhile
     st0 = dict(eng.stats)  # after the barrier: every rank's warmup work is behind it
-    mem0 = dict(lookup.stats, device_s=lookup.lookup_device_seconds(), nlat=len(lookup._lat)) \
+    mem0 = dict(lookup.stats, device_s=lookup.lookup_device_seconds(), nlat=lookup.lat_count) \
         if lookup is not None else None
     bh0 = {b: list(v) for b, v in eng.bucket_hist.items()}
     u0 = dict(llm.usage)

@@ -74,6 +74,38 @@ PYBIND11_MODULE(_runtime, m) {
       .def("published", &ShmRing::published)
       .def("unlink", &ShmRing::unlink);
 
+  py::class_<ShmGather>(m, "ShmGather")
+      .def(py::init<const std::string&, int, int, size_t, bool, double>(), py::arg("name"), py::arg("world"),
+           py::arg("rank"), py::arg("slot_bytes"), py::arg("create"), py::arg("attach_timeout_s") = 60.0)
+      // payload: bytes (<= slot_bytes) -> list of `world` bytes (rank order), or None on timeout
+      // offset / length: return only bytes [offset, offset + length) of each peer's payload
+      // (an all-to-all when every rank's payload is the concatenation of per-destination chunks)
+      .def("all_gather", [](ShmGather& g, const py::bytes& payload, double timeout_s, int64_t offset,
+                            int64_t length) -> py::object {
+             char* buf = nullptr;
+             Py_ssize_t n = 0;
+             if (PyBytes_AsStringAndSize(payload.ptr(), &buf, &n) != 0) throw py::error_already_set();
+             if ((size_t)n > g.slot_bytes()) throw std::length_error("ShmGather payload larger than the slot");
+             bool ok;
+             {
+               py::gil_scoped_release nogil;
+               ok = g.publish(buf, (size_t)n, timeout_s);
+             }
+             if (!ok) return py::none();
+             py::list res;
+             for (int q = 0; q < g.world(); ++q) {
+               const int64_t m = g.peer_size(q);
+               const int64_t a = std::min<int64_t>(std::max<int64_t>(offset, 0), m);
+               const int64_t e = length < 0 ? m : std::min<int64_t>(m, a + length);
+               res.append(py::bytes(g.peer(q) + a, (size_t)(e - a)));
+             }
+             g.finish();
+             return res;
+           }, py::arg("payload"), py::arg("timeout_s") = 600.0, py::arg("offset") = 0, py::arg("length") = -1)
+      .def_property_readonly("slot_bytes", &ShmGather::slot_bytes)
+      .def_property_readonly("waited_s", &ShmGather::waited_s)
+      .def("unlink", &ShmGather::unlink);
+
   py::class_<Tokenizer>(m, "Tokenizer")
       .def(py::init([](const std::vector<py::bytes>& vocab) {
         std::vector<std::string> v;
@@ -126,6 +158,7 @@ PYBIND11_MODULE(_runtime, m) {
         if (d.contains("dedup_inflight_prefix")) c.dedup_inflight_prefix = d["dedup_inflight_prefix"].cast<bool>();
         if (d.contains("max_prefix_defer")) c.max_prefix_defer = d["max_prefix_defer"].cast<int32_t>();
         if (d.contains("embed_first")) c.embed_first = d["embed_first"].cast<bool>();
+        if (d.contains("embed_first_max_wait")) c.embed_first_max_wait = d["embed_first_max_wait"].cast<int32_t>();
         if (d.contains("split_decode")) c.split_decode = d["split_decode"].cast<bool>();
         if (d.contains("token_align")) c.token_align = d["token_align"].cast<int32_t>();
         if (d.contains("kv_heads")) c.kv_heads = d["kv_heads"].cast<int32_t>();

@@ -113,6 +113,7 @@ void Scheduler::preempt(Sequence* s) {
   free_seq(s, true);
   s->num_computed = 0;
   s->running = false;
+  s->preempted = true;
   waiting_.push_front(s);
   ++stat_preemptions_;
 }
@@ -230,8 +231,19 @@ int32_t Scheduler::schedule(int32_t* buf) {
         const uint64_t k = prefix_key(r);
         if (k) inflight.insert(k);
       }
-  if (cfg_.embed_first)  // embedding requests ahead of generation prompts, arrival order kept
-    std::stable_partition(waiting_.begin(), waiting_.end(), [](const Sequence* s) { return s->embed; });
+  if (cfg_.embed_first) {
+    // embedding requests ahead of generation prompts, arrival order kept within each class;
+    // preempted sequences and prompts already passed over embed_first_max_wait times keep
+    // their place ahead of the embeds
+    const int32_t max_wait = cfg_.embed_first_max_wait;
+    auto ahead = [max_wait](const Sequence* s) {
+      return !s->embed && (s->preempted || s->embed_passed >= max_wait);
+    };
+    auto it = std::stable_partition(waiting_.begin(), waiting_.end(), ahead);
+    auto emb_end = std::stable_partition(it, waiting_.end(), [](const Sequence* s) { return s->embed; });
+    if (it != emb_end)  // embeds went ahead of these prompts this step
+      for (auto p = emb_end; p != waiting_.end(); ++p) ++(*p)->embed_passed;
+  }
   std::vector<Sequence*> deferred;
   while (!waiting_.empty() && (int32_t)last_plan_.size() < cfg_.max_num_seqs &&
          (int32_t)running_.size() < cfg_.max_num_seqs && tok_budget > 0 && prefill_budget > 0) {
@@ -258,6 +270,7 @@ int32_t Scheduler::schedule(int32_t* buf) {
     if (!ensure_blocks(s, s->num_computed + n)) break;
     waiting_.pop_front();
     s->running = true;
+    s->preempted = false;
     running_.push_back(s);
     if (key && s->num_computed < 2 * B) inflight.insert(key);  // its leading blocks are computed now
     last_plan_.push_back({s, n, !s->embed && s->num_computed + n == (int32_t)s->tokens.size()});

@@ -47,6 +47,10 @@ struct SchedulerConfig {
   // are admitted before waiting generation requests: they are short and an agent's next
   // step waits on them, while a generation prompt behind them loses a few tokens of budget
   bool embed_first = true;
+  // ... but never without bound: a preempted sequence (it already held KV) stays ahead of the
+  // embeds, and a generation prompt passed over by embeds for embed_first_max_wait steps is
+  // admitted in arrival order again (no starvation under a steady embed stream)
+  int32_t embed_first_max_wait = 8;
   bool split_decode = true;            // flash-decoding partitions for long contexts
   // decode-sized steps (<= small_step_tokens tokens) with few decode partitions use
   // small_step_part-key partitions (0 = the general rule); the engine sets it when those
@@ -126,6 +130,8 @@ struct Sequence {
   bool embed = false;
   int32_t embed_slot = -1;
   int32_t defer_count = 0;  // steps deferred waiting for an in-flight identical prefix
+  int32_t embed_passed = 0; // steps an embed-first admission put embeds ahead of this prompt
+  bool preempted = false;   // lost its KV to a preemption and waits to resume
   // pipelined steps (Scheduler "speculative rows"): plans not yet committed that list this
   // sequence; the plan (id) and row in which it last sampled; the plan and entry index of
   // its speculative continuation

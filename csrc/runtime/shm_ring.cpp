@@ -143,4 +143,130 @@ bool ShmRing::get(int c, int64_t* rec, double timeout_s) {
   return true;
 }
 
+namespace {
+constexpr uint64_t kGatherMagic = 0x70696c6f74676174ULL;  // "pilotgat"
+
+void* map_segment(const std::string& name, size_t bytes, bool create, double attach_timeout_s) {
+  int fd = -1;
+  if (create) {
+    shm_unlink(name.c_str());
+    fd = shm_open(name.c_str(), O_CREAT | O_EXCL | O_RDWR, 0600);
+    if (fd < 0) throw std::runtime_error("shm_open(create) failed for " + name);
+    if (ftruncate(fd, (off_t)bytes) != 0) {
+      close(fd);
+      shm_unlink(name.c_str());
+      throw std::runtime_error("ftruncate failed for " + name);
+    }
+  } else {
+    const double t0 = now_s();
+    Backoff b;
+    while (true) {
+      fd = shm_open(name.c_str(), O_RDWR, 0600);
+      if (fd >= 0) {
+        struct stat st;
+        if (fstat(fd, &st) == 0 && (size_t)st.st_size >= bytes) break;
+        close(fd);
+        fd = -1;
+      }
+      if (now_s() - t0 > attach_timeout_s) throw std::runtime_error("timed out attaching to " + name);
+      b.wait();
+    }
+  }
+  void* p = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+  close(fd);
+  if (p == MAP_FAILED) throw std::runtime_error("mmap failed for " + name);
+  return p;
+}
+}  // namespace
+
+ShmGather::ShmGather(const std::string& name, int world, int rank, size_t slot_bytes, bool create,
+                     double attach_timeout_s)
+    : name_(name.empty() || name[0] == '/' ? name : "/" + name), world_(world), rank_(rank),
+      slot_(round_up(slot_bytes, 64)), owner_(create) {
+  if (world <= 0 || rank < 0 || rank >= world || slot_bytes == 0)
+    throw std::invalid_argument("ShmGather geometry");
+  const size_t ctl = round_up(sizeof(Ctl), 64);
+  const size_t peers = sizeof(Peer) * (size_t)world;
+  bytes_ = ctl + peers + 2 * (size_t)world * slot_;
+  base_ = map_segment(name_, bytes_, create, attach_timeout_s);
+  ctl_ = reinterpret_cast<Ctl*>(base_);
+  peers_ = reinterpret_cast<Peer*>(static_cast<char*>(base_) + ctl);
+  data_ = static_cast<char*>(base_) + ctl + peers;
+  auto* magic = reinterpret_cast<std::atomic<uint64_t>*>(&ctl_->magic);
+  if (create) {
+    std::memset(base_, 0, ctl + peers);  // the data banks are zero pages already
+    ctl_->world = world;
+    ctl_->slot = (int64_t)slot_;
+    for (int q = 0; q < world; ++q) {
+      peers_[q].arrive.store(0, std::memory_order_relaxed);
+      peers_[q].done.store(0, std::memory_order_relaxed);
+    }
+    std::atomic_thread_fence(std::memory_order_release);
+    magic->store(kGatherMagic, std::memory_order_release);
+  } else {
+    const double t0 = now_s();
+    Backoff b;
+    while (magic->load(std::memory_order_acquire) != kGatherMagic) {
+      if (now_s() - t0 > attach_timeout_s) throw std::runtime_error("gather " + name_ + " never initialised");
+      b.wait();
+    }
+    if (ctl_->world != world || ctl_->slot != (int64_t)slot_)
+      throw std::runtime_error("gather " + name_ + " geometry mismatch");
+  }
+}
+
+ShmGather::~ShmGather() {
+  if (base_) munmap(base_, bytes_);
+  if (owner_) shm_unlink(name_.c_str());
+}
+
+void ShmGather::unlink() { shm_unlink(name_.c_str()); }
+
+bool ShmGather::publish(const void* in, size_t n, double timeout_s) {
+  if (n > slot_) throw std::length_error("ShmGather payload larger than the slot");
+  const int64_t s = round_ + 1;
+  const int bank = (int)(s & 1);
+  const double t0 = now_s();
+  Backoff b;
+  // the bank's previous use (round s - 2) must be fully read by every rank
+  for (int q = 0; q < world_; ++q)
+    while (peers_[q].done.load(std::memory_order_acquire) < s - 2) {
+      if (now_s() - t0 > timeout_s) return false;
+      b.wait();
+    }
+  const double t1 = now_s();
+  char* mine = data_ + ((size_t)bank * world_ + rank_) * slot_;
+  if (n) std::memcpy(mine, in, n);
+  peers_[rank_].size[bank] = (int64_t)n;
+  peers_[rank_].arrive.store(s, std::memory_order_release);
+  const double t2 = now_s();
+  for (int q = 0; q < world_; ++q)
+    while (peers_[q].arrive.load(std::memory_order_acquire) < s) {
+      if (now_s() - t0 > timeout_s) return false;
+      b.wait();
+    }
+  waited_ += (t1 - t0) + (now_s() - t2);
+  round_ = s;
+  return true;
+}
+
+const char* ShmGather::peer(int q) const {
+  return data_ + ((size_t)(round_ & 1) * world_ + q) * slot_;
+}
+
+int64_t ShmGather::peer_size(int q) const { return peers_[q].size[round_ & 1]; }
+
+void ShmGather::finish() { peers_[rank_].done.store(round_, std::memory_order_release); }
+
+bool ShmGather::all_gather(const void* in, size_t n, void* out, int64_t* sizes, double timeout_s) {
+  if (!publish(in, n, timeout_s)) return false;
+  char* o = static_cast<char*>(out);
+  for (int q = 0; q < world_; ++q) {
+    sizes[q] = peer_size(q);
+    if (sizes[q]) std::memcpy(o + (size_t)q * slot_, peer(q), (size_t)sizes[q]);
+  }
+  finish();
+  return true;
+}
+
 }  // namespace rt

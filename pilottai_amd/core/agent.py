@@ -145,6 +145,7 @@ class BaseAgent:
         self.task_history: Deque[Dict[str, Any]] = deque(maxlen=1000)
         self.task_metrics: Dict[str, int] = {"completed": 0, "failed": 0, "timeout": 0}
         self.metrics = self.task_metrics  # documented alias `agent.metrics[...]`
+        self.memory_errors: Dict[str, int] = {"store": 0, "search": 0}  # failed memory calls
         self.child_agents: Dict[str, "BaseAgent"] = {}
         self.parent: Optional["BaseAgent"] = None
         self._memory = memory
@@ -584,6 +585,7 @@ class BaseAgent:
         try:
             hits = await self.memory_lookup.search(query, limit=self.memory_top_k)
         except Exception as e:  # noqa: BLE001 — memory is advisory (reference: warn and go on)
+            self.memory_errors["search"] += 1
             self.logger.warning("memory search failed: %s", e)
             return "none"
         return "; ".join(h.text[:160] for h in hits) or "none"
@@ -596,8 +598,10 @@ class BaseAgent:
                 f"{task.description[:300]} => {'done' if ok else 'failed'}: {str(evaluation.get('reasoning', ''))[:200]}",
                 metadata={"task_id": task.id, "agent": self.id, "success": ok}, tags={self.config.role},
                 priority=1 if ok else 0)
-        except Exception as e:  # noqa: BLE001
-            self.logger.warning("memory store failed: %s", e)
+        except Exception as e:  # noqa: BLE001 -- advisory, but counted: get_metrics() reports it
+            self.memory_errors["store"] += 1
+            n = self.memory_errors["store"]
+            (self.logger.error if n >= 3 else self.logger.warning)("memory store failed (%d so far): %s", n, e)
 
     async def _execute_step(self, step: Dict[str, Any]) -> Any:
         name = step.get("tool")
@@ -652,6 +656,8 @@ class BaseAgent:
             "last_error": self.last_error,
             "resource_usage": max(cpu, mem),
             "llm_usage": dict(self.llm_usage),
+            "memory_store_failures": self.memory_errors["store"],
+            "memory_search_failures": self.memory_errors["search"],
         }
         eng = getattr(getattr(self._llm, "engine", None), "metrics", None)
         if callable(eng):

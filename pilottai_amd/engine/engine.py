@@ -582,7 +582,10 @@ class LLMEngine:
     def add_step_listener(self, fn: Callable[[int], None]):
         """fn(tokens) runs on the engine thread right after each step is launched (keep it cheap:
         e.g. loop.call_soon_threadsafe). The kind of step the device is about to run."""
-        self._step_listeners.append(fn)
+        self._step_listeners = self._step_listeners + [fn]  # copy-on-write: the engine thread iterates
+
+    def remove_step_listener(self, fn: Callable[[int], None]):
+        self._step_listeners = [f for f in self._step_listeners if f is not fn]
 
     def _notify_launch(self, T: int):
         for fn in self._step_listeners:

@@ -30,13 +30,18 @@ beside them are embedded in one call (one round trip through the engine, `shared
 from __future__ import annotations
 
 import asyncio
+import logging
 import time
+from collections import deque
 from typing import Any, Dict, List, Optional, Set, Tuple
 
 from .enhanced_memory import EnhancedMemory, MemoryItem
 
+_log = logging.getLogger("pilottai.memory")
+
 
 class MemoryLookupBatcher:
+    LAT_KEEP = 1 << 16
     def __init__(self, memory: EnhancedMemory, max_batch: int = 256, time_device: bool = True,
                  min_batch: int = 1, max_wait_s: float = 0.0):
         """min_batch / max_wait_s: before a pass, wait (in 1 ms sleeps) until `min_batch`
@@ -57,12 +62,17 @@ class MemoryLookupBatcher:
         self.stats = {"lookups": 0, "passes": 0, "stores": 0, "store_batches": 0, "host_s": 0.0,
                       "device_s": 0.0, "max_batch_seen": 0, "passes_beside_heavy": 0, "passes_capped": 0,
                       "gate_wait_s": 0.0, "shared_embeds": 0,
-                      "embed_s": 0.0, "search_s": 0.0, "queued_s": 0.0}
+                      "embed_s": 0.0, "search_s": 0.0, "queued_s": 0.0,
+                      "store_failures": 0, "lookup_failures": 0}
         self._gate_tokens = 0
         self._gate_wait = 0.0
         self._heavy: Optional[asyncio.Event] = None
         self._last_heavy = 0.0
-        self._lat: List[float] = []  # per-lookup latency (s), for p50 / p99
+        # per-lookup latency (s) for p50 / p99: the most recent LAT_KEEP, plus the running total
+        self._lat: deque = deque(maxlen=self.LAT_KEEP)
+        self.lat_count = 0
+        self._engine = None
+        self._listener = None
 
     # ----------------------------------------------------------------- engine gate
     def attach_engine(self, engine, gate_tokens: int = 1024, max_wait_s: float = 0.03):
@@ -74,9 +84,23 @@ class MemoryLookupBatcher:
         self._gate_wait = float(max_wait_s)
 
         def on_launch(T: int):
-            if T >= self._gate_tokens:
-                loop.call_soon_threadsafe(self._mark_heavy)
+            if T >= self._gate_tokens and not loop.is_closed():
+                try:
+                    loop.call_soon_threadsafe(self._mark_heavy)
+                except RuntimeError:  # the loop closed between the check and the call
+                    pass
+        self.detach_engine()
         engine.add_step_listener(on_launch)
+        self._engine, self._listener = engine, on_launch
+
+    def detach_engine(self):
+        """Remove the step listener `attach_engine` registered (no-op when none)."""
+        if self._engine is not None and self._listener is not None:
+            rm = getattr(self._engine, "remove_step_listener", None)
+            if rm is not None:
+                rm(self._listener)
+        self._engine = self._listener = None
+        self._heavy = None
 
     def _mark_heavy(self):
         self._last_heavy = time.perf_counter()
@@ -101,7 +125,10 @@ class MemoryLookupBatcher:
         self.stats["gate_wait_s"] += time.perf_counter() - t0
 
     def latency_summary(self, since: int = 0) -> dict:
-        lat = sorted(self._lat[since:])
+        """p50 / p99 of the lookups after the first `since` (a `lat_count` taken earlier); only
+        the most recent LAT_KEEP lookups are kept."""
+        n = min(len(self._lat), max(0, self.lat_count - since))
+        lat = sorted(list(self._lat)[len(self._lat) - n:]) if n else []
         if not lat:
             return {}
         pick = lambda q: round(1000 * lat[min(len(lat) - 1, int(q * len(lat)))], 2)  # noqa: E731
@@ -172,13 +199,15 @@ class MemoryLookupBatcher:
                 for w, r in zip(writes, rows):
                     if not w[4].done():
                         w[4].set_result(r)
+                self.stats["stores"] += len(writes)  # only writes the store accepted
             except Exception as e:  # noqa: BLE001
+                self.stats["store_failures"] += len(writes)
+                _log.error("memory write of %d item(s) failed: %r", len(writes), e)
                 for w in writes:
                     if not w[4].done():
                         w[4].set_exception(e)
                 if taken and pre is None:  # the shared embedding failed: the queries go again alone
                     self._pending = taken + self._pending
-            self.stats["stores"] += len(writes)
             self.stats["store_batches"] += 1
         if pre is None and self._pending and self.min_batch > 1 and self.max_wait_s > 0:
             while len(self._pending) < self.min_batch and not self._writes and \
@@ -208,10 +237,12 @@ class MemoryLookupBatcher:
                 now = time.perf_counter()
                 for b, h in zip(batch, hits):
                     self._lat.append(now - b[5])
+                    self.lat_count += 1
                     self.stats["queued_s"] += t0 - b[5]
                     if not b[4].done():
                         b[4].set_result(h[: b[3]])
             except Exception as e:  # noqa: BLE001
+                self.stats["lookup_failures"] += len(batch)
                 for b in batch:
                     if not b[4].done():
                         b[4].set_exception(e)

@@ -20,8 +20,9 @@ process per GPU that store must be node-wide, not one private copy per rank:
 
 Tags are exchanged as strings (each shard maps them to its own filter bits), expiry is
 wall-clock. With world == 1 the store degenerates to a local index (no collectives).
-Host metadata travels on a gloo group, the vectors and candidates on the device group
-(RCCL; gloo on CPU).
+Host metadata travels through the node's shared-memory all-gather (parallel/host_gather.py;
+gloo only when the ranks span hosts), the vectors and candidates on the device group (RCCL over
+xGMI; on CPU the shared-memory plane too).
 """
 from __future__ import annotations
 
@@ -69,6 +70,11 @@ class NodeSemanticStore:
         self.stats = {"rounds": 0, "idle_rounds": 0, "lookups": 0, "writes": 0, "round_s": 0.0,
                       "scan_s": 0.0, "max_queries_round": 0}
         self._dev_coll = self._pick_device()
+        # host payloads (counts, filters, tags, items; on CPU also vectors and candidates) go
+        # through a shared-memory all-gather between the node's ranks (parallel/host_gather.py)
+        from pilottai_amd.parallel.host_gather import HostGather
+
+        self._host = HostGather(self.cpu_group) if self.world > 1 else None
 
     # ------------------------------------------------------------------ setup
     def _pick_device(self) -> torch.device:
@@ -111,7 +117,7 @@ class NodeSemanticStore:
         if vecs is None:
             vecs = await loop.run_in_executor(None, self._embed, list(queries))
         else:
-            vecs = vecs.float().cpu().numpy() if isinstance(vecs, torch.Tensor) else np.asarray(vecs, np.float32)
+            vecs = _as_rows(vecs, Q, self.index.dim)
         futs = []
         with self._lock:
             self._check()
@@ -129,7 +135,9 @@ class NodeSemanticStore:
         return (await self.search_batch([query], [tags], [min_priority], limit))[0]
 
     async def store_semantic_batch(self, texts: Sequence[str], metadatas=None, tags=None, priorities=None,
-                                   ttl: Optional[float] = None) -> List[int]:
+                                   ttl: Optional[float] = None, vecs=None) -> List[int]:
+        """`vecs`: the texts' embeddings when the caller already has them (embed_queries), the
+        same contract as EnhancedMemory.store_semantic_batch (memory/store_protocol.py)."""
         if any(not t for t in texts):
             raise ValueError("Text cannot be empty")
         items = [MemoryItem(text=t, metadata=(metadatas[i] if metadatas else {}),
@@ -139,7 +147,10 @@ class NodeSemanticStore:
         if not items:
             return []
         loop = asyncio.get_running_loop()
-        vecs = await loop.run_in_executor(None, self._embed, [it.text for it in items])
+        if vecs is None:
+            vecs = await loop.run_in_executor(None, self._embed, [it.text for it in items])
+        else:
+            vecs = _as_rows(vecs, len(items), self.index.dim)
         futs = []
         with self._lock:
             self._check()
@@ -204,33 +215,63 @@ class NodeSemanticStore:
     def _gather_obj(self, obj) -> list:
         if self.world == 1:
             return [obj]
-        out = [None] * self.world
-        dist.all_gather_object(out, obj, group=self.cpu_group)
-        return out
+        return self._host.gather_obj(obj)
 
-    def _gather_tensor(self, t: torch.Tensor) -> torch.Tensor:
-        """[world, *t.shape] on the collective device."""
+    def _gather_host(self, t: torch.Tensor) -> torch.Tensor:
+        """[world, *t.shape] of a host tensor through the host plane."""
         if self.world == 1:
             return t.unsqueeze(0)
-        t = t.to(self._dev_coll).contiguous()
-        if self._dev_coll.type == "cpu":
+        return torch.from_numpy(self._host.gather_array(t.numpy()))
+
+    def _gather_tensor(self, t: torch.Tensor, device: Optional[torch.device] = None, group=None) -> torch.Tensor:
+        """[world, *t.shape] on `device` (default: the collective device of `self.group`)."""
+        if self.world == 1:
+            return t.unsqueeze(0)
+        dev = self._dev_coll if device is None else device
+        grp = self.group if group is None else group
+        t = t.to(dev).contiguous()
+        if dev.type == "cpu" and self._host is not None and self._host.transport == "shm":
+            return self._gather_host(t)
+        if dev.type == "cpu":
             parts = [torch.empty_like(t) for _ in range(self.world)]
-            dist.all_gather(parts, t, group=self.group)
+            dist.all_gather(parts, t, group=grp)
             return torch.stack(parts)
         out = torch.empty((self.world,) + tuple(t.shape), dtype=t.dtype, device=t.device)
-        dist.all_gather_into_tensor(out, t, group=self.group)
+        dist.all_gather_into_tensor(out, t, group=grp)
+        return out
+
+    def _exchange(self, t: torch.Tensor) -> torch.Tensor:
+        """All-to-all of [world, ...] (row q goes to rank q): RCCL on the device group, the
+        shared-memory plane on CPU."""
+        if self.world == 1:
+            return t.clone()
+        t = t.contiguous()
+        if t.device.type == "cpu" and self._host is not None and self._host.transport == "shm":
+            return torch.from_numpy(self._host.all_to_all_array(t.numpy()))
+        out = torch.empty_like(t)
+        dist.all_to_all_single(out, t, group=self.group)
         return out
 
     def _round(self) -> Tuple[bool, bool]:
-        """One lockstep round; returns (any work anywhere, every rank stopped and idle)."""
+        """One lockstep round; returns (any work anywhere, every rank stopped and idle).
+
+        Collectives per round: an idle round is ONE 4-int all-gather on the
+        host plane (no pickling); a busy round adds the query vectors (device group,
+        device-resident), a [QM, 3] int meta tensor, the candidates as (global row, score)
+        tensors packed on the device, and object gathers only for what has no fixed shape:
+        the written items (rounds with writes) and query tag strings (rounds with tags). The
+        host payloads travel through the node's shared-memory plane (HostGather), microseconds
+        per all-gather instead of a gloo loopback-TCP round trip."""
         with self._lock:
             qs, self._queries = self._queries[:self.max_queries], self._queries[self.max_queries:]
             ws, self._writes = self._writes, []
-        hdr = self._gather_obj((len(qs), len(ws), bool(self._stop)))
-        nq = [h[0] for h in hdr]
-        nw = [h[1] for h in hdr]
+        any_tags = any(q[2] for q in qs)
+        hdr = torch.tensor([len(qs), len(ws), int(bool(self._stop)), int(any_tags)], dtype=torch.int64)
+        hdr = self._gather_host(hdr)
+        nq = hdr[:, 0].tolist()
+        nw = hdr[:, 1].tolist()
         if sum(nq) == 0 and sum(nw) == 0:
-            return False, all(h[2] for h in hdr)
+            return False, bool(hdr[:, 2].all())
         t0 = time.perf_counter()
         self.stats["rounds"] += 1
         # ---- writes: the owner (the writer's rank) inserts the vectors into its shard; every
@@ -251,37 +292,67 @@ class NodeSemanticStore:
         if sum(nq) == 0:
             self.stats["round_s"] += time.perf_counter() - t0
             return True, False
-        # ---- queries: every rank's vectors, filters and k
+        # ---- queries: every rank's vectors (one host->device copy, then device-resident),
+        # filters and k
         QM = max(nq)
+        W = self.world
         dim = self.index.dim
         qv = torch.zeros(QM, dim, dtype=torch.float32)
-        for i, q in enumerate(qs):
-            qv[i] = torch.from_numpy(np.ascontiguousarray(q[0], dtype=np.float32))
-        allv = self._gather_tensor(qv)  # [W, QM, dim]
-        meta = self._gather_obj([(q[1], sorted(q[2]), q[3]) for q in qs])
-        kmax = max(m[2] for lst in meta for m in lst)
-        flat_v, flat_p, flat_t, owners = [], [], [], []
-        for r in range(self.world):
-            for i, (mp, tg, _k) in enumerate(meta[r]):
-                flat_v.append(allv[r, i])
-                flat_p.append(mp)
-                flat_t.append(tuple(tg))
-                owners.append((r, i))
+        if qs:
+            qv[:len(qs)] = torch.from_numpy(np.stack([q[0] for q in qs]).astype(np.float32, copy=False))
+        allv = self._gather_tensor(qv.to(self._dev_coll))  # [W, QM, dim]
+        meta = torch.zeros(QM, 2, dtype=torch.int64)
+        if qs:
+            meta[:len(qs)] = torch.from_numpy(np.array([(q[1], q[3]) for q in qs], dtype=np.int64))
+        allm = self._gather_host(meta)  # [W, QM, 2]
+        kmax = int(allm[:, :, 1].max())
+        alltags = self._gather_obj([sorted(q[2]) for q in qs]) if bool(hdr[:, 3].any()) else [[]] * W
+        valid = torch.arange(QM).unsqueeze(0) < torch.tensor(nq).unsqueeze(1)  # [W, QM]
+        vflat = valid.flatten()
+        flat_v = allv.reshape(W * QM, dim)[vflat.to(allv.device)]
+        flat_p = allm[:, :, 0].flatten()[vflat]
+        flat_t = [tuple(alltags[r][i]) if alltags[r] else () for r in range(W) for i in range(nq[r])]
         ts = time.perf_counter()
-        hits = self.index.search(torch.stack(flat_v).cpu().numpy(), kmax, flat_p, flat_t) if self.index.count else \
-            [[] for _ in flat_v]
+        n_flat = int(vflat.sum())
+        cand_s = torch.full((W * QM, kmax), float("-inf"), dtype=torch.float32, device=self._dev_coll)
+        cand_r = torch.full((W * QM, kmax), -1, dtype=torch.int64, device=self._dev_coll)
+        if self.index.count:
+            qmasks, exact = self.index.query_masks(flat_t)
+            pos = vflat.nonzero().flatten().to(self._dev_coll)
+            if all(exact):  # the common case: the kernel's tensors go straight into the gather
+                s_, r_ = self.index.search_tensors(flat_v, kmax, flat_p, qmasks)
+                if s_.is_cuda:  # the pass ran on the index's stream: order this round's stream behind it
+                    torch.cuda.current_stream(s_.device).wait_stream(self.index._stream)
+                s_, r_ = s_.to(self._dev_coll), r_.to(self._dev_coll).long()
+            else:  # overflow tags re-checked on the host (SemanticIndex.search)
+                hits = self.index.search(flat_v, kmax, flat_p.tolist(), flat_t)
+                s_ = torch.full((n_flat, kmax), float("-inf"), dtype=torch.float32)
+                r_ = torch.full((n_flat, kmax), -1, dtype=torch.int64)
+                for i, lst in enumerate(hits):
+                    if lst:
+                        a = np.asarray(lst, dtype=np.float64)
+                        r_[i, :len(lst)] = torch.from_numpy(a[:, 0].astype(np.int64))
+                        s_[i, :len(lst)] = torch.from_numpy(a[:, 1].astype(np.float32))
+                s_, r_ = s_.to(self._dev_coll), r_.to(self._dev_coll)
+            hit = r_ >= 0
+            cand_r[pos] = torch.where(hit, r_ * W + self.rank, r_)
+            cand_s[pos] = torch.where(hit, s_.float(), torch.full_like(s_, float("-inf"), dtype=torch.float32))
         self.stats["scan_s"] += time.perf_counter() - ts
-        cand = torch.full((self.world, QM, kmax, 2), -1.0, dtype=torch.float64)
-        for (r, i), lst in zip(owners, hits):
-            for j, (row, sc) in enumerate(lst[:kmax]):
-                cand[r, i, j, 0] = row * self.world + self.rank
-                cand[r, i, j, 1] = sc
-        allc = self._gather_tensor(cand).cpu()  # [W shards, W ranks, QM, kmax, 2]
+        # all-to-all: shard q's candidates for THIS rank's queries, [W shards, QM, kmax] -- each
+        # rank receives only its own queries' rows (an all-gather would move W times the bytes)
+        alls = self._exchange(cand_s.view(W, QM, kmax))
+        allr = self._exchange(cand_r.view(W, QM, kmax))
+        # merge this rank's queries: [QM, W * kmax] sorted by score on the collective device
+        ms = alls.permute(1, 0, 2).reshape(QM, W * kmax)
+        mr = allr.permute(1, 0, 2).reshape(QM, W * kmax)
+        top_s, order = torch.topk(ms[:len(qs)], min(kmax, W * kmax), dim=1, sorted=True)
+        # misses score -inf, so each row's hits lead it: one host copy, then plain slicing
+        ms = top_s.cpu().numpy()
+        mr = torch.gather(mr[:len(qs)], 1, order).cpu().numpy()
+        nhit = (mr >= 0).sum(axis=1)
         for i, q in enumerate(qs):
-            c = allc[:, self.rank, i].reshape(-1, 2)
-            c = c[c[:, 0] >= 0]
-            order = torch.argsort(c[:, 1], descending=True)[: q[3]]
-            rows = [(int(c[j, 0]), float(c[j, 1])) for j in order.tolist()]
+            m = min(int(nhit[i]), q[3])
+            rows = list(zip(mr[i, :m].tolist(), ms[i, :m].tolist()))
             _deliver(q[4], q[5], rows if q[6] else self._items_for(rows))
         self.stats["lookups"] += len(qs)
         self.stats["max_queries_round"] = max(self.stats["max_queries_round"], sum(nq))
@@ -328,6 +399,14 @@ class NodeSemanticStore:
             for v, it, f in zip(vecs, items, futs):
                 self._writes.append((np.asarray(v, np.float32), it, f, None))
         return [f.result(timeout) for f in futs]
+
+
+def _as_rows(vecs, n: int, dim: int) -> np.ndarray:
+    """Caller-provided embeddings (array or tensor, any device) as [n, dim] fp32 host rows."""
+    if isinstance(vecs, torch.Tensor):
+        vecs = vecs.detach().float().cpu().numpy()
+    v = np.asarray(vecs, dtype=np.float32).reshape(n, dim)
+    return v
 
 
 def _deliver(fut, loop, val, exc: bool = False):

@@ -109,6 +109,13 @@ class SemanticIndex:
         self.priority[:n] = old[1]
         self.tagbits[:n] = old[2]
         self.expiry[:n] = old[3]
+        if self.device.type == "cuda":
+            # the copies above may be queued on the index's side stream (add() runs _grow under
+            # _stream_ctx) while the old blocks were allocated on another stream: keep them out
+            # of the caching allocator until the copies reading them are done
+            cur = torch.cuda.current_stream(self.device)
+            for t in old[:4]:
+                t.record_stream(cur)
 
     @property
     def count(self) -> int:
@@ -227,38 +234,60 @@ class SemanticIndex:
             for r in rows:
                 self.row_tags_py.pop(r, None)
 
+    def query_masks(self, tags: Sequence[Iterable[str]]) -> Tuple[List[int], List[bool]]:
+        """Per query (tag bitmask, exact); an unknown tag gives the -1 sentinel (all bits set),
+        which no real row mask can contain."""
+        tags = list(tags)
+        if not any(tags):  # no tag filter anywhere (the common lookup): nothing to map
+            return [0] * len(tags), [True] * len(tags)
+        qmasks, exact = [], []
+        for ts in tags:
+            m, ex = self.tags.mask(frozenset(ts or ()), create=False)
+            qmasks.append(m)
+            exact.append(ex)
+        return qmasks, exact
+
+    def search_tensors(self, q: torch.Tensor, k: int, min_priority, qmasks,
+                       now: Optional[float] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+        """The raw kernel pass: `q` [Q, dim] (any device, any float dtype), `min_priority` and
+        `qmasks` lists or int tensors. Returns device tensors (scores [Q, k] fp32, rows [Q, k]
+        int32, -1 past the hits), best first, on the index's stream (which the caller must
+        order against: synchronize it or read the result inside `_stream_ctx`). Tag filters
+        on the shared overflow bit are NOT re-checked here (see `search`)."""
+        k = max(1, min(int(k), 64))
+        caller = torch.cuda.current_stream(self.device) if q.is_cuda and self.device.type == "cuda" else None
+        with self._lock, self._stream_ctx():
+            if caller is not None:  # `q` was produced on the caller's stream
+                torch.cuda.current_stream(self.device).wait_stream(caller)
+            qd = torch.nn.functional.normalize(q.to(self.device, torch.float32), dim=1).to(torch.bfloat16)
+            minp = torch.as_tensor(min_priority, dtype=torch.int32).to(self.device)
+            qt = torch.as_tensor(qmasks, dtype=torch.int64).to(self.device)
+            ev = None
+            if self.pass_events is not None and self.device.type == "cuda":
+                ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                ev[0].record()
+            s, r = ops.cosine_topk(qd, self.packed, self.count, k, self.priority, self.tagbits, self.expiry, minp, qt,
+                                   self.now() if now is None else now - self.epoch, workspace=self._ws)
+            if ev is not None:
+                ev[1].record()
+                self.pass_events.append(ev)
+        return s, r
+
     def search(self, queries, k: int, min_priority: Sequence[int], tags: Sequence[Iterable[str]],
                now: Optional[float] = None) -> List[List[Tuple[int, float]]]:
         """Batched filtered top-k: returns per query [(row, score), ...] best first."""
-        q = torch.as_tensor(np.asarray(queries, dtype=np.float32))
+        q = queries if isinstance(queries, torch.Tensor) else torch.as_tensor(np.asarray(queries, dtype=np.float32))
         Q = q.shape[0]
         if Q == 0:
             return []
         k = max(1, min(int(k), 64))
         tag_sets = [frozenset(t or ()) for t in tags]
-        qmasks, exact = [], []
-        for ts in tag_sets:
-            m, ex = self.tags.mask(ts, create=False)
-            qmasks.append(m)
-            exact.append(ex)
-        # unknown tag (-1 sentinel == all bits) can never match a real row mask
-        n = self.count
-        if n == 0:
+        qmasks, exact = self.query_masks(tag_sets)
+        if self.count == 0:
             return [[] for _ in range(Q)]
         kk = k if all(exact) else min(64, 4 * k)
-        with self._lock, self._stream_ctx():
-            qd = torch.nn.functional.normalize(q, dim=1).to(self.device, torch.bfloat16)
-            minp = torch.tensor(list(min_priority), dtype=torch.int32, device=self.device)
-            qt = torch.tensor(qmasks, dtype=torch.int64, device=self.device)
-            ev = None
-            if self.pass_events is not None and self.device.type == "cuda":
-                ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-                ev[0].record()
-            s, r = ops.cosine_topk(qd, self.packed, n, kk, self.priority, self.tagbits, self.expiry, minp, qt,
-                                   self.now() if now is None else now - self.epoch, workspace=self._ws)
-            if ev is not None:
-                ev[1].record()
-                self.pass_events.append(ev)
+        s, r = self.search_tensors(q, kk, list(min_priority), qmasks, now)
+        with self._stream_ctx():
             s, r = s.cpu().numpy(), r.cpu().numpy()
         out = []
         for i in range(Q):

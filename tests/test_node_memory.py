@@ -142,3 +142,120 @@ def test_node_store_single_rank_without_collectives():
         assert g == N and store.search_rows_blocking(queries[:1], 1, [0], [("m",)])[0][0][0] == N
     finally:
         store.stop()
+
+
+def test_both_stores_implement_the_store_protocol():
+    """The batcher's keyword contract (vecs=, ...) is the same on both stores (round 5 shipped a
+    node store without `vecs=`, and every node-mode write failed)."""
+    from pilottai_amd.memory.enhanced_memory import EnhancedMemory
+    from pilottai_amd.memory.node_store import NodeSemanticStore
+    from pilottai_amd.memory.store_protocol import signature_mismatches
+
+    assert signature_mismatches(EnhancedMemory) == []
+    assert signature_mismatches(NodeSemanticStore) == []
+
+
+class _FakeEngine:
+    """add/remove_step_listener plus a thread that announces a heavy (2,048-token) step every
+    5 ms, like LLMEngine's step listeners (the batcher's engine gate)."""
+
+    def __init__(self):
+        import threading
+
+        self.listeners = []
+        self._stop = threading.Event()
+        self._t = threading.Thread(target=self._run, daemon=True)
+        self._t.start()
+
+    def add_step_listener(self, fn):
+        self.listeners = self.listeners + [fn]
+
+    def remove_step_listener(self, fn):
+        self.listeners = [f for f in self.listeners if f is not fn]
+
+    def _run(self):
+        while not self._stop.wait(0.005):
+            for fn in self.listeners:
+                fn(2048)
+
+    def close(self):
+        self._stop.set()
+        self._t.join(5)
+
+
+def _batcher_entry(rank, world, port, q):
+    import torch.distributed as dist
+
+    from pilottai_amd.core.agent import BaseAgent
+    from pilottai_amd.core.task import Task
+    from pilottai_amd.memory.batcher import MemoryLookupBatcher
+    from pilottai_amd.memory.embedding import HashingEmbedder
+    from pilottai_amd.memory.node_store import NodeSemanticStore
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    eng = _FakeEngine()
+    try:
+        emb = HashingEmbedder(DIM)
+        local = SemanticIndex(dim=DIM, capacity=64, device="cpu")
+        grp = dist.new_group(backend="gloo")
+        store = NodeSemanticStore(local, embedder=emb, group=grp)
+        store.start()
+        out = {}
+
+        async def run():
+            batcher = MemoryLookupBatcher(store)
+            batcher.attach_engine(eng, gate_tokens=1024, max_wait_s=0.05)
+            agent = BaseAgent(role=f"worker{rank}", goal="extract findings", memory_lookup=batcher)
+            task = Task(description=f"audit ledger {rank} for the quarterly revenue of unit {rank * 7 + 3}")
+            # every rank's agent writes its finding through the production path (BaseAgent._remember
+            # -> MemoryLookupBatcher.store -> store_semantic_batch(vecs=...) with the gate's shared
+            # embedding) while lookups are pending beside it
+            pend = [asyncio.ensure_future(batcher.search(f"warm up query {rank} {i}", limit=2)) for i in range(3)]
+            await agent._remember(task, True, {"reasoning": f"unit {rank * 7 + 3} grew"})
+            await asyncio.gather(*pend)
+            await asyncio.get_running_loop().run_in_executor(None, dist.barrier)
+            # now each rank looks up the NEXT rank's finding
+            peer = (rank + 1) % world
+            hits = await batcher.search(f"audit ledger {peer} for the quarterly revenue of unit {peer * 7 + 3}",
+                                        limit=3)
+            out["hits"] = [(h.text, h.metadata) for h in hits]
+            out["stats"] = dict(batcher.stats)
+            out["agent_errors"] = dict(agent.memory_errors)
+            batcher.detach_engine()
+            out["listeners_after_detach"] = len(eng.listeners)
+
+        asyncio.run(run())
+        dist.barrier()
+        store.stop()
+        q.put((rank, out))
+    finally:
+        eng.close()
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_agent_writes_through_batcher_reach_other_ranks(world):
+    """an agent's `_remember` on rank A, through MemoryLookupBatcher (engine
+    gate attached) into NodeSemanticStore, is returned by a lookup on rank B; failed writes are
+    counted apart from stores."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_batcher_entry, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=300) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(world):
+        peer = (r + 1) % world
+        st = got[r]["stats"]
+        assert st["stores"] == 1 and st["store_failures"] == 0 and st["lookup_failures"] == 0, st
+        assert got[r]["agent_errors"] == {"store": 0, "search": 0}
+        assert got[r]["listeners_after_detach"] == 0
+        texts = [t for t, _ in got[r]["hits"]]
+        assert any(t.startswith(f"audit ledger {peer} ") for t in texts), (r, texts)
+        md = [m for t, m in got[r]["hits"] if t.startswith(f"audit ledger {peer} ")][0]
+        assert md["success"] is True and md["agent"] != ""

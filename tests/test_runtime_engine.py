@@ -169,6 +169,31 @@ def test_scheduler_admits_embedding_requests_first(embed_first):
     assert int(c[7]) == (20 if embed_first else 0)  # tokens pooled for embedding requests this step
 
 
+@pytest.mark.parametrize("max_wait", [3, 1000])
+def test_scheduler_embed_first_cannot_starve_prompts(max_wait):
+    """A steady stream of embedding requests that fills every step's token budget: with
+    embed_first a waiting generation prompt is passed over, but only for
+    embed_first_max_wait steps (embed-first admission had no bound)."""
+    s = _runtime.Scheduler({"num_blocks": 256, "block_size": 16, "max_num_seqs": 8, "max_num_batched_tokens": 128,
+                            "max_model_len": 512, "prefix_caching": False, "embed_first": True,
+                            "embed_first_max_wait": max_wait})
+    L = s.layout()
+    buf = np.zeros(L["total"], dtype=np.int32)
+    s.add_request(1, list(range(100, 300)), 0.0, 4, 1, True, [], None)  # 200-token prompt
+    first_gen = None
+    for step in range(12):
+        s.add_request(100 + step, list(range(600 + step, 728 + step)), 0.0, 1, 3, True, [], None, embed=True)
+        T = s.schedule(buf.ctypes.data)
+        c = buf[L["counts"]:L["counts"] + 8]
+        if T - int(c[7]) > 0 and first_gen is None:
+            first_gen = step
+        s.commit(np.full(8, 3, np.int32).ctypes.data, int(c[2]))
+    if max_wait == 1000:
+        assert first_gen is None  # unbounded: the prompt never got a token
+    else:
+        assert first_gen is not None and first_gen <= max_wait
+
+
 def test_engine_cpu_tiny_end_to_end(tok):
     from pilottai_amd.engine.engine import EngineConfig, LLMEngine
 
