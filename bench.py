@@ -376,6 +376,7 @@ async def run_rank(a, rank: int, world: int, device):
                                                      "host_commit_s", "host_deliver_s")},
         "bucket_tokens": st1["bucket_tokens"] - st0["bucket_tokens"],
         "prompt_total": em["prompt_tokens"], "hbm_used_gb": em.get("hbm_used_gb", 0.0),
+        "weights_gb": em.get("weights_gb", 0.0), "kv_cache_gb": em.get("kv_cache_gb", 0.0),
         "req_lat": eng.latency_summary(n_timed0), "memory": mem, "node_load": node_load,
         "buckets": {b: [v[0] - bh0.get(b, [0, 0.0])[0], v[1] - bh0.get(b, [0, 0.0])[1]]
                     for b, v in eng.bucket_hist.items()},
@@ -422,7 +423,8 @@ async def run_cpu_rank(a, rank: int, world: int, n_local: int):
     for ag in agents:
         await ag.stop()
     zero = {k: 0 for k in ("tokens", "steps", "sampled", "busy_s", "prefix_hit", "prefix_defers", "spec_rows",
-                           "spec_voided", "bucket_tokens", "prompt_total", "hbm_used_gb", "graph_captures")}
+                           "spec_voided", "bucket_tokens", "prompt_total", "hbm_used_gb", "graph_captures",
+                           "weights_gb", "kv_cache_gb")}
     return dict(zero, dt=dt, tasks=0, lat=[], init_s=init_s, requeued=0, loop_lag=[], executions_by_rank=None,
                 device=_device_identity(None),
                 managers=0, dp_mode="node", calls=len(llm.calls) if hasattr(llm, "calls") else 0, prompt_tokens=0,
@@ -608,6 +610,10 @@ def main():
             "tpot_p50_ms": round(lat0.get("tpot_p50_ms") or 0.0, 2),
             "init_s": round(max(g["init_s"] for g in gathered), 1),
             "hbm_used_gb_per_gpu": round(max(g["hbm_used_gb"] for g in gathered), 1),
+            # the weights are ONE packed copy (models/llama.py keep_dense); the KV pool takes a
+            # share of what is left, so the total above does not show the freed copy
+            "weights_gb_per_gpu": round(max(g.get("weights_gb", 0.0) for g in gathered), 1),
+            "kv_cache_gb_per_gpu": round(max(g.get("kv_cache_gb", 0.0) for g in gathered), 1),
             # rank 0's engine steps per graph bucket: [steps, ms per step]
             "step_buckets": {str(b): [v[0], round(1000 * v[1] / max(1, v[0]), 2)]
                              for b, v in sorted(gathered[0]["buckets"].items()) if v[0] > 0},

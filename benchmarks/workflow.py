@@ -42,6 +42,7 @@ def parse():
     ap.add_argument("--cpu", action="store_true")
     ap.add_argument("--max-batched-tokens", type=int, default=2048)
     ap.add_argument("--no-graphs", action="store_true", help="eager steps")
+    ap.add_argument("--library", action="store_true", help="row-major weights on library GEMMs (no packing)")
     ap.add_argument("--share-gpu", action="store_true",
                     help="1-GPU rehearsal of TP=N: every rank on GPU 0, gloo control plane "
                          "(PILOTTAI_DIST_BACKEND=gloo), TP all-reduces through the custom P2P kernel")
@@ -162,8 +163,10 @@ def main():
     eng = LLMEngine(EngineConfig(model=model, max_num_seqs=max(64, 4 * a.clients), max_num_batched_tokens=mbt,
                                  kv_cache_gb=None if a.cpu else a.kv_gb, num_kv_blocks=4096 if a.cpu else None,
                                  token_buckets=buckets, use_graphs=not a.no_graphs,
-                                 # 8 ranks x 2 copies of 17.6 GB do not fit one card: no packed copy
-                                 decode_fused=False if a.share_gpu else None),
+                                 # one packed copy per rank (the row-major one is freed): 8 ranks x
+                                 # 17.6 GB fit one card on the hand kernels; --library keeps the
+                                 # row-major weights on hipBLASLt instead
+                                 decode_fused=False if a.library else None),
                     device=device, tp=tp)
     init_s = time.time() - t0
     if tp.rank != 0:

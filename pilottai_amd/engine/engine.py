@@ -106,6 +106,9 @@ class EngineConfig:
     # largest step on the fused packed-weight path with the 256 x 256 prefill kernels (above
     # mid_max_t); 0 = such steps take the library (hipBLASLt) path; None = model default
     prefill_max_t: Optional[int] = None
+    # keep the row-major projection weights beside the packed ones (None: only when some step can
+    # leave the packed-weight path, i.e. prefill_max_t / mid_max_t below max_num_batched_tokens)
+    keep_dense: Optional[bool] = None
     # projections ("qkv", "o", "gate_up", "down") whose PF_CFG prefill-kernel rows also apply to
     # <= 256-token steps (None: model default)
     pf_midrange: Optional[List[str]] = None
@@ -217,8 +220,13 @@ class LLMEngine:
 
             self.tuned_gemms = load_tuned_gemms(mc.name, self.tp.size)
         t0 = time.time()
+        keep_dense = cfg.keep_dense
+        if keep_dense is None and (cfg.prefill_max_t is not None or cfg.mid_max_t is not None):
+            lim = max(LlamaModel.MID_MAX_T if cfg.mid_max_t is None else int(cfg.mid_max_t),
+                      LlamaModel.PREFILL_MAX_T if cfg.prefill_max_t is None else int(cfg.prefill_max_t))
+            keep_dense = True if lim < cfg.max_num_batched_tokens else None
         self.model = LlamaModel(mc, self.device, tp=self.tp, seed=cfg.seed, weights_path=cfg.weights_path,
-                                decode_pack=cfg.decode_fused)
+                                decode_pack=cfg.decode_fused, keep_dense=keep_dense)
         if cfg.decode_fused_max_t is not None:
             self.model.DECODE_FUSED_MAX_T = int(cfg.decode_fused_max_t)
         if cfg.mid_max_t is not None:

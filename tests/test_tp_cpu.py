@@ -179,3 +179,25 @@ def test_tp_topkp_threshold_matches_full_vocab(tmp_path, world):
                        start_method="spawn")
     r = torch.load(out, weights_only=True)
     assert torch.equal(r["tau"], r["want"]), (r["tau"], r["want"])
+
+
+def test_packed_weights_are_the_only_copy_and_unpack_exactly():
+    """after packing, the row-major projections are freed (keep_dense=False,
+    the GPU default); the dense reference paths unpack them on demand, bit-exact for the
+    random-init (unit RMSNorm weight) model."""
+    import torch
+
+    from pilottai_amd.models.llama import DENSE_KINDS, LlamaModel, get_config
+
+    cfg = get_config("tiny")
+    kept = LlamaModel(cfg, "cpu", dtype=torch.float32, keep_dense=True)
+    only = LlamaModel(cfg, "cpu", dtype=torch.float32, keep_dense=False)
+    assert kept.decode_packed and only.decode_packed
+    assert all(k not in L for L in only.layers for k in DENSE_KINDS)
+    assert only.weight_bytes() < kept.weight_bytes()
+    for Lk, Lo in zip(kept.layers, only.layers):
+        for k in DENSE_KINDS:
+            assert torch.equal(only.dense(Lo, k), Lk[k]), k
+    assert torch.equal(only.dense_lm_head(), kept.dense_lm_head())
+    ids = [3, 17, 5, 99, 42, 7]
+    assert torch.equal(only.reference_logits(ids), kept.reference_logits(ids))

@@ -1,9 +1,18 @@
-"""Tensor-parallel engine on the GPU with the custom P2P all-reduce (TP=2, both ranks
+"""Tensor-parallel engine on the GPU with the custom P2P all-reduce (TP=2, 4 and 8, every rank
 on GPU 0 over real IPC handles; gloo carries the host-side step headers).
 
-Mirrors tests/test_tp_cpu.py: the TP=2 engine must reproduce the TP=1 engine's
-greedy tokens (canonical sharded init -> identical weights) and keep structured
-output valid, with every row-parallel all-reduce going through csrc/ops/custom_ar.hip.
+Mirrors tests/test_tp_cpu.py: the TP=N engine (canonical sharded init -> exactly the TP=1
+weights) must choose, at every generated position, a token the TP=1 model's fp32 reference
+forward ranks as the argmax (greedy) or inside its top 20 (top-k 20 sampling), teacher-forced
+on the TP run's own tokens, and keep structured output valid, with every row-parallel
+all-reduce going through csrc/ops/custom_ar.hip.
+
+The bound: TP=N rounds each rank's row-parallel partial output to bf16 before the rank-order
+fp32 sum, TP=1 rounds the full sum once, so activations differ by up to N bf16 roundings
+(N x 2^-9 relative) per projection; through the tiny model's 2 layers that moves a logit by well
+under 1 % of the row's logit range, the tolerance used (TOL_FRAC). An exact token-for-token
+match is therefore not guaranteed at near-ties; a wrong kernel or collective (a dropped shard,
+a stale buffer) misses the reference's argmax by far more.
 The graph-on variant is the production TP mode: every bucket captured
 up front with the collectives inside, all of them on the custom P2P buffers -- the
 activations' all-reduces, the sampling winners' all-gather and the top-k / top-p
@@ -29,10 +38,14 @@ def _free_port() -> int:
     return p
 
 
+MODEL = "tiny-kv8"  # 8 KV heads: TP = 1, 2, 4 and 8 hold exact slices of the same weights
+TOL_FRAC = 0.01
+
+
 def _cfg(graphs=False):
     from pilottai_amd.engine.engine import EngineConfig
 
-    return EngineConfig(model="tiny-gqa4", max_num_seqs=8, max_num_batched_tokens=128, max_model_len=512,
+    return EngineConfig(model=MODEL, max_num_seqs=8, max_num_batched_tokens=128, max_model_len=512,
                         num_kv_blocks=96, use_graphs=graphs, token_buckets=[8, 16, 32, 64, 128])
 
 
@@ -86,18 +99,29 @@ def _worker(rank, world, port, out_path, graphs=False):
     with open(out_path, "w") as f:
         json.dump({"greedy": [o.token_ids for o in greedy], "json": js.text, "calls": tp.custom.calls,
                    "healthy": tp.custom.healthy(), "graphs": len(e._graphs), "in_graph": in_graph,
-                   "topk_lens": [len(o.token_ids) for o in tk]}, f)
+                   "topk": [o.token_ids for o in tk]}, f)
     torch.distributed.destroy_process_group()
 
 
-@pytest.mark.parametrize("graphs", [False, True])
-def test_tp2_engine_custom_allreduce_matches_tp1(tmp_path, graphs):
+def _near_rank(model, prompt, toks, k):
+    """Per generated position: (logit of the chosen token, k-th largest logit, logit range) of
+    the TP=1 fp32 reference forward, teacher-forced on prompt + toks."""
+    logits = model.reference_logits(prompt + toks[:-1]).float()
+    out = []
+    for i, t in enumerate(toks):
+        row = logits[len(prompt) - 1 + i]
+        out.append((float(row[t]), float(torch.topk(row, k).values[-1]), float(row.max() - row.min())))
+    return out
+
+
+@pytest.mark.parametrize("world,graphs", [(2, False), (2, True), (4, True), (8, True)])
+def test_tp_engine_custom_allreduce_matches_tp1(tmp_path, world, graphs):
     out = str(tmp_path / "tp.json")
     port = _free_port()
-    mp.start_processes(_worker, args=(2, port, out, graphs), nprocs=2, join=True, start_method="spawn")
+    mp.start_processes(_worker, args=(world, port, out, graphs), nprocs=world, join=True, start_method="spawn")
     res = json.load(open(out))
     assert res["calls"] > 0 and res["healthy"], res
-    assert res["topk_lens"] == [12, 12]
+    assert [len(t) for t in res["topk"]] == [12, 12]
     if graphs:
         assert res["graphs"] >= 5  # every bucket captured up front (+ first-use variants)
         assert res["in_graph"] == [], res["in_graph"]  # no RCCL / gloo call inside a graph
@@ -107,13 +131,13 @@ def test_tp2_engine_custom_allreduce_matches_tp1(tmp_path, graphs):
     from pilottai_amd.engine.engine import LLMEngine
 
     e1 = LLMEngine(_cfg(), device=torch.device("cuda", 0))
-    ref = e1.generate(_prompts(e1.tok), temperature=0.0, max_tokens=6, ignore_eos=True)
-    agree = tot = 0
-    for a, b in zip(res["greedy"], [o.token_ids for o in ref]):
-        assert a[0] == b[0]
-        for x, y in zip(a, b):
-            if x != y:
-                break
-            agree += 1
-        tot += len(b)
-    assert agree >= tot // 2
+    ps = _prompts(e1.tok)
+    ref = e1.generate(ps, temperature=0.0, max_tokens=6, ignore_eos=True)
+    exact = sum(a == o.token_ids for a, o in zip(res["greedy"], ref))
+    for p, toks in zip(ps, res["greedy"]):
+        for i, (lt, top, rng) in enumerate(_near_rank(e1.model, p, toks, 1)):
+            assert lt >= top - TOL_FRAC * rng, (world, i, lt, top, rng)
+    for p, toks in zip(ps, res["topk"]):
+        for i, (lt, kth, rng) in enumerate(_near_rank(e1.model, p, toks, 20)):
+            assert lt >= kth - TOL_FRAC * rng, (world, i, lt, kth, rng)
+    print(f"TP={world} graphs={graphs}: {exact}/{len(ps)} greedy sequences identical to TP=1")
