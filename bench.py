@@ -107,6 +107,10 @@ def parse():
                          "requests in the engine's continuous batch, SURVEY N11)")
     ap.add_argument("--share-gpu", action="store_true",
                     help="rehearsal: every rank on GPU 0 (use with PILOTTAI_DIST_BACKEND=gloo)")
+    ap.add_argument("--tp", type=int, default=1,
+                    help="tensor-parallel degree of each agent-DP replica: --gpus N runs N/T replicas, each "
+                         "one TP=T engine over T GPUs (custom P2P all-reduce); the node plane sees one rank "
+                         "per replica (its TP rank 0). Default 1 = pure agent-DP (BENCHMARKS.md cost model)")
     ap.add_argument("--hybrid-latency", type=float, default=0.0,
                     help="hybrid node rehearsal on ONE GPU (VERDICT r3 item 5): rank 0 runs the real engine, "
                          "the manager Serve, the control plane and all clients; ranks > 0 are CPU processes whose "
@@ -115,7 +119,10 @@ def parse():
     return ap.parse_args()
 
 
-async def run_rank(a, rank: int, world: int, device):
+async def run_rank(a, rank: int, world: int, device, tp=None, dp_group=None):
+    """rank / world: global. With --tp T the agent-DP replicas are the TP groups: drank / dworld
+    index the replicas, only each group's TP rank 0 runs agents and the control plane, the other
+    TP ranks follow their driver's engine steps (LLMEngine.follow)."""
     import torch
 
     from pilottai_amd.core.agent import BaseAgent
@@ -132,8 +139,15 @@ async def run_rank(a, rank: int, world: int, device):
     # workers of this rank (agent-DP sharding)
     from pilottai_amd.parallel.agent_dp import shard_workers
 
-    n_local = len(shard_workers(a.workers, world, rank))
+    from pilottai_amd.parallel.comm import TPGroup
+
+    tp = tp or TPGroup.single()
+    T = tp.size
+    dworld, drank = world // T, rank // T
+    n_local = len(shard_workers(a.workers, dworld, drank))
     t_init = time.time()
+    if T > 1 and (a.memory_rows > 0 or a.hybrid_latency > 0 or a.dp_mode != "node"):
+        raise SystemExit("--tp > 1 runs the node mode without --memory-rows / --hybrid-latency")
     if a.hybrid_latency > 0 and a.memory_rows > 0 and world > 1:
         raise SystemExit("--memory-rows needs an engine on every rank: not with --hybrid-latency")
     if a.hybrid_latency > 0 and rank > 0:
@@ -142,13 +156,14 @@ async def run_rank(a, rank: int, world: int, device):
     if a.memory_rows > 0:
         # before the engine sizes its KV pool: the index is resident beside the model
         memory, lookup = build_memory(a, device, rank, world, node=a.dp_mode == "node" and world > 1)
-    eng = LLMEngine(EngineConfig(model=a.model if not a.cpu else "tiny", max_num_seqs=max(64, 2 * n_local),
+    eng = LLMEngine(EngineConfig(model=a.model if not a.cpu else ("tiny" if T == 1 else "tiny-gqa4"),
+                                 max_num_seqs=max(64, 2 * n_local),
                                  max_num_batched_tokens=a.max_batched_tokens,
                                  max_prefill_tokens=a.max_batched_tokens,
                                  kv_cache_gb=None if a.cpu else (a.kv_gb if a.kv_gb is not None else
                                                                  (48.0 / max(1, world) if a.share_gpu else None)),
                                  kv_cache_fraction=0.85,
-                                 num_kv_blocks=4096 if a.cpu else None, seed=1234 + rank,
+                                 num_kv_blocks=4096 if a.cpu else None, seed=1234 + drank,
                                  token_align=a.token_align, align_slack=a.align_slack,
                                  decode_fused_max_t=a.fused_max_t,
                                  mid_max_t=a.mid_max_t, prefill_max_t=a.prefill_max_t,
@@ -159,7 +174,10 @@ async def run_rank(a, rank: int, world: int, device):
                                  **({"pf_midrange": [k for k in a.pf_midrange.split(",") if k and k != "none"]}
                                     if a.pf_midrange is not None else {}),
                                  **({"att_wide_min_tokens": a.att_wide_min_tokens}
-                                    if a.att_wide_min_tokens is not None else {})), device=device)
+                                    if a.att_wide_min_tokens is not None else {})), device=device, tp=tp)
+    if tp.rank != 0:  # a TP follower: replay the driver's steps until it stops the engine
+        await asyncio.to_thread(eng.follow)
+        return {"follower": True, "device": _device_identity(device)}
     register_engine(eng.model_cfg.name, eng)
     if memory is not None and a.embedder == "engine":
         # queries and write-backs are encoded by the serving model: final hidden states (last
@@ -184,7 +202,7 @@ async def run_rank(a, rank: int, world: int, device):
         agents.append(BaseAgent(cfg, llm=llm, tools=[Tool(name="echo", description="identity tool",
                                                           function=echo_tool, max_retries=1)], policy=policy,
                                 memory_lookup=lookup, memory_top_k=a.memory_top_k))
-    node = a.dp_mode == "node" and world > 1
+    node = a.dp_mode == "node" and dworld > 1
     serve_cfg = {"name": f"bench-r{rank}", "policy": "fixed", "steps_per_task": a.steps_per_task,
                  "max_queue_size": 100000, "task_timeout": 900, "agent_wait_timeout": 900}
     async def coll(fn, *args):
@@ -193,6 +211,8 @@ async def run_rank(a, rank: int, world: int, device):
         def run():
             if device.type == "cuda":
                 torch.cuda.set_device(device)
+            if fn is comm.broadcast_object or fn is comm.barrier:  # over the replicas (TP drivers)
+                return fn(*args, group=dp_group)
             return fn(*args)
         return await asyncio.to_thread(run)
 
@@ -200,7 +220,7 @@ async def run_rank(a, rank: int, world: int, device):
     if node:  # the control plane's shared secret: drawn on rank 0, broadcast to the job's ranks
         os.environ["PILOTTAI_PLANE_SECRET"] = await coll(
             comm.broadcast_object, secrets.token_hex(16) if rank == 0 else None)
-    if node and rank > 0:
+    if node and drank > 0:
         # worker rank: host this shard's agents (and this GPU's engine) for the manager
         from pilottai_amd.parallel.node_plane import PlaneWorker
 
@@ -210,13 +230,13 @@ async def run_rank(a, rank: int, world: int, device):
         def kv_load():
             m = eng.metrics()
             return {"kv_cache_utilization": 1.0 - m.get("free_kv_blocks", 1) / max(1, m.get("total_kv_blocks", 1))}
-        worker = PlaneWorker(rank, agents, llm=llm, load_fn=kv_load)
+        worker = PlaneWorker(drank, agents, llm=llm, load_fn=kv_load)
         await worker.connect()
         serving = asyncio.ensure_future(worker.serve_forever())
     elif node:
         from pilottai_amd.parallel.node_plane import DistributedLLM, NodeManager, PlaneServer
 
-        plane = PlaneServer(world)
+        plane = PlaneServer(dworld)
         await plane.start()
         serve = Serve(agents=agents, config={**serve_cfg, "max_concurrent_tasks": a.workers})
         mgr = NodeManager(plane, serve)
@@ -247,7 +267,7 @@ async def run_rank(a, rank: int, world: int, device):
                 latencies.append(dt)
 
     async def round_(n, rec):
-        if serve is not None and not (node and rank > 0):
+        if serve is not None and not (node and drank > 0):
             await asyncio.gather(*(client(i, n, rec) for i in range(n_clients)))
 
     lags = []
@@ -319,6 +339,12 @@ async def run_rank(a, rank: int, world: int, device):
                                           max(1, lookup.stats["passes"] - mem0["passes"]), 3),
                **lookup.latency_summary(mem0["nlat"]),
                "stores": lookup.stats["stores"] - mem0["stores"],
+               "store_failures": lookup.stats["store_failures"] - mem0["store_failures"],
+               "lookup_failures": lookup.stats["lookup_failures"] - mem0["lookup_failures"],
+               # node store: hits returned to this rank's agents that another rank's shard holds
+               "node_hits": memory.stats.get("hits") if hasattr(memory, "search_rows_blocking") else None,
+               "node_remote_hits": memory.stats.get("remote_hits") if hasattr(memory, "search_rows_blocking")
+               else None,
                # flushes whose writes and queries went through the engine in one embedding call
                "shared_embeds": lookup.stats.get("shared_embeds", 0) - mem0.get("shared_embeds", 0),
                # where a lookup's latency goes, ms per pass (embedding through the engine, the
@@ -361,7 +387,7 @@ async def run_rank(a, rank: int, world: int, device):
         "device": _device_identity(device),
         "mem_rows": memory.index.count if memory is not None else 0,
         "loop_lag": sorted(lags), "executions_by_rank": by_rank,
-        "managers": 1 if serve is not None else 0, "dp_mode": a.dp_mode if world > 1 else "single",
+        "managers": 1 if serve is not None else 0, "dp_mode": a.dp_mode if dworld > 1 else "single",
         "tokens": st1["tokens"] - st0["tokens"], "steps": st1["steps"] - st0["steps"],
         "sampled": st1["sampled"] - st0["sampled"], "calls": u1["calls"] - u0["calls"],
         "prompt_tokens": u1["prompt_tokens"] - u0["prompt_tokens"],
@@ -532,13 +558,22 @@ def main():
         dev_idx = 0 if a.share_gpu else local_rank
         torch.cuda.set_device(dev_idx)
         device = torch.device("cuda", dev_idx)
-    res = asyncio.run(run_rank(a, rank, world, device))
-    gathered = [res]
+    tp = dp_group = None
+    if a.tp > 1:
+        if world % a.tp:
+            raise SystemExit(f"--tp {a.tp} must divide --gpus {world}")
+        # contiguous TP groups (GPUs 0..T-1, T..2T-1, ...: xGMI is all-to-all, any T GPUs are one
+        # hop apart); the custom P2P all-reduce also in the share-GPU rehearsal (gloo groups)
+        tp = comm.new_tp_groups(a.tp, custom_ar=True if a.share_gpu else None)
+        dp_group = comm.new_dp_group(a.tp)
+    res = asyncio.run(run_rank(a, rank, world, device, tp=tp, dp_group=dp_group))
+    everyone = [res]
     if world > 1:
         import torch.distributed as dist
 
-        gathered = [None] * world
-        dist.all_gather_object(gathered, res)
+        everyone = [None] * world
+        dist.all_gather_object(everyone, res)
+    gathered = [g for g in everyone if not g.get("follower")]  # one per agent-DP replica
     if rank == 0:
         dt = max(g["dt"] for g in gathered)
         tasks = sum(g["tasks"] for g in gathered)
@@ -551,7 +586,7 @@ def main():
         value = tasks / dt if dt > 0 else 0.0
         # scale-run evidence: physical GPUs the ranks actually used (a --share-gpu or hybrid
         # rehearsal of N ranks on one card reports n_gpus 1), the process group RCCL / gloo saw
-        phys = sorted({g["device"]["physical"] for g in gathered if g["device"]["physical"]})
+        phys = sorted({g["device"]["physical"] for g in everyone if g["device"]["physical"]})
         rehearsal = "hybrid" if a.hybrid_latency > 0 else ("share-gpu" if a.share_gpu and world > 1 else None)
         import torch.distributed as dist
 
@@ -574,7 +609,7 @@ def main():
                 "model": "llama-3-8b" if not a.cpu else "tiny(cpu-smoke)",
                 "global_batch": a.workers,
                 "seq_len": round(tot("prompt_tokens") / calls, 1),
-                "parallelism": f"agent-dp{world}",
+                "parallelism": f"agent-dp{len(gathered)}" + (f"-tp{a.tp}" if a.tp > 1 else ""),
                 "managers": tot("managers"),
                 "workers": a.workers,
                 "llm_calls_per_task": round(calls / max(1, tasks), 2),
@@ -628,7 +663,7 @@ def main():
             "rehearsal": rehearsal,
             "dist_backend": dist_backend,
             "world_size": dist_world,
-            "devices": [g["device"]["device"] for g in gathered],
+            "devices": [g["device"]["device"] for g in everyone],
             "physical_devices": phys,
             "memory": (dict(gathered[0]["memory"], rows_per_rank=[g.get("mem_rows", 0) for g in gathered],
                             rows_total=sum(g.get("mem_rows", 0) for g in gathered))

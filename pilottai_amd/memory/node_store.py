@@ -67,8 +67,9 @@ class NodeSemanticStore:
         self._stop = False
         self._thread: Optional[threading.Thread] = None
         self._err: Optional[BaseException] = None
+        # hits / remote_hits: returned rows, and those held by another rank's shard
         self.stats = {"rounds": 0, "idle_rounds": 0, "lookups": 0, "writes": 0, "round_s": 0.0,
-                      "scan_s": 0.0, "max_queries_round": 0}
+                      "scan_s": 0.0, "max_queries_round": 0, "hits": 0, "remote_hits": 0}
         self._dev_coll = self._pick_device()
         # host payloads (counts, filters, tags, items; on CPU also vectors and candidates) go
         # through a shared-memory all-gather between the node's ranks (parallel/host_gather.py)
@@ -350,6 +351,10 @@ class NodeSemanticStore:
         ms = top_s.cpu().numpy()
         mr = torch.gather(mr[:len(qs)], 1, order).cpu().numpy()
         nhit = (mr >= 0).sum(axis=1)
+        for i, q in enumerate(qs):
+            got = mr[i, :min(int(nhit[i]), q[3])]
+            self.stats["hits"] += len(got)
+            self.stats["remote_hits"] += int((got % W != self.rank).sum())
         for i, q in enumerate(qs):
             m = min(int(nhit[i]), q[3])
             rows = list(zip(mr[i, :m].tolist(), ms[i, :m].tolist()))

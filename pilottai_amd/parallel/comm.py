@@ -162,12 +162,12 @@ def new_tp_groups(tp_size: int, custom_ar: Optional[bool] = None) -> TPGroup:
     return mine
 
 
-def barrier():
+def barrier(group=None):
     if dist.is_initialized():
-        if dist.get_backend() == "nccl":
-            dist.barrier(device_ids=[torch.cuda.current_device()])
+        if dist.get_backend(group) == "nccl":
+            dist.barrier(group=group, device_ids=[torch.cuda.current_device()])
         else:
-            dist.barrier()
+            dist.barrier(group=group)
 
 
 def all_reduce_max(x: float, device=None) -> float:
@@ -186,12 +186,22 @@ def all_reduce_sum(values: List[float], device=None) -> List[float]:
     return t.tolist()
 
 
-def broadcast_object(obj, src: int = 0):
+def broadcast_object(obj, src: int = 0, group=None):
+    """src: a global rank (a member of `group`)."""
     if not dist.is_initialized():
         return obj
     lst = [obj]
-    dist.broadcast_object_list(lst, src=src)
+    dist.broadcast_object_list(lst, src=src, group=group)
     return lst[0]
+
+
+def new_dp_group(tp_size: int):
+    """The group of TP drivers (global ranks 0, T, 2T, ...): the agent-DP replicas when every
+    replica is a TP group of `tp_size` ranks (contiguous, as new_tp_groups). Every rank must
+    call this (torch.distributed.new_group is collective); None without a process group."""
+    if not dist.is_initialized():
+        return None
+    return dist.new_group(list(range(0, dist.get_world_size(), max(1, tp_size))))
 
 
 def broadcast_tokens(ids: Optional[List[int]], src: int = 0) -> List[int]:

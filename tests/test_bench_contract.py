@@ -104,3 +104,28 @@ def test_bench_node_memory_is_one_sharded_store(tmp_path):
     assert len(per) == 2 and R <= sum(per) == m["rows_total"] < R + 1000
     assert all(R // 2 <= r < R // 2 + 1000 for r in per)  # a shard each, plus write-backs
     assert m["lookups"] > 0 and m["node_rounds"] > 0
+    # the agents' write-backs reach the node store (none failed), and
+    # lookups return rows held by the other rank's shard
+    assert m["stores"] > 0 and m["store_failures"] == 0 and m["lookup_failures"] == 0
+    assert m["node_hits"] > 0 and m["node_remote_hits"] > 0
+
+
+def test_bench_agent_dp_over_tp_groups(tmp_path):
+    """`--gpus 4 --tp 2` runs 2 agent-DP replicas, each a TP=2 engine (its
+    TP rank 1 follows the driver's steps); the node plane and the clients see 2 replicas, the
+    JSON line names the layout, and every rank's device is reported (4 gloo ranks on CPU)."""
+    env = dict(os.environ, PILOTTAI_DIST_BACKEND="gloo", CUDA_VISIBLE_DEVICES="")
+    env.pop("WORLD_SIZE", None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "4",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(ROOT, "bench.py"), "--gpus", "4", "--tp", "2", "--cpu", "--steps", "1", "--warmup", "1",
+           "--workers", "4", "--doc-words", "20"]
+    p = subprocess.run(cmd, cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=900)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    assert d["config"]["parallelism"] == "agent-dp2-tp2"
+    assert d["config"]["managers"] == 1 and d["tasks"] >= 4
+    assert len(d["llm_calls_per_rank"]) == 2 and all(c > 0 for c in d["llm_calls_per_rank"])
+    assert d["world_size"] == 4 and d["devices"] == ["cpu"] * 4

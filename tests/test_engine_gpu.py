@@ -174,6 +174,30 @@ def test_llama3_8b_production_large_steps(gpu, lens):
 _ENG8B = {}
 
 
+@pytest.mark.parametrize("lens", [(5,), (30,), (200,), (400,), (1300,), (700, 9, 20)])
+def test_llama3_70b_layer_dims_every_path(gpu, lens):
+    """70B at TP=1 runs on the hand kernels (one packed weight copy, the
+    row-major one freed). Two layers with the exact Llama-3-70B dimensions (d 8,192, qkv 10,240,
+    gate_up 57,344, down K 28,672, LM head 128,256 x 8,192) through the packed decode, mid-size
+    and prefill-kernel paths; greedy tokens must match the dense fp32 reference forward."""
+    from pilottai_amd.engine.engine import EngineConfig, LLMEngine
+
+    if "70b" not in _ENG8B:
+        _ENG8B["70b"] = LLMEngine(EngineConfig(model="llama-3-70b-2l", max_num_seqs=8, max_num_batched_tokens=2048,
+                                               max_model_len=4096, num_kv_blocks=512, prefix_caching=False),
+                                  device=gpu)
+    eng = _ENG8B["70b"]
+    assert eng.model.decode_packed and not eng.model.keep_dense
+    assert all("wqkv" not in L for L in eng.model.layers) and eng.model.lm_head is None
+    words = ("agents plan tasks and tools while the orchestrator checks every result " * 300).split()
+    base = eng.tok.encode(" ".join(words))
+    prompts = [base[i * 5:i * 5 + n] for i, n in enumerate(lens)]
+    outs = eng.generate(prompts, temperature=0.0, max_tokens=5, ignore_eos=True)
+    for p, o in zip(prompts, outs):
+        assert len(o.token_ids) == 5
+        _check_greedy(eng, p, o.token_ids)
+
+
 def _eng8b(gpu):
     from pilottai_amd.engine.engine import EngineConfig, LLMEngine
 
