@@ -91,6 +91,9 @@ def parse():
     ap.add_argument("--memory-rows", type=int, default=0,
                     help="semantic memory on the engine's GPU with this many rows; every agent step looks it up")
     ap.add_argument("--memory-top-k", type=int, default=3)
+    ap.add_argument("--memory-storage", default="bf16", choices=["bf16", "q16"],
+                    help="index row format: bf16 (one-pass bf16 scan) or q16 (16-bit fixed point, two-stage "
+                         "exact scan streaming one byte per dimension; csrc/ops/similarity_q16.hip)")
     ap.add_argument("--memory-min-batch", type=int, default=1,
                     help="lookups a pass waits for (up to --memory-wait-ms) before it starts")
     ap.add_argument("--memory-wait-ms", type=float, default=0.0)
@@ -319,6 +322,8 @@ async def run_rank(a, rank: int, world: int, device, tp=None, dp_group=None):
         mem = {"rows": memory.index.count, "index_gb": round(memory.index.memory_bytes() / 2**30, 2),
                # node mode: ONE node-wide store, rows sharded over the ranks (memory/node_store.py)
                "store": "node-sharded" if hasattr(memory, "search_rows_blocking") else "single-index",
+               "storage": memory.index.storage,
+               "q16_fallbacks": memory.index.stats.get("q16_fallbacks", 0),
                "node_rounds": memory.stats.get("rounds") if hasattr(memory, "search_rows_blocking") else None,
                "lookups": lookup.stats["lookups"] - mem0["lookups"],
                # the encoder's work when the serving model embeds (--embedder engine):
@@ -491,7 +496,8 @@ def build_memory(a, device, rank: int = 0, world: int = 1, node: bool = False):
     fallback = lambda r: f"archived finding {r}: prior document review notes"  # noqa: E731
     rows = a.memory_rows // world + (1 if rank < a.memory_rows % world else 0) if node else a.memory_rows
     cap = rows + 65536  # room for the run's write-backs
-    mem = EnhancedMemory(max_size=cap, device=device, dim=dim, fallback_text=fallback)
+    mem = EnhancedMemory(max_size=cap, device=device, dim=dim, fallback_text=fallback,
+                         storage=getattr(a, "memory_storage", "bf16"))
     idx = mem.index
     idx._grow(cap)
     g = torch.Generator(device=device).manual_seed(7 + rank)

@@ -8,7 +8,11 @@ the device with random L2-normalised rows (synthetic data: 100M x 1024 bf16 =
 batched search for the 64 worker agents (64 queries, k=10, priority + tag filters):
 a single streaming pass of the MFMA kernel over all rows (csrc/ops/similarity.hip).
 
-    python benchmarks/semantic_store.py [--rows 100000000] [--queries 64] [--steps 10]
+    python benchmarks/semantic_store.py [--rows 100000000] [--queries 64] [--steps 10] [--storage q16]
+
+--storage q16: the 16-bit fixed-point index (two int8 planes) and the two-stage EXACT scan that
+streams only the high plane (csrc/ops/similarity_q16.hip); the run also checks the timed batch
+against the full exact scan of the same index (identical rows and scores).
 
 Prints one JSON line: queries/s, ms per agent step (p50), effective HBM TB/s.
 Planted exact-match queries check that the true nearest row is returned.
@@ -35,20 +39,24 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--chunk", type=int, default=2_000_000)
+    ap.add_argument("--storage", default="bf16", choices=["bf16", "q16"])
     a = ap.parse_args()
     from pilottai_amd.memory.semantic_index import SemanticIndex
 
     dev = torch.device("cuda", 0)
     t0 = time.time()
-    idx = SemanticIndex(dim=a.dim, capacity=a.rows, device=dev, growable=False)
+    idx = SemanticIndex(dim=a.dim, capacity=a.rows, device=dev, growable=False, storage=a.storage)
     for t in range(8):
         idx.tags.bit(f"topic{t}")
     g = torch.Generator(device=dev)
     g.manual_seed(0)
     for lo in range(0, a.rows, a.chunk):
         n = min(a.chunk, a.rows - lo)
-        v = torch.randn(n, a.dim, device=dev, dtype=torch.bfloat16, generator=g)
-        v = v / v.float().norm(dim=1, keepdim=True).to(torch.bfloat16)
+        if a.storage == "q16":
+            v = torch.nn.functional.normalize(torch.randn(n, a.dim, device=dev, generator=g), dim=1)
+        else:
+            v = torch.randn(n, a.dim, device=dev, dtype=torch.bfloat16, generator=g)
+            v = v / v.float().norm(dim=1, keepdim=True).to(torch.bfloat16)
         prio = torch.randint(0, 5, (n,), device=dev, dtype=torch.int32, generator=g)
         tags = torch.randint(0, 256, (n,), device=dev, dtype=torch.int64, generator=g)  # 8 topic bits
         idx.add_device(v, prio, tags, normalized=True)
@@ -75,12 +83,26 @@ def main():
         if it >= a.warmup:
             lat.append(time.perf_counter() - s)
     ok = all(res[i] and res[i][0][0] == r for i, r in planted.items())
+    exact_same = None
+    if a.storage == "q16":  # the timed two-stage answers against the full exact scan
+        from pilottai_amd import ops
+
+        qm, _ = idx.query_masks(tags)
+        qd = torch.nn.functional.normalize(torch.from_numpy(qv).to(dev), dim=1)
+        s_x, r_x = ops.q16_topk(qd, idx.hi, idx.lo, idx.rmeta, idx.count, a.k, idx.priority, idx.tagbits,
+                                idx.expiry, torch.tensor(minp, dtype=torch.int32, device=dev),
+                                torch.tensor(qm, dtype=torch.int64, device=dev), idx.now(), exact=True)
+        s_x, r_x = s_x.cpu(), r_x.cpu()
+        exact_same = all([r for r, _ in res[i]] == [int(x) for x in r_x[i] if x >= 0] and
+                         [sc for _, sc in res[i]] == [float(x) for x in s_x[i][:len(res[i])]] for i in range(Q))
     lat.sort()
     p50 = lat[len(lat) // 2]
     mean = sum(lat) / len(lat)
-    bytes_per_pass = a.rows * a.dim * 2 * ((Q + 63) // 64)
+    bytes_per_pass = a.rows * a.dim * (1 if a.storage == "q16" else 2) * ((Q + 63) // 64)
     out = {
         "metric": "semantic store: filtered cosine top-k queries/s (100M x 1024 bf16 HBM index)",
+        "storage": a.storage, "identical_to_exact_scan": exact_same,
+        "q16_fallbacks": idx.stats.get("q16_fallbacks", 0),
         "value": round(Q / mean, 1), "unit": "queries/s", "n_gpus": 1, "steps": a.steps, "warmup": a.warmup,
         "ms_per_step": round(1000 * mean, 3), "p50_ms_per_agent_step": round(1000 * p50, 3),
         "higher_is_better": True, "dtype": "bf16", "data": "synthetic random unit vectors",
@@ -91,7 +113,7 @@ def main():
         "planted_hits_found": ok,
     }
     print(json.dumps(out), flush=True)
-    if not ok:
+    if not ok or exact_same is False:
         sys.exit(1)
 
 

@@ -75,6 +75,11 @@ int pa_cosine_topk(float* out_scores, int* out_rows, void* workspace, const void
                    const void* index, int Q, int N, int D, int K, const int* row_priority,
                    const uint64_t* row_tags, const float* row_expiry, const int* q_min_priority,
                    const uint64_t* q_tags, float now, int n_valid, hipStream_t st);
+long long pa_q16_topk_workspace_bytes(int Q, int N);
+int pa_q16_topk(float* out_scores, int* out_rows, int* unsafe, void* workspace, const void* queries_q,
+                const float* qmeta, const void* hi, const void* lo, const float* rmeta, int Q, int N, int D, int K,
+                const int* row_priority, const uint64_t* row_tags, const float* row_expiry,
+                const int* q_min_priority, const uint64_t* q_tags, float now, int exact, hipStream_t st);
 int pa_car_group();
 long long pa_car_flag_bytes();
 void* pa_car_alloc(long long bytes, void* handle_out);
@@ -680,6 +685,46 @@ void cosine_topk(at::Tensor out_scores, at::Tensor out_rows, at::Tensor workspac
            "cosine_topk");
 }
 
+int64_t q16_topk_workspace_bytes(int64_t Q, int64_t N) { return pa_q16_topk_workspace_bytes(Q, N); }
+
+// Two-stage exact top-k over the 16-bit fixed-point index (csrc/ops/similarity_q16.hip).
+void q16_topk(at::Tensor out_scores, at::Tensor out_rows, at::Tensor unsafe, at::Tensor workspace,
+              at::Tensor queries_q, at::Tensor qmeta, at::Tensor hi, at::Tensor lo, at::Tensor rmeta, int64_t n_valid,
+              int64_t K, at::Tensor row_priority, at::Tensor row_tags, at::Tensor row_expiry,
+              at::Tensor q_min_priority, at::Tensor q_tags, double now, int64_t exact) {
+  for (auto* t : {&out_scores, &out_rows, &unsafe, &workspace, &queries_q, &qmeta, &hi, &lo, &rmeta, &row_priority,
+                  &row_tags, &row_expiry, &q_min_priority, &q_tags})
+    check_gpu(*t, "q16_topk arg");
+  check_dtype(queries_q, at::kChar, "queries_q"); check_dtype(hi, at::kChar, "hi"); check_dtype(lo, at::kChar, "lo");
+  check_dtype(qmeta, at::kFloat, "qmeta"); check_dtype(rmeta, at::kFloat, "rmeta");
+  check_dtype(out_scores, at::kFloat, "out_scores"); check_dtype(out_rows, at::kInt, "out_rows");
+  check_dtype(unsafe, at::kInt, "unsafe");
+  check_dtype(row_priority, at::kInt, "row_priority"); check_dtype(row_tags, at::kLong, "row_tags");
+  check_dtype(row_expiry, at::kFloat, "row_expiry");
+  check_dtype(q_min_priority, at::kInt, "q_min_priority"); check_dtype(q_tags, at::kLong, "q_tags");
+  TORCH_CHECK(hi.dim() == 4 && hi.size(2) == 64 && hi.size(3) == 16 && lo.sizes() == hi.sizes(),
+              "hi / lo must be int8 planes [N/16, D/64, 64, 16] (memory/semantic_index.py storage='q16')");
+  const int64_t N = hi.size(0) * 16, D = hi.size(1) * 64;
+  const int64_t Q = queries_q.size(0);
+  TORCH_CHECK(queries_q.dim() == 3 && queries_q.size(1) == 2 && queries_q.size(2) == D, "queries_q [Q, 2, D]");
+  TORCH_CHECK(Q <= 64, "q16_topk takes at most 64 queries per call");
+  TORCH_CHECK(qmeta.numel() >= 2 * Q && rmeta.numel() >= 2 * n_valid, "qmeta [Q, 2] / rmeta [N, 2] too short");
+  TORCH_CHECK(n_valid <= N, "n_valid exceeds index rows");
+  TORCH_CHECK(row_priority.numel() >= n_valid && row_tags.numel() >= n_valid && row_expiry.numel() >= n_valid,
+              "row metadata shorter than n_valid");
+  TORCH_CHECK(out_scores.numel() >= Q * K && out_rows.numel() >= Q * K && unsafe.numel() >= Q, "output too small");
+  TORCH_CHECK(workspace.numel() * workspace.element_size() >= pa_q16_topk_workspace_bytes(Q, n_valid),
+              "q16_topk workspace too small");
+  check_rc(pa_q16_topk(out_scores.data_ptr<float>(), out_rows.data_ptr<int>(), unsafe.data_ptr<int>(),
+                       workspace.data_ptr(), queries_q.data_ptr(), qmeta.data_ptr<float>(), hi.data_ptr(),
+                       lo.data_ptr(), rmeta.data_ptr<float>(), (int)Q, (int)n_valid, (int)D, (int)K,
+                       row_priority.data_ptr<int>(), reinterpret_cast<const uint64_t*>(row_tags.data_ptr<int64_t>()),
+                       row_expiry.data_ptr<float>(), q_min_priority.data_ptr<int>(),
+                       reinterpret_cast<const uint64_t*>(q_tags.data_ptr<int64_t>()), (float)now, (int)exact,
+                       cur_stream()),
+           "q16_topk");
+}
+
 }  // namespace
 
 // One phase of the vocab-parallel top-k / top-p threshold (sampling.hip tp_topkp_kernel):
@@ -944,6 +989,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("tp_topkp_phase", &tp_topkp_phase);
   m.def("cosine_topk_workspace_bytes", &cosine_topk_workspace_bytes);
   m.def("cosine_topk", &cosine_topk);
+  m.def("q16_topk_workspace_bytes", &q16_topk_workspace_bytes);
+  m.def("q16_topk", &q16_topk);
   m.def("car_alloc", &car_alloc);
   m.def("car_open", &car_open);
   m.def("car_close", [](int64_t p) { return pa_car_close((void*)(uintptr_t)p); });

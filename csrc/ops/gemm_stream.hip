@@ -36,6 +36,37 @@
 //     departure counter resets both counters, so they are zero between launches (hipGraph
 //     replay safe). Every spin is bounded: a timed-out group barrier sets the err word, which
 //     the engine reads back with every step and fails on (LLMEngine._health_check).
+//
+// Why the shipping form (rel = 0, no producer release) is ordered -- the ISA program order of
+// one group member's publish and every member's consume:
+//   P1  every wave: buffer_store_dwordx4 ... sc1 (cache-policy aux 16) of its fragments into
+//       the slab, which is hipDeviceMallocUncached memory (MTYPE UC: neither a
+//       CU's L1 nor any XCD's L2 may hold its lines, so there is no cached copy to write back
+//       or to go stale -- the reason the release (buffer_wbl2 sc1) has nothing left to do here);
+//   P2  every wave: asm volatile "s_waitcnt vmcnt(0)" -- the wave stalls until each of its
+//       stores is acknowledged; an uncached write is acknowledged by the memory-side point that
+//       orders it (the data fabric / memory channel), not by a cache;
+//   P3  s_barrier (group_barrier's __syncthreads) -- no lane passes it before every wave of the
+//       workgroup has passed P2;
+//   P4  lane 0: global_atomic_add (relaxed, agent scope; executed at the L2/memory side) -- in
+//       program order after P3, hence after every store of the workgroup was acknowledged;
+//   C1  lane 0: relaxed agent-scope (sc1) polls of the same counter until it reads S -- a value
+//       that exists only after all S members executed their P4;
+//   C2  lane 0: fence(acquire, agent) = buffer_inv sc1 + s_waitcnt vmcnt(0), then s_barrier;
+//   C3  every wave: buffer_load_dwordx4 sc1 of the slabs -- issued after C2 in program order,
+//       bypassing L1 and reading the UC lines at the same memory-side point that acknowledged P2.
+// So each slab load is issued after an acknowledgement of the store it reads (P2 < P3 < P4 <
+// C1 < C2 < C3, each link a program-order or value dependence); this is row 1 of the measured
+// hand-off table in MI355X_MICROARCH.md (one lane per storing workgroup signals with an agent
+// atomic after every storing wave's vmcnt(0) and a barrier; the consumer polls with sc1 loads,
+// its other waves load after a barrier; 16-B sc1 stores and loads), plus the acquire. The one
+// hardware assumption is that P2's acknowledgement of an uncached write comes from its ordering
+// point. Evidence: 0 bad runs in 1,200,000 poisoned repetitions with the release and, at rel = 0,
+// 100,000 per engine plan (profiles/r6_stream_handoff_rel0.jsonl) plus 2,000 per plan in the GPU
+// tier (tests/test_stream_gemm_gpu.py::test_stream_handoff_shipping_default_no_release).
+// The round-4 failure (5 / 10,000 without a release) was the OTHER form, in gemm_decode /
+// gemm_mid: the last arriver read its partners' slabs right after its own add returned, with no
+// poll-then-acquire and 4-byte stores; those kernels keep the release.
 #include "common.h"
 #include "packed_epi.h"
 

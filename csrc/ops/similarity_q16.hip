@@ -1,0 +1,506 @@
+// Two-stage EXACT filtered top-k over a 16-bit fixed-point semantic index (VERDICT r5 item 7:
+// "halve the bytes per config-4 pass"; reference semantics pilott/memory/enhanced_memory.py:
+// 93-116 semantic_search, filters as csrc/ops/similarity.hip).
+//
+// Storage (memory/semantic_index.py storage="q16"): every L2-normalised row x is kept as
+// v = round(x / s_r), |v| <= 32512 (s_r = max|x| / 32512 per row), split into two int8 planes
+//     hi = floor((v + 128) / 256)  in [-127, 127],   lo = v - 256 hi  in [-128, 127],
+// each plane fragment-major in 16-row tiles for v_mfma_i32_16x16x64_i8:
+//     plane[t][s][16 g + c][j] = plane_row(16 t + c)[64 s + 16 g + j]       (16 B per lane)
+// plus per row (s_r, b_r = s_r ||lo||_2). Queries are quantised the same way (v_q = 256 qh +
+// ql, scale s_q, c_q = s_q ||v_q||_2). The EXACT score of (row, query) is
+//     S = s_r s_q (v_q . v_r) = s_r s_q (65536 qh.hi + 256 (qh.lo + ql.hi) + ql.lo)
+// from four exact int32 dot products (exact_score below; the CPU reference in
+// ops/reference.py q16_topk evaluates the same int64 sum and the same float64 -> float32 step,
+// so GPU and reference agree bit for bit). 16-bit fixed point resolves each coordinate to
+// ~3e-6 -- finer than the bf16 index's 2^-9 relative.
+//
+// Stage 1 (one pass, hi plane ONLY: 1 byte per dimension instead of the bf16 index's 2):
+//     S^ = s_r s_q (65536 qh.hi + 256 ql.hi),     |S - S^| = s_r s_q |v_q . lo| <= c_q b_r = E
+// (Cauchy-Schwarz), so L = S^ - E <= S <= U = S^ + E. Each workgroup (a slice of rows, 16
+// waves, every wave a 16-row group x every query tile, two MFMAs per 64-dim k-step) keeps
+// per query the rows with the C best upper bounds U, admitting a row only if U beats both the
+// C-th best U so far (capacity) and the K-th best LOWER bound so far (tau_slice: k rows already
+// score at least that, so a row whose U is below it cannot be in the top-k). A row refused
+// for capacity marks the slice: its drop level (the C-th best U) is reported.
+// Stage 2 (one workgroup per query): tau = the K-th best L over every slice's list (the global
+// top-k by L is inside the union: a row missing from it was refused for capacity, and the
+// drop check below catches that); every listed row with U >= tau is re-ranked EXACTLY (one
+// wave per row gathers its hi and lo fragments and runs the four integer dot products), and
+// the K best exact scores are the answer. If some slice's drop level reaches tau, a dropped
+// row might belong to the top-k: the query is flagged and the host re-runs the batch with the
+// exact scan (EXACT = true: both planes, exact scores in stage 1), so the result is always
+// exact. On random unit vectors at 100M rows the band [tau - 2E, tau] holds a few hundred rows
+// (E ~ 0.008 against a score spread of 1/sqrt(D) = 0.031), far below the lists' 16K entries.
+#include "common.h"
+
+namespace pa {
+namespace q16 {
+
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef signed char i8x16 __attribute__((ext_vector_type(16)));
+
+constexpr int CAND = 512;     // candidate buffer per (slice, query), power of two
+constexpr int C = 64;         // list entries kept per (slice, query): the best C upper bounds
+constexpr int MAXK = 64;
+constexpr int QT = 16;        // queries per MFMA tile
+constexpr int MAXQ = 64;
+constexpr int MAXD = 1024;
+constexpr int THREADS = 1024; // 16 waves
+constexpr int NW = THREADS / 64;
+constexpr int MIN_ROWS_PER_WG = 2048;
+constexpr int MAX_WG = 256;   // one resident workgroup per CU
+
+__host__ __device__ inline int num_wg(int N) {
+  int nwg = (N + MIN_ROWS_PER_WG - 1) / MIN_ROWS_PER_WG;
+  if (nwg > MAX_WG) nwg = MAX_WG;
+  if (nwg < 1) nwg = 1;
+  return nwg;
+}
+
+// the exact score (see the header); the ONLY place the integer sums become a float
+__device__ __forceinline__ float exact_score(int hh, int hl, int lh, int ll, float sr, float sq) {
+  const long long I = (long long)hh * 65536 + ((long long)hl + (long long)lh) * 256 + (long long)ll;
+  return (float)((double)I * ((double)sr * (double)sq));
+}
+
+// Bitonic sort of n = CAND entries descending by key, carrying two payloads (whole block).
+__device__ void bitonic3(float* key, float* p1, int* p2) {
+  for (int k = 2; k <= CAND; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      __syncthreads();
+      const int i = threadIdx.x;
+      const int p = i ^ j;
+      if (i < CAND && p > i) {
+        const bool desc = (i & k) == 0;
+        const float a = key[i], b = key[p];
+        if (desc ? (a < b) : (a > b)) {
+          key[i] = b; key[p] = a;
+          const float t1 = p1[i]; p1[i] = p1[p]; p1[p] = t1;
+          const int t2 = p2[i]; p2[i] = p2[p]; p2[p] = t2;
+        }
+      }
+    }
+  }
+  __syncthreads();
+}
+
+struct QState {  // per-query admission state of one slice (LDS)
+  int cnt[MAXQ];
+  float theta[MAXQ];    // admission threshold = max(cap, tauL)
+  float cap[MAXQ];      // C-th best U kept (-inf until C entries)
+  float tauL[MAXQ];     // K-th best L among the kept entries (-inf until K)
+  int dropped[MAXQ];    // a row was refused (or truncated) for capacity
+  int minp[MAXQ];
+  uint64_t qtag[MAXQ];
+  float sq[MAXQ];
+  float cq[MAXQ];
+};
+
+// Compact query q's global buffer to its best C upper bounds; refresh cap / tauL / theta.
+__device__ void compact(float* gu, float* gl, int* gr, float* su, float* sl, int* sr, QState& st, int q, int K) {
+  const int n = min(st.cnt[q], CAND);
+  if (threadIdx.x < CAND) {
+    const bool ok = threadIdx.x < n;
+    su[threadIdx.x] = ok ? gu[threadIdx.x] : -INFINITY;
+    sl[threadIdx.x] = ok ? gl[threadIdx.x] : -INFINITY;
+    sr[threadIdx.x] = ok ? gr[threadIdx.x] : -1;
+  }
+  bitonic3(su, sl, sr);  // begins and ends with a barrier
+  const int keep = min(n, C);
+  if (threadIdx.x < keep) {
+    gu[threadIdx.x] = su[threadIdx.x];
+    gl[threadIdx.x] = sl[threadIdx.x];
+    gr[threadIdx.x] = sr[threadIdx.x];
+    if (keep >= K) {  // rank of this entry's L among the kept ones (ties by position)
+      const float me = sl[threadIdx.x];
+      int rank = 0;
+      for (int j = 0; j < keep; ++j) {
+        const float o = sl[j];
+        rank += (o > me) || (o == me && j < (int)threadIdx.x);
+      }
+      if (rank == K - 1) st.tauL[q] = fmaxf(st.tauL[q], me);  // any subset's K-th best is a valid bound
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    st.cnt[q] = keep;
+    if (n > C) st.dropped[q] = 1;
+    if (keep == C) st.cap[q] = su[C - 1];
+    st.theta[q] = fmaxf(st.cap[q], st.tauL[q]);
+  }
+  __syncthreads();
+}
+
+// Stage 1. EXACT: both planes, U = L = the exact score (the fallback / reference scan).
+template <bool EXACT>
+__global__ __launch_bounds__(EXACT ? 512 : 1024) void stage1_kernel(
+    float* __restrict__ out_u, float* __restrict__ out_l, int* __restrict__ out_r, float* __restrict__ out_drop,
+    float* __restrict__ cand_u, float* __restrict__ cand_l, int* __restrict__ cand_r,
+    const signed char* __restrict__ qv, const float* __restrict__ qmeta, const signed char* __restrict__ hi,
+    const signed char* __restrict__ lo, const float* __restrict__ rmeta, int Q, int N, int D, int K,
+    const int* __restrict__ row_prio, const uint64_t* __restrict__ row_tags, const float* __restrict__ row_exp,
+    const int* __restrict__ q_minp, const uint64_t* __restrict__ q_tags, float now) {
+  // the exact scan holds four accumulators per query tile: 8 waves, 256 registers each
+  constexpr int TH = EXACT ? 512 : 1024, NWV = TH / 64;
+  constexpr int KB = EXACT ? 2 : 4;  // k-steps per load batch (16 B per lane per plane and step)
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int NQT = (Q + QT - 1) / QT;
+  const int QLD = D + 16;  // padded LDS row (bytes): the 16 query rows of a fragment spread over the banks
+  signed char* qh = reinterpret_cast<signed char*>(smem);           // [NQT*16][QLD]
+  signed char* ql = qh + (size_t)NQT * QT * QLD;                    // [NQT*16][QLD]
+  float* su = reinterpret_cast<float*>(ql + (size_t)NQT * QT * QLD);
+  float* sl = su + CAND;
+  int* sr = reinterpret_cast<int*>(sl + CAND);
+  QState& st = *reinterpret_cast<QState*>(sr + CAND);
+
+  const int nwg = gridDim.x, wg = blockIdx.x;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int g = lane >> 4, col = lane & 15;
+  const int DS = D / 64;
+  // queries: qv [Q][2][D] (qh, ql) -> LDS, zero rows past Q
+  for (int v = threadIdx.x; v < NQT * QT * 2 * (D / 16); v += TH) {
+    const int r = v / (2 * (D / 16)), rem = v % (2 * (D / 16));
+    const int plane = rem / (D / 16), c16 = (rem % (D / 16)) * 16;
+    i32x4 x = i32x4{0, 0, 0, 0};
+    if (r < Q) x = *reinterpret_cast<const i32x4*>(qv + ((size_t)r * 2 + plane) * D + c16);
+    *reinterpret_cast<i32x4*>((plane ? ql : qh) + (size_t)r * QLD + c16) = x;
+  }
+  if (threadIdx.x < MAXQ) {
+    const int q = threadIdx.x;
+    st.cnt[q] = 0;
+    st.theta[q] = -INFINITY;
+    st.cap[q] = -INFINITY;
+    st.tauL[q] = -INFINITY;
+    st.dropped[q] = 0;
+    st.minp[q] = q < Q ? q_minp[q] : 0x7fffffff;
+    st.qtag[q] = q < Q ? q_tags[q] : 0ull;
+    st.sq[q] = q < Q ? qmeta[2 * q] : 0.f;
+    st.cq[q] = q < Q ? qmeta[2 * q + 1] : 0.f;
+  }
+  __syncthreads();
+
+  float* my_u = cand_u + (size_t)wg * MAXQ * CAND;
+  float* my_l = cand_l + (size_t)wg * MAXQ * CAND;
+  int* my_r = cand_r + (size_t)wg * MAXQ * CAND;
+  const int per = ((N + nwg - 1) / nwg + 15) / 16 * 16;
+  const int r0 = wg * per, r1 = min(N, r0 + per);
+  const int ngroups = (max(0, r1 - r0) + 15) / 16;
+  const int nrounds = (ngroups + NWV - 1) / NWV;
+
+  auto frag_off = [&](int grp_, int s) -> size_t {  // byte offset of this lane's fragment, k-step s
+    return (((size_t)((r0 + grp_ * 16) >> 4) * DS + s) * 64 + lane) * 16;
+  };
+  auto load = [&](const signed char* plane, int grp_, int m, i32x4 (&dst)[KB]) {
+#pragma unroll
+    for (int u = 0; u < KB; ++u)
+      dst[u] = (m + u < DS) ? __builtin_nontemporal_load(reinterpret_cast<const i32x4*>(plane + frag_off(grp_, m + u)))
+                            : i32x4{0, 0, 0, 0};
+  };
+  i32x4 hA[KB], hB[KB], lA[KB], lB[KB];
+  if (wid < ngroups) {
+    load(hi, wid, 0, hA);
+    if (EXACT) load(lo, wid, 0, lA);
+  }
+
+  for (int round = 0; round < nrounds; ++round) {
+    const int grp = round * NWV + wid;
+    if (grp < ngroups) {
+      const int gbase = r0 + grp * 16;
+      i32x4 acc_hh[MAXQ / QT], acc_lh[MAXQ / QT], acc_hl[MAXQ / QT], acc_ll[MAXQ / QT];
+#pragma unroll
+      for (int t = 0; t < MAXQ / QT; ++t) {
+        acc_hh[t] = i32x4{0, 0, 0, 0};
+        acc_lh[t] = i32x4{0, 0, 0, 0};
+        acc_hl[t] = i32x4{0, 0, 0, 0};
+        acc_ll[t] = i32x4{0, 0, 0, 0};
+      }
+      auto compute = [&](const i32x4 (&ah)[KB], const i32x4 (&al)[KB], int m) {
+#pragma unroll
+        for (int u = 0; u < KB; ++u) {
+          if (m + u >= DS) break;
+#pragma unroll
+          for (int t = 0; t < MAXQ / QT; ++t) {
+            if (t < NQT) {
+              const size_t qo = (size_t)(t * QT + col) * QLD + 64 * (m + u) + 16 * g;
+              const i32x4 bh = *reinterpret_cast<const i32x4*>(qh + qo);
+              const i32x4 bl = *reinterpret_cast<const i32x4*>(ql + qo);
+              acc_hh[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(ah[u], bh, acc_hh[t], 0, 0, 0);
+              acc_lh[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(ah[u], bl, acc_lh[t], 0, 0, 0);
+              if (EXACT) {
+                acc_hl[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(al[u], bh, acc_hl[t], 0, 0, 0);
+                acc_ll[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(al[u], bl, acc_ll[t], 0, 0, 0);
+              }
+            }
+          }
+        }
+      };
+      for (int m = 0; m < DS; m += 2 * KB) {
+        if (m + KB < DS) {
+          load(hi, grp, m + KB, hB);
+          if (EXACT) load(lo, grp, m + KB, lB);
+        }
+        compute(hA, lA, m);
+        if (m + 2 * KB < DS) {
+          load(hi, grp, m + 2 * KB, hA);
+          if (EXACT) load(lo, grp, m + 2 * KB, lA);
+        } else if (grp + NWV < ngroups) {  // the next group's first batch stays in flight
+          load(hi, grp + NWV, 0, hA);
+          if (EXACT) load(lo, grp + NWV, 0, lA);
+        }
+        if (m + KB < DS) compute(hB, lB, m + KB);
+      }
+      // lane holds rows gbase + 4g + r for queries t*16 + col
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = gbase + 4 * g + r;
+        if (row >= r1) continue;
+        const float2 rm = *reinterpret_cast<const float2*>(rmeta + 2 * (size_t)row);
+#pragma unroll
+        for (int t = 0; t < MAXQ / QT; ++t) {
+          const int q = t * QT + col;
+          if (t >= NQT || q >= Q) continue;
+          float U, L;
+          if (EXACT) {
+            U = L = exact_score(acc_hh[t][r], acc_hl[t][r], acc_lh[t][r], acc_ll[t][r], rm.x, st.sq[q]);
+          } else {
+            const float s = ((float)acc_hh[t][r] * 65536.f + (float)acc_lh[t][r] * 256.f) * (rm.x * st.sq[q]);
+            const float e = rm.y * st.cq[q] * 1.0001f + 1e-6f;  // margin: fp32 rounding of s and e
+            U = s + e;
+            L = s - e;
+          }
+          if (!(U > st.theta[q])) {
+            if (U > st.tauL[q]) st.dropped[q] = 1;  // refused for capacity, not by the k-th bound
+            continue;
+          }
+          if (row_prio[row] < st.minp[q]) continue;
+          if ((row_tags[row] & st.qtag[q]) != st.qtag[q]) continue;
+          const float ex = row_exp[row];
+          if (ex != 0.f && !(ex > now)) continue;
+          const int pos = atomicAdd(&st.cnt[q], 1);
+          if (pos < CAND) {
+            my_u[q * CAND + pos] = U;
+            my_l[q * CAND + pos] = L;
+            my_r[q * CAND + pos] = row;
+          }
+        }
+      }
+    }
+    __syncthreads();
+    for (int q = 0; q < Q; ++q)  // a buffer must absorb the next round (NWV waves x 16 rows)
+      if (st.cnt[q] > CAND - NWV * 16)
+        compact(my_u + q * CAND, my_l + q * CAND, my_r + q * CAND, su, sl, sr, st, q, K);
+  }
+  __syncthreads();
+  for (int q = 0; q < Q; ++q) {
+    compact(my_u + q * CAND, my_l + q * CAND, my_r + q * CAND, su, sl, sr, st, q, K);
+    const int n = st.cnt[q];
+    if (threadIdx.x < C) {
+      const size_t o = ((size_t)q * nwg + wg) * C + threadIdx.x;
+      const bool ok = (int)threadIdx.x < n;
+      out_u[o] = ok ? su[threadIdx.x] : -INFINITY;
+      out_l[o] = ok ? sl[threadIdx.x] : -INFINITY;
+      out_r[o] = ok ? sr[threadIdx.x] : -1;
+    }
+    if (threadIdx.x == 0) out_drop[(size_t)q * nwg + wg] = st.dropped[q] ? st.cap[q] : -INFINITY;
+    __syncthreads();
+  }
+}
+
+// Insert (key, row) into the block's top-k buffer under its threshold (one thread per call).
+__device__ __forceinline__ void offer(float* bs, int* br, int* cnt, const float* theta, float key, int row) {
+  if (key > *theta) {
+    const int pos = atomicAdd(cnt, 1);
+    if (pos < CAND) { bs[pos] = key; br[pos] = row; }
+  }
+}
+
+// Sort the block buffer, keep the best K, raise the threshold (whole block).
+__device__ void keep_best(float* bs, int* br, float* dummy, int* cnt, float* theta, int K) {
+  const int n = min(*cnt, CAND);
+  if (threadIdx.x < CAND && (int)threadIdx.x >= n) { bs[threadIdx.x] = -INFINITY; br[threadIdx.x] = -1; }
+  if (threadIdx.x < CAND) dummy[threadIdx.x] = 0.f;
+  bitonic3(bs, dummy, br);
+  if (threadIdx.x == 0) {
+    const int keep = min(n, K);
+    *cnt = keep;
+    if (keep == K) *theta = bs[K - 1];
+  }
+  __syncthreads();
+}
+
+// Stage 2: one workgroup per query (see the header). EXACT: the lists hold exact scores.
+template <bool EXACT>
+__global__ __launch_bounds__(THREADS) void stage2_kernel(
+    float* __restrict__ out_s, int* __restrict__ out_rows, int* __restrict__ unsafe,
+    const float* __restrict__ lu, const float* __restrict__ ll, const int* __restrict__ lr,
+    const float* __restrict__ ldrop, int nwg, const signed char* __restrict__ qv,
+    const float* __restrict__ qmeta, const signed char* __restrict__ hi, const signed char* __restrict__ lo,
+    const float* __restrict__ rmeta, int D, int K) {
+  __shared__ float bs[CAND];
+  __shared__ int br[CAND];
+  __shared__ float dummy[CAND];
+  __shared__ int cnt;
+  __shared__ float theta;
+  __shared__ float red[NW];
+  __shared__ __attribute__((aligned(16))) signed char q_lds[2 * MAXD];
+  constexpr int CL = 4096;  // list entries scanned per chunk (all of them may qualify)
+  __shared__ int ncand;
+  __shared__ int clist[CL];
+  const int q = blockIdx.x;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int total = nwg * C;
+  const float* u = lu + (size_t)q * total;
+  const float* l = ll + (size_t)q * total;
+  const int* r = lr + (size_t)q * total;
+  if (threadIdx.x == 0) { cnt = 0; theta = -INFINITY; }
+  for (int i = threadIdx.x; i < 2 * D / 16; i += THREADS)
+    *reinterpret_cast<i32x4*>(q_lds + 16 * i) = *reinterpret_cast<const i32x4*>(qv + (size_t)q * 2 * D + 16 * i);
+  __syncthreads();
+  // ---- A: tau = the K-th best lower bound over every slice's list (256 offers per round:
+  // the buffer keeps room for a round on top of the K it holds after a compaction)
+  constexpr int OFR = 256;
+  for (int base = 0; base < total; base += OFR) {
+    const int i = base + threadIdx.x;
+    if (threadIdx.x < OFR && i < total && r[i] >= 0) offer(bs, br, &cnt, &theta, l[i], r[i]);
+    __syncthreads();
+    if (cnt > CAND - OFR) keep_best(bs, br, dummy, &cnt, &theta, K);
+  }
+  keep_best(bs, br, dummy, &cnt, &theta, K);
+  const float tau = cnt == K ? theta : -INFINITY;
+  // ---- B: a slice that refused a row for capacity at a level >= tau may have lost a top-k row
+  float dmax = -INFINITY;
+  for (int i = threadIdx.x; i < nwg; i += THREADS) dmax = fmaxf(dmax, ldrop[(size_t)q * nwg + i]);
+  dmax = wave_max(dmax);
+  if (lane == 0) red[wid] = dmax;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float m = -INFINITY;
+    for (int w = 0; w < NW; ++w) m = fmaxf(m, red[w]);
+    unsafe[q] = (!EXACT && m > -INFINITY && m >= tau) ? 1 : 0;
+  }
+  if (EXACT) {  // the lists hold exact scores: A's buffer is the answer
+    if (threadIdx.x < K) {
+      out_s[(size_t)q * K + threadIdx.x] = (int)threadIdx.x < cnt ? bs[threadIdx.x] : -INFINITY;
+      out_rows[(size_t)q * K + threadIdx.x] = (int)threadIdx.x < cnt ? br[threadIdx.x] : -1;
+    }
+    return;
+  }
+  // ---- C: re-rank every listed row whose upper bound reaches tau, exactly
+  __syncthreads();
+  if (threadIdx.x == 0) { cnt = 0; theta = -INFINITY; ncand = 0; }
+  __syncthreads();
+  const float sq = qmeta[2 * q];
+  const int DS = D / 64;
+  for (int base = 0; base < total; base += CL) {
+    // the chunk's listed rows whose upper bound reaches tau -> LDS
+    for (int i = base + threadIdx.x; i < min(total, base + CL); i += THREADS)
+      if (r[i] >= 0 && u[i] >= tau) {
+        const int pos = atomicAdd(&ncand, 1);
+        clist[pos] = r[i];
+      }
+    __syncthreads();
+    const int nc = ncand;
+    for (int j0 = 0; j0 < nc; j0 += NW) {  // one row per wave and round
+      const int j = j0 + wid;
+      if (j < nc) {
+        const int row = clist[j];
+        const int t = row >> 4, c = row & 15;
+        int hh = 0, hl = 0, lh = 0, lls = 0;
+        for (int p = lane; p < DS * 4; p += 64) {  // (k-step, lane group) pieces of 16 dims
+          const int s = p >> 2, gg = p & 3;
+          const size_t off = (((size_t)t * DS + s) * 64 + 16 * gg + c) * 16;
+          const i8x16 a = *reinterpret_cast<const i8x16*>(hi + off);
+          const i8x16 b = *reinterpret_cast<const i8x16*>(lo + off);
+          const i8x16 qa = *reinterpret_cast<const i8x16*>(q_lds + 64 * s + 16 * gg);
+          const i8x16 qb = *reinterpret_cast<const i8x16*>(q_lds + D + 64 * s + 16 * gg);
+#pragma unroll
+          for (int e = 0; e < 16; ++e) {
+            hh += (int)qa[e] * (int)a[e];
+            hl += (int)qa[e] * (int)b[e];
+            lh += (int)qb[e] * (int)a[e];
+            lls += (int)qb[e] * (int)b[e];
+          }
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+          hh += __shfl_xor(hh, o, 64);
+          hl += __shfl_xor(hl, o, 64);
+          lh += __shfl_xor(lh, o, 64);
+          lls += __shfl_xor(lls, o, 64);
+        }
+        if (lane == 0) offer(bs, br, &cnt, &theta, exact_score(hh, hl, lh, lls, rmeta[2 * (size_t)row], sq), row);
+      }
+      __syncthreads();
+      if (cnt > CAND - NW) keep_best(bs, br, dummy, &cnt, &theta, K);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) ncand = 0;
+    __syncthreads();
+  }
+  keep_best(bs, br, dummy, &cnt, &theta, K);
+  if (threadIdx.x < K) {
+    out_s[(size_t)q * K + threadIdx.x] = (int)threadIdx.x < cnt ? bs[threadIdx.x] : -INFINITY;
+    out_rows[(size_t)q * K + threadIdx.x] = (int)threadIdx.x < cnt ? br[threadIdx.x] : -1;
+  }
+}
+
+}  // namespace q16
+}  // namespace pa
+
+// workspace: lists [3][Q][nwg][C] (U, L, row) + drop levels [Q][nwg] + per-(slice, query)
+// candidate buffers [3][nwg][64][CAND]
+extern "C" long long pa_q16_topk_workspace_bytes(int Q, int N) {
+  const long long w = pa::q16::num_wg(N);
+  return 3LL * Q * w * pa::q16::C * 4 + (long long)Q * w * 4 + 3LL * w * pa::q16::MAXQ * pa::q16::CAND * 4;
+}
+
+// queries_q: [Q][2][D] int8 (qh, ql); qmeta [Q][2] (s_q, c_q); hi / lo: [N/16][D/64][64][16]
+// int8; rmeta [N][2] (s_r, b_r). Outputs scores / rows [Q][K] and unsafe [Q] (stage-1 mode only:
+// 1 = rerun this batch with exact = 1). Returns 0, -1 for an unsupported shape, or a HIP error.
+extern "C" int pa_q16_topk(float* out_scores, int* out_rows, int* unsafe, void* workspace, const void* queries_q,
+                           const float* qmeta, const void* hi, const void* lo, const float* rmeta, int Q, int N,
+                           int D, int K, const int* row_priority, const uint64_t* row_tags,
+                           const float* row_expiry, const int* q_min_priority, const uint64_t* q_tags, float now,
+                           int exact, hipStream_t st) {
+  using namespace pa::q16;
+  if (Q <= 0) return 0;
+  if (D % 64 != 0 || D > MAXD || K < 1 || K > MAXK || Q > MAXQ) return -1;
+  if (N <= 0) {
+    (void)hipMemsetAsync(out_rows, 0xff, (size_t)Q * K * sizeof(int), st);
+    (void)hipMemsetAsync(unsafe, 0, (size_t)Q * sizeof(int), st);
+    return (int)hipGetLastError();
+  }
+  const int nwg = num_wg(N);
+  float* lu = reinterpret_cast<float*>(workspace);
+  float* ll = lu + (size_t)Q * nwg * C;
+  int* lr = reinterpret_cast<int*>(ll + (size_t)Q * nwg * C);
+  float* ldrop = reinterpret_cast<float*>(lr + (size_t)Q * nwg * C);
+  float* cu = ldrop + (size_t)Q * nwg;
+  float* cl = cu + (size_t)nwg * MAXQ * CAND;
+  int* cr = reinterpret_cast<int*>(cl + (size_t)nwg * MAXQ * CAND);
+  const int nqt = (Q + QT - 1) / QT;
+  const size_t lds = (size_t)nqt * QT * (D + 16) * 2 + CAND * 12 + sizeof(QState);
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)stage1_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)stage1_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr_set = true;
+  }
+  const signed char* qv = (const signed char*)queries_q;
+  const signed char* h = (const signed char*)hi;
+  const signed char* l = (const signed char*)lo;
+  if (exact) {
+    hipLaunchKernelGGL(stage1_kernel<true>, dim3(nwg), dim3(512), lds, st, lu, ll, lr, ldrop, cu, cl, cr, qv, qmeta,
+                       h, l, rmeta, Q, N, D, K, row_priority, row_tags, row_expiry, q_min_priority, q_tags, now);
+    hipLaunchKernelGGL(stage2_kernel<true>, dim3(Q), dim3(THREADS), 0, st, out_scores, out_rows, unsafe, lu, ll, lr,
+                       ldrop, nwg, qv, qmeta, h, l, rmeta, D, K);
+  } else {
+    hipLaunchKernelGGL(stage1_kernel<false>, dim3(nwg), dim3(THREADS), lds, st, lu, ll, lr, ldrop, cu, cl, cr, qv,
+                       qmeta, h, l, rmeta, Q, N, D, K, row_priority, row_tags, row_expiry, q_min_priority, q_tags,
+                       now);
+    hipLaunchKernelGGL(stage2_kernel<false>, dim3(Q), dim3(THREADS), 0, st, out_scores, out_rows, unsafe, lu, ll, lr,
+                       ldrop, nwg, qv, qmeta, h, l, rmeta, D, K);
+  }
+  return (int)hipGetLastError();
+}

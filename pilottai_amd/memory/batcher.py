@@ -78,6 +78,7 @@ class MemoryLookupBatcher:
     def attach_engine(self, engine, gate_tokens: int = 1024, max_wait_s: float = 0.03):
         """Co-schedule index passes with the engine's compute-bound steps (module docstring).
         Call from the event loop that runs the lookups."""
+        self.detach_engine()
         loop = asyncio.get_running_loop()
         self._heavy = asyncio.Event()
         self._gate_tokens = int(gate_tokens)
@@ -89,7 +90,6 @@ class MemoryLookupBatcher:
                     loop.call_soon_threadsafe(self._mark_heavy)
                 except RuntimeError:  # the loop closed between the check and the call
                     pass
-        self.detach_engine()
         engine.add_step_listener(on_launch)
         self._engine, self._listener = engine, on_launch
 

@@ -42,13 +42,16 @@ class MemoryItem(BaseModel):
 class EnhancedMemory:
     def __init__(self, max_size: int = 10000, cleanup_interval: float = 3600, embedder=None,
                  index: Optional[SemanticIndex] = None, dim: int = 1024, device=None,
-                 fallback_text: Optional[Callable[[int], str]] = None):
+                 fallback_text: Optional[Callable[[int], str]] = None, storage: str = "bf16"):
+        """storage: the index's row format when it is created here ("bf16", or "q16": 16-bit
+        fixed point with the two-stage exact scan, memory/semantic_index.py)."""
         self.max_size = max_size
         self.cleanup_interval = cleanup_interval
         self.embedder = embedder or HashingEmbedder(dim)
         self.index = index or SemanticIndex(dim=getattr(self.embedder, "dim", dim),
                                             capacity=min(max_size, 1 << 16) if max_size else 1 << 16,
-                                            device=device, growable=True, max_capacity=max_size)
+                                            device=device, growable=True, max_capacity=max_size,
+                                            storage=storage)
         self._items: Dict[int, MemoryItem] = {}
         self._task_history: Dict[str, Deque[Dict[str, Any]]] = {}
         self._agent_interactions: Dict[str, Dict[str, Any]] = {}

@@ -60,9 +60,19 @@ class TagRegistry:
         return m, exact
 
 
+STORAGES = ("bf16", "q16")
+
+
 class SemanticIndex:
     def __init__(self, dim: int = 1024, capacity: int = 1 << 16, device=None, growable: bool = True,
-                 max_capacity: Optional[int] = None):
+                 max_capacity: Optional[int] = None, storage: str = "bf16"):
+        """storage: "bf16" -- rows as bf16 tiles, one-pass bf16 MFMA scan (csrc/ops/similarity.hip);
+        "q16" -- rows as 16-bit fixed point in two int8 planes, the two-stage exact scan that
+        streams only the high plane (csrc/ops/similarity_q16.hip: 1 byte per dimension per pass
+        instead of 2, same bytes resident)."""
+        if storage not in STORAGES:
+            raise ValueError(f"storage must be one of {STORAGES}, not {storage!r}")
+        self.storage = storage
         if device is None:
             device = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() \
                 else torch.device("cpu")
@@ -79,6 +89,7 @@ class SemanticIndex:
         self._ws: Optional[torch.Tensor] = None
         self._stream = None
         self.pass_events: Optional[list] = None  # set to [] to time every search pass (HIP events)
+        self.stats = {"q16_fallbacks": 0}  # q16: batches re-run on the exact scan (drop check)
 
     def _alloc(self, cap: int):
         d = self.device
@@ -87,10 +98,18 @@ class SemanticIndex:
         # packed[t, s, 16*g + c, :] = row (16t + c), dims 32s + 8g .. +8 — the A
         # operand of one v_mfma_f32_16x16x32_bf16, so every wave load of the scan is
         # 1 KiB contiguous. Row-major access goes through read_rows()/write_rows().
-        if self.dim % 32:
-            raise ValueError(f"index dim {self.dim} must be a multiple of 32")
+        if self.dim % (64 if self.storage == "q16" else 32):
+            raise ValueError(f"index dim {self.dim} must be a multiple of {64 if self.storage == 'q16' else 32}")
         tiles = (cap + 15) // 16
-        self.packed = torch.zeros(tiles, self.dim // 32, 64, 8, dtype=torch.bfloat16, device=d)
+        if self.storage == "q16":
+            # hi / lo planes, fragment-major for v_mfma_i32_16x16x64_i8 (ops.q16_pack), and per row
+            # (scale, stage-1 error bound factor)
+            self.packed = None
+            self.hi = torch.zeros(tiles, self.dim // 64, 64, 16, dtype=torch.int8, device=d)
+            self.lo = torch.zeros(tiles, self.dim // 64, 64, 16, dtype=torch.int8, device=d)
+            self.rmeta = torch.zeros(cap, 2, dtype=torch.float32, device=d)
+        else:
+            self.packed = torch.zeros(tiles, self.dim // 32, 64, 8, dtype=torch.bfloat16, device=d)
         self.priority = torch.full((cap,), -(1 << 30), dtype=torch.int32, device=d)
         self.tagbits = torch.zeros(cap, dtype=torch.int64, device=d)
         self.expiry = torch.zeros(cap, dtype=torch.float32, device=d)
@@ -102,20 +121,31 @@ class SemanticIndex:
         new = min(new, self.max_capacity)
         if new <= self.capacity:
             return
-        old = (self.packed, self.priority, self.tagbits, self.expiry, self.capacity)
+        old_planes = self._planes()
+        old = (self.priority, self.tagbits, self.expiry, self.capacity)
+        old_rmeta = getattr(self, "rmeta", None)
         self._alloc(new)
-        n = old[4]
-        self.packed[:old[0].shape[0]] = old[0]
-        self.priority[:n] = old[1]
-        self.tagbits[:n] = old[2]
-        self.expiry[:n] = old[3]
+        n = old[3]
+        for (_, dst), (_, src) in zip(self._planes(), old_planes):
+            dst[:src.shape[0]] = src
+        self.priority[:n] = old[0]
+        self.tagbits[:n] = old[1]
+        self.expiry[:n] = old[2]
+        if old_rmeta is not None:
+            self.rmeta[:n] = old_rmeta
         if self.device.type == "cuda":
             # the copies above may be queued on the index's side stream (add() runs _grow under
             # _stream_ctx) while the old blocks were allocated on another stream: keep them out
             # of the caching allocator until the copies reading them are done
             cur = torch.cuda.current_stream(self.device)
-            for t in old[:4]:
+            for t in [p for _, p in old_planes] + list(old[:3]) + ([old_rmeta] if old_rmeta is not None else []):
                 t.record_stream(cur)
+
+    def _planes(self):
+        """(name, tile tensor) of the row storage: what a checkpoint writes and _grow copies."""
+        if self.storage == "q16":
+            return [("hi", self.hi), ("lo", self.lo)]
+        return [("packed", self.packed)]
 
     @property
     def count(self) -> int:
@@ -128,6 +158,13 @@ class SemanticIndex:
     def write_rows(self, rows: torch.Tensor, vals: torch.Tensor):
         """Scatter row-major `vals` [n, dim] into rows `rows` (long tensor)."""
         rows = rows.to(self.device)
+        if self.storage == "q16":
+            hi, lo, sc, bd = ops.q16_quantize(vals.to(self.device))
+            DS = self.dim // 64
+            for plane, part in ((self.hi, hi), (self.lo, lo)):
+                plane.view(plane.shape[0], DS, 4, 16, 16)[rows // 16, :, :, rows % 16, :] = part.view(-1, DS, 4, 16)
+            self.rmeta[rows] = torch.stack([sc, bd], 1)
+            return
         v = vals.to(self.device, torch.bfloat16).reshape(-1, self.dim // 32, 4, 8)
         self._p5()[rows // 16, :, :, rows % 16, :] = v
 
@@ -136,7 +173,14 @@ class SemanticIndex:
         m = int(vals.shape[0])
         if m == 0:
             return
-        if r0 % 16 == 0 and m % 16 == 0:
+        if self.storage == "q16" and r0 % 16 == 0 and m % 16 == 0:
+            hi, lo, sc, bd = ops.q16_quantize(vals.to(self.device))
+            self.hi[r0 // 16:(r0 + m) // 16].copy_(ops.q16_pack(hi))
+            self.lo[r0 // 16:(r0 + m) // 16].copy_(ops.q16_pack(lo))
+            self.rmeta[r0:r0 + m].copy_(torch.stack([sc, bd], 1))
+        elif self.storage == "q16":
+            self.write_rows(torch.arange(r0, r0 + m, device=self.device), vals)
+        elif r0 % 16 == 0 and m % 16 == 0:
             v = vals.to(self.device, torch.bfloat16).reshape(m // 16, 16, self.dim // 32, 4, 8)
             self.packed[r0 // 16:(r0 + m) // 16].view(m // 16, self.dim // 32, 4, 16, 8).copy_(
                 v.permute(0, 2, 3, 1, 4))
@@ -144,8 +188,11 @@ class SemanticIndex:
             self.write_rows(torch.arange(r0, r0 + m, device=self.device), vals)
 
     def read_rows(self, r0: int, r1: int) -> torch.Tensor:
-        """Row-major copy of rows [r0, r1) as [r1 - r0, dim] bf16."""
+        """Row-major copy of rows [r0, r1) as [r1 - r0, dim] bf16 (q16: the dequantised fp32 rows)."""
         t0, t1 = r0 // 16, (r1 + 15) // 16
+        if self.storage == "q16":
+            v = 256 * ops.q16_unpack(self.hi[t0:t1]).float() + ops.q16_unpack(self.lo[t0:t1]).float()
+            return v[r0 - 16 * t0:r1 - 16 * t0] * self.rmeta[r0:r1, :1]
         blk = self._p5()[t0:t1].permute(0, 3, 1, 2, 4).reshape((t1 - t0) * 16, self.dim)
         return blk[r0 - 16 * t0:r1 - 16 * t0]
 
@@ -259,15 +306,22 @@ class SemanticIndex:
         with self._lock, self._stream_ctx():
             if caller is not None:  # `q` was produced on the caller's stream
                 torch.cuda.current_stream(self.device).wait_stream(caller)
-            qd = torch.nn.functional.normalize(q.to(self.device, torch.float32), dim=1).to(torch.bfloat16)
+            qd = torch.nn.functional.normalize(q.to(self.device, torch.float32), dim=1)
+            if self.storage != "q16":  # q16 quantises the fp32 query itself (16-bit fixed point)
+                qd = qd.to(torch.bfloat16)
             minp = torch.as_tensor(min_priority, dtype=torch.int32).to(self.device)
             qt = torch.as_tensor(qmasks, dtype=torch.int64).to(self.device)
             ev = None
             if self.pass_events is not None and self.device.type == "cuda":
                 ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                 ev[0].record()
-            s, r = ops.cosine_topk(qd, self.packed, self.count, k, self.priority, self.tagbits, self.expiry, minp, qt,
-                                   self.now() if now is None else now - self.epoch, workspace=self._ws)
+            t_now = self.now() if now is None else now - self.epoch
+            if self.storage == "q16":
+                s, r = ops.q16_topk(qd, self.hi, self.lo, self.rmeta, self.count, k, self.priority,
+                                    self.tagbits, self.expiry, minp, qt, t_now, workspace=self._ws, stats=self.stats)
+            else:
+                s, r = ops.cosine_topk(qd, self.packed, self.count, k, self.priority, self.tagbits, self.expiry, minp,
+                                       qt, t_now, workspace=self._ws)
             if ev is not None:
                 ev[1].record()
                 self.pass_events.append(ev)
@@ -323,7 +377,8 @@ class SemanticIndex:
         return st
 
     def memory_bytes(self) -> int:
-        return self.packed.numel() * 2 + self.capacity * (4 + 8 + 4)
+        rows = sum(p.numel() * p.element_size() for _, p in self._planes())
+        return rows + self.capacity * (4 + 8 + 4 + (8 if self.storage == "q16" else 0))
 
     # -- checkpoint / resume (the embedding matrix as per-GPU binary shards
     # next to the JSON metadata; reference item form pilott/memory/enhanced_memory.py:9-21) --
@@ -350,33 +405,41 @@ class SemanticIndex:
         with self._lock:
             n = self.count
             tiles = (n + 15) // 16
-            tile_bytes = self.dim // 32 * 64 * 8 * 2
-            per = max(1, chunk_bytes // tile_bytes)
-            out = np.lib.format.open_memmap(tmp / "packed.npy", mode="w+", dtype=np.uint16,
-                                            shape=(tiles, self.dim // 32, 64, 8))
-            stage = None
-            for t in range(0, tiles, per):
-                m = min(per, tiles - t)
-                src = self.packed[t:t + m].view(torch.int16)
-                if self.device.type == "cuda":
-                    if stage is None:
-                        stage = torch.empty((per,) + tuple(src.shape[1:]), dtype=torch.int16, pin_memory=True)
-                    stage[:m].copy_(src)  # synchronous D2H into pinned memory
-                    out[t:t + m] = stage[:m].numpy().view(np.uint16)
-                else:
-                    out[t:t + m] = src.numpy().view(np.uint16)
-            out.flush()
-            del out
-            for name, ten in (("priority", self.priority), ("tagbits", self.tagbits), ("expiry", self.expiry)):
-                arr = np.lib.format.open_memmap(tmp / f"{name}.npy", mode="w+",
-                                                dtype={"priority": np.int32, "tagbits": np.int64,
-                                                       "expiry": np.float32}[name], shape=(n,))
+            tile_bytes = 0
+            for name, plane in self._planes():  # bf16: packed.npy (uint16); q16: hi.npy / lo.npy (int8)
+                raw = plane.view(torch.int16) if plane.dtype == torch.bfloat16 else plane
+                npdt = np.uint16 if plane.dtype == torch.bfloat16 else np.int8
+                pb = int(np.prod(plane.shape[1:])) * plane.element_size()
+                tile_bytes += pb
+                per = max(1, chunk_bytes // pb)
+                out = np.lib.format.open_memmap(tmp / f"{name}.npy", mode="w+", dtype=npdt,
+                                                shape=(tiles,) + tuple(plane.shape[1:]))
+                stage = None
+                for t in range(0, tiles, per):
+                    m = min(per, tiles - t)
+                    src = raw[t:t + m]
+                    if self.device.type == "cuda":
+                        if stage is None:
+                            stage = torch.empty((per,) + tuple(src.shape[1:]), dtype=raw.dtype, pin_memory=True)
+                        stage[:m].copy_(src)  # synchronous D2H into pinned memory
+                        out[t:t + m] = stage[:m].numpy().view(npdt)
+                    else:
+                        out[t:t + m] = src.numpy().view(npdt)
+                out.flush()
+                del out
+            rowarrs = [("priority", self.priority, np.int32), ("tagbits", self.tagbits, np.int64),
+                       ("expiry", self.expiry, np.float32)]
+            if self.storage == "q16":
+                rowarrs.append(("rmeta", self.rmeta, np.float32))
+            for name, ten, npdt in rowarrs:
+                arr = np.lib.format.open_memmap(tmp / f"{name}.npy", mode="w+", dtype=npdt,
+                                                shape=(n,) + tuple(ten.shape[1:]))
                 rows = max(1, chunk_bytes // 8)
                 for r in range(0, n, rows):
                     arr[r:r + rows] = ten[r:min(n, r + rows)].cpu().numpy()
                 arr.flush()
                 del arr
-            meta = {"version": self.CKPT_VERSION, "dim": self.dim, "count": n, "size": self.size,
+            meta = {"version": self.CKPT_VERSION, "storage": self.storage, "dim": self.dim, "count": n, "size": self.size,
                     "capacity": self.capacity, "epoch": self.epoch, "tags": self.tags.bits,
                     "row_tags": {str(k): sorted(v) for k, v in self.row_tags_py.items()}}
         (tmp / "meta.json").write_text(json.dumps(meta))
@@ -410,27 +473,32 @@ class SemanticIndex:
             raise ValueError(f"index checkpoint is a wrapped ring of capacity {meta['capacity']}: "
                              f"it can only be restored at that capacity, not {cap}")
         idx = cls(dim=dim, capacity=cap, device=device, growable=growable,
-                  max_capacity=max_capacity or max(cap, int(meta["capacity"])))
-        packed = np.load(path / "packed.npy", mmap_mode="r", allow_pickle=False)
-        tiles = packed.shape[0]
-        if tiles != (n + 15) // 16 or packed.shape[1:] != (dim // 32, 64, 8):
-            raise ValueError("index checkpoint packed.npy does not match meta.json")
-        tile_bytes = dim // 32 * 64 * 8 * 2
-        per = max(1, chunk_bytes // tile_bytes)
-        stage = None
-        for t in range(0, tiles, per):
-            m = min(per, tiles - t)
-            host = torch.from_numpy(np.array(packed[t:t + m]).view(np.int16))
-            if idx.device.type == "cuda":
-                if stage is None:
-                    stage = torch.empty((per,) + tuple(host.shape[1:]), dtype=torch.int16, pin_memory=True)
-                stage[:m].copy_(host)
-                idx.packed[t:t + m].view(torch.int16).copy_(stage[:m], non_blocking=False)
-            else:
-                idx.packed[t:t + m].view(torch.int16).copy_(host)
-        for name, ten in (("priority", idx.priority), ("tagbits", idx.tagbits), ("expiry", idx.expiry)):
+                  max_capacity=max_capacity or max(cap, int(meta["capacity"])), storage=meta.get("storage", "bf16"))
+        for name, plane in idx._planes():
             arr = np.load(path / f"{name}.npy", mmap_mode="r", allow_pickle=False)
-            if arr.shape != (n,):
+            tiles = arr.shape[0]
+            if tiles != (n + 15) // 16 or arr.shape[1:] != tuple(plane.shape[1:]):
+                raise ValueError(f"index checkpoint {name}.npy does not match meta.json")
+            raw = plane.view(torch.int16) if plane.dtype == torch.bfloat16 else plane
+            npdt = np.int16 if plane.dtype == torch.bfloat16 else np.int8
+            per = max(1, chunk_bytes // (int(np.prod(plane.shape[1:])) * plane.element_size()))
+            stage = None
+            for t in range(0, tiles, per):
+                m = min(per, tiles - t)
+                host = torch.from_numpy(np.array(arr[t:t + m]).view(npdt))
+                if idx.device.type == "cuda":
+                    if stage is None:
+                        stage = torch.empty((per,) + tuple(host.shape[1:]), dtype=raw.dtype, pin_memory=True)
+                    stage[:m].copy_(host)
+                    raw[t:t + m].copy_(stage[:m], non_blocking=False)
+                else:
+                    raw[t:t + m].copy_(host)
+        rowarrs = [("priority", idx.priority), ("tagbits", idx.tagbits), ("expiry", idx.expiry)]
+        if idx.storage == "q16":
+            rowarrs.append(("rmeta", idx.rmeta))
+        for name, ten in rowarrs:
+            arr = np.load(path / f"{name}.npy", mmap_mode="r", allow_pickle=False)
+            if arr.shape != (n,) + tuple(ten.shape[1:]):
                 raise ValueError(f"index checkpoint {name}.npy has {arr.shape}, expected ({n},)")
             rows = max(1, chunk_bytes // 8)
             for r in range(0, n, rows):

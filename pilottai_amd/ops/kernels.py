@@ -229,6 +229,80 @@ def cosine_topk(queries, index, n_valid: int, K: int, row_priority, row_tags, ro
                            q_min_priority, q_tags, now)
 
 
+# ---- 16-bit fixed-point index (csrc/ops/similarity_q16.hip; memory/semantic_index.py storage="q16")
+Q16_MAX = 32512  # |v| <= 127 * 256: hi = floor((v + 128) / 256) stays in [-127, 127]
+
+
+def q16_quantize(x: torch.Tensor):
+    """Rows of x (any float) -> (hi int8 [n, D], lo int8 [n, D], scale fp32 [n], bound fp32 [n]):
+    v = round(x / scale) = 256 hi + lo exactly (|v| <= Q16_MAX, scale = max|x| / Q16_MAX), and
+    bound = scale * ||lo||_2 (a hair above: the stage-1 error bound's row factor)."""
+    x = x.float()
+    m = x.abs().amax(1)
+    sc = torch.where(m > 0, m / Q16_MAX, torch.ones_like(m))
+    v = torch.round(x / sc[:, None]).clamp_(-Q16_MAX, Q16_MAX)
+    hi = torch.floor((v + 128) / 256)
+    lo = v - 256 * hi
+    bound = (sc.double() * lo.double().norm(dim=1)).float() * (1 + 1e-6)
+    return hi.to(torch.int8), lo.to(torch.int8), sc, bound
+
+
+def q16_pack(plane: torch.Tensor) -> torch.Tensor:
+    """int8 [n = 16 T, D] -> fragment-major tiles [T, D/64, 64, 16]: lane 16 g + c of (t, s) holds
+    row 16 t + c, dims 64 s + 16 g .. + 16 (the v_mfma_i32_16x16x64_i8 operand)."""
+    n, D = plane.shape
+    return plane.reshape(n // 16, 16, D // 64, 4, 16).permute(0, 2, 3, 1, 4).reshape(n // 16, D // 64, 64, 16)
+
+
+def q16_unpack(tiles: torch.Tensor) -> torch.Tensor:
+    T, DS = tiles.shape[0], tiles.shape[1]
+    return tiles.view(T, DS, 4, 16, 16).permute(0, 3, 1, 2, 4).reshape(T * 16, DS * 64)
+
+
+def q16_queries(q: torch.Tensor):
+    """Queries -> (qv int8 [Q, 2, D] = (qh, ql), qmeta fp32 [Q, 2] = (scale, scale * ||v||_2))."""
+    hi, lo, sc, _ = q16_quantize(q)
+    v = 256 * hi.double() + lo.double()
+    cq = (sc.double() * v.norm(dim=1)).float() * (1 + 1e-6)
+    return torch.stack([hi, lo], 1).contiguous(), torch.stack([sc, cq], 1).contiguous()
+
+
+def q16_topk(queries, hi, lo, rmeta, n_valid: int, K: int, row_priority, row_tags, row_expiry,
+             q_min_priority, q_tags, now: float, workspace: Optional[torch.Tensor] = None, exact: bool = False,
+             stats: Optional[dict] = None):
+    """Exact filtered top-k over a q16 index (scores of the 16-bit fixed-point vectors, the
+    same on the GPU and in ops.reference.q16_topk). GPU: the two-stage kernel, hi plane only in
+    the streaming pass; a batch whose drop check fails is re-run with the exact scan (counted
+    in stats["q16_fallbacks"]). queries: fp32 / bf16 [Q, D] (quantised here)."""
+    qv, qm = q16_queries(queries)
+    if _on_gpu(hi):
+        C = require_native()
+        Q = qv.shape[0]
+        out_s = torch.empty(Q, K, dtype=torch.float32, device=hi.device)
+        out_r = torch.empty(Q, K, dtype=torch.int32, device=hi.device)
+        unsafe = torch.zeros(Q, dtype=torch.int32, device=hi.device)
+        qc = min(Q, COSINE_MAX_Q)
+        need = C.q16_topk_workspace_bytes(qc, max(1, int(n_valid)))
+        if workspace is None or workspace.numel() * workspace.element_size() < need:
+            workspace = torch.empty(max(need, 16), dtype=torch.uint8, device=hi.device)
+        for q0 in range(0, Q, COSINE_MAX_Q):
+            q1 = min(Q, q0 + COSINE_MAX_Q)
+            C.q16_topk(out_s[q0:q1], out_r[q0:q1], unsafe[q0:q1], workspace, qv[q0:q1], qm[q0:q1], hi, lo, rmeta,
+                       int(n_valid), int(K), row_priority, row_tags, row_expiry,
+                       q_min_priority[q0:q1].contiguous(), q_tags[q0:q1].contiguous(), float(now), int(exact))
+        if not exact and bool(unsafe.any()):  # a slice refused a row that might be in the top-k
+            if stats is not None:
+                stats["q16_fallbacks"] = stats.get("q16_fallbacks", 0) + 1
+            for q0 in range(0, Q, COSINE_MAX_Q):
+                q1 = min(Q, q0 + COSINE_MAX_Q)
+                C.q16_topk(out_s[q0:q1], out_r[q0:q1], unsafe[q0:q1], workspace, qv[q0:q1], qm[q0:q1], hi, lo,
+                           rmeta, int(n_valid), int(K), row_priority, row_tags, row_expiry,
+                           q_min_priority[q0:q1].contiguous(), q_tags[q0:q1].contiguous(), float(now), 1)
+        return out_s, out_r
+    return ref.q16_topk(qv, qm, hi, lo, rmeta, n_valid, K, row_priority, row_tags, row_expiry,
+                        q_min_priority, q_tags, now)
+
+
 def skinny_gemm(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """y = x @ w.T via the weight-streaming MFMA kernel (csrc/ops/gemm_skinny.hip)."""
     y = out if out is not None else torch.empty(x.shape[0], w.shape[0], dtype=x.dtype, device=x.device)

