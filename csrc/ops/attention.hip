@@ -495,14 +495,28 @@ constexpr int PW_NBUF = 4;     // staged tiles (3 in flight while one is compute
 template <int N>
 __device__ __forceinline__ void att_wait_vm() { __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8)); }
 
+// Split wide items: the scheduler cuts the longest causal items' key range
+// into nparts partitions of whole 32-key tiles (item.z bits 8-19 = part, 20+ = nparts; item.w =
+// the partition's first partial slot, 8 slots = 64 KiB of fp32 per KV head, partitions p0 + 8p).
+// Each partition keeps its unnormalised O accumulators in their 32x32 register layout and the
+// per-column (running max, summed denominator), stores them write-through into the uncached
+// partial slab and takes a ticket; the last partition merges lane by lane (same register layout,
+// no transpose) and runs the normal epilogue -- the decode path's partition hand-off
+// (common.h handoff_last), with its own counter per split item (pf_counters).
+constexpr int PW_PART_SLOTS = 8;
+
 template <int G>
 __device__ __forceinline__ void prefill_item_wg(
     const int4 it, char* smem, bf16* __restrict__ out, const bf16* __restrict__ q,
     const bf16* __restrict__ k_cache, const bf16* __restrict__ v_cache,
     const int* __restrict__ q_start, const int* __restrict__ q_len, const int* __restrict__ ctx_len,
-    const int* __restrict__ block_table, int max_blocks, int H, int KV, int kvh, float scale_log2) {
+    const int* __restrict__ block_table, int max_blocks, int H, int KV, int kvh, float scale_log2,
+    float* __restrict__ part_o, float* __restrict__ part_ml, int* __restrict__ pf_counters, int acq) {
   constexpr int TPWV = 32 / G;  // tokens per wave
   const int s = it.x, qb = it.y, nq = it.z & 0xff;
+  // without ticket room (pf_counters null) a split item computes its whole key range
+  const int part = pf_counters ? (it.z >> 8) & 0xfff : 0, nparts = pf_counters ? max(1, it.z >> 20) : 1;
+  const int pidx = it.w;
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int r = lane & 31, h = lane >> 5;
@@ -513,7 +527,10 @@ __device__ __forceinline__ void prefill_item_wg(
   const int key_limit = colvalid ? (ctx - ql + tok + 1) : 0;
   const int head = kvh * G + hg;
   const int wave_keys = wid * TPWV < nq ? ctx - ql + qb + min(nq, (wid + 1) * TPWV) : 0;  // wave's causal end
-  const int ntiles = (ctx - ql + qb + nq + 31) >> 5;
+  const int ntiles_all = (ctx - ql + qb + nq + 31) >> 5;
+  const int tpp = (ntiles_all + nparts - 1) / nparts;  // this partition: tiles [t_begin, t_begin + ntiles)
+  const int t_begin = min(ntiles_all, part * tpp);
+  const int ntiles = min(ntiles_all, t_begin + tpp) - t_begin;
   const int kmin = ctx - ql + qb + wid * TPWV + 1;  // smallest causal end of the wave's columns
 
   bf16x8 qf[8];
@@ -560,17 +577,18 @@ __device__ __forceinline__ void prefill_item_wg(
   // to wait out: the 2048-token case ran at 0.3 PFLOP/s).
 #pragma unroll
   for (int p = 0; p < PW_NBUF - 1; ++p)
-    if (p < ntiles) stage(p, p);
-  for (int t = 0; t < ntiles; ++t) {
-    const int buf = t % PW_NBUF;
-    const int after = min(PW_NBUF - 2, ntiles - 1 - t);  // tiles issued after t, still in flight
+    if (p < ntiles) stage(t_begin + p, p);
+  for (int u = 0; u < ntiles; ++u) {
+    const int t = t_begin + u;
+    const int buf = u % PW_NBUF;
+    const int after = min(PW_NBUF - 2, ntiles - 1 - u);  // tiles issued after t, still in flight
     if (after >= 2) att_wait_vm<8>();  // this wave's pieces of tile t have landed ...
     else if (after == 1) att_wait_vm<4>();
     else att_wait_vm<0>();
     asm volatile("" ::: "memory");
     __builtin_amdgcn_s_barrier();  // ... and everyone's; every wave is also done with tile t-1
     asm volatile("" ::: "memory");
-    if (t + PW_NBUF - 1 < ntiles) stage(t + PW_NBUF - 1, (t + PW_NBUF - 1) % PW_NBUF);  // tile t-1's buffer
+    if (u + PW_NBUF - 1 < ntiles) stage(t + PW_NBUF - 1, (u + PW_NBUF - 1) % PW_NBUF);  // tile t-1's buffer
     if (32 * t >= wave_keys) continue;  // wave-uniform: beyond this wave's causal end
     const char* tb = smem + buf * PW_TILE;
     // K rows: dims 16i + 8h = chunk 2i + h; key krow & 15 of page krow >> 4
@@ -589,6 +607,64 @@ __device__ __forceinline__ void prefill_item_wg(
     softmax_pv_tile(sc, 32 * t + 32 > kmin, 32 * t + 8 * h, key_limit, scale_log2, m_run, l_run, o, vf);
   }
   l_run += __shfl_xor(l_run, 32, 64);
+  if (nparts > 1) {
+    // ---- partition hand-off: slab chunk j = 2 wid + (m >> 1) of the partition's 8 slots holds
+    // registers o[m] of the wave's 64 lanes; (m, l) of column 32 wid + r in slot (32 wid + r) / 16
+    const int p0 = pidx - PW_PART_SLOTS * part;
+    auto chunk = [&](int slot0, int j) { return part_o + ((size_t)(slot0 + j) * KV + kvh) * 16 * ATT_HD; };
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const __amdgpu_buffer_rsrc_t ps = __builtin_amdgcn_make_buffer_rsrc(chunk(pidx, 2 * wid + (m >> 1)), 0,
+                                                                          16 * ATT_HD * 4, 0x00020000);
+#pragma unroll
+      for (int c4 = 0; c4 < 4; ++c4)
+        __builtin_amdgcn_raw_buffer_store_b128(
+            __builtin_bit_cast(u32x4, f32x4{o[m][4 * c4], o[m][4 * c4 + 1], o[m][4 * c4 + 2], o[m][4 * c4 + 3]}), ps,
+            ((((m & 1) * 64 + lane) * 16) + 4 * c4) * 4, 0, 16);
+    }
+    const int pcol = 32 * wid + r;
+    if (h == 0) {
+      const unsigned long long mlv =
+          ((unsigned long long)__float_as_uint(l_run) << 32) | (unsigned long long)__float_as_uint(m_run);
+      __hip_atomic_store((gu64*)(part_ml + ((size_t)(pidx + pcol / 16) * KV + kvh) * 32 + (pcol % 16) * 2), mlv,
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    int* lflag = reinterpret_cast<int*>(smem + PW_NBUF * PW_TILE);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (!handoff_last(pf_counters + (size_t)p0 * KV + kvh, nparts, lflag, acq)) return;
+    // ---- the last partition: merge every partition lane by lane (sc1 loads, after the acquire)
+    float gm = NEG_BIG;
+    for (int p = 0; p < nparts; ++p) {
+      const unsigned long long v = __hip_atomic_load(
+          (gu64*)(part_ml + ((size_t)(p0 + PW_PART_SLOTS * p + pcol / 16) * KV + kvh) * 32 + (pcol % 16) * 2),
+          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      gm = fmaxf(gm, __uint_as_float((unsigned)v));
+    }
+    float GL = 0.f;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) o[m] = f32x16{};
+    for (int p = 0; p < nparts; ++p) {
+      const int sp = p0 + PW_PART_SLOTS * p;
+      const unsigned long long v = __hip_atomic_load(
+          (gu64*)(part_ml + ((size_t)(sp + pcol / 16) * KV + kvh) * 32 + (pcol % 16) * 2), __ATOMIC_RELAXED,
+          __HIP_MEMORY_SCOPE_AGENT);
+      const float w = __builtin_amdgcn_exp2f(__uint_as_float((unsigned)v) - gm);
+      GL += w * __uint_as_float((unsigned)(v >> 32));
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(chunk(sp, 2 * wid + (m >> 1)), 0,
+                                                                            16 * ATT_HD * 4, 0x00020000);
+#pragma unroll
+        for (int c4 = 0; c4 < 4; ++c4) {
+          const f32x4 a = __builtin_bit_cast(
+              f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, ((((m & 1) * 64 + lane) * 16) + 4 * c4) * 4, 0, 16));
+#pragma unroll
+          for (int e = 0; e < 4; ++e) o[m][4 * c4 + e] += w * a[e];
+        }
+      }
+    }
+    l_run = GL;
+  }
   const float inv = l_run > 0.f ? 1.f / l_run : 0.f;
 
   // transpose O^T through LDS (the tile buffers are free once every wave passed here):
@@ -623,14 +699,15 @@ __device__ __forceinline__ void prefill_any(
     const int4 it, char* smem, bf16* __restrict__ out, const bf16* __restrict__ q,
     const bf16* __restrict__ k_cache, const bf16* __restrict__ v_cache,
     const int* __restrict__ q_start, const int* __restrict__ q_len, const int* __restrict__ ctx_len,
-    const int* __restrict__ block_table, int max_blocks, int H, int KV, int kvh, float scale_log2) {
+    const int* __restrict__ block_table, int max_blocks, int H, int KV, int kvh, float scale_log2,
+    float* __restrict__ part_o, float* __restrict__ part_ml, int* __restrict__ pf_counters, int acq) {
   const int nq = it.z & 0xff;
   if (nq <= 32 / G) {
     prefill_item<G, NW>(it, smem, out, q, k_cache, v_cache, q_start, q_len, ctx_len, block_table, max_blocks,
                             H, KV, kvh, scale_log2);
   } else if constexpr (NW == 4) {
     prefill_item_wg<G>(it, smem, out, q, k_cache, v_cache, q_start, q_len, ctx_len, block_table, max_blocks, H, KV,
-                       kvh, scale_log2);
+                       kvh, scale_log2, part_o, part_ml, pf_counters, acq);
   } else {
     for (int sb = 0; sb < nq; sb += 32 / G) {
       const int4 sub = {it.x, it.y + sb, min(32 / G, nq - sb) | (it.z & ~0xff), it.w};
@@ -646,7 +723,8 @@ constexpr int ATT_LDS_DECODE = ATT_LDS_DECODE_BYTES + 16;  // + last-arriver fla
 constexpr int ATT_LDS_BYTES8 = std::max(att_lds_decode_bytes<8>() + 16, (8 * 32 * PF_LD + 2 * 8 * 32) * 4);
 constexpr int ATT_LDS_PREFILL = (4 * 32 * PF_LD + 2 * 4 * 32) * 4;
 constexpr int ATT_LDS_BYTES0 = ATT_LDS_PREFILL > ATT_LDS_DECODE ? ATT_LDS_PREFILL : ATT_LDS_DECODE;
-constexpr int ATT_LDS_BYTES = ATT_LDS_BYTES0 > PW_NBUF * PW_TILE ? ATT_LDS_BYTES0 : PW_NBUF * PW_TILE;
+constexpr int ATT_LDS_BYTES0W = ATT_LDS_BYTES0 > PW_NBUF * PW_TILE + 16 ? ATT_LDS_BYTES0 : PW_NBUF * PW_TILE + 16;
+constexpr int ATT_LDS_BYTES = ATT_LDS_BYTES0W;  // + the split items' last-arriver flag after the tiles
 
 // One launch serves a whole ragged step: items (seq, q_begin, nq | part<<8 |
 // nparts<<20, partial slot) are strided over the grid, so the shape-stable
@@ -661,7 +739,8 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void paged_attn_kernel(
     const bf16* __restrict__ v_cache, const int4* __restrict__ items,
     const int* __restrict__ n_items, const int* __restrict__ part_size, const int* __restrict__ q_start,
     const int* __restrict__ q_len, const int* __restrict__ ctx_len,
-    const int* __restrict__ block_table, int max_blocks, int H, int KV, float scale_log2, int acq) {
+    const int* __restrict__ block_table, int max_blocks, int H, int KV, float scale_log2, int acq,
+    int* __restrict__ pf_counters) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int TPW = 16 / G;
   const int psz_q = part_size ? part_size[0] : ATT_PART;
@@ -692,7 +771,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void paged_attn_kernel(
                          block_table, max_blocks, H, KV, kvh, scale_log2, psz, acq);
     else
       prefill_any<G, NW>(it, smem, out, q, k_cache, v_cache, q_start, q_len, ctx_len, block_table, max_blocks, H,
-                         KV, kvh, scale_log2);
+                         KV, kvh, scale_log2, part_o, part_ml, pf_counters, acq);
     __syncthreads();  // LDS reuse by the next item
   }
 }
@@ -703,7 +782,8 @@ extern "C" int pa_paged_attention(void* out, float* part_o, float* part_ml, cons
                                   const void* k_cache, const void* v_cache, const int* items,
                                   const int* n_items, int max_items, const int* part_size, int* counters,
                                   const int* q_start, const int* q_len, const int* ctx_len, const int* block_table,
-                                  int max_blocks, int H, int KV, float scale_log2, int waves, hipStream_t st) {
+                                  int max_blocks, int H, int KV, float scale_log2, int waves, int* pf_counters,
+                                  hipStream_t st) {
   if (H % KV != 0) return -1;
   if (waves != 4 && waves != 8) return -1;
   const int G = H / KV;
@@ -724,7 +804,7 @@ extern "C" int pa_paged_attention(void* out, float* part_o, float* part_ml, cons
                          (pa::bf16*)out, part_o, part_ml, counters, (const pa::bf16*)q,         \
                          (const pa::bf16*)k_cache, (const pa::bf16*)v_cache, (const int4*)items, \
                          n_items, part_size, q_start, q_len, ctx_len, block_table, max_blocks, H, \
-                         KV, scale_log2, pa::g_handoff_attn);                                   \
+                         KV, scale_log2, pa::g_handoff_attn, pf_counters);                      \
       break;                                                                                    \
     }                                                                                           \
     static bool attr4 = false;                                                                  \
@@ -737,7 +817,7 @@ extern "C" int pa_paged_attention(void* out, float* part_o, float* part_ml, cons
                        (pa::bf16*)out, part_o, part_ml, counters, (const pa::bf16*)q,           \
                        (const pa::bf16*)k_cache, (const pa::bf16*)v_cache, (const int4*)items,   \
                        n_items, part_size, q_start, q_len, ctx_len, block_table, max_blocks, H,  \
-                       KV, scale_log2, pa::g_handoff_attn);                                     \
+                       KV, scale_log2, pa::g_handoff_attn, pf_counters);                        \
   } while (0)
   switch (G) {
     case 1: PA_ATT(1); break;

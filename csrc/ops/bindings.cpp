@@ -18,7 +18,8 @@ int pa_paged_attention(void* out, float* part_o, float* part_ml, const void* q, 
                        const void* v_cache, const int* items, const int* n_items, int max_items,
                        const int* part_size, int* counters, const int* q_start,
                        const int* q_len, const int* ctx_len, const int* block_table,
-                       int max_blocks, int H, int KV, float scale_log2, int waves, hipStream_t st);
+                       int max_blocks, int H, int KV, float scale_log2, int waves, int* pf_counters,
+                       hipStream_t st);
 int pa_sample_workspace_floats(int rows, int V);
 int pa_patch_pending_ids(int* ids, const int* sampled, int T, int n_sampled, hipStream_t st);
 int pa_sample(int* out_tokens, float* out_keys, float* workspace, const void* logits, int rows,
@@ -197,6 +198,12 @@ void paged_attention(at::Tensor out, at::Tensor part_o, at::Tensor part_ml, at::
   TORCH_CHECK(part_ml.numel() >= (int64_t)max_items * KV * 16 * 2, "part_ml workspace too small");
   TORCH_CHECK(counters.numel() >= block_table.size(0) * KV,
               "counters must hold one zero-initialised int per (sequence, KV head)");
+  // split prefill items (attention.hip prefill_item_wg) take their tickets after the per-sequence
+  // counters: one per (partial slot, KV head); without that room a split item computes its whole
+  // key range (correct, only slower)
+  int* pf_counters = counters.numel() >= (block_table.size(0) + (int64_t)max_items) * KV
+                         ? counters.data_ptr<int>() + block_table.size(0) * KV
+                         : nullptr;
   const float scale_log2 = (float)(scale * 1.4426950408889634);
   check_rc(pa_paged_attention(out.data_ptr(), part_o.data_ptr<float>(), part_ml.data_ptr<float>(),
                               q.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(),
@@ -205,7 +212,7 @@ void paged_attention(at::Tensor out, at::Tensor part_o, at::Tensor part_ml, at::
                               counters.data_ptr<int>(),
                               q_start.data_ptr<int>(), q_len.data_ptr<int>(),
                               ctx_len.data_ptr<int>(), block_table.data_ptr<int>(),
-                              block_table.size(1), H, KV, scale_log2, (int)waves, cur_stream()),
+                              block_table.size(1), H, KV, scale_log2, (int)waves, pf_counters, cur_stream()),
            "paged_attention");
 }
 

@@ -154,6 +154,7 @@ PYBIND11_MODULE(_runtime, m) {
         if (d.contains("gqa_group")) c.gqa_group = d["gqa_group"].cast<int32_t>();
         if (d.contains("att_qcols")) c.att_qcols = d["att_qcols"].cast<int32_t>();
         if (d.contains("att_wide_min_tokens")) c.att_wide_min_tokens = d["att_wide_min_tokens"].cast<int32_t>();
+        if (d.contains("prefill_split_keys")) c.prefill_split_keys = d["prefill_split_keys"].cast<int32_t>();
         if (d.contains("prefix_caching")) c.prefix_caching = d["prefix_caching"].cast<bool>();
         if (d.contains("dedup_inflight_prefix")) c.dedup_inflight_prefix = d["dedup_inflight_prefix"].cast<bool>();
         if (d.contains("max_prefix_defer")) c.max_prefix_defer = d["max_prefix_defer"].cast<int32_t>();

@@ -417,11 +417,6 @@ int32_t Scheduler::schedule(int32_t* buf) {
       pre.push_back({c0 + qb + nq, (int32_t)si, qb, nq | (1 << 20), 0});
     }
   }
-  std::stable_sort(pre.begin(), pre.end(), [](const ItemCost& x, const ItemCost& y) { return x.keys > y.keys; });
-  for (const ItemCost& c : pre) {
-    int32_t* it = items + 4 * nit++;
-    it[0] = c.a; it[1] = c.b; it[2] = c.c; it[3] = c.d;
-  }
   const int64_t plan_id = next_plan_id_;
   for (size_t pi = 0; pi < last_plan_.size(); ++pi) {
     Planned& p = last_plan_[pi];
@@ -484,6 +479,35 @@ int32_t Scheduler::schedule(int32_t* buf) {
     }
     T += n;
     ++ns;
+  }
+  // split the longest wide prefill items (prefill_split_keys; slots after the decode partitions'
+  // -- 8 partial slots per partition -- within the part_o / part_ml workspace of max_items slots)
+  int32_t t_step_all = 0;
+  for (const Planned& p : last_plan_) t_step_all += p.n;
+  const int32_t G = std::max(1, cfg_.gqa_group);
+  if (cfg_.prefill_split_keys > 0 && qtile * G > 32 && t_step_all > cfg_.small_step_tokens) {
+    std::vector<ItemCost> split;
+    int64_t n_items_total = (int64_t)pre.size() + (int64_t)dec.size();
+    for (const ItemCost& c : pre) {
+      const int32_t nq = c.c & 0xff;
+      int32_t np = std::min<int32_t>(4, c.keys / cfg_.prefill_split_keys);
+      if (nq > 32 / G && np >= 2 && pslot + 8 * np <= L.max_items && n_items_total + np - 1 <= L.max_items) {
+        const int32_t tiles = (c.keys + 31) / 32;
+        const int32_t per = ((tiles + np - 1) / np) * 32;
+        for (int32_t q = 0; q < np; ++q)
+          split.push_back({per, c.a, c.b, nq | (q << 8) | (np << 20), pslot + 8 * q});
+        pslot += 8 * np;
+        n_items_total += np - 1;
+      } else {
+        split.push_back(c);
+      }
+    }
+    pre.swap(split);
+  }
+  std::stable_sort(pre.begin(), pre.end(), [](const ItemCost& x, const ItemCost& y) { return x.keys > y.keys; });
+  for (const ItemCost& c : pre) {
+    int32_t* it = items + 4 * nit++;
+    it[0] = c.a; it[1] = c.b; it[2] = c.c; it[3] = c.d;
   }
   std::stable_sort(dec.begin(), dec.end(), [](const ItemCost& x, const ItemCost& y) { return x.keys > y.keys; });
   for (const ItemCost& c : dec) {

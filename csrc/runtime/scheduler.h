@@ -34,7 +34,12 @@ struct SchedulerConfig {
   int32_t gqa_group = 4;               // query heads per KV head (attention work items)
   int32_t att_qcols = 128;             // MFMA columns (heads x tokens) per prefill attention item:
                                        // 128 = the LDS-staged 4-wave path, 32 = one wave per item
-  int32_t att_wide_min_tokens = 2048;  // ... used only when the step's prefill tokens reach this
+  int32_t att_wide_min_tokens = 2048;
+  // wide prefill items whose causal key range reaches this many keys are cut into
+  // min(4, keys / prefill_split_keys) partitions of whole 32-key tiles, merged in-kernel by the
+  // last partition (attention.hip prefill_item_wg): the longest causal item stops being the
+  // step's critical path. 0 = off. Not on decode-sized (8-wave) steps.
+  int32_t prefill_split_keys = 1024;  // ... used only when the step's prefill tokens reach this
                                        // (fewer, 4x wider items underfill the chip below it)
   bool prefix_caching = true;
   // A request whose first two blocks are being prefilled right now by another sequence

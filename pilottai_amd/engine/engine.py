@@ -119,6 +119,9 @@ class EngineConfig:
     # ... used only for steps with at least this many prefill tokens (1,024: 1,024-2,048-token steps
     # 1-2 % faster than with 2,048, which most mixed steps never reached; profiles/r2_att_wide_min_ab.jsonl)
     att_wide_min_tokens: int = 1024
+    # wide prefill items of at least this many causal keys are split into partitions merged
+    # in-kernel (scheduler.h prefill_split_keys); 0 = off
+    prefill_split_keys: int = int(os.environ.get("PILOTTAI_PREFILL_SPLIT_KEYS", "1024"))
     # attention workgroup width on decode-sized steps (<= the model's DECODE_FUSED_MAX_T
     # tokens): 8 waves stream a whole context per workgroup (the scheduler then skips the
     # flash-decoding split for such steps when they have few rows); None = model default
@@ -281,6 +284,7 @@ class LLMEngine:
             "gqa_group": self.model.h_local // self.model.kv_local,
             "att_qcols": cfg.att_qcols,
             "att_wide_min_tokens": cfg.att_wide_min_tokens,
+            "prefill_split_keys": cfg.prefill_split_keys,
             "prefix_caching": cfg.prefix_caching, "split_decode": cfg.split_decode,
             "dedup_inflight_prefix": cfg.dedup_inflight_prefix,
             "embed_first": bool(cfg.embed_first),
@@ -303,7 +307,10 @@ class LLMEngine:
         self._host_np = self._host_meta.numpy()
         self._dev_meta = torch.zeros(L["total"], dtype=torch.int32, device=self.device) \
             if (self.on_gpu or self._async) else self._host_meta
-        self._att_counters = torch.zeros(L["max_seqs"] * kv_local, dtype=torch.int32, device=self.device)
+        # attention tickets: one per (sequence, KV head) for split decode rows, then one per
+        # (partial slot, KV head) for split prefill items (csrc/ops/attention.hip prefill_item_wg)
+        self._att_counters = torch.zeros((L["max_seqs"] + L["max_items"]) * kv_local, dtype=torch.int32,
+                                         device=self.device)
         self._init_views()
         V = mc.vocab_size
         self._mask_words = (V + 31) // 32

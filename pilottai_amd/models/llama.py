@@ -321,7 +321,10 @@ class LlamaModel:
                 for k in DENSE_KINDS:
                     del L[k]
         self.lm_head_p = ops.pack_decode_weight(self.lm_head)
-        if not self.keep_dense and self.lm_head is not self.embed:
+        # the row-major LM head goes too when the prefill kernels take its shard (N % 256 == 0:
+        # the vocabulary at TP = 1 / 8B and 70B); a TP shard of another width (128,256 / 8 =
+        # 16,032) keeps it for the library GEMM of > 32-row steps (0.26 GB at 70B TP = 8)
+        if not self.keep_dense and self.lm_head is not self.embed and self.lm_head.shape[0] % 256 == 0:
             self.lm_head = None
         if self.device.type == "cuda":
             ops.decode_workspace(self.device)  # split-K slabs + tickets, before any graph capture

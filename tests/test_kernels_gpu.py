@@ -70,7 +70,7 @@ def test_rope_cache(gpu):
 
 
 def _run_attention(gpu, H, KV, q_lens, ctx_lens, seed=0, split=True, part=512, qcols=128, pad=1,
-                   launches=1, waves=4):
+                   launches=1, waves=4, split_keys=0):
     torch.manual_seed(seed)
     G = H // KV
     blk = 16
@@ -89,9 +89,10 @@ def _run_attention(gpu, H, KV, q_lens, ctx_lens, seed=0, split=True, part=512, q
     T = int(sum(q_lens))
     q = _bf(T, H, 128, dev=gpu)
     items, nslots = ops.build_attention_items(q_lens, ctx_lens, G, split=split, part=part,
-                                               qcols=qcols, wide_min_tokens=0)
-    it = torch.tensor(items + [(0, 0, 0, 0)] * pad, dtype=torch.int32, device=gpu)
-    cnt = torch.zeros(ns * KV, dtype=torch.int32, device=gpu)
+                                               qcols=qcols, wide_min_tokens=0, split_keys=split_keys)
+    it = torch.tensor(items + [(0, 0, 0, 0)] * max(pad, nslots - len(items)), dtype=torch.int32, device=gpu)
+    # per-(sequence, KV head) tickets, then per-(partial slot, KV head) ones for split prefill items
+    cnt = torch.zeros((ns + it.shape[0]) * KV, dtype=torch.int32, device=gpu)
     n_it = torch.tensor([len(items)], dtype=torch.int32, device=gpu)
     maxit = it.shape[0]
     part_o = torch.empty(maxit * KV * 16 * 128, dtype=torch.float32, device=gpu)
@@ -124,6 +125,21 @@ def test_attention_prefill_and_mixed(gpu, H, KV, qcols):
     q_lens = [37, 1, 100, 3, 16, 5, 250, 129, 33]
     ctx = [37, 700, 164, 40, 16, 1029, 260, 1000, 2100]
     o, r = _run_attention(gpu, H, KV, q_lens, ctx, seed=5, qcols=qcols)
+    torch.testing.assert_close(o, r, atol=2e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("split_keys", [512, 1024])
+@pytest.mark.parametrize("H,KV", [(32, 8), (64, 8), (8, 1)])
+def test_attention_prefill_split_items(gpu, H, KV, split_keys):
+    """the longest wide prefill items cut into 2-4 key partitions, merged
+    in-kernel by the last partition (register-layout partials through the uncached slab),
+    beside unsplit items and split decode rows; twice, so the tickets reset themselves."""
+    q_lens = [2048, 1100, 300, 1, 700, 3]
+    ctx = [2048, 1100, 1500, 900, 2600, 4000]
+    G = H // KV
+    items, _ = ops.build_attention_items(q_lens, ctx, G, qcols=128, wide_min_tokens=0, split_keys=split_keys)
+    assert any((z >> 20) > 1 and (z & 0xFF) > 32 // G for _, _, z, _ in items), "no split prefill item"
+    o, r = _run_attention(gpu, H, KV, q_lens, ctx, seed=13, split_keys=split_keys, launches=2)
     torch.testing.assert_close(o, r, atol=2e-2, rtol=2e-2)
 
 

@@ -757,6 +757,34 @@ def test_scheduler_lists_attention_items_heaviest_first():
     assert T == int(ql.sum())
 
 
+def test_scheduler_splits_long_prefill_items():
+    """prefill_split_keys (scheduler.h): wide prefill items of >= 2 x split_keys causal keys
+    become 2-4 tile partitions with 8 partial slots each after the decode partitions' slots;
+    the ops.attn_meta mirror builds the same list."""
+    cfg = {"num_blocks": 4096, "block_size": 16, "max_num_seqs": 16, "max_num_batched_tokens": 4096,
+           "max_prefill_tokens": 4096, "max_model_len": 8192, "gqa_group": 4, "kv_heads": 8,
+           "att_wide_min_tokens": 1024, "prefill_split_keys": 512, "eos_ids": [128009]}
+    s = _runtime.Scheduler(cfg)
+    L = s.layout()
+    buf = np.zeros(L["total"], dtype=np.int32)
+    rng = np.random.default_rng(5)
+    s.add_request(1, list(rng.integers(1000, 9000, 2100)), 0.0, 5, 1, True, [], None)
+    s.add_request(2, list(rng.integers(1000, 9000, 900)), 0.0, 5, 2, True, [], None)
+    T = s.schedule(buf.ctypes.data)
+    c = buf[L["counts"]:L["counts"] + 8]
+    items = buf[L["items"]:L["items"] + 4 * c[3]].reshape(-1, 4)
+    ql, cl = buf[L["q_len"]:L["q_len"] + c[1]], buf[L["ctx_len"]:L["ctx_len"] + c[1]]
+    nparts = items[:, 2] >> 20
+    assert (nparts > 1).any() and int(nparts.max()) == 4
+    split = items[nparts > 1]
+    assert len(set(int(x) for x in split[:, 3])) == len(split)  # every partition its own slot base
+    assert int(c[5]) == 8 * len(split)  # partial slots used
+    ref_items, nslots = build_attention_items(list(ql), list(cl), 4, qcols=128, wide_min_tokens=1024,
+                                              split_keys=512, max_items=L["max_items"])
+    assert [tuple(int(v) for v in x) for x in items] == ref_items and nslots == int(c[5])
+    assert T == int(ql.sum())
+
+
 @pytest.mark.parametrize("rows", [16, 64])
 def test_scheduler_decode_part_target_one_balanced_round(rows):
     """decode_part_target (csrc/runtime/scheduler.cpp): a mid / large step sizes its decode
