@@ -526,6 +526,45 @@ def build_memory(a, device, rank: int = 0, world: int = 1, node: bool = False):
     return mem, MemoryLookupBatcher(mem, min_batch=a.memory_min_batch, max_wait_s=a.memory_wait_ms / 1000.0)
 
 
+def tp_selftest(tp, device, reps: int = 20) -> dict:
+    """Start-up check of a TP group's all-reduce (bench --tp): a correctness round trip (every
+    rank contributes rank-dependent values, the sum is known in closed form) and the measured
+    latency of the two message sizes the cost model needs -- a 64-row decode step's o / down
+    output (64 x 4,096 bf16) and a 2,048-token step's (2,048 x 4,096) -- in microseconds, max
+    over the group. Collective over the TP group (all its ranks call it)."""
+    import torch
+
+    out = {"tp": tp.size, "transport": "custom-p2p" if tp.custom is not None else "process-group"}
+    rows = (64, 2048)
+    for n in rows:
+        t = torch.full((n, 4096), float(tp.rank + 1), dtype=torch.bfloat16, device=device)
+        tp.all_reduce(t)
+        want = tp.size * (tp.size + 1) / 2
+        ok = bool((t.float() == want).all())
+        times = []
+        for _ in range(reps):
+            if device.type == "cuda":
+                torch.cuda.synchronize(device)
+            t0 = time.perf_counter()
+            tp.all_reduce(t)
+            if device.type == "cuda":
+                torch.cuda.synchronize(device)
+            times.append(time.perf_counter() - t0)
+        times.sort()
+        out[f"ok_{n}x4096"] = ok
+        out[f"us_{n}x4096"] = round(1e6 * times[len(times) // 2], 1)
+    import torch.distributed as dist
+
+    if tp.size > 1 and dist.is_initialized():  # the group's worst rank
+        v = torch.tensor([out[f"us_{n}x4096"] for n in rows] + [0.0 if all(out[f"ok_{n}x4096"] for n in rows)
+                                                               else 1.0], dtype=torch.float64)
+        dist.all_reduce(v, op=dist.ReduceOp.MAX, group=tp.cpu_group)
+        for i, n in enumerate(rows):
+            out[f"us_{n}x4096"] = float(v[i])
+        out["ok"] = v[-1].item() == 0.0
+    return out
+
+
 def _launch_ranks(n: int) -> int:
     """`bench.py --gpus N` (N > 1) started without a launcher: run N rank processes under
     torch.distributed.run as a CHILD process (nothing here has touched the GPU; never exec)
@@ -572,6 +611,9 @@ def main():
         # hop apart); the custom P2P all-reduce also in the share-GPU rehearsal (gloo groups)
         tp = comm.new_tp_groups(a.tp, custom_ar=True if a.share_gpu else None)
         dp_group = comm.new_dp_group(a.tp)
+        a._tp_selftest = tp_selftest(tp, device)
+        if not a._tp_selftest.get("ok", True):
+            raise SystemExit(f"TP all-reduce self-test failed: {a._tp_selftest}")
     res = asyncio.run(run_rank(a, rank, world, device, tp=tp, dp_group=dp_group))
     everyone = [res]
     if world > 1:
@@ -675,6 +717,8 @@ def main():
                             rows_total=sum(g.get("mem_rows", 0) for g in gathered))
                        if gathered[0]["memory"] else None),
             "node_load": gathered[0]["node_load"],
+            # bench --tp: the start-up all-reduce check and latencies (BENCHMARKS.md, DP x TP cost model)
+            "tp_selftest": getattr(a, "_tp_selftest", None),
             "notes": "BASELINE.md publishes no number for this config (vs_baseline null); the reference's "
                      "structural bound with a remote LLM is ~0.8 tasks/s per LLMHandler (BASELINE.md §2).",
         }

@@ -129,3 +129,5 @@ def test_bench_agent_dp_over_tp_groups(tmp_path):
     assert d["config"]["managers"] == 1 and d["tasks"] >= 4
     assert len(d["llm_calls_per_rank"]) == 2 and all(c > 0 for c in d["llm_calls_per_rank"])
     assert d["world_size"] == 4 and d["devices"] == ["cpu"] * 4
+    st = d["tp_selftest"]  # the start-up all-reduce round trip of the TP groups
+    assert st["ok"] and st["tp"] == 2 and st["us_64x4096"] > 0 and st["us_2048x4096"] > 0

@@ -23,7 +23,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from pilottai_amd import ops  # noqa: E402
 
 
-def setup(q_lens, ctx_lens, H=32, KV=8, pad_items=0, dev="cuda", part=512, qcols=128):
+def setup(q_lens, ctx_lens, H=32, KV=8, pad_items=0, dev="cuda", part=512, qcols=128, split_keys=0):
     G = H // KV
     blk = 16
     ns = len(q_lens)
@@ -41,11 +41,12 @@ def setup(q_lens, ctx_lens, H=32, KV=8, pad_items=0, dev="cuda", part=512, qcols
     q_start = np.concatenate([[0], np.cumsum(q_lens)[:-1]]).astype(np.int32)
     T = int(sum(q_lens))
     q = (torch.randn(T, H, 128, device=dev) * 0.5).to(torch.bfloat16)
-    items, _ = ops.build_attention_items(q_lens, ctx_lens, G, part=part, qcols=qcols, wide_min_tokens=0)
+    items, nslots = ops.build_attention_items(q_lens, ctx_lens, G, part=part, qcols=qcols, wide_min_tokens=0,
+                                              split_keys=split_keys)
     n_items = len(items)
-    items = items + [(0, 0, 0, 0)] * max(1, pad_items - len(items))
+    items = items + [(0, 0, 0, 0)] * max(1, pad_items - len(items), nslots - len(items))
     it = torch.tensor(items, dtype=torch.int32, device=dev)
-    cnt = torch.zeros(ns * KV, dtype=torch.int32, device=dev)
+    cnt = torch.zeros((ns + it.shape[0]) * KV, dtype=torch.int32, device=dev)
     di = lambda a: torch.tensor(a, dtype=torch.int32, device=dev)  # noqa: E731
     n_it = di([n_items])
     part_o = torch.empty(it.shape[0] * KV * 16 * 128, dtype=torch.float32, device=dev)
@@ -80,6 +81,7 @@ def main():
     ap.add_argument("--cases", default="", help="comma-separated subset of the step cases")
     ap.add_argument("--qcols", default="32,128", help="prefill item widths to time")
     ap.add_argument("--waves", default="4", help="waves per workgroup to time (4, 8), comma-separated")
+    ap.add_argument("--split-keys", default="0", help="prefill item split thresholds to time (0 = off), comma-separated")
     a = ap.parse_args()
     torch.manual_seed(0)
     cases = {
@@ -112,12 +114,14 @@ def main():
         cases = {k: v for k, v in cases.items() if k in a.cases.split(",")}
     for name, (ql, cl) in cases.items():
         for qcols in [int(x) for x in a.qcols.split(",")]:
-            for pad in ((0,) if a.scan else (0, a.pad)):
-                args, kvb, fl, n = setup(ql, cl, pad_items=pad, qcols=qcols)
-                us = timeit(args, a.iters)
-                print(json.dumps({"case": name, "qcols": qcols, "items": n, "grid_items": args[6].shape[0],
-                                  "us": round(us, 1), "kv_TBps": round(kvb / us / 1e6, 2),
-                                  "TFLOPs": round(fl / us / 1e6, 1)}), flush=True)
+            for sk in [int(x) for x in a.split_keys.split(",")]:
+                for pad in ((0,) if a.scan else (0, a.pad)):
+                    args, kvb, fl, n = setup(ql, cl, pad_items=pad, qcols=qcols, split_keys=sk)
+                    us = timeit(args, a.iters)
+                    print(json.dumps({"case": name, "qcols": qcols, "split_keys": sk, "items": n,
+                                      "grid_items": args[6].shape[0], "us": round(us, 1),
+                                      "kv_TBps": round(kvb / us / 1e6, 2), "TFLOPs": round(fl / us / 1e6, 1)}),
+                          flush=True)
 
 
 if __name__ == "__main__":
