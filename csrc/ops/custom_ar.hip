@@ -35,7 +35,20 @@
 
 namespace pa {
 
-constexpr int AR_G = 128;            // workgroups per rank (fixed: ownership must not depend on size)
+constexpr int AR_G = 128;            // workgroups per rank: flag / epoch slots (ownership must not depend on size)
+// Workgroups actually launched per rank: AR_G, or PILOTTAI_CAR_WG (1..AR_G, the same on every rank
+// of a group: chunk c belongs to workgroup c % G). A share-GPU rehearsal of TP=4/8 lowers it: each
+// rank's all-reduce workgroups spin until their peers arrive, and with 3-7 peers' worth of
+// spinning workgroups on the card a peer's GEMM that needs a whole CU finds none free.
+static int car_wg() {
+  static int g = 0;
+  if (g == 0) {
+    const char* e = getenv("PILOTTAI_CAR_WG");
+    const int v = e ? atoi(e) : AR_G;
+    g = v >= 1 && v <= AR_G ? v : AR_G;
+  }
+  return g;
+}
 constexpr int AR_THREADS = 256;      // one 16-byte vector per thread per chunk
 constexpr int AR_VPB = AR_THREADS;   // vectors per chunk (4 KiB)
 constexpr int AR_MAXW = 8;
@@ -157,7 +170,7 @@ __global__ __launch_bounds__(AR_THREADS) void ar_kernel(ArPeers P, ArIO io, int 
 
   // 1) stage this rank's input into its own (uncached) buffer
   u32x4* mine = data(rank);
-  for (long long c = b; c < nchunk; c += AR_G) {
+  for (long long c = b; c < nchunk; c += (long long)gridDim.x) {
     const long long v = c * AR_VPB + t;
     if (v < nvec) __builtin_nontemporal_store(in[v], mine + v);
   }
@@ -167,7 +180,7 @@ __global__ __launch_bounds__(AR_THREADS) void ar_kernel(ArPeers P, ArIO io, int 
 
   if (!TWO) {
     // 2) one-shot: every rank sums all W buffers for the chunks this workgroup owns
-    for (long long c = b; c < nchunk; c += AR_G) {
+    for (long long c = b; c < nchunk; c += (long long)gridDim.x) {
       const long long v = c * AR_VPB + t;
       float sq = 0.f;
       if (v < nvec) {
@@ -190,7 +203,7 @@ __global__ __launch_bounds__(AR_THREADS) void ar_kernel(ArPeers P, ArIO io, int 
     // (with RES the owner adds the residual: h is replicated, so h + sum is the same on every
     // rank and the gathered chunks are final)
     long long j = 0;
-    for (long long c = b; c < nchunk; c += AR_G, ++j) {
+    for (long long c = b; c < nchunk; c += (long long)gridDim.x, ++j) {
       if ((int)(j % W) != rank) continue;
       const long long v = c * AR_VPB + t;
       float sq = 0.f;
@@ -215,7 +228,7 @@ __global__ __launch_bounds__(AR_THREADS) void ar_kernel(ArPeers P, ArIO io, int 
     ar_signal_wait(P, rank, W, b, 1, ep, err);
     // 2b) all-gather: copy every other rank's reduced chunks
     j = 0;
-    for (long long c = b; c < nchunk; c += AR_G, ++j) {
+    for (long long c = b; c < nchunk; c += (long long)gridDim.x, ++j) {
       const int owner = (int)(j % W);
       if (owner == rank) continue;
       const long long v = c * AR_VPB + t;
@@ -256,14 +269,14 @@ __global__ __launch_bounds__(AR_THREADS) void co_kernel(ArPeers P, ArIO io, int 
   const long long nchunk = (nvec + AR_VPB - 1) / AR_VPB;
   auto data = [&](int r) { return reinterpret_cast<u32x4*>(P.base[r] + AR_FLAG_BYTES) + par_off; };
   u32x4* mine = data(rank);
-  for (long long c = b; c < nchunk; c += AR_G) {
+  for (long long c = b; c < nchunk; c += (long long)gridDim.x) {
     const long long v = c * AR_VPB + t;
     if (v < nvec) __builtin_nontemporal_store(in[v], mine + v);
   }
   ar_stores_done();
   __syncthreads();
   ar_signal_wait(P, rank, W, b, 0, ep, err);
-  for (long long c = b; c < nchunk; c += AR_G) {
+  for (long long c = b; c < nchunk; c += (long long)gridDim.x) {
     const long long v = c * AR_VPB + t;
     if (v >= nvec) continue;
     u32x4 x[W];
@@ -341,7 +354,7 @@ int pa_car_all_reduce(void* const* bases, int W, int rank0, int nranks_local, co
   ArPeers P;
   for (int i = 0; i < AR_MAXW; ++i) P.base[i] = i < W ? (char*)bases[i] : nullptr;
   const long long nvec = nelem / 8, cap_vec = cap_bytes / 16;
-  dim3 grid(AR_G, nranks_local);
+  dim3 grid(car_wg(), nranks_local);
   ArIO io;
   for (int i = 0; i < AR_MAXW; ++i) {
     const bool on = i < nranks_local;
@@ -399,7 +412,7 @@ int pa_car_collective(void* const* bases, int W, int rank0, int nranks_local, co
     io.out[i] = on ? (u32x4*)outs[i] : nullptr;
   }
   const long long nvec = n4 / 4, cap_vec = cap_bytes / 16;
-  dim3 grid(AR_G, nranks_local);
+  dim3 grid(car_wg(), nranks_local);
 #define CO_KERN(WW, OO) \
   hipLaunchKernelGGL((co_kernel<WW, OO>), grid, dim3(AR_THREADS), 0, st, P, io, rank0, nvec, cap_vec, epochs, err)
 #define CO_LAUNCH(WW)                                  \

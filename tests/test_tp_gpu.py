@@ -114,11 +114,26 @@ def _near_rank(model, prompt, toks, k):
     return out
 
 
-@pytest.mark.parametrize("world,graphs", [(2, False), (2, True), (4, True), (8, True)])
+@pytest.mark.parametrize("world,graphs", [(2, False), (2, True), (4, False), (4, True), (8, False), (8, True)])
 def test_tp_engine_custom_allreduce_matches_tp1(tmp_path, world, graphs):
     out = str(tmp_path / "tp.json")
     port = _free_port()
-    mp.start_processes(_worker, args=(world, port, out, graphs), nprocs=world, join=True, start_method="spawn")
+    # all `world` ranks share GPU 0 here: every rank's all-reduce workgroups spin until their
+    # peers' arrive, so the ranks' kernels must run side by side. At the default 128 all-reduce
+    # workgroups per rank, 3+ spinning ranks occupy every CU and a peer's GEMM that needs a whole
+    # CU never starts (round 6: TP=4 hit the 5 s all-reduce watchdog); the rehearsal runs 8
+    # all-reduce workgroups per rank and one hardware queue per process. A node has one rank per GPU.
+    saved = {k: os.environ.get(k) for k in ("GPU_MAX_HW_QUEUES", "PILOTTAI_CAR_WG")}
+    if world >= 4:
+        os.environ.update(GPU_MAX_HW_QUEUES="1", PILOTTAI_CAR_WG="8")
+    try:
+        mp.start_processes(_worker, args=(world, port, out, graphs), nprocs=world, join=True, start_method="spawn")
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
     res = json.load(open(out))
     assert res["calls"] > 0 and res["healthy"], res
     assert [len(t) for t in res["topk"]] == [12, 12]

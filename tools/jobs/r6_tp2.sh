@@ -8,7 +8,7 @@ export TMPDIR=/tmp
 timeout -k 10 500 python -u -m pytest tests/test_tp_gpu.py -x -v -s --timeout 240 --timeout-method thread \
   > $O/tests.log 2>&1 || { tail -40 $O/tests.log; exit 1; }
 grep -E "PASSED|FAILED|greedy sequences|passed|failed" $O/tests.log | tail -10
-PILOTTAI_DIST_BACKEND=gloo timeout -k 10 420 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 8 \
+PILOTTAI_CAR_WG=8 GPU_MAX_HW_QUEUES=1 PILOTTAI_DIST_BACKEND=gloo timeout -k 10 420 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 8 \
   --master-addr 127.0.0.1 --master-port 29551 benchmarks/workflow.py --share-gpu --clients 2 \
   --workflows 4 --warmup 1 --doc-words 120 --kv-gb 4 > $O/tp8.log 2>&1 || { grep -v Gloo $O/tp8.log | tail -40; exit 1; }
 grep '"metric"' $O/tp8.log > $O/wf_tp8.json && cut -c1-900 $O/wf_tp8.json
