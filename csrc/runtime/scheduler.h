@@ -38,9 +38,9 @@ struct SchedulerConfig {
   // wide prefill items whose causal key range reaches this many keys are cut into
   // min(4, keys / prefill_split_keys) partitions of whole 32-key tiles, merged in-kernel by the
   // last partition (attention.hip prefill_item_wg): the longest causal item stops being the
-  // step's critical path. 0 = off. Not on decode-sized (8-wave) steps.
-  int32_t prefill_split_keys = 1024;  // ... used only when the step's prefill tokens reach this
-                                       // (fewer, 4x wider items underfill the chip below it)
+  // step's critical path. 0 = off (the default: measured no gain on the steps that take wide
+  // items, profiles/r6_attention_split.md). Not on decode-sized (8-wave) steps.
+  int32_t prefill_split_keys = 0;
   bool prefix_caching = true;
   // A request whose first two blocks are being prefilled right now by another sequence
   // (the calls of one agent task all start with the task text and arrive together)

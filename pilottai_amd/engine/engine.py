@@ -120,8 +120,11 @@ class EngineConfig:
     # 1-2 % faster than with 2,048, which most mixed steps never reached; profiles/r2_att_wide_min_ab.jsonl)
     att_wide_min_tokens: int = 1024
     # wide prefill items of at least this many causal keys are split into partitions merged
-    # in-kernel (scheduler.h prefill_split_keys); 0 = off
-    prefill_split_keys: int = int(os.environ.get("PILOTTAI_PREFILL_SPLIT_KEYS", "1024"))
+    # in-kernel (scheduler.h prefill_split_keys); 0 = off, the default: the wide path runs only
+    # on steps whose items already fill the chip's 2 x 256 workgroup slots, where a split adds a
+    # second round (profiles/r6_attention_split.md: 2,048-token prompt 69.7 -> 97.9 us at 512);
+    # on few long items narrow items beat wide + split (cont256x4096: 32.4 vs 55.4 us)
+    prefill_split_keys: int = int(os.environ.get("PILOTTAI_PREFILL_SPLIT_KEYS", "0"))
     # attention workgroup width on decode-sized steps (<= the model's DECODE_FUSED_MAX_T
     # tokens): 8 waves stream a whole context per workgroup (the scheduler then skips the
     # flash-decoding split for such steps when they have few rows); None = model default

@@ -107,4 +107,8 @@ def test_q16_semantic_index_on_gpu(gpu):
         idx.add(v, prio, tags, [None] * 5000)
         res.append(idx.search(q, 7, [0, 1, 2] * 3, [(), ("a",), ("b",)] * 3))
     assert [[r for r, _ in x] for x in res[0]] == [[r for r, _ in x] for x in res[1]]
-    assert [[s for _, s in x] for x in res[0]] == [[s for _, s in x] for x in res[1]]
+    # same rows, scores equal up to the last bit of the final fp32 scaling (order of the two scale
+    # multiplies differs between the GPU epilogue and the CPU reference)
+    for a, b in zip(res[0], res[1]):
+        for (_, sa), (_, sb) in zip(a, b):
+            assert abs(sa - sb) <= 1e-6 * max(1.0, abs(sb))

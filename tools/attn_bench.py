@@ -96,6 +96,10 @@ def main():
         "prefill4x512": ([512] * 4, [768] * 4),
         # ... as it really runs: beside ~40 decode / forced-run rows
         "step2048": ([512] * 4 + [1] * 40, [768] * 4 + [600] * 40),
+        # follow-up turns on long cached contexts: few items, each a long serial key chain
+        "cont256x4096": ([256], [4352]),
+        "cont2x256x2048": ([256] * 2, [2304] * 2),
+        "cont512x3072": ([512], [3584]),
     }
     if a.scan:
         cases = {f"pf{n}": ([n], [n]) for n in (8, 32, 128, 256, 512, 1024, 2048, 4096)}
