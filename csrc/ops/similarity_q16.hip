@@ -32,6 +32,8 @@
 // exact scan (EXACT = true: both planes, exact scores in stage 1), so the result is always
 // exact. On random unit vectors at 100M rows the band [tau - 2E, tau] holds a few hundred rows
 // (E ~ 0.008 against a score spread of 1/sqrt(D) = 0.031), far below the lists' 16K entries.
+#include <cstdlib>
+
 #include "common.h"
 
 namespace pa {
@@ -64,14 +66,15 @@ __device__ __forceinline__ float exact_score(int hh, int hl, int lh, int ll, flo
   return (float)((double)I * ((double)sr * (double)sq));
 }
 
-// Bitonic sort of n = CAND entries descending by key, carrying two payloads (whole block).
+// Bitonic sort of NC entries descending by key, carrying two payloads (whole block, >= NC threads).
+template <int NC = CAND>
 __device__ void bitonic3(float* key, float* p1, int* p2) {
-  for (int k = 2; k <= CAND; k <<= 1) {
+  for (int k = 2; k <= NC; k <<= 1) {
     for (int j = k >> 1; j > 0; j >>= 1) {
       __syncthreads();
       const int i = threadIdx.x;
       const int p = i ^ j;
-      if (i < CAND && p > i) {
+      if (i < NC && p > i) {
         const bool desc = (i & k) == 0;
         const float a = key[i], b = key[p];
         if (desc ? (a < b) : (a > b)) {
@@ -97,16 +100,18 @@ struct QState {  // per-query admission state of one slice (LDS)
   float cq[MAXQ];
 };
 
-// Compact query q's global buffer to its best C upper bounds; refresh cap / tauL / theta.
+// Compact query q's global buffer (NC entries) to its best C upper bounds; refresh cap / tauL /
+// theta.
+template <int NC = CAND>
 __device__ void compact(float* gu, float* gl, int* gr, float* su, float* sl, int* sr, QState& st, int q, int K) {
-  const int n = min(st.cnt[q], CAND);
-  if (threadIdx.x < CAND) {
+  const int n = min(st.cnt[q], NC);
+  if (threadIdx.x < NC) {
     const bool ok = threadIdx.x < n;
     su[threadIdx.x] = ok ? gu[threadIdx.x] : -INFINITY;
     sl[threadIdx.x] = ok ? gl[threadIdx.x] : -INFINITY;
     sr[threadIdx.x] = ok ? gr[threadIdx.x] : -1;
   }
-  bitonic3(su, sl, sr);  // begins and ends with a barrier
+  bitonic3<NC>(su, sl, sr);  // begins and ends with a barrier
   const int keep = min(n, C);
   if (threadIdx.x < keep) {
     gu[threadIdx.x] = su[threadIdx.x];
@@ -191,11 +196,12 @@ __global__ __launch_bounds__(EXACT ? 512 : 1024) void stage1_kernel(
   auto frag_off = [&](int grp_, int s) -> size_t {  // byte offset of this lane's fragment, k-step s
     return (((size_t)((r0 + grp_ * 16) >> 4) * DS + s) * 64 + lane) * 16;
   };
+  // branch-free: k-steps past D re-read the last one (never used: compute stops at DS) -- a
+  // conditional load splits the block and the wait-count pass then drains every load in flight
   auto load = [&](const signed char* plane, int grp_, int m, i32x4 (&dst)[KB]) {
 #pragma unroll
     for (int u = 0; u < KB; ++u)
-      dst[u] = (m + u < DS) ? __builtin_nontemporal_load(reinterpret_cast<const i32x4*>(plane + frag_off(grp_, m + u)))
-                            : i32x4{0, 0, 0, 0};
+      dst[u] = __builtin_nontemporal_load(reinterpret_cast<const i32x4*>(plane + frag_off(grp_, min(m + u, DS - 1))));
   };
   i32x4 hA[KB], hB[KB], lA[KB], lB[KB];
   if (wid < ngroups) {
@@ -207,6 +213,12 @@ __global__ __launch_bounds__(EXACT ? 512 : 1024) void stage1_kernel(
     const int grp = round * NWV + wid;
     if (grp < ngroups) {
       const int gbase = r0 + grp * 16;
+      // the rows' (s_r, b_r) are read here, ahead of the next batches: a global load issued
+      // after them would make the epilogue's wait drain every row load in flight
+      float2 rmv[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        rmv[r] = *reinterpret_cast<const float2*>(rmeta + 2 * (size_t)min(gbase + 4 * g + r, r1 - 1));
       i32x4 acc_hh[MAXQ / QT], acc_lh[MAXQ / QT], acc_hl[MAXQ / QT], acc_ll[MAXQ / QT];
 #pragma unroll
       for (int t = 0; t < MAXQ / QT; ++t) {
@@ -255,7 +267,7 @@ __global__ __launch_bounds__(EXACT ? 512 : 1024) void stage1_kernel(
       for (int r = 0; r < 4; ++r) {
         const int row = gbase + 4 * g + r;
         if (row >= r1) continue;
-        const float2 rm = *reinterpret_cast<const float2*>(rmeta + 2 * (size_t)row);
+        const float2 rm = rmv[r];
 #pragma unroll
         for (int t = 0; t < MAXQ / QT; ++t) {
           const int q = t * QT + col;
@@ -294,6 +306,261 @@ __global__ __launch_bounds__(EXACT ? 512 : 1024) void stage1_kernel(
   __syncthreads();
   for (int q = 0; q < Q; ++q) {
     compact(my_u + q * CAND, my_l + q * CAND, my_r + q * CAND, su, sl, sr, st, q, K);
+    const int n = st.cnt[q];
+    if (threadIdx.x < C) {
+      const size_t o = ((size_t)q * nwg + wg) * C + threadIdx.x;
+      const bool ok = (int)threadIdx.x < n;
+      out_u[o] = ok ? su[threadIdx.x] : -INFINITY;
+      out_l[o] = ok ? sl[threadIdx.x] : -INFINITY;
+      out_r[o] = ok ? sr[threadIdx.x] : -1;
+    }
+    if (threadIdx.x == 0) out_drop[(size_t)q * nwg + wg] = st.dropped[q] ? st.cap[q] : -INFINITY;
+    __syncthreads();
+  }
+}
+
+// Stage 1, the bound scan as run (stage1_kernel<false> is the first form, kept as variant 0 for
+// A/B; profiles/r6_q16_stage1.md). 8 waves, two per SIMD (the 32x32 accumulators of 64 queries
+// and two 4-k-step batches need ~170 registers); a wave owns 32-row groups and runs
+// v_mfma_i32_32x32x32_i8 (rows x 32 queries): per byte of index it reads half the LDS query
+// fragments of the 16x16x64 form (4 KiB per KiB of rows instead of 8) at the same MFMA cycles.
+// The A fragments come straight from the 16-row fragment-major planes: lane (r = l & 31,
+// h = l >> 5) of k-half kh of k-step s takes row tile 2G + r/16, lane position 16 (2 kh + h) +
+// r % 16 -- 16 B, in 256-B runs. The group streams in batches of 4 k-steps, double-buffered, the
+// next group's first batch issued before the epilogue. Everything that decides what stays in
+// flight is static: the k-step count is a template constant (queries zero-padded to DSC*64
+// dims and 64 rows, loads past D clamped), the row loads are unconditional (clamped to the
+// slice's last tile), the load batches are pinned by sched_barrier, and the round barrier waits
+// for LDS only -- a branchy load block, a fenced __syncthreads or loads left to the scheduler
+// each made the wait-count pass drain the row loads in flight (the first form: 3.2 TB/s).
+// Candidate stores are made visible by a full barrier only before a compaction.
+constexpr int CAND_B = CAND;  // per-(slice, query) candidate buffer: a round admits up to 8 x 32 rows
+template <int DSC, int ABL = 0>  // ABL (timing ablations, tools/q16_ablate): 1 = no epilogue, 2 = loads only
+__global__ __launch_bounds__(512) void stage1_bound_kernel(
+    float* __restrict__ out_u, float* __restrict__ out_l, int* __restrict__ out_r, float* __restrict__ out_drop,
+    float* __restrict__ cand_u, float* __restrict__ cand_l, int* __restrict__ cand_r,
+    const signed char* __restrict__ qv, const float* __restrict__ qmeta, const signed char* __restrict__ hi,
+    const float* __restrict__ rmeta, int Q, int N, int D, int K, const int* __restrict__ row_prio,
+    const uint64_t* __restrict__ row_tags, const float* __restrict__ row_exp, const int* __restrict__ q_minp,
+    const uint64_t* __restrict__ q_tags, float now) {
+  constexpr int TH = 512, NWV = TH / 64, KB = DSC >= 8 ? 4 : 2, NTQ = MAXQ / 32;
+  constexpr int QLD = DSC * 64 + 16;  // padded LDS row (bytes)
+  static_assert(DSC % (2 * KB) == 0, "k-steps in whole batch pairs");
+  typedef int i32x16 __attribute__((ext_vector_type(16)));
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  signed char* qh = reinterpret_cast<signed char*>(smem);  // [64][QLD]
+  signed char* ql = qh + (size_t)MAXQ * QLD;                // [64][QLD]
+  float* su = reinterpret_cast<float*>(ql + (size_t)MAXQ * QLD);
+  float* sl = su + CAND_B;
+  int* sr = reinterpret_cast<int*>(sl + CAND_B);
+  QState& st = *reinterpret_cast<QState*>(sr + CAND_B);
+  int* need = reinterpret_cast<int*>(&st + 1);  // some query's buffer must be compacted
+  // [NWV][32] per group row: (s_r, b_r), then the filter words (priority, expiry, tags)
+  float2* rm_lds = reinterpret_cast<float2*>(need + 4);
+  int* pr_lds = reinterpret_cast<int*>(rm_lds + NWV * 32);
+  float* ex_lds = reinterpret_cast<float*>(pr_lds + NWV * 32);
+  uint64_t* tg_lds = reinterpret_cast<uint64_t*>(ex_lds + NWV * 32);
+
+  const int nwg = gridDim.x, wg = blockIdx.x;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int lr = lane & 31, lh = lane >> 5;
+  const int DS = D / 64;
+  for (int v = threadIdx.x; v < MAXQ * 2 * (DSC * 4); v += TH) {
+    const int r = v / (2 * DSC * 4), rem = v % (2 * DSC * 4);
+    const int plane = rem / (DSC * 4), c16 = (rem % (DSC * 4)) * 16;
+    i32x4 x = i32x4{0, 0, 0, 0};
+    if (r < Q && c16 < D) x = *reinterpret_cast<const i32x4*>(qv + ((size_t)r * 2 + plane) * D + c16);
+    *reinterpret_cast<i32x4*>((plane ? ql : qh) + (size_t)r * QLD + c16) = x;
+  }
+  if (threadIdx.x < MAXQ) {
+    const int q = threadIdx.x;
+    st.cnt[q] = 0;
+    st.theta[q] = -INFINITY;
+    st.cap[q] = -INFINITY;
+    st.tauL[q] = -INFINITY;
+    st.dropped[q] = 0;
+    st.minp[q] = q < Q ? q_minp[q] : 0x7fffffff;
+    st.qtag[q] = q < Q ? q_tags[q] : 0ull;
+    st.sq[q] = q < Q ? qmeta[2 * q] : 0.f;
+    st.cq[q] = q < Q ? qmeta[2 * q + 1] : 0.f;
+  }
+  if (threadIdx.x == 0) *need = 0;
+  __syncthreads();
+
+  float* my_u = cand_u + (size_t)wg * MAXQ * CAND_B;
+  float* my_l = cand_l + (size_t)wg * MAXQ * CAND_B;
+  int* my_r = cand_r + (size_t)wg * MAXQ * CAND_B;
+  const int per = ((N + nwg - 1) / nwg + 31) / 32 * 32;
+  const int r0 = wg * per, r1 = min(N, r0 + per);
+  const int ngroups = (max(0, r1 - r0) + 31) / 32;
+  if (ngroups > 0) {  // workgroup-uniform
+    const int nrounds = (ngroups + NWV - 1) / NWV;
+    const int last_tile = (r1 - 1) >> 4;
+    const int CUT = CAND_B - NWV * 32;  // a buffer must absorb the next round
+    // this lane's two 16-B A pieces (k-halves) of k-step m + u, group grp_
+    auto load = [&](int grp_, int m, i32x4 (&dst)[KB][2]) {
+      const int tile = min((r0 >> 4) + 2 * min(grp_, ngroups - 1) + (lr >> 4), last_tile);
+      const signed char* base = hi + (size_t)tile * DS * 1024 + (size_t)(lr & 15) * 16;
+#pragma unroll
+      for (int u = 0; u < KB; ++u)
+#pragma unroll
+        for (int kh = 0; kh < 2; ++kh)
+          dst[u][kh] = __builtin_nontemporal_load(reinterpret_cast<const i32x4*>(
+              base + (size_t)min(m + u, DS - 1) * 1024 + (size_t)(2 * kh + lh) * 256));
+    };
+    // one round; X holds the group's first batch on entry and the next group's on exit
+    auto body = [&](int round, i32x4 (&X)[KB][2], i32x4 (&Y)[KB][2]) {
+      const int grp = round * NWV + wid;
+      const int gbase = r0 + grp * 32;
+      // (s_r, b_r) of row gbase + lr, issued ahead of the group's later batches; the epilogue
+      // reads every row's pair back from this wave's LDS slot
+      const int rowc = max(0, min(gbase + lr, r1 - 1));
+      const float2 rmine = *reinterpret_cast<const float2*>(rmeta + 2 * (size_t)rowc);
+      // the row's filter words ride along (16 B per 1-KiB row): the admission path reads them
+      // from LDS instead of waiting on global loads behind the row stream
+      const int prmine = row_prio[rowc];
+      const float exmine = row_exp[rowc];
+      const uint64_t tgmine = row_tags[rowc];
+      i32x16 acc_hh[NTQ], acc_lh[NTQ];
+#pragma unroll
+      for (int t = 0; t < NTQ; ++t)
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          acc_hh[t][j] = 0;
+          acc_lh[t][j] = 0;
+        }
+      auto compute = [&](const i32x4 (&ah)[KB][2], int m) {
+#pragma unroll
+        for (int u = 0; u < KB; ++u)
+#pragma unroll
+          for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+            for (int t = 0; t < NTQ; ++t) {
+              const int qo = (32 * t + lr) * QLD + 64 * (m + u) + 32 * kh + 16 * lh;
+              const i32x4 bh = *reinterpret_cast<const i32x4*>(qh + qo);
+              const i32x4 bl = *reinterpret_cast<const i32x4*>(ql + qo);
+              if constexpr (ABL == 2) {
+                acc_hh[t][0] ^= ah[u][kh][0] ^ ah[u][kh][1] ^ ah[u][kh][2] ^ ah[u][kh][3];
+              } else {
+                acc_hh[t] = __builtin_amdgcn_mfma_i32_32x32x32_i8(ah[u][kh], bh, acc_hh[t], 0, 0, 0);
+                acc_lh[t] = __builtin_amdgcn_mfma_i32_32x32x32_i8(ah[u][kh], bl, acc_lh[t], 0, 0, 0);
+              }
+            }
+      };
+      // sched_barrier pins each batch's loads where they are issued: left to the scheduler they
+      // sink next to their first use and only ~1 load per wave stays in flight
+      // double-buffered batches: X holds the group's first batch on entry and the next group's
+      // on exit (a third buffer, two batches ahead, spilled registers at 64 queries)
+#pragma unroll
+      for (int m = 0; m < DSC; m += 2 * KB) {
+        load(grp, m + KB, Y);
+        __builtin_amdgcn_sched_barrier(0);
+        if (m == 0 && lh == 0) {  // the row words to LDS: older than Y, waited with X
+          rm_lds[wid * 32 + lr] = rmine;
+          pr_lds[wid * 32 + lr] = prmine;
+          ex_lds[wid * 32 + lr] = exmine;
+          tg_lds[wid * 32 + lr] = tgmine;
+        }
+        compute(X, m);
+        __builtin_amdgcn_sched_barrier(0);
+        load(m + 2 * KB < DSC ? grp : grp + NWV, m + 2 * KB < DSC ? m + 2 * KB : 0, X);
+        __builtin_amdgcn_sched_barrier(0);
+        compute(Y, m + KB);
+      }
+      if constexpr (ABL != 0) {
+        int x = 0;
+#pragma unroll
+        for (int t = 0; t < NTQ; ++t)
+#pragma unroll
+          for (int j = 0; j < 16; ++j) x ^= acc_hh[t][j] ^ acc_lh[t][j];
+        if (x == 0x7fffffff && rmine.x == 12345.f) my_u[0] = 1.f;  // keeps the work alive
+      } else if (grp < ngroups) {
+        // lane holds queries 32 t + lr, rows gbase + (j & 3) + 8 (j >> 2) + 4 lh (j = 0..15).
+        // Fast path, branch-free: every (row, query) bound against its query's admission threshold
+        // theta (-> adm) and k-th lower bound tauL (tauL < U <= theta: refused for capacity ->
+        // one drop flag per query); only a lane holding an admissible bound takes the per-pair
+        // path (rare once the first compaction has set the thresholds). The branchy per-pair form,
+        // whose global loads drained the row stream at every refused-for-capacity row, cost
+        // ~10 ms of the 28.6-ms 100M-row pass (profiles/r6_q16_stage1.md)
+        const int nrow = r1 - gbase;  // rows ri < nrow are in the slice
+        float th[NTQ], tl[NTQ], sqv[NTQ], cqv[NTQ];
+#pragma unroll
+        for (int t = 0; t < NTQ; ++t) {
+          const int q = 32 * t + lr;
+          th[t] = q < Q ? st.theta[q] : INFINITY;
+          tl[t] = q < Q ? st.tauL[q] : INFINITY;
+          sqv[t] = st.sq[q];
+          cqv[t] = st.cq[q] * 1.0001f;
+        }
+        unsigned admbits = 0;  // bit 16 t + j: pair (query 32 t + lr, row j) is admissible
+        bool drp[NTQ];
+#pragma unroll
+        for (int t = 0; t < NTQ; ++t) drp[t] = false;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          const int ri = (j & 3) + 8 * (j >> 2) + 4 * lh;
+          const float2 rsv = rm_lds[wid * 32 + ri];  // written by this wave (LDS order holds)
+          const float rsx = rsv.x, rsy = rsv.y;
+          const bool rv = ri < nrow;
+#pragma unroll
+          for (int t = 0; t < NTQ; ++t) {
+            const float sc = fmaf((float)acc_hh[t][j], 65536.f, (float)acc_lh[t][j] * 256.f) * (rsx * sqv[t]);
+            const float U = sc + fmaf(rsy, cqv[t], 1e-6f);
+            admbits |= (unsigned)((U > th[t]) & rv) << (16 * t + j);
+            drp[t] |= (U > tl[t]) & !(U > th[t]) & rv;  // refused for capacity, not by the k-th bound
+          }
+        }
+#pragma unroll
+        for (int t = 0; t < NTQ; ++t)
+          if (drp[t]) st.dropped[32 * t + lr] = 1;
+        if (admbits) {  // ~2 admissions per group: LDS reads and stores only on this path
+          const float2* rmw = rm_lds + wid * 32;
+#pragma unroll
+          for (int t = 0; t < NTQ; ++t) {
+            const int q = 32 * t + lr;
+            const float sq = sqv[t], cq = cqv[t];
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+              if (!((admbits >> (16 * t + j)) & 1u)) continue;
+              const int ri = (j & 3) + 8 * (j >> 2) + 4 * lh;
+              const float2 rm = rmw[ri];  // == the shuffled pair of the fast path
+              const float sc = fmaf((float)acc_hh[t][j], 65536.f, (float)acc_lh[t][j] * 256.f) * (rm.x * sq);
+              const float e = fmaf(rm.y, cq, 1e-6f);  // margin: fp32 rounding of sc and e
+              if (pr_lds[wid * 32 + ri] < st.minp[q]) continue;
+              if ((tg_lds[wid * 32 + ri] & st.qtag[q]) != st.qtag[q]) continue;
+              const float ex = ex_lds[wid * 32 + ri];
+              if (ex != 0.f && !(ex > now)) continue;
+              const int pos = atomicAdd(&st.cnt[q], 1);
+              if (pos < CAND_B) {
+                my_u[q * CAND_B + pos] = sc + e;
+                my_l[q * CAND_B + pos] = sc - e;
+                my_r[q * CAND_B + pos] = gbase + ri;
+              }
+              if (pos == CUT) *need = 1;
+            }
+          }
+        }
+      }
+      // LDS-only barrier: the row loads stay in flight across it
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      if (*need) {  // workgroup-uniform; rare after the first rounds
+        __syncthreads();  // candidate stores complete and visible
+        for (int q = 0; q < Q; ++q)
+          if (st.cnt[q] > CUT)
+            compact<CAND_B>(my_u + q * CAND_B, my_l + q * CAND_B, my_r + q * CAND_B, su, sl, sr, st, q, K);
+        if (threadIdx.x == 0) *need = 0;
+        __syncthreads();
+      }
+    };
+    i32x4 bA[KB][2], bB[KB][2];
+    load(wid, 0, bA);
+    for (int round = 0; round < nrounds; ++round) body(round, bA, bB);
+  }
+  __syncthreads();
+  for (int q = 0; q < Q; ++q) {
+    compact<CAND_B>(my_u + q * CAND_B, my_l + q * CAND_B, my_r + q * CAND_B, su, sl, sr, st, q, K);
     const int n = st.cnt[q];
     if (threadIdx.x < C) {
       const size_t o = ((size_t)q * nwg + wg) * C + threadIdx.x;
@@ -452,7 +719,7 @@ __global__ __launch_bounds__(THREADS) void stage2_kernel(
 // candidate buffers [3][nwg][64][CAND]
 extern "C" long long pa_q16_topk_workspace_bytes(int Q, int N) {
   const long long w = pa::q16::num_wg(N);
-  return 3LL * Q * w * pa::q16::C * 4 + (long long)Q * w * 4 + 3LL * w * pa::q16::MAXQ * pa::q16::CAND * 4;
+  return 3LL * Q * w * pa::q16::C * 4 + (long long)Q * w * 4 + 3LL * w * pa::q16::MAXQ * pa::q16::CAND_B * 4;
 }
 
 // queries_q: [Q][2][D] int8 (qh, ql); qmeta [Q][2] (s_q, c_q); hi / lo: [N/16][D/64][64][16]
@@ -477,12 +744,19 @@ extern "C" int pa_q16_topk(float* out_scores, int* out_rows, int* unsafe, void* 
   int* lr = reinterpret_cast<int*>(ll + (size_t)Q * nwg * C);
   float* ldrop = reinterpret_cast<float*>(lr + (size_t)Q * nwg * C);
   float* cu = ldrop + (size_t)Q * nwg;
-  float* cl = cu + (size_t)nwg * MAXQ * CAND;
-  int* cr = reinterpret_cast<int*>(cl + (size_t)nwg * MAXQ * CAND);
+  // candidate buffers laid out for the bound kernel's CAND_B (the first form / the exact scan
+  // use the first CAND entries of each)
+  float* cl = cu + (size_t)nwg * MAXQ * CAND_B;
+  int* cr = reinterpret_cast<int*>(cl + (size_t)nwg * MAXQ * CAND_B);
   const int nqt = (Q + QT - 1) / QT;
   const size_t lds = (size_t)nqt * QT * (D + 16) * 2 + CAND * 12 + sizeof(QState);
   static bool attr_set = false;
   if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)stage1_bound_kernel<4>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)stage1_bound_kernel<8>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)stage1_bound_kernel<16>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)stage1_bound_kernel<16, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)stage1_bound_kernel<16, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     (void)hipFuncSetAttribute((const void*)stage1_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     (void)hipFuncSetAttribute((const void*)stage1_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr_set = true;
@@ -496,9 +770,26 @@ extern "C" int pa_q16_topk(float* out_scores, int* out_rows, int* unsafe, void* 
     hipLaunchKernelGGL(stage2_kernel<true>, dim3(Q), dim3(THREADS), 0, st, out_scores, out_rows, unsafe, lu, ll, lr,
                        ldrop, nwg, qv, qmeta, h, l, rmeta, D, K);
   } else {
-    hipLaunchKernelGGL(stage1_kernel<false>, dim3(nwg), dim3(THREADS), lds, st, lu, ll, lr, ldrop, cu, cl, cr, qv,
-                       qmeta, h, l, rmeta, Q, N, D, K, row_priority, row_tags, row_expiry, q_min_priority, q_tags,
-                       now);
+    static const int variant = [] { const char* e = getenv("PILOTTAI_Q16_STAGE1"); return e ? atoi(e) : 1; }();
+    if (variant == 0) {
+      hipLaunchKernelGGL(stage1_kernel<false>, dim3(nwg), dim3(THREADS), lds, st, lu, ll, lr, ldrop, cu, cl, cr, qv,
+                         qmeta, h, l, rmeta, Q, N, D, K, row_priority, row_tags, row_expiry, q_min_priority, q_tags,
+                         now);
+    } else {
+      const int dsc = D <= 256 ? 4 : (D <= 512 ? 8 : 16);
+      const size_t ldsb = (size_t)MAXQ * (dsc * 64 + 16) * 2 + CAND_B * 12 + sizeof(QState) + 16 + 8 * 32 * 24;
+#define COMMA ,
+#define Q16_BOUND(KERN_)                                                                                     \
+      hipLaunchKernelGGL(KERN_, dim3(nwg), dim3(512), ldsb, st, lu, ll, lr, ldrop, cu, cl, cr, \
+                         qv, qmeta, h, rmeta, Q, N, D, K, row_priority, row_tags, row_expiry, q_min_priority,       \
+                         q_tags, now)
+      if (dsc == 4) Q16_BOUND((stage1_bound_kernel<4>));
+      else if (dsc == 8) Q16_BOUND((stage1_bound_kernel<8>));
+      else if (variant == 2) Q16_BOUND((stage1_bound_kernel<16, 1>));
+      else if (variant == 3) Q16_BOUND((stage1_bound_kernel<16, 2>));
+      else Q16_BOUND((stage1_bound_kernel<16>));
+#undef Q16_BOUND
+    }
     hipLaunchKernelGGL(stage2_kernel<false>, dim3(Q), dim3(THREADS), 0, st, out_scores, out_rows, unsafe, lu, ll, lr,
                        ldrop, nwg, qv, qmeta, h, l, rmeta, D, K);
   }

@@ -6,5 +6,5 @@ O=gpurun_out/r6_stress${RUN:-}
 mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 1100 python -u tools/stream_handoff_stress.py --reps 100000 --rel 0 --out $O/handoff_rel0.jsonl \
-  > $O/stress.log 2>&1 || { tail -20 $O/stress.log; exit 1; }
+  > $O/stress.log 2>&1 || { rc=$?; tail -20 $O/stress.log; exit $rc; }
 cat $O/handoff_rel0.jsonl
