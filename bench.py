@@ -91,9 +91,10 @@ def parse():
     ap.add_argument("--memory-rows", type=int, default=0,
                     help="semantic memory on the engine's GPU with this many rows; every agent step looks it up")
     ap.add_argument("--memory-top-k", type=int, default=3)
-    ap.add_argument("--memory-storage", default="bf16", choices=["bf16", "q16"],
-                    help="index row format: bf16 (one-pass bf16 scan) or q16 (16-bit fixed point, two-stage "
-                         "exact scan streaming one byte per dimension; csrc/ops/similarity_q16.hip)")
+    ap.add_argument("--memory-storage", default="q16", choices=["bf16", "q16"],
+                    help="index row format: q16 (default: 16-bit fixed point, two-stage exact scan streaming "
+                         "one byte per dimension, csrc/ops/similarity_q16.hip; config 4 32.4 vs 28.6 tasks/s, "
+                         "profiles/r6_q16_stage1.md) or bf16 (one-pass bf16 scan)")
     ap.add_argument("--memory-min-batch", type=int, default=1,
                     help="lookups a pass waits for (up to --memory-wait-ms) before it starts")
     ap.add_argument("--memory-wait-ms", type=float, default=0.0)
@@ -497,7 +498,7 @@ def build_memory(a, device, rank: int = 0, world: int = 1, node: bool = False):
     rows = a.memory_rows // world + (1 if rank < a.memory_rows % world else 0) if node else a.memory_rows
     cap = rows + 65536  # room for the run's write-backs
     mem = EnhancedMemory(max_size=cap, device=device, dim=dim, fallback_text=fallback,
-                         storage=getattr(a, "memory_storage", "bf16"))
+                         storage=getattr(a, "memory_storage", "q16"))
     idx = mem.index
     idx._grow(cap)
     g = torch.Generator(device=device).manual_seed(7 + rank)
