@@ -505,7 +505,7 @@ __device__ __forceinline__ void att_wait_vm() { __builtin_amdgcn_s_waitcnt((N & 
 // (common.h handoff_last), with its own counter per split item (pf_counters).
 constexpr int PW_PART_SLOTS = 8;
 
-template <int G>
+template <int G, bool SPLIT>
 __device__ __forceinline__ void prefill_item_wg(
     const int4 it, char* smem, bf16* __restrict__ out, const bf16* __restrict__ q,
     const bf16* __restrict__ k_cache, const bf16* __restrict__ v_cache,
@@ -514,8 +514,11 @@ __device__ __forceinline__ void prefill_item_wg(
     float* __restrict__ part_o, float* __restrict__ part_ml, int* __restrict__ pf_counters, int acq) {
   constexpr int TPWV = 32 / G;  // tokens per wave
   const int s = it.x, qb = it.y, nq = it.z & 0xff;
-  // without ticket room (pf_counters null) a split item computes its whole key range
-  const int part = pf_counters ? (it.z >> 8) & 0xfff : 0, nparts = pf_counters ? max(1, it.z >> 20) : 1;
+  // without ticket room (pf_counters null) a split item computes its whole key range; SPLIT =
+  // false (the engine's default, prefill_split_keys = 0) compiles the partition hand-off out --
+  // it cost 8 spilled registers in every prefill item
+  const int part = SPLIT && pf_counters ? (it.z >> 8) & 0xfff : 0;
+  const int nparts = SPLIT && pf_counters ? max(1, it.z >> 20) : 1;
   const int pidx = it.w;
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -607,7 +610,7 @@ __device__ __forceinline__ void prefill_item_wg(
     softmax_pv_tile(sc, 32 * t + 32 > kmin, 32 * t + 8 * h, key_limit, scale_log2, m_run, l_run, o, vf);
   }
   l_run += __shfl_xor(l_run, 32, 64);
-  if (nparts > 1) {
+  if (SPLIT && nparts > 1) {
     // ---- partition hand-off: slab chunk j = 2 wid + (m >> 1) of the partition's 8 slots holds
     // registers o[m] of the wave's 64 lanes; (m, l) of column 32 wid + r in slot (32 wid + r) / 16
     const int p0 = pidx - PW_PART_SLOTS * part;
@@ -694,7 +697,7 @@ __device__ __forceinline__ void prefill_item_wg(
 
 // A q-split item of either width. 8-wave workgroups run no LDS-staged wide items (their 4-wave
 // image layout): a wide item (128/G tokens) runs there as its 32-column sub-items.
-template <int G, int NW>
+template <int G, int NW, bool SPLIT>
 __device__ __forceinline__ void prefill_any(
     const int4 it, char* smem, bf16* __restrict__ out, const bf16* __restrict__ q,
     const bf16* __restrict__ k_cache, const bf16* __restrict__ v_cache,
@@ -706,7 +709,7 @@ __device__ __forceinline__ void prefill_any(
     prefill_item<G, NW>(it, smem, out, q, k_cache, v_cache, q_start, q_len, ctx_len, block_table, max_blocks,
                             H, KV, kvh, scale_log2);
   } else if constexpr (NW == 4) {
-    prefill_item_wg<G>(it, smem, out, q, k_cache, v_cache, q_start, q_len, ctx_len, block_table, max_blocks, H, KV,
+    prefill_item_wg<G, SPLIT>(it, smem, out, q, k_cache, v_cache, q_start, q_len, ctx_len, block_table, max_blocks, H, KV,
                        kvh, scale_log2, part_o, part_ml, pf_counters, acq);
   } else {
     for (int sb = 0; sb < nq; sb += 32 / G) {
@@ -732,7 +735,7 @@ constexpr int ATT_LDS_BYTES = ATT_LDS_BYTES0W;  // + the split items' last-arriv
 // (Round 4 measured and removed two alternatives: a persistent work-queue launch and idle
 // workgroups warming the next projection's weights into the Infinity Cache; neither paid
 // end to end, BENCHMARKS.md.)
-template <int G, int NW = 4>
+template <int G, int NW = 4, bool SPLIT = false>
 __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void paged_attn_kernel(
     bf16* __restrict__ out, float* __restrict__ part_o, float* __restrict__ part_ml,
     int* __restrict__ counters, const bf16* __restrict__ q, const bf16* __restrict__ k_cache,
@@ -770,7 +773,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void paged_attn_kernel(
       decode_item<G, NW>(it, smem, out, part_o, part_ml, counters, q, k_cache, v_cache, q_start, q_len, ctx_len,
                          block_table, max_blocks, H, KV, kvh, scale_log2, psz, acq);
     else
-      prefill_any<G, NW>(it, smem, out, q, k_cache, v_cache, q_start, q_len, ctx_len, block_table, max_blocks, H,
+      prefill_any<G, NW, SPLIT>(it, smem, out, q, k_cache, v_cache, q_start, q_len, ctx_len, block_table, max_blocks, H,
                          KV, kvh, scale_log2, part_o, part_ml, pf_counters, acq);
     __syncthreads();  // LDS reuse by the next item
   }
@@ -809,15 +812,24 @@ extern "C" int pa_paged_attention(void* out, float* part_o, float* part_ml, cons
     }                                                                                           \
     static bool attr4 = false;                                                                  \
     if (!attr4) {                                                                               \
-      (void)hipFuncSetAttribute((const void*)pa::paged_attn_kernel<GG, 4>,                      \
+      (void)hipFuncSetAttribute((const void*)pa::paged_attn_kernel<GG, 4, false>,               \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, pa::ATT_LDS_BYTES); \
+      (void)hipFuncSetAttribute((const void*)pa::paged_attn_kernel<GG, 4, true>,                \
                                 hipFuncAttributeMaxDynamicSharedMemorySize, pa::ATT_LDS_BYTES); \
       attr4 = true;                                                                             \
     }                                                                                           \
-    hipLaunchKernelGGL((pa::paged_attn_kernel<GG, 4>), grid, dim3(256), pa::ATT_LDS_BYTES, st,  \
-                       (pa::bf16*)out, part_o, part_ml, counters, (const pa::bf16*)q,           \
-                       (const pa::bf16*)k_cache, (const pa::bf16*)v_cache, (const int4*)items,   \
-                       n_items, part_size, q_start, q_len, ctx_len, block_table, max_blocks, H,  \
-                       KV, scale_log2, pa::g_handoff_attn, pf_counters);                        \
+    if (pf_counters)  /* ticket room for split prefill items: the SPLIT instantiation */        \
+      hipLaunchKernelGGL((pa::paged_attn_kernel<GG, 4, true>), grid, dim3(256), pa::ATT_LDS_BYTES, st, \
+                         (pa::bf16*)out, part_o, part_ml, counters, (const pa::bf16*)q,         \
+                         (const pa::bf16*)k_cache, (const pa::bf16*)v_cache, (const int4*)items, \
+                         n_items, part_size, q_start, q_len, ctx_len, block_table, max_blocks, H, \
+                         KV, scale_log2, pa::g_handoff_attn, pf_counters);                      \
+    else                                                                                        \
+      hipLaunchKernelGGL((pa::paged_attn_kernel<GG, 4, false>), grid, dim3(256), pa::ATT_LDS_BYTES, st, \
+                         (pa::bf16*)out, part_o, part_ml, counters, (const pa::bf16*)q,         \
+                         (const pa::bf16*)k_cache, (const pa::bf16*)v_cache, (const int4*)items, \
+                         n_items, part_size, q_start, q_len, ctx_len, block_table, max_blocks, H, \
+                         KV, scale_log2, pa::g_handoff_attn, nullptr);                          \
   } while (0)
   switch (G) {
     case 1: PA_ATT(1); break;

@@ -310,9 +310,12 @@ class LLMEngine:
         self._host_np = self._host_meta.numpy()
         self._dev_meta = torch.zeros(L["total"], dtype=torch.int32, device=self.device) \
             if (self.on_gpu or self._async) else self._host_meta
-        # attention tickets: one per (sequence, KV head) for split decode rows, then one per
-        # (partial slot, KV head) for split prefill items (csrc/ops/attention.hip prefill_item_wg)
-        self._att_counters = torch.zeros((L["max_seqs"] + L["max_items"]) * kv_local, dtype=torch.int32,
+        # attention tickets: one per (sequence, KV head) for split decode rows, then -- only with
+        # prefill_split_keys on -- one per (partial slot, KV head) for split prefill items
+        # (csrc/ops/attention.hip prefill_item_wg). Without that room the kernel runs its
+        # instantiation with the partition hand-off compiled out (no register spills).
+        pf_slots = L["max_items"] if cfg.prefill_split_keys > 0 else 0
+        self._att_counters = torch.zeros((L["max_seqs"] + pf_slots) * kv_local, dtype=torch.int32,
                                          device=self.device)
         self._init_views()
         V = mc.vocab_size

@@ -91,8 +91,10 @@ def _run_attention(gpu, H, KV, q_lens, ctx_lens, seed=0, split=True, part=512, q
     items, nslots = ops.build_attention_items(q_lens, ctx_lens, G, split=split, part=part,
                                                qcols=qcols, wide_min_tokens=0, split_keys=split_keys)
     it = torch.tensor(items + [(0, 0, 0, 0)] * max(pad, nslots - len(items)), dtype=torch.int32, device=gpu)
-    # per-(sequence, KV head) tickets, then per-(partial slot, KV head) ones for split prefill items
-    cnt = torch.zeros((ns + it.shape[0]) * KV, dtype=torch.int32, device=gpu)
+    # per-(sequence, KV head) tickets, then -- with split prefill items, as the engine -- per-(partial
+    # slot, KV head) ones; without them the kernel runs its instantiation with the partition
+    # hand-off compiled out (both instantiations are covered: split_keys > 0 cases take the other)
+    cnt = torch.zeros((ns + (it.shape[0] if split_keys else 0)) * KV, dtype=torch.int32, device=gpu)
     n_it = torch.tensor([len(items)], dtype=torch.int32, device=gpu)
     maxit = it.shape[0]
     part_o = torch.empty(maxit * KV * 16 * 128, dtype=torch.float32, device=gpu)

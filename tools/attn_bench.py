@@ -46,7 +46,9 @@ def setup(q_lens, ctx_lens, H=32, KV=8, pad_items=0, dev="cuda", part=512, qcols
     n_items = len(items)
     items = items + [(0, 0, 0, 0)] * max(1, pad_items - len(items), nslots - len(items))
     it = torch.tensor(items, dtype=torch.int32, device=dev)
-    cnt = torch.zeros((ns + it.shape[0]) * KV, dtype=torch.int32, device=dev)
+    # ticket room for split prefill items only when splitting (as the engine): without it the
+    # kernel runs the instantiation with the partition hand-off compiled out
+    cnt = torch.zeros((ns + (it.shape[0] if split_keys else 0)) * KV, dtype=torch.int32, device=dev)
     di = lambda a: torch.tensor(a, dtype=torch.int32, device=dev)  # noqa: E731
     n_it = di([n_items])
     part_o = torch.empty(it.shape[0] * KV * 16 * 128, dtype=torch.float32, device=dev)
