@@ -1,6 +1,7 @@
 """Native runtime (tokenizer, grammar automaton, scheduler, block manager) and the
 CPU execution of the full inference engine (tiny model, fp32 reference kernels)."""
 import json
+import os
 
 import numpy as np
 import pytest
@@ -889,3 +890,20 @@ def test_scheduler_small_step_target_splits_few_rows():
         assert len(items) == 8 * want_parts
         if target:
             assert part == 224  # ceil(601 / 3) rounded up to 32 keys
+
+
+def test_engine_split_ticket_room_only_with_split_keys():
+    """The attention launcher runs its SPLIT instantiation (partition hand-off compiled in, 8
+    spilled registers) only when the ticket buffer has room for split prefill items; the engine
+    gives that room only with prefill_split_keys > 0 (the default is 0)."""
+    from pilottai_amd.engine.engine import EngineConfig, LLMEngine
+
+    kw = dict(model="tiny", max_num_seqs=8, max_num_batched_tokens=128, max_model_len=512, num_kv_blocks=64)
+    off = LLMEngine(EngineConfig(**kw), device="cpu")
+    on = LLMEngine(EngineConfig(prefill_split_keys=512, **kw), device="cpu")
+    if "PILOTTAI_PREFILL_SPLIT_KEYS" not in os.environ:
+        assert EngineConfig().prefill_split_keys == 0
+    kv = off.model_cfg.num_kv_heads
+    # per (sequence, KV head) tickets only, vs + per (partial slot, KV head) ones
+    assert off._att_counters.numel() < on._att_counters.numel()
+    assert off._att_counters.numel() % kv == 0 and on._att_counters.numel() % kv == 0
